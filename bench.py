@@ -1,0 +1,294 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json's metric on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    (N > 1: launched by torch.distributed.run, one process per GPU, RCCL)
+
+Headline `value` (files/s, whole job): one STEP = one identifier pass over a
+batch resident in HBM -- BASELINE config 2 per GPU (1 M synthetic files,
+log-normal sizes, 20 % duplicates, 0.1 % empty; only the cas windows exist) --
+consisting of K1 (sampled cas_id of every file) followed by the cas_id ->
+Object grouping of all files of all GPUs (hash-sharded, RCCL all-to-all at
+N > 1).  Weak scaling: every GPU brings its own 1 M files.
+
+Components reported on the same line (each timed the same way, K steps after W
+warm-up, barrier + synchronize on both sides, max over ranks):
+  cas      K1 alone over config 2                              files/s
+  dedup    config 4: 12.5 M rows per GPU (100 M at 8 GPUs)     rows/s
+  checksum config 3: 64 x 4 GiB files per GPU, device-resident GB/s
+`roofline` is for the dominant kernel (K1 "cas_chunks"), timed live with HIP
+events on its launch stream; `cpu_baseline` times the scalar C oracle port of
+generate_cas_id's hashing on this host's cores over a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+VALU_PEAK_SPEC = 256 * 4 * 32 * 2.4e9  # 256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz (lane-ops/s)
+HBM_PEAK = 8.0e12                       # B/s (MI355X spec)
+ISA_PER_COMPRESSION = 680               # fused VALU instructions per BLAKE3 compression
+METRIC = "cas_id files/sec + full-file BLAKE3 GB/s + dedup rows/sec at 1/2/4/8 MI355X"
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def compressions(lens: np.ndarray):
+    """(chunk-block compressions, parent compressions) of messages of these lengths."""
+    L = lens.astype(np.int64)
+    full = L // 1024
+    rem = L % 1024
+    blocks = full * 16 + (rem + 63) // 64
+    blocks = np.where(L == 0, 1, blocks)
+    chunks = np.maximum(1, (L + 1023) // 1024)
+    return int(blocks.sum()), int((chunks - 1).sum())
+
+
+class Runner:
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=self.dev)
+        from spacedrive_amd._native import default_context
+        self.ctx = default_context(self.local)
+        self.args = args
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max_over_ranks(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(self, fn, steps, warmup) -> float:
+        torch = self.torch
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        self.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        self.barrier()
+        torch.cuda.synchronize()
+        return self.max_over_ranks(time.perf_counter() - t0)
+
+    # ---------------------------------------------------------------- config 2
+    def run_cas(self, steps, warmup):
+        torch = self.torch
+        from spacedrive_amd import cas, corpus, dedup
+        n = self.args.files
+        sizes, seeds = corpus.config2_files(n, seed=2 + 1000 * self.rank)
+        arena, off, ln = corpus.synth_arena_device(sizes, seeds, device=self.local, ctx=self.ctx)
+        out = torch.empty((n, 8), dtype=torch.uint8, device=self.dev)
+        st = torch.empty(n, dtype=torch.int32, device=self.dev)
+        has = torch.from_numpy((sizes != 0).astype(np.uint8)).to(self.dev)
+        grank = torch.arange(self.rank * n, (self.rank + 1) * n, dtype=torch.int64,
+                             device=self.dev).to(torch.int32)
+        ops = dedup.HipOps(self.ctx)
+        torch.cuda.synchronize()
+        lens = ln.cpu().numpy().view(np.uint32)
+        blk, par = compressions(lens)
+        res = {}
+
+        def k1():
+            cas.cas_batch_device(arena, off, ln, out, st, ctx=self.ctx)
+
+        def job():
+            k1()
+            key = out.view(torch.int64).view(-1)
+            dedup.sharded_group_reps(key, has, grank, 100, ops=ops)
+
+        # K1 alone, with live per-kernel event timing on its launch stream
+        self.ctx.set_timing(True)
+        t_cas = self.timed(k1, steps, warmup)
+        kt = self.ctx.kernel_times()
+        self.ctx.set_timing(False)
+        assert int(st.abs().sum()) == 0
+        res["cas"] = {"value": self.world * n * steps / t_cas, "unit": "files/s",
+                      "ms_per_step": 1e3 * t_cas / steps,
+                      "config": {"workload": "config2: 1M log-normal files/GPU, 20% dup, 0.1% empty",
+                                 "files_per_gpu": n, "window_bytes_per_gpu": int(lens.sum())}}
+        ms_chunks, nl = kt.get("cas_chunks", (0.0, 1))
+        ms_par, _ = kt.get("cas_parents", (0.0, 1))
+        avg_chunks = ms_chunks / max(nl, 1) * 1e-3
+        avg_par = ms_par / max(nl, 1) * 1e-3
+        res["kernels"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in kt.items()}
+        # identifier job step: K1 + sharded grouping (RCCL all-to-all at N > 1)
+        t_job = self.timed(job, steps, warmup)
+        res["job"] = {"value": self.world * n * steps / t_job, "ms_per_step": 1e3 * t_job / steps}
+        res["roofline_inputs"] = {"chunk_blocks": blk, "parents": par,
+                                  "avg_chunks_s": avg_chunks, "avg_parents_s": avg_par,
+                                  "bytes": int(lens.sum())}
+        self._cpu_sample = (arena, off, ln, min(n, self.args.cpu_files))
+        return res
+
+    # ---------------------------------------------------------------- config 4
+    def run_dedup(self, steps, warmup):
+        torch = self.torch
+        from spacedrive_amd import corpus, dedup
+        per = self.args.dedup_rows
+        total = per * self.world
+        key, has, rank = corpus.synth_dedup_rows_device(4, total, int(total * 0.8),
+                                                        self.rank * per, per,
+                                                        device=self.local, ctx=self.ctx)
+        ops = dedup.HipOps(self.ctx)
+        self.ctx.set_timing(True)
+        t = self.timed(lambda: dedup.sharded_group_reps(key, has, rank, 100, ops=ops), steps,
+                       warmup)
+        kt = self.ctx.kernel_times()
+        self.ctx.set_timing(False)
+        return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
+                "config": {"workload": "config4: 80% distinct u64 keys + 20% dups, 0.1% keyless",
+                           "rows_per_gpu": per, "rows_total": total},
+                "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
+                            for k, v in kt.items()}}
+
+    # ---------------------------------------------------------------- config 3
+    def run_checksum(self, steps, warmup):
+        torch = self.torch
+        from spacedrive_amd import corpus, validation
+        nf, flen = self.args.checksum_files, self.args.checksum_bytes
+        files = []
+        try:
+            for i in range(nf):
+                files.append(corpus.synth_file_device(3 + 7919 * i + 104729 * self.rank, flen,
+                                                      device=self.local, ctx=self.ctx))
+        except (RuntimeError, MemoryError) as e:  # torch OOM
+            log(f"checksum: only {len(files)} of {nf} files fit: {e}")
+        torch.cuda.synchronize()
+        out = torch.empty((len(files), 32), dtype=torch.uint8, device=self.dev)
+        self.ctx.set_timing(True)
+        t = self.timed(lambda: validation.checksum_batch_device(files, out=out, ctx=self.ctx),
+                       steps, warmup)
+        kt = self.ctx.kernel_times()
+        self.ctx.set_timing(False)
+        nbytes = len(files) * flen
+        res = {"value": self.world * nbytes * steps / t / 1e9, "unit": "GB/s",
+               "ms_per_step": 1e3 * t / steps,
+               "config": {"workload": "config3: 4 GiB files, device-resident",
+                          "files_per_gpu": len(files), "file_bytes": flen},
+               "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
+                           for k, v in kt.items()}}
+        # VALU roofline of the leaf kernel: 16 compressions per chunk + parents
+        chunks = nbytes // 1024
+        comp = chunks * 16 + (chunks - len(files))
+        lv = kt.get("tree_leaves", (0.0, 1))
+        if lv[0] > 0:
+            res["leaf_valu_frac_spec"] = comp * ISA_PER_COMPRESSION / (lv[0] / lv[1] * 1e-3) \
+                / VALU_PEAK_SPEC
+        del files
+        return res
+
+    def cpu_baseline(self):
+        from oracle import oracle as O
+        arena, off, ln, m = self._cpu_sample
+        h_off = off[:m].cpu().numpy().view(np.uint64)
+        h_len = ln[:m].cpu().numpy().view(np.uint32)
+        end = int(h_off[-1] + h_len[-1])
+        host = arena[:end].cpu().numpy()
+        threads = min(16, os.cpu_count() or 1)
+        O.cas_batch(host, h_off[:100], h_len[:100], threads)  # warm
+        t0 = time.perf_counter()
+        O.cas_batch(host, h_off, h_len, threads)
+        dt = time.perf_counter() - t0
+        return {"value": m / dt, "unit": "files/s", "cores": threads, "kind": "port",
+                "sample": f"first {m} files of config 2 (their {int(h_len.sum())} window bytes "
+                          f"in host RAM), scalar C BLAKE3 oracle, {threads} threads, "
+                          f"{dt:.2f} s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--files", type=int, default=1_000_000)
+    ap.add_argument("--dedup-rows", type=int, default=12_500_000)
+    ap.add_argument("--checksum-files", type=int, default=64)
+    ap.add_argument("--checksum-bytes", type=int, default=1 << 32)
+    ap.add_argument("--cpu-files", type=int, default=100_000)
+    ap.add_argument("--components", default="cas,dedup,checksum")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    comps = set(args.components.split(","))
+
+    R = Runner(args)
+    torch = R.torch
+    valu_peak = R.ctx.valu_peak()
+    log(f"measured int32 VALU peak: {valu_peak / 1e12:.1f} T lane-ops/s "
+        f"(spec {VALU_PEAK_SPEC / 1e12:.1f})")
+    c = R.run_cas(args.steps, args.warmup)
+    log("cas:", json.dumps(c["cas"]), json.dumps(c["kernels"]))
+    cpu = None
+    if R.rank == 0 and not args.no_cpu:
+        cpu = R.cpu_baseline()
+        log("cpu:", json.dumps(cpu))
+    R._cpu_sample = None
+    torch.cuda.empty_cache()
+    comp = {"cas": c["cas"], "identifier_job": c["job"]}
+    if "dedup" in comps:
+        d = R.run_dedup(args.steps, args.warmup)
+        log("dedup:", json.dumps(d))
+        comp["dedup"] = d
+        torch.cuda.empty_cache()
+    if "checksum" in comps:
+        k = R.run_checksum(args.steps, args.warmup)
+        log("checksum:", json.dumps(k))
+        comp["checksum"] = k
+        torch.cuda.empty_cache()
+
+    ri = c["roofline_inputs"]
+    ops = ri["chunk_blocks"] * ISA_PER_COMPRESSION
+    achieved = ops / ri["avg_chunks_s"] if ri["avg_chunks_s"] > 0 else 0.0
+    roof = {"bound": "valu", "kernel": "cas_chunks (K1)",
+            "achieved": achieved / 1e12, "peak": VALU_PEAK_SPEC / 1e12, "unit": "Tops/s",
+            "frac": achieved / VALU_PEAK_SPEC, "traffic": None,
+            "peak_measured": valu_peak / 1e12,
+            "frac_of_measured": achieved / valu_peak if valu_peak else None,
+            "algorithmic_per_launch": {"compressions": ri["chunk_blocks"],
+                                       "int32_ops": ops, "window_bytes": ri["bytes"]},
+            "hbm_GBps": ri["bytes"] / ri["avg_chunks_s"] / 1e9 if ri["avg_chunks_s"] else None,
+            "hbm_frac": ri["bytes"] / ri["avg_chunks_s"] / HBM_PEAK if ri["avg_chunks_s"] else None}
+    job = c["job"]
+    line = {"metric": METRIC, "value": job["value"], "unit": "files/s", "n_gpus": R.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": job["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (BASELINE configs 2/3/4 shapes, generated in HBM)",
+            "config": {"workload": "identifier job step: config2 (1M files/GPU) cas_id + "
+                                   "sharded cas_id->Object grouping",
+                       "files_per_gpu": args.files, "global_files": args.files * R.world,
+                       "parallelism": f"dp{R.world} (files) + hash-sharded dedup, RCCL all-to-all"},
+            "components": comp, "kernels": c["kernels"], "roofline": roof, "cpu_baseline": cpu}
+    if R.rank == 0:
+        print(json.dumps(line), flush=True)
+    if R.world > 1:
+        R.dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

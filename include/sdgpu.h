@@ -1,0 +1,197 @@
+/*
+ * sdgpu.h -- C ABI of libsdgpu.so: MI355X (gfx950) content identification for
+ * Spacedrive's sd-core.
+ *
+ * This is the drop-in boundary for the hot path named in BASELINE.json: the
+ * sampled-BLAKE3 cas_id, the full-file BLAKE3 integrity checksum and the
+ * cas_id -> Object grouping step.  Every entry point below replaces a
+ * reference function; the replaced interface is cited (file:line, paths
+ * relative to the Spacedrive repository).  INTEGRATION.md shows the Rust FFI
+ * binding (`extern "C"` block + wrappers keeping the reference signatures).
+ *
+ * Conventions
+ *  - Plain C types only; no C++ or torch types cross this boundary.
+ *  - Return value: 0 on success, a negative errno on failure (-EINVAL bad
+ *    argument, -ENOMEM allocation, -ENODEV no usable GPU, -EIO HIP runtime
+ *    error, or the -errno of a failed open/read/seek).  Per-item statuses use
+ *    the same encoding, so a Rust caller maps them with
+ *    io::Error::from_raw_os_error(-status) (FileIOError, core/src/util/error.rs:5-20).
+ *  - "_device" entry points take device pointers and a hipStream_t passed as
+ *    `void* stream` (NULL = the context's own stream) and return without
+ *    synchronising; all others take host pointers and return when done.
+ *  - A context is used by one host thread at a time (the reference runs one
+ *    job at a time, core/src/job/manager.rs:32); its device workspace is
+ *    shared by all calls made through it.
+ *  - Hex formatting stays with the caller: cas_id = lowercase hex of the 8
+ *    returned bytes (cas.rs:61 `to_hex()[..16]`), checksum = lowercase hex of
+ *    the 32 returned bytes (validation/hash.rs:21-23).  The path-based helpers
+ *    additionally return the formatted strings.
+ */
+#ifndef SDGPU_H
+#define SDGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDGPU_ABI_VERSION 1
+
+/* cas.rs:10-15 */
+#define SDGPU_CAS_SAMPLE_COUNT 4u
+#define SDGPU_CAS_SAMPLE_SIZE 10240u
+#define SDGPU_CAS_HEADER_OR_FOOTER_SIZE 8192u
+#define SDGPU_CAS_MINIMUM_FILE_SIZE 102400u
+/* Largest cas message: u64 size || whole 100 KiB file. */
+#define SDGPU_CAS_MAX_MSG_LEN (8u + SDGPU_CAS_MINIMUM_FILE_SIZE)
+/* Message of a sampled (> 100 KiB) file: 8 + 8192 + 4 * 10240 + 8192. */
+#define SDGPU_CAS_SAMPLED_MSG_LEN 57352u
+/* identifier_job_step batch size, file_identifier/mod.rs:36 */
+#define SDGPU_IDENTIFIER_CHUNK_SIZE 100u
+
+typedef struct sdgpu_ctx sdgpu_ctx;
+
+int sdgpu_abi_version(void);
+const char *sdgpu_strerror(int rc);
+
+/* ---- context / memory ------------------------------------------------------ */
+int sdgpu_device_count(int *count);
+int sdgpu_open(int device, sdgpu_ctx **out);
+int sdgpu_close(sdgpu_ctx *ctx);
+/* Waits for all work issued through ctx (its stream and the last stream
+ * passed to a _device call). */
+int sdgpu_sync(sdgpu_ctx *ctx);
+/* The context's hipStream_t. */
+void *sdgpu_stream(sdgpu_ctx *ctx);
+int sdgpu_alloc_pinned(sdgpu_ctx *ctx, size_t bytes, void **out);
+int sdgpu_free_pinned(sdgpu_ctx *ctx, void *p);
+int sdgpu_alloc_device(sdgpu_ctx *ctx, size_t bytes, void **out);
+int sdgpu_free_device(sdgpu_ctx *ctx, void *p);
+/* Asynchronous copy on `stream` (direction inferred by the runtime). */
+int sdgpu_memcpy_async(sdgpu_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
+
+/* ---- K1: sampled cas_id ------------------------------------------------------
+ * Replaces the hashing of generate_cas_id (core/src/object/cas.rs:23-62) for a
+ * whole batch of files (identifier_job_step, file_identifier/mod.rs:107-134).
+ * Message i is msg_arena[msg_off[i] .. msg_off[i] + msg_len[i]) and must be
+ * the exact byte sequence the reference feeds its Hasher:
+ *   u64 size little-endian || file bytes          (size <= 100 KiB, cas.rs:27-29)
+ *   u64 size LE || file[0,8192) || 4 x file[8192 + k*((size-16384)/4), +10240)
+ *     || file[len-8192, len)                       (size > 100 KiB, cas.rs:30-58)
+ * msg_off[i] % 16 == 0 and msg_len[i] <= SDGPU_CAS_MAX_MSG_LEN, else
+ * status[i] = -EINVAL and out8[i] is zeroed.  out8[i] = BLAKE3(M_i)[0..8).
+ * status may be NULL. */
+int sdgpu_cas_batch(sdgpu_ctx *ctx, const uint8_t *msg_arena, const uint64_t *msg_off,
+                    const uint32_t *msg_len, uint32_t n, uint8_t (*out8)[8], int32_t *status);
+/* Device-resident variant; arena_bytes bounds the arena (sizes workspace). */
+int sdgpu_cas_batch_device(sdgpu_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes,
+                           const uint64_t *d_off, const uint32_t *d_len, uint32_t n,
+                           uint8_t *d_out8, int32_t *d_status, void *stream);
+
+/* Path-based drop-in for generate_cas_id(path, size) (cas.rs:23): same reads
+ * as the reference (open, header, 4 samples by seek, footer from the actual
+ * end), hash on the GPU, out_hex = 16 lowercase hex chars + NUL. */
+int sdgpu_generate_cas_id(sdgpu_ctx *ctx, const char *path, uint64_t size, char out_hex[17]);
+
+/* Batched file identifier staging (file_identifier/mod.rs:107-134 join_all of
+ * FileMetadata::new -> generate_cas_id): reads the cas windows of n files with
+ * pread into pinned buffers, pipelines H2D copies with K1 in slabs.  size[i] is
+ * the fs::metadata length (mod.rs:65,80-81); size 0 yields status 0 and
+ * has_key[i] = 0 (cas_id None, mod.rs:80-88); I/O errors yield status -errno
+ * and has_key 0 (row dropped, mod.rs:113,127).  has_key may be NULL. */
+int sdgpu_identify_files(sdgpu_ctx *ctx, const char *const *paths, const uint64_t *size,
+                         uint32_t n, uint8_t (*out8)[8], uint8_t *has_key, int32_t *status);
+
+/* ---- K2/K3: full-file checksum -------------------------------------------------
+ * Replaces file_checksum (core/src/object/validation/hash.rs:10-24). */
+/* BLAKE3 of a host buffer. */
+int sdgpu_checksum(sdgpu_ctx *ctx, const void *bytes, uint64_t len, uint8_t out32[32]);
+/* BLAKE3 of n device-resident files (pointers 16-B aligned); d_files and lens
+ * are HOST arrays of device addresses / byte lengths, d_out32 is device [n][32]. */
+int sdgpu_checksum_batch_device(sdgpu_ctx *ctx, const uint8_t *const *d_files,
+                                const uint64_t *lens, uint32_t n, uint8_t *d_out32, void *stream);
+/* Chaining value of one aligned subtree slice (for streaming hosts): len bytes
+ * starting at chunk counter chunk_offset; chunk_offset must be a multiple of
+ * the slice's chunk count rounded up to a power of two.  root=1 gives the digest
+ * of a whole message (chunk_offset 0). */
+int sdgpu_subtree_device(sdgpu_ctx *ctx, const uint8_t *d_bytes, uint64_t len,
+                         uint64_t chunk_offset, int root, uint8_t *d_out32, void *stream);
+/* Path-based drop-in for file_checksum(path): streams the file in 64 MiB
+ * power-of-two slices through double-buffered pinned memory; out_hex = 64
+ * lowercase hex chars + NUL. */
+int sdgpu_file_checksum(sdgpu_ctx *ctx, const char *path, char out_hex[65]);
+
+/* ---- K4-K6: cas_id -> Object grouping ------------------------------------------
+ * Replaces the Object link/create decisions of identifier_job_step
+ * (file_identifier/mod.rs:167-333) over the orphan rows in ascending id order
+ * processed in chunks of chunk_rows (=100, mod.rs:36; file_identifier_job.rs:286-309).
+ * Rows are identified by their rank r (position in id order).  Output rep[r]:
+ * the rank of the row whose Object row r is linked to:
+ *   - has_key[r] == 0 (empty file, cas_id None): rep[r] = r;
+ *   - r in the chunk holding the lowest-rank row f of its key: rep[r] = r
+ *     (a new Object per row, mod.rs:233-297);
+ *   - otherwise rep[r] = f (linked to an existing Object, mod.rs:189-225).
+ * key = the 8 cas bytes read as a little-endian u64 (equality is all the
+ * grouping uses, mod.rs:136-141,196-203). */
+int sdgpu_dedup(sdgpu_ctx *ctx, const uint64_t *key, const uint8_t *has_key, uint32_t n,
+                uint32_t chunk_rows, uint32_t *rep);
+/* Device-resident, one GPU: rows given as (key, rank) pairs (rows without a
+ * key are simply not passed); writes rep for each pair at the same index.
+ * skip_bits: number of top key bits that are constant on this shard (log2 of
+ * the number of GPUs the keys were hash-partitioned over; 0 on one GPU). */
+int sdgpu_group_pairs_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint32_t *d_rank,
+                             uint64_t n, uint32_t chunk_rows, uint32_t skip_bits, uint32_t *d_rep,
+                             void *stream);
+/* Sharding helpers for the multi-GPU dedup (one process per GPU, RCCL
+ * all-to-all between them): shard of a key = its top shard_bits bits.
+ * count: h_counts[s] = rows with has_key destined to shard s (host array of
+ * 2^shard_bits; synchronises).  partition: packs those rows by shard into
+ * d_out_key/d_out_rank (shard s at exclusive prefix of counts) and records each
+ * packed row's source index in d_out_pos. */
+int sdgpu_shard_count_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t *d_has_key,
+                             uint64_t n, uint32_t shard_bits, uint64_t *h_counts, void *stream);
+int sdgpu_shard_partition_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t *d_has_key,
+                                 const uint32_t *d_rank, uint64_t n, uint32_t shard_bits,
+                                 uint64_t *d_out_key, uint32_t *d_out_rank, uint32_t *d_out_pos,
+                                 void *stream);
+/* d_dst[d_pos[i]] = d_src[i] for i < n.  With init != 0 every row of d_dst is
+ * first set to d_init[r] (or to r when d_init is NULL), so rows without a key
+ * keep their own rank (mod.rs:238-239). */
+int sdgpu_scatter_rep_device(sdgpu_ctx *ctx, const uint32_t *d_src, const uint32_t *d_pos,
+                             uint64_t n, uint32_t *d_dst, uint64_t n_dst, const uint32_t *d_init,
+                             int init, void *stream);
+
+/* ---- synthetic corpora (bench / tests; same content function as oracle/) ---- */
+int sdgpu_synth_cas_arena_device(sdgpu_ctx *ctx, const uint64_t *d_sizes, const uint64_t *d_seeds,
+                                 const uint64_t *d_off, uint32_t n, uint8_t *d_arena, void *stream);
+int sdgpu_synth_file_device(sdgpu_ctx *ctx, uint64_t seed, uint64_t offset, uint64_t len,
+                            uint8_t *d_out, void *stream);
+/* Dedup corpus (BASELINE config 4 shape): global rows [first_rank, first_rank+n)
+ * of a table of total_rows rows whose keys are a random permutation of
+ * `distinct` distinct keys plus (total_rows - distinct) duplicates of them;
+ * one row in 1000 has no key.  Writes key, has_key and rank (= global row). */
+int sdgpu_synth_dedup_rows_device(sdgpu_ctx *ctx, uint64_t seed, uint64_t total_rows,
+                                  uint64_t distinct, uint64_t first_rank, uint64_t n,
+                                  uint64_t *d_key, uint8_t *d_has_key, uint32_t *d_rank,
+                                  void *stream);
+
+/* ---- instrumentation (bench / profiling) ---------------------------------------
+ * With timing enabled every main kernel launched through ctx is bracketed by
+ * HIP events on its own stream; sdgpu_timing_read returns, per kernel name
+ * (e.g. "cas_chunks", "tree_leaves", "bucket_group"), the accumulated device
+ * milliseconds and launch count (-ENOENT past the last entry). */
+int sdgpu_set_timing(sdgpu_ctx *ctx, int enable);
+int sdgpu_timing_reset(sdgpu_ctx *ctx);
+int sdgpu_timing_read(sdgpu_ctx *ctx, uint32_t idx, char name[32], double *total_ms,
+                      uint64_t *launches);
+/* Measured int32 VALU issue rate (lane-ops/s) of a BLAKE3-G-shaped
+ * add3/xor/alignbit stream at full occupancy: the VALU roofline's peak. */
+int sdgpu_valu_probe(sdgpu_ctx *ctx, double *lane_ops_per_s);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SDGPU_H */

@@ -1,0 +1,204 @@
+"""ctypes wrapper of the C oracle (oracle/liboracle.so) -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  The product path (spacedrive_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(_LIB_PATH) or (
+            os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "sd_oracle.c"))):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.orc_blake3.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.orc_blake3_mt.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        L.orc_blake3_incremental.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                             ctypes.c_void_p]
+        L.orc_blake3_derive_key.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
+                                            ctypes.c_size_t, ctypes.c_void_p]
+        L.orc_blake3_keyed.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                       ctypes.c_void_p]
+        L.orc_cas_msg_len.argtypes = [ctypes.c_uint64]
+        L.orc_cas_msg_len.restype = ctypes.c_uint32
+        L.orc_cas_build_message.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                            ctypes.c_void_p]
+        L.orc_cas_build_message.restype = ctypes.c_int64
+        L.orc_cas_id_of_message.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p]
+        L.orc_cas_id_path.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p]
+        L.orc_cas_id_path.restype = ctypes.c_int
+        L.orc_file_checksum_path.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_file_checksum_path.restype = ctypes.c_int
+        L.orc_cas_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
+        L.orc_synth_file_bytes.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                           ctypes.c_void_p]
+        L.orc_synth_cas_message.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+        L.orc_synth_cas_message.restype = ctypes.c_uint32
+        L.orc_synth_arena_layout.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                             ctypes.c_void_p]
+        L.orc_synth_arena_layout.restype = ctypes.c_uint64
+        L.orc_synth_arena_fill.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
+        L.orc_group_reps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                     ctypes.c_uint32, ctypes.c_void_p]
+        L.orc_group_reps.restype = ctypes.c_int
+        L.orc_synth_dedup_rows.argtypes = [ctypes.c_uint64] * 5 + [ctypes.c_void_p] * 3
+        del u8p
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _buf(data: bytes | np.ndarray) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+def blake3(data, threads: int = 1) -> bytes:
+    a = _buf(data)
+    out = np.zeros(32, np.uint8)
+    if threads > 1:
+        lib().orc_blake3_mt(_ptr(a), a.size, threads, _ptr(out))
+    else:
+        lib().orc_blake3(_ptr(a), a.size, _ptr(out))
+    return out.tobytes()
+
+
+def blake3_incremental(data, piece: int) -> bytes:
+    a = _buf(data)
+    out = np.zeros(32, np.uint8)
+    lib().orc_blake3_incremental(_ptr(a), a.size, piece, _ptr(out))
+    return out.tobytes()
+
+
+def derive_key(context: str, material: bytes) -> bytes:
+    a = _buf(material)
+    out = np.zeros(32, np.uint8)
+    c = context.encode()
+    lib().orc_blake3_derive_key(c, len(c), _ptr(a), a.size, _ptr(out))
+    return out.tobytes()
+
+
+def keyed_hash(key32: bytes, data) -> bytes:
+    k = _buf(key32)
+    a = _buf(data)
+    out = np.zeros(32, np.uint8)
+    lib().orc_blake3_keyed(_ptr(k), _ptr(a), a.size, _ptr(out))
+    return out.tobytes()
+
+
+def cas_msg_len(size: int) -> int:
+    return int(lib().orc_cas_msg_len(size))
+
+
+def cas_build_message(file: bytes, size: int | None = None) -> bytes | None:
+    f = _buf(file)
+    if size is None:
+        size = f.size
+    out = np.zeros(max(8 + f.size, 57352), np.uint8)
+    n = lib().orc_cas_build_message(_ptr(f), f.size, size, _ptr(out))
+    return None if n < 0 else out[:n].tobytes()
+
+
+def cas_id_of_message(msg) -> str:
+    a = _buf(msg)
+    out = ctypes.create_string_buffer(17)
+    lib().orc_cas_id_of_message(_ptr(a), a.size, out)
+    return out.value.decode()
+
+
+def cas_id_of_file_bytes(file: bytes, size: int | None = None) -> str:
+    msg = cas_build_message(file, size)
+    if msg is None:
+        raise EOFError("read_exact: UnexpectedEof")
+    return cas_id_of_message(msg)
+
+
+def cas_id_path(path: str, size: int) -> str:
+    out = ctypes.create_string_buffer(17)
+    rc = lib().orc_cas_id_path(os.fsencode(path), size, out)
+    if rc:
+        raise OSError(-rc, os.strerror(-rc), path)
+    return out.value.decode()
+
+
+def file_checksum_path(path: str) -> str:
+    out = ctypes.create_string_buffer(65)
+    rc = lib().orc_file_checksum_path(os.fsencode(path), out)
+    if rc:
+        raise OSError(-rc, os.strerror(-rc), path)
+    return out.value.decode()
+
+
+def cas_batch(arena: np.ndarray, off: np.ndarray, length: np.ndarray, threads: int = 1) -> np.ndarray:
+    off = np.ascontiguousarray(off, np.uint64)
+    length = np.ascontiguousarray(length, np.uint32)
+    out = np.zeros((off.size, 8), np.uint8)
+    lib().orc_cas_batch(_ptr(arena), _ptr(off), _ptr(length), off.size, _ptr(out), threads)
+    return out
+
+
+def synth_file_bytes(seed: int, offset: int, n: int) -> bytes:
+    out = np.zeros(n, np.uint8)
+    lib().orc_synth_file_bytes(seed, offset, n, _ptr(out))
+    return out.tobytes()
+
+
+def synth_cas_message(size: int, seed: int) -> bytes:
+    out = np.zeros(57352 if size > 102400 else 8 + size, np.uint8)
+    n = lib().orc_synth_cas_message(size, seed, _ptr(out))
+    return out[:n].tobytes()
+
+
+def synth_arena(sizes: np.ndarray, seeds: np.ndarray, threads: int = 8):
+    """(arena, off, len) of synthetic cas messages packed at 128-B offsets."""
+    sizes = np.ascontiguousarray(sizes, np.uint64)
+    seeds = np.ascontiguousarray(seeds, np.uint64)
+    off = np.zeros(sizes.size, np.uint64)
+    ln = np.zeros(sizes.size, np.uint32)
+    total = lib().orc_synth_arena_layout(_ptr(sizes), sizes.size, _ptr(off), _ptr(ln))
+    arena = np.zeros(int(total) + 128, np.uint8)
+    lib().orc_synth_arena_fill(_ptr(sizes), _ptr(seeds), _ptr(off), sizes.size, _ptr(arena), threads)
+    return arena, off, ln
+
+
+def group_reps(key: np.ndarray, has_key: np.ndarray, chunk_rows: int = 100) -> np.ndarray:
+    key = np.ascontiguousarray(key, np.uint64)
+    has_key = np.ascontiguousarray(has_key, np.uint8)
+    rep = np.zeros(key.size, np.uint32)
+    rc = lib().orc_group_reps(_ptr(key), _ptr(has_key), key.size, chunk_rows, _ptr(rep))
+    if rc:
+        raise OSError(-rc, os.strerror(-rc))
+    return rep
+
+
+def synth_dedup_rows(seed: int, total: int, distinct: int, first: int, n: int):
+    key = np.zeros(n, np.uint64)
+    has = np.zeros(n, np.uint8)
+    rank = np.zeros(n, np.uint32)
+    lib().orc_synth_dedup_rows(seed, total, distinct, first, n, _ptr(key), _ptr(has), _ptr(rank))
+    return key, has, rank

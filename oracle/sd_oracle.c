@@ -1,0 +1,825 @@
+/*
+ * sd_oracle.c -- CPU ORACLE for the Spacedrive content-identification hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product path (spacedrive_amd/,
+ * libsdgpu.so) links, loads or calls this file.  Only tests/, the smoke() check
+ * in __graft_entry__.py and bench.py's cpu_baseline leg use it, and only as the
+ * checker / the timed CPU baseline, never as the thing measured on the GPU.
+ *
+ * What it restates (plain C, scalar, written from the specs below):
+ *
+ *  - BLAKE3 (third-party crate `blake3` 1.4.1, /root/reference/Cargo.lock:620-631;
+ *    NOT vendored under /root/reference).  Restated from the published BLAKE3
+ *    specification: SHA-256 IV, 7 rounds, G rotations 16/12/8/7, message
+ *    permutation [2,6,3,10,7,0,4,13,1,11,12,5,9,14,15,8], 1 KiB chunks of 16
+ *    64-byte blocks, flags CHUNK_START=1 CHUNK_END=2 PARENT=4 ROOT=8
+ *    KEYED_HASH=16 DERIVE_KEY_CONTEXT=32 DERIVE_KEY_MATERIAL=64, left-complete
+ *    binary tree of chunk chaining values.
+ *    The tree here is built RECURSIVELY (split at the largest power of two
+ *    strictly below the chunk count), deliberately unlike the incremental
+ *    CV-stack formulation of oracle/blake3_py.py, so the two restatements
+ *    cross-check each other's tree shape.
+ *    Pinned by the reference's only BLAKE3 known-answer test,
+ *    /root/reference/crates/crypto/src/keys/hashing.rs:324-327 (derive_b3,
+ *    expected bytes :210-213, inputs :121,132-141, concatenation order
+ *    /root/reference/crates/crypto/src/types.rs:163-170), and by the spec's
+ *    hash of the empty input.
+ *
+ *  - generate_cas_id  (/root/reference/core/src/object/cas.rs:23-62), incl. the
+ *    exact file-I/O pattern (open, read_exact header, 4 x {read_exact 10 KiB,
+ *    seek}, seek End(-8192), read_exact footer) for the CPU baseline.
+ *
+ *  - file_checksum    (/root/reference/core/src/object/validation/hash.rs:10-24),
+ *    1 MiB reads, stop at the first short read.
+ *
+ *  - the cas_id -> Object grouping rule of identifier_job_step
+ *    (/root/reference/core/src/object/file_identifier/mod.rs:167-333) over
+ *    CHUNK_SIZE=100 chunks (mod.rs:36, file_identifier_job.rs:286-309), in the
+ *    canonical form fixed in SURVEY.md §8(a) row a6.
+ *
+ *  - the synthetic corpus content function shared with the device generator
+ *    (spacedrive_amd/csrc/synth.hip); see DESIGN.md "Synthetic corpora".
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+/* ------------------------------------------------------------------------- */
+/* BLAKE3 core                                                               */
+/* ------------------------------------------------------------------------- */
+
+enum {
+  B3_CHUNK_START = 1,
+  B3_CHUNK_END = 2,
+  B3_PARENT = 4,
+  B3_ROOT = 8,
+  B3_KEYED_HASH = 16,
+  B3_DERIVE_KEY_CONTEXT = 32,
+  B3_DERIVE_KEY_MATERIAL = 64,
+};
+
+#define B3_BLOCK 64u
+#define B3_CHUNK 1024u
+
+static const uint32_t B3_IV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u,
+                                  0xA54FF53Au, 0x510E527Fu, 0x9B05688Cu,
+                                  0x1F83D9ABu, 0x5BE0CD19u};
+
+static const uint8_t B3_PERM[16] = {2, 6, 3, 10, 7, 0, 4, 13,
+                                    1, 11, 12, 5, 9, 14, 15, 8};
+
+static inline uint32_t rotr32(uint32_t x, int n) {
+  return (x >> n) | (x << (32 - n));
+}
+
+static inline uint32_t load32le(const uint8_t *p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+         ((uint32_t)p[3] << 24);
+}
+
+static inline void store32le(uint8_t *p, uint32_t w) {
+  p[0] = (uint8_t)w;
+  p[1] = (uint8_t)(w >> 8);
+  p[2] = (uint8_t)(w >> 16);
+  p[3] = (uint8_t)(w >> 24);
+}
+
+static inline void b3_g(uint32_t *s, int a, int b, int c, int d, uint32_t x,
+                        uint32_t y) {
+  s[a] = s[a] + s[b] + x;
+  s[d] = rotr32(s[d] ^ s[a], 16);
+  s[c] = s[c] + s[d];
+  s[b] = rotr32(s[b] ^ s[c], 12);
+  s[a] = s[a] + s[b] + y;
+  s[d] = rotr32(s[d] ^ s[a], 8);
+  s[c] = s[c] + s[d];
+  s[b] = rotr32(s[b] ^ s[c], 7);
+}
+
+/* Full compression; writes the 16-word output (first 8 words = new CV). */
+static void b3_compress(const uint32_t cv[8], const uint8_t block[64],
+                        uint64_t counter, uint32_t block_len, uint32_t flags,
+                        uint32_t out[16]) {
+  uint32_t m[16], t[16], s[16];
+  for (int i = 0; i < 16; i++) m[i] = load32le(block + 4 * i);
+  for (int i = 0; i < 8; i++) s[i] = cv[i];
+  s[8] = B3_IV[0];
+  s[9] = B3_IV[1];
+  s[10] = B3_IV[2];
+  s[11] = B3_IV[3];
+  s[12] = (uint32_t)counter;
+  s[13] = (uint32_t)(counter >> 32);
+  s[14] = block_len;
+  s[15] = flags;
+  for (int r = 0; r < 7; r++) {
+    b3_g(s, 0, 4, 8, 12, m[0], m[1]);
+    b3_g(s, 1, 5, 9, 13, m[2], m[3]);
+    b3_g(s, 2, 6, 10, 14, m[4], m[5]);
+    b3_g(s, 3, 7, 11, 15, m[6], m[7]);
+    b3_g(s, 0, 5, 10, 15, m[8], m[9]);
+    b3_g(s, 1, 6, 11, 12, m[10], m[11]);
+    b3_g(s, 2, 7, 8, 13, m[12], m[13]);
+    b3_g(s, 3, 4, 9, 14, m[14], m[15]);
+    if (r < 6) {
+      for (int i = 0; i < 16; i++) t[i] = m[B3_PERM[i]];
+      memcpy(m, t, sizeof m);
+    }
+  }
+  for (int i = 0; i < 8; i++) {
+    out[i] = s[i] ^ s[i + 8];
+    out[i + 8] = s[i + 8] ^ cv[i];
+  }
+}
+
+/* Output of a node: either a chunk's last block or a parent block, kept
+ * un-compressed so the caller decides between CV and ROOT output. */
+typedef struct {
+  uint32_t cv[8];
+  uint8_t block[64];
+  uint64_t counter;
+  uint32_t block_len;
+  uint32_t flags;
+} b3_output;
+
+static void b3_output_cv(const b3_output *o, uint32_t cv[8]) {
+  uint32_t w[16];
+  b3_compress(o->cv, o->block, o->counter, o->block_len, o->flags, w);
+  memcpy(cv, w, 32);
+}
+
+static void b3_output_root(const b3_output *o, uint8_t out32[32]) {
+  uint32_t w[16];
+  /* root output block 0: counter 0, ROOT flag added */
+  b3_compress(o->cv, o->block, 0, o->block_len, o->flags | B3_ROOT, w);
+  for (int i = 0; i < 8; i++) store32le(out32 + 4 * i, w[i]);
+}
+
+/* Chunk `chunk_index` holding `len` (0..1024) bytes at `in`. */
+static void b3_chunk_output(const uint32_t key[8], uint32_t base_flags,
+                            const uint8_t *in, size_t len,
+                            uint64_t chunk_index, b3_output *o) {
+  uint32_t cv[8];
+  memcpy(cv, key, 32);
+  size_t nblocks = len == 0 ? 1 : (len + B3_BLOCK - 1) / B3_BLOCK;
+  for (size_t b = 0; b < nblocks; b++) {
+    uint8_t blk[64];
+    size_t off = b * B3_BLOCK;
+    size_t bl = len - off < B3_BLOCK ? len - off : B3_BLOCK;
+    if (len == 0) bl = 0;
+    memset(blk, 0, sizeof blk);
+    if (bl) memcpy(blk, in + off, bl);
+    uint32_t flags = base_flags;
+    if (b == 0) flags |= B3_CHUNK_START;
+    if (b == nblocks - 1) {
+      flags |= B3_CHUNK_END;
+      memcpy(o->cv, cv, 32);
+      memcpy(o->block, blk, 64);
+      o->counter = chunk_index;
+      o->block_len = (uint32_t)bl;
+      o->flags = flags;
+      return;
+    }
+    uint32_t w[16];
+    b3_compress(cv, blk, chunk_index, (uint32_t)bl, flags, w);
+    memcpy(cv, w, 32);
+  }
+}
+
+static void b3_parent_output(const uint32_t key[8], uint32_t base_flags,
+                             const uint32_t l[8], const uint32_t r[8],
+                             b3_output *o) {
+  memcpy(o->cv, key, 32);
+  for (int i = 0; i < 8; i++) {
+    store32le(o->block + 4 * i, l[i]);
+    store32le(o->block + 32 + 4 * i, r[i]);
+  }
+  o->counter = 0;
+  o->block_len = 64;
+  o->flags = base_flags | B3_PARENT;
+}
+
+static uint64_t largest_pow2_below(uint64_t n) { /* n >= 2 */
+  uint64_t p = 1;
+  while (p * 2 < n) p *= 2;
+  return p;
+}
+
+/* Recursive subtree over chunks [first_chunk, first_chunk + n_chunks). */
+static void b3_subtree_output(const uint32_t key[8], uint32_t base_flags,
+                              const uint8_t *in, size_t len,
+                              uint64_t first_chunk, b3_output *o) {
+  uint64_t n_chunks = len <= B3_CHUNK ? 1 : (len + B3_CHUNK - 1) / B3_CHUNK;
+  if (n_chunks == 1) {
+    b3_chunk_output(key, base_flags, in, len, first_chunk, o);
+    return;
+  }
+  uint64_t left_chunks = largest_pow2_below(n_chunks);
+  size_t left_len = (size_t)(left_chunks * B3_CHUNK);
+  b3_output lo, ro;
+  uint32_t lcv[8], rcv[8];
+  b3_subtree_output(key, base_flags, in, left_len, first_chunk, &lo);
+  b3_subtree_output(key, base_flags, in + left_len, len - left_len,
+                    first_chunk + left_chunks, &ro);
+  b3_output_cv(&lo, lcv);
+  b3_output_cv(&ro, rcv);
+  b3_parent_output(key, base_flags, lcv, rcv, o);
+}
+
+static void b3_hash_keyed_flags(const uint32_t key[8], uint32_t flags,
+                                const uint8_t *in, size_t len,
+                                uint8_t out32[32]) {
+  b3_output o;
+  b3_subtree_output(key, flags, in, len, 0, &o);
+  b3_output_root(&o, out32);
+}
+
+/* BLAKE3 hash mode (key = IV, flags 0) -- blake3::Hasher::new / hash. */
+void orc_blake3(const uint8_t *in, size_t len, uint8_t out32[32]) {
+  b3_hash_keyed_flags(B3_IV, 0, in, len, out32);
+}
+
+/* blake3::derive_key(context, material). */
+void orc_blake3_derive_key(const char *context, size_t context_len,
+                           const uint8_t *material, size_t material_len,
+                           uint8_t out32[32]) {
+  uint8_t ck[32];
+  uint32_t ckw[8];
+  b3_hash_keyed_flags(B3_IV, B3_DERIVE_KEY_CONTEXT, (const uint8_t *)context,
+                      context_len, ck);
+  for (int i = 0; i < 8; i++) ckw[i] = load32le(ck + 4 * i);
+  b3_hash_keyed_flags(ckw, B3_DERIVE_KEY_MATERIAL, material, material_len,
+                      out32);
+}
+
+/* blake3::keyed_hash(key, input). */
+void orc_blake3_keyed(const uint8_t key32[32], const uint8_t *in, size_t len,
+                      uint8_t out32[32]) {
+  uint32_t kw[8];
+  for (int i = 0; i < 8; i++) kw[i] = load32le(key32 + 4 * i);
+  b3_hash_keyed_flags(kw, B3_KEYED_HASH, in, len, out32);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Multi-threaded full-input hash (for multi-GiB parity checks and the CPU   */
+/* baseline of the validator).  Splits the input at the top levels of the    */
+/* BLAKE3 tree: the subtrees are hashed in parallel, the top is recombined     */
+/* with the same recursive rule, so the result equals orc_blake3().           */
+/* ------------------------------------------------------------------------- */
+
+typedef struct {
+  const uint8_t *in;
+  size_t len;
+  uint64_t first;
+  int threads;
+  b3_output out;
+} mt_job;
+
+static void mt_subtree_output(const uint8_t *in, size_t len,
+                              uint64_t first_chunk, int threads,
+                              b3_output *o);
+
+static void *mt_worker(void *arg) {
+  mt_job *j = (mt_job *)arg;
+  mt_subtree_output(j->in, j->len, j->first, j->threads, &j->out);
+  return NULL;
+}
+
+/* Output of the subtree over [first_chunk, +len) using up to `threads`
+ * threads: the left (power-of-two) subtree runs on a new thread, the right
+ * one on this thread, then the parent is formed exactly as the recursive
+ * single-thread rule does. */
+static void mt_subtree_output(const uint8_t *in, size_t len,
+                              uint64_t first_chunk, int threads,
+                              b3_output *o) {
+  uint64_t n_chunks = len <= B3_CHUNK ? 1 : (len + B3_CHUNK - 1) / B3_CHUNK;
+  if (threads <= 1 || n_chunks < 64) {
+    b3_subtree_output(B3_IV, 0, in, len, first_chunk, o);
+    return;
+  }
+  uint64_t left_chunks = largest_pow2_below(n_chunks);
+  size_t left_len = (size_t)(left_chunks * B3_CHUNK);
+  int lt = threads / 2, rt = threads - lt;
+  mt_job jl = {in, left_len, first_chunk, lt, {{0}, {0}, 0, 0, 0}};
+  b3_output ro;
+  uint32_t lcv[8], rcv[8];
+  pthread_t th;
+  int spawned = pthread_create(&th, NULL, mt_worker, &jl) == 0;
+  if (!spawned) mt_worker(&jl);
+  mt_subtree_output(in + left_len, len - left_len, first_chunk + left_chunks,
+                    rt, &ro);
+  if (spawned) pthread_join(th, NULL);
+  b3_output_cv(&jl.out, lcv);
+  b3_output_cv(&ro, rcv);
+  b3_parent_output(B3_IV, 0, lcv, rcv, o);
+}
+
+void orc_blake3_mt(const uint8_t *in, size_t len, int threads,
+                   uint8_t out32[32]) {
+  b3_output o;
+  mt_subtree_output(in, len, 0, threads, &o);
+  b3_output_root(&o, out32);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Incremental hasher with the reference crate's update()/finalize() shape.   */
+/* Used by the path-based restatements below (bytes arrive in reads).        */
+/* ------------------------------------------------------------------------- */
+
+typedef struct {
+  uint32_t cv_stack[64][8];
+  int stack_len;
+  uint32_t chunk_cv[8];
+  uint64_t chunk_counter;
+  uint8_t buf[64];
+  uint32_t buf_len;
+  uint32_t blocks_compressed;
+} orc_hasher;
+
+static void h_init(orc_hasher *h) {
+  memset(h, 0, sizeof *h);
+  memcpy(h->chunk_cv, B3_IV, 32);
+}
+
+static void h_push_cv(orc_hasher *h, const uint32_t cv_in[8],
+                      uint64_t total_chunks) {
+  uint32_t cv[8];
+  memcpy(cv, cv_in, 32);
+  while ((total_chunks & 1) == 0) {
+    b3_output o;
+    h->stack_len--;
+    b3_parent_output(B3_IV, 0, h->cv_stack[h->stack_len], cv, &o);
+    b3_output_cv(&o, cv);
+    total_chunks >>= 1;
+  }
+  memcpy(h->cv_stack[h->stack_len++], cv, 32);
+}
+
+static void h_update(orc_hasher *h, const uint8_t *in, size_t len) {
+  while (len) {
+    /* a full chunk is finished only when more input arrives */
+    if (h->blocks_compressed == 15 && h->buf_len == 64) {
+      b3_output o;
+      memcpy(o.cv, h->chunk_cv, 32);
+      memcpy(o.block, h->buf, 64);
+      o.counter = h->chunk_counter;
+      o.block_len = 64;
+      o.flags = B3_CHUNK_END | (h->blocks_compressed == 0 ? B3_CHUNK_START : 0);
+      uint32_t cv[8];
+      b3_output_cv(&o, cv);
+      h->chunk_counter++;
+      h_push_cv(h, cv, h->chunk_counter);
+      memcpy(h->chunk_cv, B3_IV, 32);
+      h->buf_len = 0;
+      h->blocks_compressed = 0;
+    }
+    if (h->buf_len == 64) {
+      uint32_t w[16];
+      uint32_t flags = h->blocks_compressed == 0 ? B3_CHUNK_START : 0;
+      b3_compress(h->chunk_cv, h->buf, h->chunk_counter, 64, flags, w);
+      memcpy(h->chunk_cv, w, 32);
+      h->blocks_compressed++;
+      h->buf_len = 0;
+    }
+    size_t take = 64 - h->buf_len;
+    if (take > len) take = len;
+    memcpy(h->buf + h->buf_len, in, take);
+    h->buf_len += (uint32_t)take;
+    in += take;
+    len -= take;
+  }
+}
+
+static void h_finalize(orc_hasher *h, uint8_t out32[32]) {
+  b3_output o;
+  memcpy(o.cv, h->chunk_cv, 32);
+  memset(o.block, 0, 64);
+  memcpy(o.block, h->buf, h->buf_len);
+  o.counter = h->chunk_counter;
+  o.block_len = h->buf_len;
+  o.flags = B3_CHUNK_END | (h->blocks_compressed == 0 ? B3_CHUNK_START : 0);
+  for (int i = h->stack_len - 1; i >= 0; i--) {
+    uint32_t cv[8];
+    b3_output_cv(&o, cv);
+    b3_parent_output(B3_IV, 0, h->cv_stack[i], cv, &o);
+  }
+  b3_output_root(&o, out32);
+}
+
+/* ------------------------------------------------------------------------- */
+/* generate_cas_id  -- /root/reference/core/src/object/cas.rs:10-62          */
+/* ------------------------------------------------------------------------- */
+
+#define CAS_SAMPLE_COUNT 4u              /* cas.rs:10 */
+#define CAS_SAMPLE_SIZE (1024u * 10u)    /* cas.rs:11 */
+#define CAS_HEADER_OR_FOOTER (1024u * 8u) /* cas.rs:12 */
+#define CAS_MINIMUM_FILE_SIZE (1024u * 100u) /* cas.rs:15 */
+#define CAS_LARGE_MSG_LEN (8u + 2u * CAS_HEADER_OR_FOOTER + CAS_SAMPLE_COUNT * CAS_SAMPLE_SIZE)
+
+static const char HEXD[] = "0123456789abcdef";
+
+static void hex_of(const uint8_t *d, int n, char *out) {
+  for (int i = 0; i < n; i++) {
+    out[2 * i] = HEXD[d[i] >> 4];
+    out[2 * i + 1] = HEXD[d[i] & 15];
+  }
+  out[2 * n] = 0;
+}
+
+/* Length of the cas message M for a file whose stat size is `size` and whose
+ * content length is `size` (the synthetic / consistent case). */
+uint32_t orc_cas_msg_len(uint64_t size) {
+  return size <= CAS_MINIMUM_FILE_SIZE ? (uint32_t)(8 + size) : CAS_LARGE_MSG_LEN;
+}
+
+/* Builds M from the full file bytes `file[0..file_len)` and the `size`
+ * argument passed to generate_cas_id, following cas.rs:24-58 exactly:
+ *  - size <= 100 KiB: the whole file as read (cas.rs:29);
+ *  - else header file[0,8192) (:35-38), samples at 8192 + k*seek_jump
+ *    with seek_jump = (size - 16384)/4 computed from `size` (:41-51),
+ *    footer = last 8192 bytes of the ACTUAL file (SeekFrom::End, :54-58).
+ * Returns the message length, or -1 where the reference's read_exact fails
+ * (UnexpectedEof).  `out` must hold max(8 + file_len, 57352) bytes. */
+int64_t orc_cas_build_message(const uint8_t *file, uint64_t file_len,
+                              uint64_t size, uint8_t *out) {
+  for (int i = 0; i < 8; i++) out[i] = (uint8_t)(size >> (8 * i));
+  if (size <= CAS_MINIMUM_FILE_SIZE) {
+    memcpy(out + 8, file, file_len);
+    return (int64_t)(8 + file_len);
+  }
+  uint8_t *p = out + 8;
+  if (file_len < CAS_HEADER_OR_FOOTER) return -1;
+  memcpy(p, file, CAS_HEADER_OR_FOOTER);
+  p += CAS_HEADER_OR_FOOTER;
+  uint64_t current_pos = CAS_HEADER_OR_FOOTER; /* read_exact returns 8192 */
+  uint64_t seek_jump = (size - CAS_HEADER_OR_FOOTER * 2) / CAS_SAMPLE_COUNT;
+  uint64_t file_pos = CAS_HEADER_OR_FOOTER; /* cursor after the header read */
+  for (;;) {
+    if (file_pos + CAS_SAMPLE_SIZE > file_len) return -1;
+    memcpy(p, file + file_pos, CAS_SAMPLE_SIZE);
+    p += CAS_SAMPLE_SIZE;
+    if (current_pos >= CAS_HEADER_OR_FOOTER + seek_jump * (CAS_SAMPLE_COUNT - 1))
+      break;
+    current_pos = current_pos + seek_jump; /* seek(Start(..)) returns it */
+    file_pos = current_pos;
+  }
+  if (file_len < CAS_HEADER_OR_FOOTER) return -1;
+  memcpy(p, file + file_len - CAS_HEADER_OR_FOOTER, CAS_HEADER_OR_FOOTER);
+  p += CAS_HEADER_OR_FOOTER;
+  return (int64_t)(p - out);
+}
+
+/* cas_id hex (16 chars) of an already-built message. */
+void orc_cas_id_of_message(const uint8_t *msg, size_t len, char out_hex[17]) {
+  uint8_t h[32];
+  orc_blake3(msg, len, h);
+  hex_of(h, 8, out_hex); /* to_hex()[..16], cas.rs:61 */
+}
+
+static int read_exact_fd(int fd, uint8_t *buf, size_t n) {
+  size_t got = 0;
+  while (got < n) {
+    ssize_t r = read(fd, buf + got, n - got);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return -errno;
+    }
+    if (r == 0) return -ENODATA; /* io::ErrorKind::UnexpectedEof */
+    got += (size_t)r;
+  }
+  return 0;
+}
+
+/* Path-based restatement with the reference's I/O pattern (cas.rs:23-62).
+ * Returns 0, or -errno (-ENODATA stands for UnexpectedEof). */
+int orc_cas_id_path(const char *path, uint64_t size, char out_hex[17]) {
+  orc_hasher h;
+  h_init(&h);
+  uint8_t sz[8];
+  for (int i = 0; i < 8; i++) sz[i] = (uint8_t)(size >> (8 * i));
+  h_update(&h, sz, 8);
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  int rc = 0;
+  if (size <= CAS_MINIMUM_FILE_SIZE) {
+    /* fs::read: read the whole file whatever its current length */
+    uint8_t buf[65536];
+    for (;;) {
+      ssize_t r = read(fd, buf, sizeof buf);
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        rc = -errno;
+        break;
+      }
+      if (r == 0) break;
+      h_update(&h, buf, (size_t)r);
+    }
+  } else {
+    uint8_t buf[CAS_SAMPLE_SIZE];
+    rc = read_exact_fd(fd, buf, CAS_HEADER_OR_FOOTER);
+    if (!rc) {
+      uint64_t current_pos = CAS_HEADER_OR_FOOTER;
+      h_update(&h, buf, CAS_HEADER_OR_FOOTER);
+      uint64_t seek_jump = (size - CAS_HEADER_OR_FOOTER * 2) / CAS_SAMPLE_COUNT;
+      for (;;) {
+        rc = read_exact_fd(fd, buf, CAS_SAMPLE_SIZE);
+        if (rc) break;
+        h_update(&h, buf, CAS_SAMPLE_SIZE);
+        if (current_pos >=
+            CAS_HEADER_OR_FOOTER + seek_jump * (CAS_SAMPLE_COUNT - 1))
+          break;
+        off_t np = lseek(fd, (off_t)(current_pos + seek_jump), SEEK_SET);
+        if (np < 0) {
+          rc = -errno;
+          break;
+        }
+        current_pos = (uint64_t)np;
+      }
+      if (!rc) {
+        if (lseek(fd, -(off_t)CAS_HEADER_OR_FOOTER, SEEK_END) < 0) rc = -errno;
+        if (!rc) rc = read_exact_fd(fd, buf, CAS_HEADER_OR_FOOTER);
+        if (!rc) h_update(&h, buf, CAS_HEADER_OR_FOOTER);
+      }
+    }
+  }
+  close(fd);
+  if (rc) return rc;
+  uint8_t out[32];
+  h_finalize(&h, out);
+  hex_of(out, 8, out_hex);
+  return 0;
+}
+
+/* file_checksum -- validation/hash.rs:8-24: 1 MiB reads, stop on the first
+ * read shorter than 1 MiB, full 64-char hex. */
+int orc_file_checksum_path(const char *path, char out_hex[65]) {
+  enum { BLOCK_LEN = 1048576 };
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  uint8_t *buf = (uint8_t *)malloc(BLOCK_LEN);
+  if (!buf) {
+    close(fd);
+    return -ENOMEM;
+  }
+  orc_hasher h;
+  h_init(&h);
+  int rc = 0;
+  for (;;) {
+    /* tokio File::read on a regular file returns min(len, its buffer cap);
+     * modelled as a full read of up to BLOCK_LEN (open
+     * assumption): loop read() until BLOCK_LEN or EOF. */
+    size_t got = 0;
+    while (got < BLOCK_LEN) {
+      ssize_t r = read(fd, buf + got, BLOCK_LEN - got);
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        rc = -errno;
+        break;
+      }
+      if (r == 0) break;
+      got += (size_t)r;
+    }
+    if (rc) break;
+    h_update(&h, buf, got);
+    if (got != BLOCK_LEN) break;
+  }
+  free(buf);
+  close(fd);
+  if (rc) return rc;
+  uint8_t out[32];
+  h_finalize(&h, out);
+  hex_of(out, 32, out_hex);
+  return 0;
+}
+
+/* Streaming-shape hash of an in-memory buffer through the incremental hasher
+ * fed in `piece`-byte updates (cross-checks the recursive tree). */
+void orc_blake3_incremental(const uint8_t *in, size_t len, size_t piece,
+                            uint8_t out32[32]) {
+  orc_hasher h;
+  h_init(&h);
+  if (piece == 0) piece = 1;
+  for (size_t off = 0; off < len; off += piece) {
+    size_t n = len - off < piece ? len - off : piece;
+    h_update(&h, in + off, n);
+  }
+  h_finalize(&h, out32);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Batched in-memory cas (CPU baseline, threads over files)                  */
+/* ------------------------------------------------------------------------- */
+
+typedef struct {
+  const uint8_t *arena;
+  const uint64_t *off;
+  const uint32_t *len;
+  uint8_t *out8;
+  uint64_t begin, end;
+} cas_job;
+
+static void *cas_worker(void *arg) {
+  cas_job *j = (cas_job *)arg;
+  for (uint64_t i = j->begin; i < j->end; i++) {
+    uint8_t h[32];
+    orc_blake3(j->arena + j->off[i], j->len[i], h);
+    memcpy(j->out8 + 8 * i, h, 8);
+  }
+  return NULL;
+}
+
+void orc_cas_batch(const uint8_t *arena, const uint64_t *off,
+                   const uint32_t *len, uint64_t n, uint8_t *out8,
+                   int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  cas_job jobs[256];
+  for (int t = 0; t < threads; t++) {
+    jobs[t].arena = arena;
+    jobs[t].off = off;
+    jobs[t].len = len;
+    jobs[t].out8 = out8;
+    jobs[t].begin = n * (uint64_t)t / (uint64_t)threads;
+    jobs[t].end = n * (uint64_t)(t + 1) / (uint64_t)threads;
+    pthread_create(&th[t], NULL, cas_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Synthetic corpus content (shared definition with csrc/synth.hip)          */
+/* ------------------------------------------------------------------------- */
+
+static inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* Byte at offset `o` of the synthetic file with content seed `seed`. */
+static inline uint8_t synth_byte(uint64_t seed, uint64_t o) {
+  uint64_t w = mix64(seed + (o >> 3) * 0x9E3779B97F4A7C15ull);
+  return (uint8_t)(w >> (8 * (o & 7)));
+}
+
+void orc_synth_file_bytes(uint64_t seed, uint64_t offset, uint64_t n,
+                          uint8_t *out) {
+  for (uint64_t i = 0; i < n; i++) out[i] = synth_byte(seed, offset + i);
+}
+
+/* cas message of a synthetic file (size, seed); returns its length. */
+uint32_t orc_synth_cas_message(uint64_t size, uint64_t seed, uint8_t *out) {
+  for (int i = 0; i < 8; i++) out[i] = (uint8_t)(size >> (8 * i));
+  if (size <= CAS_MINIMUM_FILE_SIZE) {
+    orc_synth_file_bytes(seed, 0, size, out + 8);
+    return (uint32_t)(8 + size);
+  }
+  uint8_t *p = out + 8;
+  uint64_t jump = (size - 2 * CAS_HEADER_OR_FOOTER) / CAS_SAMPLE_COUNT;
+  orc_synth_file_bytes(seed, 0, CAS_HEADER_OR_FOOTER, p);
+  p += CAS_HEADER_OR_FOOTER;
+  for (uint32_t k = 0; k < CAS_SAMPLE_COUNT; k++) {
+    orc_synth_file_bytes(seed, CAS_HEADER_OR_FOOTER + k * jump,
+                         CAS_SAMPLE_SIZE, p);
+    p += CAS_SAMPLE_SIZE;
+  }
+  orc_synth_file_bytes(seed, size - CAS_HEADER_OR_FOOTER, CAS_HEADER_OR_FOOTER,
+                       p);
+  return CAS_LARGE_MSG_LEN;
+}
+
+/* Synthetic cas arena for n files, packed at 128-byte aligned offsets
+ * (the same packing rule as the device generator).  Returns total bytes. */
+uint64_t orc_synth_arena_layout(const uint64_t *sizes, uint64_t n,
+                                uint64_t *off, uint32_t *len) {
+  uint64_t pos = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    len[i] = orc_cas_msg_len(sizes[i]);
+    off[i] = pos;
+    pos += ((uint64_t)len[i] + 127u) & ~(uint64_t)127u;
+  }
+  return pos;
+}
+
+typedef struct {
+  const uint64_t *sizes, *seeds, *off;
+  uint8_t *arena;
+  uint64_t begin, end;
+} synth_job;
+
+static void *synth_worker(void *arg) {
+  synth_job *j = (synth_job *)arg;
+  for (uint64_t i = j->begin; i < j->end; i++)
+    orc_synth_cas_message(j->sizes[i], j->seeds[i], j->arena + j->off[i]);
+  return NULL;
+}
+
+void orc_synth_arena_fill(const uint64_t *sizes, const uint64_t *seeds,
+                          const uint64_t *off, uint64_t n, uint8_t *arena,
+                          int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  synth_job jobs[256];
+  for (int t = 0; t < threads; t++) {
+    jobs[t].sizes = sizes;
+    jobs[t].seeds = seeds;
+    jobs[t].off = off;
+    jobs[t].arena = arena;
+    jobs[t].begin = n * (uint64_t)t / (uint64_t)threads;
+    jobs[t].end = n * (uint64_t)(t + 1) / (uint64_t)threads;
+    pthread_create(&th[t], NULL, synth_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}
+
+/* Dedup corpus rows (same definition as csrc/synth.hip k_synth_dedup). */
+static uint64_t orc_perm(uint64_t x, uint64_t T, uint64_t seed) {
+  uint32_t bits = 2;
+  while ((1ull << bits) < T) bits += 2;
+  uint32_t h = bits / 2;
+  uint64_t mask = (1ull << h) - 1;
+  do {
+    uint64_t L = x >> h, R = x & mask;
+    for (uint32_t r = 0; r < 4; r++) {
+      uint64_t F = mix64(R ^ (seed + 0x632BE59BD9B4E019ull * (r + 1))) & mask;
+      uint64_t nl = R;
+      R = L ^ F;
+      L = nl;
+    }
+    x = (L << h) | R;
+  } while (x >= T);
+  return x;
+}
+
+void orc_synth_dedup_rows(uint64_t seed, uint64_t total, uint64_t distinct,
+                          uint64_t first, uint64_t n, uint64_t *key,
+                          uint8_t *has_key, uint32_t *rank) {
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t g = first + i;
+    uint64_t u = orc_perm(g, total, seed);
+    uint64_t item =
+        u < distinct ? u : mix64(u ^ seed ^ 0xD6E8FEB86659FD93ull) % distinct;
+    key[i] = mix64(seed * 0x9E3779B97F4A7C15ull + item + 1);
+    has_key[i] = (mix64(g ^ (seed << 1) ^ 0xA0761D6478BD642Full) % 1000) != 0;
+    rank[i] = (uint32_t)g;
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* cas_id -> Object grouping (identifier_job_step, canonical form)           */
+/* ------------------------------------------------------------------------- */
+/*
+ * Rows are the orphan file_paths in ascending id; rank r = position.  The job
+ * processes chunks of `chunk_rows` (=CHUNK_SIZE 100, mod.rs:36).  Within the
+ * chunk that first contains cas key X every row with X becomes its own new
+ * Object (mod.rs:233-297, nothing links them because the Object rows did not
+ * exist when find_many ran, :168-175); rows with X in later chunks link to an
+ * existing Object (:189-225) -- canonically the one of the lowest-rank row of
+ * X.  Rows without a key (empty files, cas_id None, mod.rs:80-88) are
+ * singletons (:238-239).  rep[r] = rank of the row whose Object r ends up in.
+ */
+typedef struct {
+  uint64_t key;
+  uint32_t rank;
+} kr_pair;
+
+static int kr_cmp(const void *a, const void *b) {
+  const kr_pair *x = (const kr_pair *)a, *y = (const kr_pair *)b;
+  if (x->key != y->key) return x->key < y->key ? -1 : 1;
+  return x->rank < y->rank ? -1 : (x->rank > y->rank);
+}
+
+int orc_group_reps(const uint64_t *key, const uint8_t *has_key, uint32_t n,
+                   uint32_t chunk_rows, uint32_t *rep) {
+  if (chunk_rows == 0) return -EINVAL;
+  kr_pair *v = (kr_pair *)malloc((size_t)n * sizeof *v + 1);
+  if (!v) return -ENOMEM;
+  uint32_t m = 0;
+  for (uint32_t r = 0; r < n; r++) {
+    rep[r] = r;
+    if (has_key[r]) {
+      v[m].key = key[r];
+      v[m].rank = r;
+      m++;
+    }
+  }
+  qsort(v, m, sizeof *v, kr_cmp);
+  for (uint32_t i = 0; i < m;) {
+    uint32_t j = i;
+    while (j < m && v[j].key == v[i].key) j++;
+    uint32_t first = v[i].rank; /* lowest rank of the segment */
+    uint32_t c0 = first / chunk_rows;
+    for (uint32_t k = i; k < j; k++)
+      rep[v[k].rank] = (v[k].rank / chunk_rows == c0) ? v[k].rank : first;
+    i = j;
+  }
+  free(v);
+  return 0;
+}

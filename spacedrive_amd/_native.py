@@ -1,0 +1,179 @@
+"""ctypes binding of libsdgpu.so (the C ABI in include/sdgpu.h).
+
+The product path has no CPU fallback: if the library or a gfx950 device is
+missing, the calls below raise instead of computing anything elsewhere.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsdgpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "sdgpu.h")
+
+_lib = None
+
+c_u8p = ctypes.c_void_p
+c_vp = ctypes.c_void_p
+
+
+class SdgpuError(OSError):
+    """A negative errno returned by libsdgpu (maps to Rust's io::Error)."""
+
+    def __init__(self, rc: int, what: str = ""):
+        msg = load().sdgpu_strerror(rc).decode()
+        super().__init__(-rc, f"{what}: {msg}" if what else msg)
+        self.rc = rc
+
+
+def _proto(L):
+    P = ctypes.POINTER
+    i32, u32, u64, sz = ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
+    ctx = c_vp
+    sig = {
+        "sdgpu_abi_version": (i32, []),
+        "sdgpu_strerror": (ctypes.c_char_p, [i32]),
+        "sdgpu_device_count": (i32, [P(i32)]),
+        "sdgpu_open": (i32, [i32, P(c_vp)]),
+        "sdgpu_close": (i32, [ctx]),
+        "sdgpu_sync": (i32, [ctx]),
+        "sdgpu_stream": (c_vp, [ctx]),
+        "sdgpu_alloc_pinned": (i32, [ctx, sz, P(c_vp)]),
+        "sdgpu_free_pinned": (i32, [ctx, c_vp]),
+        "sdgpu_alloc_device": (i32, [ctx, sz, P(c_vp)]),
+        "sdgpu_free_device": (i32, [ctx, c_vp]),
+        "sdgpu_memcpy_async": (i32, [ctx, c_vp, c_vp, sz, c_vp]),
+        "sdgpu_cas_batch": (i32, [ctx, c_vp, c_vp, c_vp, u32, c_vp, c_vp]),
+        "sdgpu_cas_batch_device": (i32, [ctx, c_vp, u64, c_vp, c_vp, u32, c_vp, c_vp, c_vp]),
+        "sdgpu_generate_cas_id": (i32, [ctx, ctypes.c_char_p, u64, ctypes.c_char_p]),
+        "sdgpu_identify_files": (i32, [ctx, c_vp, c_vp, u32, c_vp, c_vp, c_vp]),
+        "sdgpu_checksum": (i32, [ctx, c_vp, u64, c_vp]),
+        "sdgpu_checksum_batch_device": (i32, [ctx, c_vp, c_vp, u32, c_vp, c_vp]),
+        "sdgpu_subtree_device": (i32, [ctx, c_vp, u64, u64, i32, c_vp, c_vp]),
+        "sdgpu_file_checksum": (i32, [ctx, ctypes.c_char_p, ctypes.c_char_p]),
+        "sdgpu_dedup": (i32, [ctx, c_vp, c_vp, u32, u32, c_vp]),
+        "sdgpu_group_pairs_device": (i32, [ctx, c_vp, c_vp, u64, u32, u32, c_vp, c_vp]),
+        "sdgpu_shard_count_device": (i32, [ctx, c_vp, c_vp, u64, u32, c_vp, c_vp]),
+        "sdgpu_shard_partition_device": (i32, [ctx, c_vp, c_vp, c_vp, u64, u32, c_vp, c_vp, c_vp,
+                                               c_vp]),
+        "sdgpu_scatter_rep_device": (i32, [ctx, c_vp, c_vp, u64, c_vp, u64, c_vp, i32, c_vp]),
+        "sdgpu_synth_cas_arena_device": (i32, [ctx, c_vp, c_vp, c_vp, u32, c_vp, c_vp]),
+        "sdgpu_synth_file_device": (i32, [ctx, u64, u64, u64, c_vp, c_vp]),
+        "sdgpu_synth_dedup_rows_device": (i32, [ctx, u64, u64, u64, u64, u64, c_vp, c_vp, c_vp,
+                                                c_vp]),
+        "sdgpu_set_timing": (i32, [ctx, i32]),
+        "sdgpu_timing_reset": (i32, [ctx]),
+        "sdgpu_timing_read": (i32, [ctx, u32, ctypes.c_char_p, P(ctypes.c_double),
+                                    P(ctypes.c_uint64)]),
+        "sdgpu_valu_probe": (i32, [ctx, P(ctypes.c_double)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def load():
+    """Loads libsdgpu.so from the package directory (raises if it is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()); "
+                "there is no CPU fallback for the content-identification path")
+        L = ctypes.CDLL(LIB_PATH)
+        _proto(L)
+        _lib = L
+    return _lib
+
+
+def declared_symbols() -> list[str]:
+    """Function names declared in include/sdgpu.h."""
+    text = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"\b(sdgpu_[a-z0-9_]+)\s*\(", text)))
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        raise SdgpuError(rc, what)
+
+
+class Context:
+    """An open device context (sdgpu_open / sdgpu_close)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        check(self.lib.sdgpu_open(device, ctypes.byref(h)), f"sdgpu_open({device})")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            self.lib.sdgpu_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(self.lib.sdgpu_sync(self.h), "sdgpu_sync")
+
+    @property
+    def stream(self) -> int:
+        return self.lib.sdgpu_stream(self.h) or 0
+
+    def set_timing(self, enable: bool = True):
+        check(self.lib.sdgpu_set_timing(self.h, 1 if enable else 0), "sdgpu_set_timing")
+        check(self.lib.sdgpu_timing_reset(self.h), "sdgpu_timing_reset")
+
+    def kernel_times(self) -> dict[str, tuple[float, int]]:
+        """{kernel name: (total device ms, launches)} since set_timing()."""
+        res = {}
+        i = 0
+        while True:
+            name = ctypes.create_string_buffer(32)
+            ms = ctypes.c_double()
+            n = ctypes.c_uint64()
+            rc = self.lib.sdgpu_timing_read(self.h, i, name, ctypes.byref(ms), ctypes.byref(n))
+            if rc == -2:
+                break
+            check(rc, "sdgpu_timing_read")
+            res[name.value.decode()] = (ms.value, n.value)
+            i += 1
+        return res
+
+    def valu_peak(self) -> float:
+        """Measured int32 VALU lane-ops/s (BLAKE3-shaped instruction mix)."""
+        v = ctypes.c_double()
+        check(self.lib.sdgpu_valu_probe(self.h, ctypes.byref(v)), "sdgpu_valu_probe")
+        return v.value
+
+
+_default: dict[int, Context] = {}
+
+
+def default_context(device: int | None = None) -> Context:
+    """Process-wide context per device (the reference runs one job at a time)."""
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", "0")) if "LOCAL_RANK" in os.environ else 0
+        try:
+            import torch
+            if torch.cuda.is_available():
+                device = torch.cuda.current_device()
+        except Exception:
+            pass
+    if device not in _default:
+        _default[device] = Context(device)
+    return _default[device]

@@ -1,0 +1,98 @@
+"""cas_id generation -- host mirror of core/src/object/cas.rs over libsdgpu.
+
+Same names, argument meaning and error behaviour as the reference:
+
+* ``generate_cas_id(path, size) -> str``      (cas.rs:23-62): 16 lowercase hex
+  chars; raises OSError (io::Error) on open/read/seek failures, e.g. ENODATA for
+  read_exact's UnexpectedEof on a file shorter than its samples.
+* constants SAMPLE_COUNT / SAMPLE_SIZE / HEADER_OR_FOOTER_SIZE /
+  MINIMUM_FILE_SIZE (cas.rs:10-15).
+
+Batched entry points (what file_identifier uses): ``cas_batch`` over a host
+arena of cas messages and ``cas_batch_device`` over device tensors.  All
+hashing happens in the K1 HIP kernel (spacedrive_amd/csrc/b3_batch.hip).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from ._native import SdgpuError, check, default_context, load
+
+SAMPLE_COUNT = 4                  # cas.rs:10
+SAMPLE_SIZE = 1024 * 10           # cas.rs:11
+HEADER_OR_FOOTER_SIZE = 1024 * 8  # cas.rs:12
+MINIMUM_FILE_SIZE = 1024 * 100    # cas.rs:15
+MAX_MSG_LEN = 8 + MINIMUM_FILE_SIZE
+SAMPLED_MSG_LEN = 8 + 2 * HEADER_OR_FOOTER_SIZE + SAMPLE_COUNT * SAMPLE_SIZE  # 57352
+
+
+def cas_message_len(size: int) -> int:
+    """Length of the bytes generate_cas_id feeds BLAKE3 for a consistent file."""
+    return 8 + size if size <= MINIMUM_FILE_SIZE else SAMPLED_MSG_LEN
+
+
+def sample_offsets(size: int) -> list[int]:
+    """File offsets of the 4 samples (cas.rs:41-51)."""
+    jump = (size - HEADER_OR_FOOTER_SIZE * 2) // SAMPLE_COUNT
+    return [HEADER_OR_FOOTER_SIZE + k * jump for k in range(SAMPLE_COUNT)]
+
+
+def generate_cas_id(path, size: int, ctx=None) -> str:
+    """Drop-in for `generate_cas_id(path, size)` (cas.rs:23)."""
+    ctx = ctx or default_context()
+    out = ctypes.create_string_buffer(17)
+    p = os.fsencode(os.fspath(path))
+    rc = ctx.lib.sdgpu_generate_cas_id(ctx.h, p, int(size), out)
+    if rc:
+        raise SdgpuError(rc, os.fspath(path))
+    return out.value.decode()
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def cas_batch(arena: np.ndarray, off: np.ndarray, length: np.ndarray, ctx=None):
+    """cas ids (n x 8 bytes) + per-message status for a HOST arena of messages."""
+    ctx = ctx or default_context()
+    arena = np.ascontiguousarray(arena, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
+    length = np.ascontiguousarray(length, np.uint32)
+    n = off.size
+    out = np.zeros((n, 8), np.uint8)
+    status = np.zeros(n, np.int32)
+    check(ctx.lib.sdgpu_cas_batch(ctx.h, _ptr(arena), _ptr(off), _ptr(length), n, _ptr(out),
+                                  _ptr(status)), "sdgpu_cas_batch")
+    return out, status
+
+
+def cas_batch_device(arena, off, length, out=None, status=None, ctx=None, stream=None):
+    """K1 over device tensors (torch): arena uint8, off int64, length int32.
+
+    Returns (out[n,8] uint8, status[n] int32) on the same device; asynchronous
+    on `stream` (default: torch's current stream)."""
+    import torch
+    ctx = ctx or default_context(arena.device.index)
+    n = off.numel()
+    if out is None:
+        out = torch.empty((n, 8), dtype=torch.uint8, device=arena.device)
+    if status is None:
+        status = torch.empty(n, dtype=torch.int32, device=arena.device)
+    s = stream if stream is not None else torch.cuda.current_stream(arena.device).cuda_stream
+    check(ctx.lib.sdgpu_cas_batch_device(ctx.h, arena.data_ptr(), arena.numel(), off.data_ptr(),
+                                         length.data_ptr(), n, out.data_ptr(), status.data_ptr(),
+                                         s), "sdgpu_cas_batch_device")
+    return out, status
+
+
+def hex_ids(out8: np.ndarray) -> list[str]:
+    """`to_hex()[..16]` of each 8-byte cas digest prefix (cas.rs:61)."""
+    return [bytes(r).hex() for r in np.asarray(out8, np.uint8).reshape(-1, 8)]
+
+
+def keys_of(out8) -> np.ndarray:
+    """8 digest bytes as little-endian u64 grouping keys."""
+    return np.ascontiguousarray(out8, np.uint8).reshape(-1, 8).view("<u8").reshape(-1)

@@ -1,0 +1,319 @@
+// K4-K6: cas_id -> Object grouping as a radix partition + per-bucket group-by.
+//
+// Replaces the Object link/create decisions of identifier_job_step
+// (/root/reference/core/src/object/file_identifier/mod.rs:136-333): the
+// HashSet of chunk cas_ids (:136-141), the library-wide find_many over
+// file_path.cas_id (:168-175), the per-row `find` of an Object owning the same
+// cas_id (:196-206) and the one-new-Object-per-remaining-row rule (:233-297),
+// evaluated for ALL orphan rows at once instead of 100 per job step.
+//
+// Rows are (key, rank): key = the cas_id's 8 digest bytes as a little-endian
+// u64, rank = position of the file_path in ascending-id order.  The grouping
+// rule (canonical form):
+//   f      = lowest rank carrying key k
+//   rep(r) = r  if r / chunk_rows == f / chunk_rows   (new Object in f's chunk)
+//            f  otherwise                               (linked to f's Object)
+//
+// Pipeline (all asynchronous, no host synchronisation):
+//   K6 partition: digit = `bits` key bits below the top `skip` bits.
+//      hist:    each of P blocks histograms its contiguous tile in LDS and
+//               writes counts[digit][block] (no global atomics);
+//      scan:    exclusive scan of counts (digit-major) -> (digit, block) offsets;
+//      scatter: each block re-reads its tile and scatters (key, rank, index)
+//               through LDS cursors.
+//      Used twice: by shard (top bits, multi-GPU exchange) and by bucket.
+//   K5 group:   one workgroup per bucket builds a linear-probing hash table of
+//               (key -> min rank) in LDS (ds_cmpst_b64 / ds_min_u32), then maps
+//               every row to its rep.  Buckets too large for LDS use a private
+//               region of a global table instead (same code path, agent-scope
+//               atomics), so any key distribution (e.g. one file duplicated a
+//               million times) is handled.
+#include <errno.h>
+
+#include "internal.hpp"
+#include "scan_device.hpp"
+
+#include <algorithm>
+
+namespace sdgpu {
+
+namespace {
+
+constexpr int kPartThreads = 1024;
+constexpr uint32_t kPartBlocks = 256;  // one per CU
+constexpr int kGroupThreads = 256;
+constexpr uint32_t kLdsSlots = 4096;   // table slots in LDS
+constexpr uint32_t kLdsCap = 3072;     // rows per bucket handled in LDS (load <= 75%)
+constexpr uint64_t kEmpty = ~0ull;
+
+__device__ __forceinline__ uint32_t digit_of(uint64_t key, uint32_t skip, uint32_t bits) {
+  return bits == 0 ? 0u : static_cast<uint32_t>((key << skip) >> (64u - bits));
+}
+
+__device__ __forceinline__ void tile_of(uint64_t n, uint64_t& t0, uint64_t& t1) {
+  const uint64_t per = (n + kPartBlocks - 1) / kPartBlocks;
+  t0 = min<uint64_t>(n, per * blockIdx.x);
+  t1 = min<uint64_t>(n, t0 + per);
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_part_hist(const uint64_t* __restrict__ key,
+                                                            const uint8_t* __restrict__ valid,
+                                                            uint64_t n, uint32_t skip,
+                                                            uint32_t bits,
+                                                            uint32_t* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
+  const uint32_t nbins = 1u << bits;
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) cnt[b] = 0;
+  __syncthreads();
+  uint64_t t0, t1;
+  tile_of(n, t0, t1);
+  for (uint64_t i = t0 + threadIdx.x; i < t1; i += kPartThreads) {
+    if (valid && !valid[i]) continue;
+    atomicAdd(&cnt[digit_of(key[i], skip, bits)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
+    hist[static_cast<uint64_t>(b) * kPartBlocks + blockIdx.x] = cnt[b];
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_part_scatter(
+    const uint64_t* __restrict__ key, const uint32_t* __restrict__ rank,
+    const uint8_t* __restrict__ valid, uint64_t n, uint32_t skip, uint32_t bits,
+    const uint32_t* __restrict__ offs, uint64_t* __restrict__ out_key,
+    uint32_t* __restrict__ out_rank, uint32_t* __restrict__ out_pos) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
+  const uint32_t nbins = 1u << bits;
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
+    cur[b] = offs[static_cast<uint64_t>(b) * kPartBlocks + blockIdx.x];
+  __syncthreads();
+  uint64_t t0, t1;
+  tile_of(n, t0, t1);
+  for (uint64_t i = t0 + threadIdx.x; i < t1; i += kPartThreads) {
+    if (valid && !valid[i]) continue;
+    const uint64_t k = key[i];
+    const uint32_t p = atomicAdd(&cur[digit_of(k, skip, bits)], 1u);
+    out_key[p] = k;
+    out_rank[p] = rank ? rank[i] : static_cast<uint32_t>(i);
+    out_pos[p] = static_cast<uint32_t>(i);
+  }
+}
+
+__device__ __forceinline__ uint32_t slot_hash(uint64_t k) {
+  return static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> 32);
+}
+
+// One workgroup per bucket.  Rows of bucket b: [offs[b*P], offs[(b+1)*P]).
+__global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
+    const uint64_t* __restrict__ skey, const uint32_t* __restrict__ srank,
+    const uint32_t* __restrict__ spos, const uint32_t* __restrict__ offs, uint32_t nbuckets,
+    uint32_t chunk_rows, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
+    uint32_t* __restrict__ rep) {
+  __shared__ uint64_t lkey[kLdsSlots];
+  __shared__ uint32_t lmin[kLdsSlots];
+  __shared__ uint32_t special_min;  // min rank of key == kEmpty (sentinel clash)
+  const uint32_t b = blockIdx.x;
+  const uint32_t start = offs[static_cast<uint64_t>(b) * kPartBlocks];
+  const uint32_t end = offs[static_cast<uint64_t>(b + 1) * kPartBlocks];  // offs[nb*P] = total
+  const uint32_t m = end - start;
+  if (m == 0) return;
+  const bool in_lds = m <= kLdsCap;
+  uint32_t tsize = kLdsSlots;
+  uint64_t* tk = lkey;
+  uint32_t* tm = lmin;
+  if (!in_lds) {
+    tsize = 1u;
+    while (tsize * 2u <= 4u * m) tsize *= 2u;  // 2m < tsize <= 4m
+    tk = gkey + 4ull * start;
+    tm = gmin + 4ull * start;
+  }
+  for (uint32_t s = threadIdx.x; s < tsize; s += kGroupThreads) {
+    tk[s] = kEmpty;
+    tm[s] = 0xFFFFFFFFu;
+  }
+  if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
+  __syncthreads();
+  const uint32_t mask = tsize - 1;
+  for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
+    const uint64_t k = skey[i];
+    const uint32_t r = srank[i];
+    if (k == kEmpty) {
+      atomicMin(&special_min, r);
+      continue;
+    }
+    uint32_t h = slot_hash(k) & mask;
+    for (;;) {
+      const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tk[h]),
+                                      static_cast<unsigned long long>(kEmpty),
+                                      static_cast<unsigned long long>(k));
+      if (prev == kEmpty || prev == k) {
+        atomicMin(&tm[h], r);
+        break;
+      }
+      h = (h + 1) & mask;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
+    const uint64_t k = skey[i];
+    const uint32_t r = srank[i];
+    uint32_t f;
+    if (k == kEmpty) {
+      f = special_min;
+    } else {
+      uint32_t h = slot_hash(k) & mask;
+      for (;;) {
+        const uint64_t kk = in_lds ? tk[h]
+                                   : __hip_atomic_load(&tk[h], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        if (kk == k) break;
+        h = (h + 1) & mask;
+      }
+      f = in_lds ? tm[h] : __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    rep[spos[i]] = (r / chunk_rows == f / chunk_rows) ? r : f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fill_init(uint32_t* __restrict__ dst, uint64_t n,
+                                                   const uint32_t* __restrict__ init) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride)
+    dst[i] = init ? init[i] : static_cast<uint32_t>(i);
+}
+
+__global__ __launch_bounds__(256) void k_scatter(const uint32_t* __restrict__ src,
+                                                 const uint32_t* __restrict__ pos, uint64_t n,
+                                                 uint32_t* __restrict__ dst) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride)
+    dst[pos[i]] = src[i];
+}
+
+__global__ void k_copy_counts(const uint32_t* __restrict__ offs, uint32_t nbins,
+                              uint64_t* __restrict__ counts) {
+  const uint32_t b = threadIdx.x;
+  if (b < nbins)
+    counts[b] = offs[static_cast<uint64_t>(b + 1) * kPartBlocks] -
+                offs[static_cast<uint64_t>(b) * kPartBlocks];
+}
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+uint32_t bucket_bits_for(uint64_t n) {
+  uint32_t bits = 1;
+  while (bits < 13 && (n >> bits) > 1024) ++bits;
+  return bits;
+}
+
+struct GroupLayout {
+  uint32_t bits;
+  size_t hist, tiles, skey, srank, spos, gkey, gmin, total;
+};
+
+GroupLayout group_layout(uint64_t n) {
+  GroupLayout L;
+  L.bits = bucket_bits_for(n);
+  const uint64_t nh = (static_cast<uint64_t>(1) << L.bits) * kPartBlocks;
+  size_t o = 0;
+  L.hist = o; o = align_up(o + 4 * (nh + 1), 256);
+  L.tiles = o; o = align_up(o + 4 * (scan::tiles_for(nh) + 1), 256);
+  L.skey = o; o = align_up(o + 8 * n, 256);
+  L.srank = o; o = align_up(o + 4 * n, 256);
+  L.spos = o; o = align_up(o + 4 * n, 256);
+  L.gkey = o; o = align_up(o + 8 * 4 * n, 256);
+  L.gmin = o; o = align_up(o + 4 * 4 * n, 256);
+  L.total = o;
+  return L;
+}
+
+hipError_t partition(const uint64_t* key, const uint8_t* valid, const uint32_t* rank, uint64_t n,
+                     uint32_t skip, uint32_t bits, uint32_t* hist, uint32_t* tiles,
+                     uint64_t* okey, uint32_t* orank, uint32_t* opos, hipStream_t s,
+                     KTimer* timer, const char* hname, const char* sname) {
+  const uint64_t nh = (static_cast<uint64_t>(1) << bits) * kPartBlocks;
+  const size_t lds = sizeof(uint32_t) << bits;
+  {
+    KScope k(timer, hname, s);
+    k_part_hist<<<kPartBlocks, kPartThreads, lds, s>>>(key, valid, n, skip, bits, hist);
+  }
+  scan::exclusive(hist, nh, hist, tiles, nullptr, s);
+  if (okey) {
+    KScope k(timer, sname, s);
+    k_part_scatter<<<kPartBlocks, kPartThreads, lds, s>>>(key, rank, valid, n, skip, bits, hist,
+                                                          okey, orank, opos);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t dedup_workspace_bytes(uint64_t n) { return group_layout(n).total; }
+
+hipError_t dedup_local_launch(const uint64_t* key, const uint32_t* rank, uint64_t n,
+                              uint32_t chunk_rows, uint32_t shard_bits, uint32_t* rep, void* ws,
+                              hipStream_t s, KTimer* timer) {
+  if (n == 0) return hipSuccess;
+  const GroupLayout L = group_layout(n);
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w + L.hist);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + L.tiles);
+  uint64_t* skey = reinterpret_cast<uint64_t*>(w + L.skey);
+  uint32_t* srank = reinterpret_cast<uint32_t*>(w + L.srank);
+  uint32_t* spos = reinterpret_cast<uint32_t*>(w + L.spos);
+  uint64_t* gkey = reinterpret_cast<uint64_t*>(w + L.gkey);
+  uint32_t* gmin = reinterpret_cast<uint32_t*>(w + L.gmin);
+  const uint32_t bits = std::min<uint32_t>(L.bits, 64u - shard_bits);
+  hipError_t e = partition(key, nullptr, rank, n, shard_bits, bits, hist, tiles, skey, srank,
+                           spos, s, timer, "bucket_hist", "bucket_scatter");
+  if (e != hipSuccess) return e;
+  KScope k(timer, "bucket_group", s);
+  k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(skey, srank, spos, hist, 1u << bits,
+                                                      chunk_rows, gkey, gmin, rep);
+  return hipGetLastError();
+}
+
+size_t shard_workspace_bytes(uint32_t shard_bits) {
+  const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
+  return align_up(4 * (nh + 1), 256) + align_up(4 * (scan::tiles_for(nh) + 1), 256) +
+         align_up(8 * (static_cast<uint64_t>(1) << shard_bits), 256);
+}
+
+hipError_t shard_count_launch(const uint64_t* key, const uint8_t* has_key, uint64_t n,
+                              uint32_t shard_bits, uint64_t* d_counts, void* ws, hipStream_t s) {
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + align_up(4 * (nh + 1), 256));
+  hipError_t e = partition(key, has_key, nullptr, n, 0, shard_bits, hist, tiles, nullptr, nullptr,
+                           nullptr, s, nullptr, "shard_hist", "shard_scatter");
+  if (e != hipSuccess) return e;
+  k_copy_counts<<<1, 256, 0, s>>>(hist, 1u << shard_bits, d_counts);
+  return hipGetLastError();
+}
+
+hipError_t shard_partition_launch(const uint64_t* key, const uint8_t* has_key,
+                                  const uint32_t* rank, uint64_t n, uint32_t shard_bits,
+                                  uint64_t* out_key, uint32_t* out_rank, uint32_t* out_pos,
+                                  void* ws, hipStream_t s, KTimer* timer) {
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + align_up(4 * (nh + 1), 256));
+  return partition(key, has_key, rank, n, 0, shard_bits, hist, tiles, out_key, out_rank, out_pos,
+                   s, timer, "shard_hist", "shard_scatter");
+}
+
+hipError_t scatter_rep_launch(const uint32_t* src, const uint32_t* pos, uint64_t n, uint32_t* dst,
+                              uint64_t n_dst, const uint32_t* init, bool do_init, hipStream_t s) {
+  if (do_init && n_dst) {
+    const uint64_t g = std::min<uint64_t>((n_dst + 255) / 256, 16384);
+    k_fill_init<<<static_cast<uint32_t>(g), 256, 0, s>>>(dst, n_dst, init);
+  }
+  if (n) {
+    const uint64_t g = std::min<uint64_t>((n + 255) / 256, 16384);
+    k_scatter<<<static_cast<uint32_t>(g), 256, 0, s>>>(src, pos, n, dst);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace sdgpu

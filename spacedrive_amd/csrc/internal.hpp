@@ -1,0 +1,103 @@
+// Internal (C++) interfaces between the C-ABI layer (sdgpu.cpp) and the HIP
+// kernel translation units.  Nothing here crosses the public boundary.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace sdgpu {
+
+// Optional per-kernel timing: the C-ABI layer passes a recorder that brackets
+// each main kernel with HIP events on the stream it is launched on.
+struct KTimer {
+  virtual void begin(const char* name, hipStream_t s) = 0;
+  virtual void end(hipStream_t s) = 0;
+  virtual ~KTimer() = default;
+};
+struct KScope {
+  KTimer* t;
+  hipStream_t s;
+  KScope(KTimer* t_, const char* name, hipStream_t s_) : t(t_), s(s_) {
+    if (t) t->begin(name, s);
+  }
+  ~KScope() {
+    if (t) t->end(s);
+  }
+};
+
+// ---- batched short-message BLAKE3 (cas_id, K1) ------------------------------
+// Workspace for one batch of n messages and at most max_chunks chunks.
+struct BatchWork {
+  uint32_t* n_chunks = nullptr;    // [n]
+  uint32_t* chunk_base = nullptr;  // [n + 1]  exclusive prefix of n_chunks
+  uint32_t* block_sums = nullptr;  // [scan tiles of n]
+  uint32_t* chunk_msg = nullptr;   // [max_chunks]
+  uint32_t* cvs = nullptr;         // [max_chunks][8]
+  uint32_t* total = nullptr;       // [1]   == chunk_base[n]
+  uint64_t max_chunks = 0;
+};
+
+// Largest message the batched cas kernel accepts: 8 + 100 KiB (cas.rs:15,27-29).
+constexpr uint32_t CAS_MAX_MSG_LEN = 8u + 100u * 1024u;
+
+// Hash n messages arena[off[i] .. off[i]+len[i]) (off 16-B aligned) and write
+// out_words (2 => cas_id's 8 bytes, 8 => full 32-byte digest) words per message.
+// status[i] = 0, or -EINVAL for len > max_len / misaligned offset.
+// All pointers are device pointers; fully asynchronous on `s`.
+hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                             uint32_t n, uint32_t max_len, uint32_t out_words, uint8_t* out,
+                             int32_t* status, const BatchWork& w, hipStream_t s,
+                             KTimer* timer = nullptr);
+
+// ---- tree BLAKE3 of large segments (file_checksum, K2/K3) -------------------
+struct TreeSeg {
+  const uint8_t* data;    // device pointer, 16-B aligned (bytes, or CVs when cv_input)
+  uint64_t len;           // bytes (or number of CVs when cv_input)
+  uint64_t chunk_offset;  // chunk counter of the first chunk
+  uint32_t root;          // 1: emit the ROOT digest, 0: emit the subtree CV
+  uint32_t pad;
+};
+
+struct TreePlan;  // opaque, built on the host per call
+// cv_input: every segment's `data` holds `len` 32-byte chaining values of
+// consecutive equal, aligned power-of-two subtrees (the last may be partial);
+// they are folded into the digest / CV of their concatenation.
+size_t tree_workspace_bytes(const TreeSeg* segs, uint32_t nseg, bool cv_input);
+// Bytes of the plan prefix of the workspace (what h_ws must hold).
+size_t tree_plan_bytes(uint32_t nseg);
+// d_ws: device workspace of tree_workspace_bytes(); h_ws: host scratch of
+// tree_plan_bytes() (pinned; must stay untouched until the plan copy on `s`
+// has executed).  out: device [nseg][32].
+hipError_t tree_hash_launch(const TreeSeg* segs, uint32_t nseg, bool cv_input, uint8_t* out,
+                            void* d_ws, void* h_ws, hipStream_t s, KTimer* timer = nullptr);
+
+// ---- synthetic corpora (bench / tests only) -----------------------------------
+hipError_t synth_cas_arena_launch(const uint64_t* sizes, const uint64_t* seeds,
+                                  const uint64_t* off, uint32_t n, uint8_t* arena, hipStream_t s);
+hipError_t synth_file_launch(uint64_t seed, uint64_t offset, uint64_t len, uint8_t* out,
+                             hipStream_t s);
+// Integer VALU throughput microbenchmark (add3/xor/alignbit mix of BLAKE3's G).
+hipError_t valu_probe_launch(uint32_t* sink, uint32_t iters, uint32_t blocks, hipStream_t s);
+hipError_t synth_dedup_rows_launch(uint64_t seed, uint64_t total_rows, uint64_t distinct,
+                                   uint64_t first_rank, uint64_t n, uint64_t* key,
+                                   uint8_t* has_key, uint32_t* rank, hipStream_t s);
+
+// ---- dedup (K4-K6) ------------------------------------------------------------
+size_t dedup_workspace_bytes(uint64_t n);
+// Group (key, rank) pairs; rep[i] for pair i.  Keys' top shard_bits bits are
+// constant on this shard (skipped by the bucket digit).
+hipError_t dedup_local_launch(const uint64_t* key, const uint32_t* rank, uint64_t n,
+                              uint32_t chunk_rows, uint32_t shard_bits, uint32_t* rep, void* ws,
+                              hipStream_t s, KTimer* timer = nullptr);
+size_t shard_workspace_bytes(uint32_t shard_bits);
+hipError_t shard_count_launch(const uint64_t* key, const uint8_t* has_key, uint64_t n,
+                              uint32_t shard_bits, uint64_t* d_counts, void* ws, hipStream_t s);
+hipError_t shard_partition_launch(const uint64_t* key, const uint8_t* has_key,
+                                  const uint32_t* rank, uint64_t n, uint32_t shard_bits,
+                                  uint64_t* out_key, uint32_t* out_rank, uint32_t* out_pos,
+                                  void* ws, hipStream_t s, KTimer* timer = nullptr);
+hipError_t scatter_rep_launch(const uint32_t* src, const uint32_t* pos, uint64_t n, uint32_t* dst,
+                              uint64_t n_dst, const uint32_t* init, bool do_init, hipStream_t s);
+
+}  // namespace sdgpu

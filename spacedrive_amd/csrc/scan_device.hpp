@@ -1,0 +1,99 @@
+// Exclusive prefix sum of u32 counts on the device (reduce-then-scan, three
+// launches, no host synchronisation).  Used by the K1 planner and the K4/K6
+// radix partitions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sdgpu {
+namespace scan {
+
+constexpr int kThreads = 256;
+constexpr uint32_t kTile = 1024;  // elements per tile (4 per thread)
+
+inline uint32_t tiles_for(uint64_t n) { return static_cast<uint32_t>((n + kTile - 1) / kTile); }
+
+__global__ __launch_bounds__(kThreads) static void k_tiles(const uint32_t* __restrict__ in,
+                                                           uint64_t n, uint32_t* __restrict__ out,
+                                                           uint32_t* __restrict__ tile_sums) {
+  __shared__ uint32_t sh[kThreads];
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x * 4;
+  uint32_t v[4];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = base + k < n ? in[base + k] : 0u;
+    s += v[k];
+  }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < kThreads; d <<= 1) {
+    const uint32_t t = threadIdx.x >= d ? sh[threadIdx.x - d] : 0u;
+    __syncthreads();
+    sh[threadIdx.x] += t;
+    __syncthreads();
+  }
+  uint32_t run = sh[threadIdx.x] - s;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (base + k < n) out[base + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == kThreads - 1) tile_sums[blockIdx.x] = sh[threadIdx.x];
+}
+
+// Single block: exclusive scan of tile sums; writes the grand total to
+// out[n] (if out_total_slot) and *total (if non-null).
+__global__ __launch_bounds__(kThreads) static void k_sums(uint32_t* __restrict__ tile_sums,
+                                                          uint32_t ntiles,
+                                                          uint32_t* __restrict__ out_total_slot,
+                                                          uint32_t* __restrict__ total) {
+  __shared__ uint32_t sh[kThreads];
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < ntiles; b0 += kThreads) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint32_t v = i < ntiles ? tile_sums[i] : 0u;
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int d = 1; d < kThreads; d <<= 1) {
+      const uint32_t t = threadIdx.x >= d ? sh[threadIdx.x - d] : 0u;
+      __syncthreads();
+      sh[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < ntiles) tile_sums[i] = carry + sh[threadIdx.x] - v;
+    const uint32_t blk = sh[kThreads - 1];
+    __syncthreads();
+    carry += blk;
+  }
+  if (threadIdx.x == 0) {
+    if (out_total_slot) *out_total_slot = carry;
+    if (total) *total = carry;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) static void k_add(uint32_t* __restrict__ out, uint64_t n,
+                                                         const uint32_t* __restrict__ tile_sums) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (i < n) out[i] += tile_sums[i / kTile];
+}
+
+// out[0..n) = exclusive scan of in[0..n); out[n] = total (out must hold n+1);
+// tile_sums must hold tiles_for(n) entries.  in may alias out.
+inline void exclusive(const uint32_t* in, uint64_t n, uint32_t* out, uint32_t* tile_sums,
+                      uint32_t* total, hipStream_t s) {
+  const uint32_t tiles = tiles_for(n);
+  if (tiles == 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(uint32_t), s);
+    if (total) (void)hipMemsetAsync(total, 0, sizeof(uint32_t), s);
+    return;
+  }
+  k_tiles<<<tiles, kThreads, 0, s>>>(in, n, out, tile_sums);
+  k_sums<<<1, kThreads, 0, s>>>(tile_sums, tiles, out + n, total);
+  k_add<<<static_cast<uint32_t>((n + kThreads - 1) / kThreads), kThreads, 0, s>>>(out, n,
+                                                                                   tile_sums);
+}
+
+}  // namespace scan
+}  // namespace sdgpu

@@ -1,0 +1,1004 @@
+// libsdgpu.so -- C ABI (include/sdgpu.h) over the gfx950 kernels.
+//
+// Host side of the MI355X content-identification path.  The reference host is
+// Rust (sd-core); its toolchain is absent here, so the host logic that would sit
+// in core/src/object/{cas.rs, validation/hash.rs, file_identifier/mod.rs} is
+// written in C++ below the C ABI, and the Rust binding a maintainer adds is in
+// INTEGRATION.md.
+//
+// Nothing here computes a hash on the CPU: every BLAKE3 compression runs in the
+// HIP kernels (b3_batch.hip, b3_tree.hip).  The host only reads files, packs the
+// cas messages into pinned memory and moves bytes.
+#include <errno.h>
+#include <fcntl.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/sdgpu.h"
+#include "internal.hpp"
+#include "scan_device.hpp"
+
+using namespace sdgpu;
+
+namespace {
+
+int map_err(hipError_t e) {
+  switch (e) {
+    case hipSuccess: return 0;
+    case hipErrorOutOfMemory: return -ENOMEM;
+    case hipErrorNoDevice:
+    case hipErrorInvalidDevice: return -ENODEV;
+    case hipErrorInvalidValue: return -EINVAL;
+    default: return -EIO;
+  }
+}
+
+#define SD_TRY(expr)                       \
+  do {                                     \
+    const hipError_t e_ = (expr);          \
+    if (e_ != hipSuccess) return map_err(e_); \
+  } while (0)
+
+#define SD_TRY_RC(expr)          \
+  do {                           \
+    const int rc_ = (expr);      \
+    if (rc_ != 0) return rc_;    \
+  } while (0)
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+constexpr uint64_t kChunkLen = 1024;  // BLAKE3 chunk
+constexpr size_t kSlabBytes = size_t(256) << 20;   // pinned staging per slab
+constexpr uint32_t kSlabFiles = 1u << 16;          // files per slab
+constexpr size_t kSliceBytes = size_t(64) << 20;   // file_checksum slice = 2^16 chunks
+constexpr uint32_t kStageMaxMsg = 8u + (64u << 20);  // largest staged cas message
+
+// Brackets kernels with HIP events on their own stream; elapsed times are
+// resolved (one sync per event pair) only when read.
+struct EventTimer final : KTimer {
+  struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+  };
+  struct Acc {
+    std::string name;
+    double ms = 0;
+    uint64_t n = 0;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> pool;
+  std::vector<Acc> acc;
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  void begin(const char* name, hipStream_t s) override {
+    Pending p{name, get(), get()};
+    (void)hipEventRecord(p.a, s);
+    pending.push_back(p);
+  }
+  void end(hipStream_t s) override {
+    if (!pending.empty()) (void)hipEventRecord(pending.back().b, s);
+  }
+  void resolve() {
+    for (auto& p : pending) {
+      float ms = 0;
+      (void)hipEventSynchronize(p.b);
+      (void)hipEventElapsedTime(&ms, p.a, p.b);
+      Acc* a = nullptr;
+      for (auto& x : acc)
+        if (x.name == p.name) a = &x;
+      if (!a) {
+        acc.push_back(Acc{p.name, 0, 0});
+        a = &acc.back();
+      }
+      a->ms += ms;
+      a->n += 1;
+      pool.push_back(p.a);
+      pool.push_back(p.b);
+    }
+    pending.clear();
+  }
+  ~EventTimer() override {
+    resolve();
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
+}  // namespace
+
+struct sdgpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t last = nullptr;
+  std::mutex mu;
+  DevBuf batch_ws, tree_ws, dedup_ws, shard_ws, io_a, io_b;
+  PinBuf plan_pin;
+  hipEvent_t plan_evt = nullptr;
+  bool plan_pending = false;
+  bool timing = false;
+  EventTimer timer;
+  KTimer* kt() { return timing ? &timer : nullptr; }
+};
+
+namespace {
+
+hipStream_t pick(sdgpu_ctx* c, void* stream) {
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  c->last = s;
+  return s;
+}
+
+// Grow-only device buffer; frees the old one only after the context's work
+// has drained (a kernel may still read it).
+int ensure_dev(sdgpu_ctx* c, DevBuf& b, size_t bytes) {
+  if (bytes <= b.cap) return 0;
+  if (b.p) {
+    (void)hipStreamSynchronize(c->stream);
+    if (c->last && c->last != c->stream) (void)hipStreamSynchronize(c->last);
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  const size_t want = align_up(std::max<size_t>(bytes, 1), size_t(1) << 20);
+  SD_TRY(hipMalloc(&b.p, want));
+  b.cap = want;
+  return 0;
+}
+
+// Grow-only device buffer that keeps its first `keep` bytes.
+int grow_dev_keep(sdgpu_ctx* c, DevBuf& b, size_t bytes, size_t keep) {
+  if (bytes <= b.cap) return 0;
+  void* np = nullptr;
+  const size_t want = align_up(std::max<size_t>(bytes, 2 * b.cap), size_t(1) << 20);
+  SD_TRY(hipMalloc(&np, want));
+  if (b.p) {
+    SD_TRY(hipStreamSynchronize(c->stream));
+    if (keep) SD_TRY(hipMemcpy(np, b.p, std::min(keep, b.cap), hipMemcpyDeviceToDevice));
+    (void)hipFree(b.p);
+  }
+  b.p = np;
+  b.cap = want;
+  return 0;
+}
+
+int ensure_pin(PinBuf& b, size_t bytes) {
+  if (bytes <= b.cap) return 0;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  const size_t want = align_up(std::max<size_t>(bytes, 1), size_t(1) << 16);
+  SD_TRY(hipHostMalloc(&b.p, want, hipHostMallocDefault));
+  b.cap = want;
+  return 0;
+}
+
+// Carves the K1 workspace for n messages / max_chunks chunks out of ctx->batch_ws.
+int batch_work(sdgpu_ctx* c, uint32_t n, uint64_t max_chunks, BatchWork& w) {
+  const size_t o_nch = 0;
+  const size_t o_base = align_up(o_nch + 4ull * n, 256);
+  const size_t o_sums = align_up(o_base + 4ull * (n + 1), 256);
+  const size_t o_tot = align_up(o_sums + 4ull * (scan::tiles_for(n) + 1), 256);
+  const size_t o_map = align_up(o_tot + 4, 256);
+  const size_t o_cvs = align_up(o_map + 4ull * max_chunks, 256);
+  const size_t total = align_up(o_cvs + 32ull * max_chunks, 256);
+  SD_TRY_RC(ensure_dev(c, c->batch_ws, total));
+  uint8_t* b = static_cast<uint8_t*>(c->batch_ws.p);
+  w.n_chunks = reinterpret_cast<uint32_t*>(b + o_nch);
+  w.chunk_base = reinterpret_cast<uint32_t*>(b + o_base);
+  w.block_sums = reinterpret_cast<uint32_t*>(b + o_sums);
+  w.total = reinterpret_cast<uint32_t*>(b + o_tot);
+  w.chunk_msg = reinterpret_cast<uint32_t*>(b + o_map);
+  w.cvs = reinterpret_cast<uint32_t*>(b + o_cvs);
+  w.max_chunks = max_chunks;
+  return 0;
+}
+
+// Tree launch with the context's pinned plan scratch (waits for the previous
+// plan copy before rewriting the scratch).
+int tree_launch(sdgpu_ctx* c, const TreeSeg* segs, uint32_t nseg, bool cv_input, uint8_t* d_out,
+                hipStream_t s) {
+  SD_TRY_RC(ensure_dev(c, c->tree_ws, tree_workspace_bytes(segs, nseg, cv_input)));
+  if (c->plan_pending) {
+    SD_TRY(hipEventSynchronize(c->plan_evt));
+    c->plan_pending = false;
+  }
+  SD_TRY_RC(ensure_pin(c->plan_pin, tree_plan_bytes(nseg)));
+  SD_TRY(tree_hash_launch(segs, nseg, cv_input, d_out, c->tree_ws.p, c->plan_pin.p, s, c->kt()));
+  SD_TRY(hipEventRecord(c->plan_evt, s));
+  c->plan_pending = true;
+  return 0;
+}
+
+const char HEXD[] = "0123456789abcdef";
+void to_hex(const uint8_t* d, int n, char* out) {
+  for (int i = 0; i < n; ++i) {
+    out[2 * i] = HEXD[d[i] >> 4];
+    out[2 * i + 1] = HEXD[d[i] & 15];
+  }
+  out[2 * n] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// File reads with the reference's semantics (cas.rs:23-62)
+// ---------------------------------------------------------------------------
+
+int pread_exact(int fd, uint8_t* buf, size_t n, off_t pos) {
+  size_t got = 0;
+  while (got < n) {
+    const ssize_t r = pread(fd, buf + got, n - got, pos + static_cast<off_t>(got));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return -errno;
+    }
+    if (r == 0) return -ENODATA;  // read_exact: io::ErrorKind::UnexpectedEof
+    got += static_cast<size_t>(r);
+  }
+  return 0;
+}
+
+// Writes the cas message of the file at `path` (stat size `size`) into dst
+// (capacity cap).  Returns its length, or -errno.
+int64_t read_cas_message(const char* path, uint64_t size, uint8_t* dst, size_t cap) {
+  if (cap < 8) return -ENOBUFS;
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  for (int i = 0; i < 8; ++i) dst[i] = static_cast<uint8_t>(size >> (8 * i));
+  int64_t len = 8;
+  int rc = 0;
+  if (size <= SDGPU_CAS_MINIMUM_FILE_SIZE) {
+    // fs::read(path): the whole current content, whatever its length
+    for (;;) {
+      if (static_cast<size_t>(len) == cap) {
+        uint8_t probe;
+        const ssize_t r = read(fd, &probe, 1);
+        rc = r == 0 ? 0 : (r < 0 ? -errno : -EFBIG);
+        break;
+      }
+      const ssize_t r = read(fd, dst + len, cap - static_cast<size_t>(len));
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        rc = -errno;
+        break;
+      }
+      if (r == 0) break;
+      len += r;
+    }
+  } else if (cap < SDGPU_CAS_SAMPLED_MSG_LEN) {
+    rc = -ENOBUFS;
+  } else {
+    const uint64_t hf = SDGPU_CAS_HEADER_OR_FOOTER_SIZE, ss = SDGPU_CAS_SAMPLE_SIZE;
+    rc = pread_exact(fd, dst + len, hf, 0);  // header (cas.rs:35-38)
+    len += hf;
+    const uint64_t jump = (size - 2 * hf) / SDGPU_CAS_SAMPLE_COUNT;  // cas.rs:41
+    for (uint32_t k = 0; k < SDGPU_CAS_SAMPLE_COUNT && rc == 0; ++k) {  // cas.rs:42-51
+      rc = pread_exact(fd, dst + len, ss, static_cast<off_t>(hf + k * jump));
+      len += ss;
+    }
+    if (rc == 0) {  // footer from the ACTUAL end (SeekFrom::End, cas.rs:54-57)
+      struct stat st;
+      if (fstat(fd, &st) != 0) {
+        rc = -errno;
+      } else if (static_cast<uint64_t>(st.st_size) < hf) {
+        rc = -EINVAL;  // seek before byte 0
+      } else {
+        rc = pread_exact(fd, dst + len, hf, static_cast<off_t>(st.st_size - hf));
+        len += hf;
+      }
+    }
+  }
+  close(fd);
+  return rc ? rc : len;
+}
+
+template <typename F>
+void parallel_for(uint32_t n, F&& f) {
+  const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const uint32_t nt = std::min<uint32_t>(hw, (n + 63) / 64);
+  if (nt <= 1) {
+    for (uint32_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<uint32_t> next{0};
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (uint32_t t = 0; t < nt; ++t)
+    th.emplace_back([&] {
+      for (;;) {
+        const uint32_t i0 = next.fetch_add(64);
+        if (i0 >= n) break;
+        const uint32_t i1 = std::min(n, i0 + 64);
+        for (uint32_t i = i0; i < i1; ++i) f(i);
+      }
+    });
+  for (auto& t : th) t.join();
+}
+
+// ---------------------------------------------------------------------------
+// K1 staging pipeline: slabs of messages packed into pinned memory by a
+// producer, H2D + K1 + D2H on the context stream, two slabs in flight so the
+// host fills slab k+1 while the GPU works on slab k.
+// ---------------------------------------------------------------------------
+
+struct Slab {
+  PinBuf h;          // [arena | off | len | out | status]
+  DevBuf d;          // same layout on the device
+  hipEvent_t done = nullptr;
+  bool busy = false;
+  uint32_t first = 0, count = 0;
+};
+
+struct SlabLayout {
+  size_t arena, off, len, out, status, total;
+};
+
+SlabLayout slab_layout() {
+  SlabLayout L;
+  L.arena = 0;
+  L.off = align_up(kSlabBytes, 256);
+  L.len = align_up(L.off + 8ull * kSlabFiles, 256);
+  L.out = align_up(L.len + 4ull * kSlabFiles, 256);
+  L.status = align_up(L.out + 8ull * kSlabFiles, 256);
+  L.total = align_up(L.status + 4ull * kSlabFiles, 256);
+  return L;
+}
+
+// producer(i, dst, cap) -> message length (>= 0), or -errno, or 0x7fffffff
+// meaning "no message for this file" (size 0).  est(i) = bytes to reserve.
+template <typename Est, typename Produce, typename Finish>
+int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&& finish) {
+  const SlabLayout L = slab_layout();
+  Slab slabs[2];
+  int rc = 0;
+  for (auto& sl : slabs) {
+    if ((rc = ensure_pin(sl.h, L.total)) != 0) break;
+    if ((rc = ensure_dev(c, sl.d, L.total)) != 0) break;
+    if (hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+  }
+  auto drain = [&](Slab& sl) -> int {
+    if (!sl.busy) return 0;
+    if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
+    sl.busy = false;
+    uint8_t* hb = static_cast<uint8_t*>(sl.h.p);
+    finish(sl.first, sl.count, reinterpret_cast<const uint8_t(*)[8]>(hb + L.out),
+           reinterpret_cast<const int32_t*>(hb + L.status));
+    return 0;
+  };
+  uint32_t i = 0, k = 0;
+  while (rc == 0 && i < n) {
+    Slab& sl = slabs[k & 1];
+    if ((rc = drain(sl)) != 0) break;
+    // assign files to this slab
+    uint8_t* hb = static_cast<uint8_t*>(sl.h.p);
+    uint64_t* off = reinterpret_cast<uint64_t*>(hb + L.off);
+    uint32_t* len = reinterpret_cast<uint32_t*>(hb + L.len);
+    int32_t* pst = reinterpret_cast<int32_t*>(hb + L.status);
+    sl.first = i;
+    uint64_t pos = 0;
+    uint32_t cnt = 0;
+    while (i + cnt < n && cnt < kSlabFiles) {
+      const uint64_t need = align_up(est(i + cnt), 16);
+      if (pos + need > kSlabBytes && cnt > 0) break;
+      off[cnt] = pos;
+      pos += std::min<uint64_t>(need, kSlabBytes);
+      ++cnt;
+    }
+    sl.count = cnt;
+    // fill (threads): message bytes + per-file pre-status
+    parallel_for(cnt, [&](uint32_t j) {
+      const uint64_t cap = (j + 1 < cnt ? off[j + 1] : std::min<uint64_t>(pos, kSlabBytes)) - off[j];
+      const int64_t r = produce(sl.first + j, hb + off[j], static_cast<size_t>(cap));
+      if (r >= 0 && r != 0x7fffffff) {
+        len[j] = static_cast<uint32_t>(r);
+        pst[j] = 0;
+      } else {
+        len[j] = 0;  // hashed as an empty message; status says why it is void
+        pst[j] = r == 0x7fffffff ? 1 : static_cast<int32_t>(r);
+      }
+    });
+    // device: copy, hash, copy back
+    hipStream_t s = c->stream;
+    uint8_t* db = static_cast<uint8_t*>(sl.d.p);
+    BatchWork w;
+    if ((rc = batch_work(c, cnt, pos / kChunkLen + cnt, w)) != 0) break;
+    if (hipMemcpyAsync(db, hb, pos, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(db + L.off, hb + L.off, 8ull * cnt, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(db + L.len, hb + L.len, 4ull * cnt, hipMemcpyHostToDevice, s) != hipSuccess ||
+        batch_hash_launch(db, reinterpret_cast<const uint64_t*>(db + L.off),
+                          reinterpret_cast<const uint32_t*>(db + L.len), cnt, kStageMaxMsg, 2,
+                          db + L.out, nullptr, w, s) != hipSuccess ||
+        hipMemcpyAsync(hb + L.out, db + L.out, 8ull * cnt, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipEventRecord(sl.done, s) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+    sl.busy = true;
+    i += cnt;
+    ++k;
+  }
+  for (auto& sl : slabs) {
+    const int r2 = drain(sl);
+    if (rc == 0) rc = r2;
+  }
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& sl : slabs) {
+    if (sl.done) (void)hipEventDestroy(sl.done);
+    if (sl.h.p) (void)hipHostFree(sl.h.p);
+    if (sl.d.p) (void)hipFree(sl.d.p);
+  }
+  return rc;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+
+extern "C" {
+
+int sdgpu_abi_version(void) { return SDGPU_ABI_VERSION; }
+
+const char* sdgpu_strerror(int rc) {
+  if (rc == 0) return "success";
+  if (rc == -EIO) return "HIP runtime error";
+  if (rc == -ENODEV) return "no usable gfx950 device";
+  return strerror(-rc);
+}
+
+int sdgpu_device_count(int* count) {
+  if (!count) return -EINVAL;
+  int n = 0;
+  const hipError_t e = hipGetDeviceCount(&n);
+  *count = e == hipSuccess ? n : 0;
+  return e == hipSuccess ? 0 : -ENODEV;
+}
+
+int sdgpu_open(int device, sdgpu_ctx** out) {
+  if (!out) return -EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -ENODEV;
+  if (device < 0 || device >= n) return -ENODEV;
+  hipDeviceProp_t prop;
+  SD_TRY(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return -ENODEV;
+  SD_TRY(hipSetDevice(device));
+  sdgpu_ctx* c = new (std::nothrow) sdgpu_ctx;
+  if (!c) return -ENOMEM;
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->plan_evt, hipEventDisableTiming) != hipSuccess) {
+    delete c;
+    return -EIO;
+  }
+  c->last = c->stream;
+  *out = c;
+  return 0;
+}
+
+int sdgpu_close(sdgpu_ctx* c) {
+  if (!c) return -EINVAL;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (c->last && c->last != c->stream) (void)hipStreamSynchronize(c->last);
+  for (DevBuf* b : {&c->batch_ws, &c->tree_ws, &c->dedup_ws, &c->shard_ws, &c->io_a, &c->io_b})
+    if (b->p) (void)hipFree(b->p);
+  if (c->plan_pin.p) (void)hipHostFree(c->plan_pin.p);
+  (void)hipEventDestroy(c->plan_evt);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+int sdgpu_sync(sdgpu_ctx* c) {
+  if (!c) return -EINVAL;
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY(hipStreamSynchronize(c->stream));
+  if (c->last && c->last != c->stream) SD_TRY(hipStreamSynchronize(c->last));
+  return 0;
+}
+
+void* sdgpu_stream(sdgpu_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+int sdgpu_alloc_pinned(sdgpu_ctx* c, size_t bytes, void** out) {
+  if (!c || !out) return -EINVAL;
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY(hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+  return 0;
+}
+
+int sdgpu_free_pinned(sdgpu_ctx* c, void* p) {
+  if (!c) return -EINVAL;
+  SD_TRY(hipHostFree(p));
+  return 0;
+}
+
+int sdgpu_alloc_device(sdgpu_ctx* c, size_t bytes, void** out) {
+  if (!c || !out) return -EINVAL;
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY(hipMalloc(out, std::max<size_t>(bytes, 1)));
+  return 0;
+}
+
+int sdgpu_free_device(sdgpu_ctx* c, void* p) {
+  if (!c) return -EINVAL;
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY(hipFree(p));
+  return 0;
+}
+
+int sdgpu_memcpy_async(sdgpu_ctx* c, void* dst, const void* src, size_t bytes, void* stream) {
+  if (!c) return -EINVAL;
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, pick(c, stream)));
+  return 0;
+}
+
+// ---- K1 ---------------------------------------------------------------------
+
+int sdgpu_cas_batch_device(sdgpu_ctx* c, const uint8_t* d_arena, uint64_t arena_bytes,
+                           const uint64_t* d_off, const uint32_t* d_len, uint32_t n,
+                           uint8_t* d_out8, int32_t* d_status, void* stream) {
+  if (!c || (n && (!d_arena || !d_off || !d_len || !d_out8))) return -EINVAL;
+  if (reinterpret_cast<uintptr_t>(d_arena) % 16 || reinterpret_cast<uintptr_t>(d_out8) % 4)
+    return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  BatchWork w;
+  SD_TRY_RC(batch_work(c, n, arena_bytes / kChunkLen + n, w));
+  SD_TRY(batch_hash_launch(d_arena, d_off, d_len, n, CAS_MAX_MSG_LEN, 2, d_out8, d_status, w, s,
+                           c->kt()));
+  return 0;
+}
+
+int sdgpu_cas_batch(sdgpu_ctx* c, const uint8_t* msg_arena, const uint64_t* msg_off,
+                    const uint32_t* msg_len, uint32_t n, uint8_t (*out8)[8], int32_t* status) {
+  if (!c || (n && (!msg_arena || !msg_off || !msg_len || !out8))) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  std::vector<uint8_t> bad(n, 0);
+  for (uint32_t i = 0; i < n; ++i) bad[i] = msg_len[i] > CAS_MAX_MSG_LEN;
+  const int rc = run_pipeline(
+      c, n, [&](uint32_t i) -> uint64_t { return bad[i] ? 16 : msg_len[i]; },
+      [&](uint32_t i, uint8_t* dst, size_t cap) -> int64_t {
+        if (bad[i]) return -EINVAL;
+        if (msg_len[i] > cap) return -ENOBUFS;
+        memcpy(dst, msg_arena + msg_off[i], msg_len[i]);
+        return msg_len[i];
+      },
+      [&](uint32_t first, uint32_t cnt, const uint8_t (*o)[8], const int32_t* st) {
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const int32_t sj = st[j];
+          if (sj == 0) memcpy(out8[first + j], o[j], 8);
+          else memset(out8[first + j], 0, 8);
+          if (status) status[first + j] = sj == 1 ? 0 : sj;
+        }
+      });
+  return rc;
+}
+
+int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t* size, uint32_t n,
+                         uint8_t (*out8)[8], uint8_t* has_key, int32_t* status) {
+  if (!c || (n && (!paths || !size || !out8))) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  return run_pipeline(
+      c, n,
+      [&](uint32_t i) -> uint64_t {
+        if (size[i] == 0) return 16;
+        return size[i] <= SDGPU_CAS_MINIMUM_FILE_SIZE ? 8 + size[i] + 4096  // room to grow
+                                                      : SDGPU_CAS_SAMPLED_MSG_LEN;
+      },
+      [&](uint32_t i, uint8_t* dst, size_t cap) -> int64_t {
+        if (size[i] == 0) return 0x7fffffff;  // cas_id None (file_identifier/mod.rs:80-88)
+        return read_cas_message(paths[i], size[i], dst, cap);
+      },
+      [&](uint32_t first, uint32_t cnt, const uint8_t (*o)[8], const int32_t* st) {
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const int32_t sj = st[j];
+          const bool ok = sj == 0;
+          if (ok) memcpy(out8[first + j], o[j], 8);
+          else memset(out8[first + j], 0, 8);
+          if (has_key) has_key[first + j] = ok ? 1 : 0;
+          if (status) status[first + j] = sj == 1 ? 0 : sj;
+        }
+      });
+}
+
+int sdgpu_generate_cas_id(sdgpu_ctx* c, const char* path, uint64_t size, char out_hex[17]) {
+  if (!c || !path || !out_hex) return -EINVAL;
+  uint8_t out[8];
+  int32_t st = 0;
+  // the single-file call keeps the reference's semantics for size 0 too
+  // (non_indexed.rs:161 hashes the 8 zero bytes of an empty file)
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  const int rc = run_pipeline(
+      c, 1,
+      [&](uint32_t) -> uint64_t {
+        return size <= SDGPU_CAS_MINIMUM_FILE_SIZE ? 8 + size + 4096 : SDGPU_CAS_SAMPLED_MSG_LEN;
+      },
+      [&](uint32_t, uint8_t* dst, size_t cap) -> int64_t {
+        return read_cas_message(path, size, dst, cap);
+      },
+      [&](uint32_t, uint32_t, const uint8_t (*o)[8], const int32_t* s) {
+        st = s[0];
+        memcpy(out, o[0], 8);
+      });
+  if (rc) return rc;
+  if (st) return st;
+  to_hex(out, 8, out_hex);
+  return 0;
+}
+
+// ---- K2/K3 ------------------------------------------------------------------
+
+int sdgpu_checksum_batch_device(sdgpu_ctx* c, const uint8_t* const* d_files, const uint64_t* lens,
+                                uint32_t n, uint8_t* d_out32, void* stream) {
+  if (!c || (n && (!d_files || !lens || !d_out32))) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  std::vector<TreeSeg> segs(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (reinterpret_cast<uintptr_t>(d_files[i]) % 16) return -EINVAL;
+    segs[i] = TreeSeg{d_files[i], lens[i], 0, 1, 0};
+  }
+  return tree_launch(c, segs.data(), n, false, d_out32, s);
+}
+
+int sdgpu_subtree_device(sdgpu_ctx* c, const uint8_t* d_bytes, uint64_t len, uint64_t chunk_offset,
+                         int root, uint8_t* d_out32, void* stream) {
+  if (!c || !d_bytes || !d_out32 || reinterpret_cast<uintptr_t>(d_bytes) % 16) return -EINVAL;
+  if (root && chunk_offset != 0) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  const TreeSeg seg{d_bytes, len, chunk_offset, root ? 1u : 0u, 0};
+  return tree_launch(c, &seg, 1, false, d_out32, s);
+}
+
+int sdgpu_checksum(sdgpu_ctx* c, const void* bytes, uint64_t len, uint8_t out32[32]) {
+  if (!c || (len && !bytes) || !out32) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  c->last = s;
+  SD_TRY_RC(ensure_dev(c, c->io_a, align_up(len, 256) + 256));
+  uint8_t* d = static_cast<uint8_t*>(c->io_a.p);
+  if (len) SD_TRY(hipMemcpyAsync(d, bytes, len, hipMemcpyHostToDevice, s));
+  uint8_t* dout = d + align_up(len, 256);
+  const TreeSeg seg{d, len, 0, 1, 0};
+  SD_TRY_RC(tree_launch(c, &seg, 1, false, dout, s));
+  SD_TRY(hipMemcpyAsync(out32, dout, 32, hipMemcpyDeviceToHost, s));
+  SD_TRY(hipStreamSynchronize(s));
+  return 0;
+}
+
+int sdgpu_file_checksum(sdgpu_ctx* c, const char* path, char out_hex[65]) {
+  if (!c || !path || !out_hex) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  hipStream_t s = c->stream;
+  c->last = s;
+  // two pinned + two device slices; slice k's subtree CV lands in cvs[k]
+  PinBuf hp[2];
+  int rc = 0;
+  uint64_t nslices = 0;
+  uint64_t total = 0;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  bool inflight[2] = {false, false};
+  std::vector<uint8_t> out(32);
+  do {
+    if ((rc = ensure_pin(hp[0], kSliceBytes)) || (rc = ensure_pin(hp[1], kSliceBytes))) break;
+    struct stat st;
+    if (fstat(fd, &st) == 0 && st.st_size > 0 &&
+        (rc = grow_dev_keep(c, c->io_b, 32 * (static_cast<uint64_t>(st.st_size) / kSliceBytes + 2) + 256, 0)))
+      break;
+    if ((rc = ensure_dev(c, c->io_a, 2 * kSliceBytes + 4096))) break;
+    if (hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+    uint8_t* dslice[2] = {static_cast<uint8_t*>(c->io_a.p),
+                          static_cast<uint8_t*>(c->io_a.p) + kSliceBytes};
+    uint8_t* droot = static_cast<uint8_t*>(c->io_a.p) + 2 * kSliceBytes;
+    // CV list lives in io_b, grown as slices arrive
+    bool eof = false;
+    while (!eof) {
+      const int k = static_cast<int>(nslices & 1);
+      if (inflight[k]) {
+        if (hipEventSynchronize(ev[k]) != hipSuccess) { rc = -EIO; break; }
+        inflight[k] = false;
+      }
+      // file_checksum reads BLOCK_LEN = 1 MiB at a time until a short read
+      // (hash.rs:14-20); a slice is 64 such reads.
+      uint8_t* hb = static_cast<uint8_t*>(hp[k].p);
+      size_t got = 0;
+      while (got < kSliceBytes) {
+        const ssize_t r = read(fd, hb + got, kSliceBytes - got);
+        if (r < 0) {
+          if (errno == EINTR) continue;
+          rc = -errno;
+          break;
+        }
+        if (r == 0) {
+          eof = true;
+          break;
+        }
+        got += static_cast<size_t>(r);
+      }
+      if (rc) break;
+      if (got == 0 && nslices > 0) break;  // previous slice ended exactly at EOF
+      // peek whether more data follows (to know if this slice is the last)
+      if (!eof) {
+        uint8_t probe;
+        const ssize_t r = pread(fd, &probe, 1, static_cast<off_t>(total + got));
+        if (r == 0) eof = true;
+      }
+      const bool only = eof && nslices == 0;
+      if ((rc = grow_dev_keep(c, c->io_b, 32 * (nslices + 1) + 256, 32 * nslices))) break;
+      uint8_t* cvs = static_cast<uint8_t*>(c->io_b.p);
+      if (got && hipMemcpyAsync(dslice[k], hb, got, hipMemcpyHostToDevice, s) != hipSuccess) {
+        rc = -EIO;
+        break;
+      }
+      const TreeSeg seg{dslice[k], got, (total / kChunkLen), only ? 1u : 0u, 0};
+      if ((rc = tree_launch(c, &seg, 1, false, only ? droot : cvs + 32 * nslices, s))) break;
+      if (hipEventRecord(ev[k], s) != hipSuccess) { rc = -EIO; break; }
+      inflight[k] = true;
+      total += got;
+      ++nslices;
+    }
+    if (rc) break;
+    if (nslices > 1) {
+      // fold the slice CVs (equal aligned power-of-two subtrees, last partial)
+      const TreeSeg seg{static_cast<uint8_t*>(c->io_b.p), nslices, 0, 1, 0};
+      if ((rc = tree_launch(c, &seg, 1, true, droot, s))) break;
+    }
+    if (hipMemcpyAsync(out.data(), droot, 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = -EIO;
+  } while (false);
+  (void)hipStreamSynchronize(s);
+  for (int k = 0; k < 2; ++k) {
+    if (ev[k]) (void)hipEventDestroy(ev[k]);
+    if (hp[k].p) (void)hipHostFree(hp[k].p);
+  }
+  close(fd);
+  if (rc) return rc;
+  to_hex(out.data(), 32, out_hex);
+  return 0;
+}
+
+// ---- K4-K6 ------------------------------------------------------------------
+
+int sdgpu_group_pairs_device(sdgpu_ctx* c, const uint64_t* d_key, const uint32_t* d_rank,
+                             uint64_t n, uint32_t chunk_rows, uint32_t skip_bits, uint32_t* d_rep,
+                             void* stream) {
+  if (!c || chunk_rows == 0 || skip_bits > 32 || (n && (!d_key || !d_rank || !d_rep)))
+    return -EINVAL;
+  if (n >= (1ull << 32)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  if (n == 0) return 0;
+  SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(n)));
+  SD_TRY(dedup_local_launch(d_key, d_rank, n, chunk_rows, skip_bits, d_rep, c->dedup_ws.p, s,
+                            c->kt()));
+  return 0;
+}
+
+int sdgpu_shard_count_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8_t* d_has_key,
+                             uint64_t n, uint32_t shard_bits, uint64_t* h_counts, void* stream) {
+  if (!c || !h_counts || shard_bits > 8 || (n && !d_key)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  const size_t ws = shard_workspace_bytes(shard_bits);
+  SD_TRY_RC(ensure_dev(c, c->shard_ws, ws));
+  uint8_t* w = static_cast<uint8_t*>(c->shard_ws.p);
+  uint64_t* dcounts = reinterpret_cast<uint64_t*>(w + ws - align_up(8ull << shard_bits, 256));
+  SD_TRY(shard_count_launch(d_key, d_has_key, n, shard_bits, dcounts, w, s));
+  SD_TRY(hipMemcpyAsync(h_counts, dcounts, 8ull << shard_bits, hipMemcpyDeviceToHost, s));
+  SD_TRY(hipStreamSynchronize(s));
+  return 0;
+}
+
+int sdgpu_shard_partition_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8_t* d_has_key,
+                                 const uint32_t* d_rank, uint64_t n, uint32_t shard_bits,
+                                 uint64_t* d_out_key, uint32_t* d_out_rank, uint32_t* d_out_pos,
+                                 void* stream) {
+  if (!c || shard_bits > 8 || (n && (!d_key || !d_out_key || !d_out_rank || !d_out_pos)))
+    return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  SD_TRY_RC(ensure_dev(c, c->shard_ws, shard_workspace_bytes(shard_bits)));
+  SD_TRY(shard_partition_launch(d_key, d_has_key, d_rank, n, shard_bits, d_out_key, d_out_rank,
+                                d_out_pos, c->shard_ws.p, s, c->kt()));
+  return 0;
+}
+
+int sdgpu_scatter_rep_device(sdgpu_ctx* c, const uint32_t* d_src, const uint32_t* d_pos,
+                             uint64_t n, uint32_t* d_dst, uint64_t n_dst, const uint32_t* d_init,
+                             int init, void* stream) {
+  if (!c || (n && (!d_src || !d_pos)) || ((n || init) && !d_dst)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY(scatter_rep_launch(d_src, d_pos, n, d_dst, n_dst, d_init, init != 0, pick(c, stream)));
+  return 0;
+}
+
+int sdgpu_dedup(sdgpu_ctx* c, const uint64_t* key, const uint8_t* has_key, uint32_t n,
+                uint32_t chunk_rows, uint32_t* rep) {
+  if (!c || chunk_rows == 0 || (n && (!key || !has_key || !rep))) return -EINVAL;
+  if (n == 0) return 0;
+  uint8_t* d = nullptr;
+  int rc = 0;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    SD_TRY(hipSetDevice(c->device));
+  }
+  // [key n*8 | has n | pkey n*8 | prank n*4 | ppos n*4 | prep n*4 | rep n*4]
+  const size_t o_key = 0, o_has = align_up(8ull * n, 256), o_pkey = align_up(o_has + n, 256);
+  const size_t o_prank = align_up(o_pkey + 8ull * n, 256), o_ppos = align_up(o_prank + 4ull * n, 256);
+  const size_t o_prep = align_up(o_ppos + 4ull * n, 256), o_rep = align_up(o_prep + 4ull * n, 256);
+  const size_t total = align_up(o_rep + 4ull * n, 256);
+  if (hipMalloc(&d, total) != hipSuccess) return -ENOMEM;
+  hipStream_t s = c->stream;
+  do {
+    if (hipMemcpyAsync(d + o_key, key, 8ull * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d + o_has, has_key, n, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+    uint64_t cnt = 0;
+    const uint64_t* dk = reinterpret_cast<const uint64_t*>(d + o_key);
+    if ((rc = sdgpu_shard_count_device(c, dk, d + o_has, n, 0, &cnt, s))) break;
+    uint64_t* pkey = reinterpret_cast<uint64_t*>(d + o_pkey);
+    uint32_t* prank = reinterpret_cast<uint32_t*>(d + o_prank);
+    uint32_t* ppos = reinterpret_cast<uint32_t*>(d + o_ppos);
+    uint32_t* prep = reinterpret_cast<uint32_t*>(d + o_prep);
+    uint32_t* drep = reinterpret_cast<uint32_t*>(d + o_rep);
+    if ((rc = sdgpu_shard_partition_device(c, dk, d + o_has, nullptr, n, 0, pkey, prank, ppos, s)))
+      break;
+    if ((rc = sdgpu_group_pairs_device(c, pkey, prank, cnt, chunk_rows, 0, prep, s))) break;
+    if ((rc = sdgpu_scatter_rep_device(c, prep, ppos, cnt, drep, n, nullptr, 1, s))) break;
+    if (hipMemcpyAsync(rep, drep, 4ull * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = -EIO;
+  } while (false);
+  (void)hipStreamSynchronize(s);
+  (void)hipFree(d);
+  return rc;
+}
+
+// ---- synthetic corpora -------------------------------------------------------
+
+int sdgpu_synth_cas_arena_device(sdgpu_ctx* c, const uint64_t* d_sizes, const uint64_t* d_seeds,
+                                 const uint64_t* d_off, uint32_t n, uint8_t* d_arena, void* stream) {
+  if (!c || (n && (!d_sizes || !d_seeds || !d_off || !d_arena))) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY(synth_cas_arena_launch(d_sizes, d_seeds, d_off, n, d_arena, pick(c, stream)));
+  return 0;
+}
+
+int sdgpu_synth_file_device(sdgpu_ctx* c, uint64_t seed, uint64_t offset, uint64_t len,
+                            uint8_t* d_out, void* stream) {
+  if (!c || (len && !d_out) || offset % 8 || reinterpret_cast<uintptr_t>(d_out) % 16)
+    return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY(synth_file_launch(seed, offset, len, d_out, pick(c, stream)));
+  return 0;
+}
+
+// ---- instrumentation -----------------------------------------------------------
+
+int sdgpu_set_timing(sdgpu_ctx* c, int enable) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->timing = enable != 0;
+  return 0;
+}
+
+int sdgpu_timing_reset(sdgpu_ctx* c) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->timer.resolve();
+  c->timer.acc.clear();
+  return 0;
+}
+
+int sdgpu_timing_read(sdgpu_ctx* c, uint32_t idx, char name[32], double* total_ms,
+                      uint64_t* launches) {
+  if (!c || !name || !total_ms || !launches) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  c->timer.resolve();
+  if (idx >= c->timer.acc.size()) return -ENOENT;
+  const auto& a = c->timer.acc[idx];
+  snprintf(name, 32, "%s", a.name.c_str());
+  *total_ms = a.ms;
+  *launches = a.n;
+  return 0;
+}
+
+int sdgpu_valu_probe(sdgpu_ctx* c, double* lane_ops_per_s) {
+  if (!c || !lane_ops_per_s) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY_RC(ensure_dev(c, c->io_b, 1 << 20));
+  hipEvent_t a, b;
+  SD_TRY(hipEventCreate(&a));
+  SD_TRY(hipEventCreate(&b));
+  const uint32_t iters = 4096, blocks = 256 * 8 * 4;  // 32 waves per CU
+  uint32_t* sink = static_cast<uint32_t*>(c->io_b.p);
+  SD_TRY(valu_probe_launch(sink, 64, blocks, c->stream));  // warm
+  SD_TRY(hipEventRecord(a, c->stream));
+  SD_TRY(valu_probe_launch(sink, iters, blocks, c->stream));
+  SD_TRY(hipEventRecord(b, c->stream));
+  SD_TRY(hipEventSynchronize(b));
+  float ms = 0;
+  SD_TRY(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  // per iteration per chain: add3, xor, alignbit, add3, xor, alignbit = 6 VALU
+  const double ops = double(iters) * 8 * 6 * blocks * 256;
+  *lane_ops_per_s = ops / (ms * 1e-3);
+  return 0;
+}
+
+int sdgpu_synth_dedup_rows_device(sdgpu_ctx* c, uint64_t seed, uint64_t total_rows,
+                                  uint64_t distinct, uint64_t first_rank, uint64_t n,
+                                  uint64_t* d_key, uint8_t* d_has_key, uint32_t* d_rank,
+                                  void* stream) {
+  if (!c || distinct == 0 || distinct > total_rows || first_rank + n > total_rows ||
+      total_rows >= (1ull << 32) || (n && (!d_key || !d_has_key || !d_rank)))
+    return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY(synth_dedup_rows_launch(seed, total_rows, distinct, first_rank, n, d_key, d_has_key,
+                                 d_rank, pick(c, stream)));
+  return 0;
+}
+
+}  // extern "C"

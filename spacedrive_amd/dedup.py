@@ -1,0 +1,152 @@
+"""cas_id -> Object grouping (K4-K6), one GPU or sharded over a node.
+
+Replaces the grouping half of identifier_job_step
+(/root/reference/core/src/object/file_identifier/mod.rs:136-333) with the
+canonical rule of SURVEY.md §8 a6 (see include/sdgpu.h, sdgpu_dedup):
+rep[r] = r for rows without a key and for rows in the chunk of their key's
+lowest-rank row f; rep[r] = f otherwise.
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL/xGMI): rows are
+hash-partitioned by the top 8 bits of the cas key (256 shards, shard s owned
+by rank s*W//256), exchanged with ONE all-to-all of (key, rank), grouped locally
+(the chunk rule only needs the global rank carried in the payload) and the
+representatives return with a second all-to-all.  The exchange logic below is
+backend-agnostic (`ops`), so it is tested with gloo on CPU; the product ops are
+the HIP kernels of libsdgpu.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from ._native import check, default_context
+
+CHUNK_SIZE = 100  # file_identifier/mod.rs:36
+
+
+def group_reps(key, has_key, chunk_rows: int = CHUNK_SIZE, ctx=None) -> np.ndarray:
+    """rep (uint32, ranks) for rows in rank order; host arrays, one GPU."""
+    ctx = ctx or default_context()
+    key = np.ascontiguousarray(key, np.uint64)
+    has_key = np.ascontiguousarray(has_key, np.uint8)
+    rep = np.zeros(key.size, np.uint32)
+    check(ctx.lib.sdgpu_dedup(ctx.h, key.ctypes.data, has_key.ctypes.data, key.size, chunk_rows,
+                              rep.ctypes.data), "sdgpu_dedup")
+    return rep
+
+
+class HipOps:
+    """Local steps of the sharded dedup on device tensors (libsdgpu kernels)."""
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx
+
+    def _c(self, t):
+        return self.ctx or default_context(t.device.index)
+
+    @staticmethod
+    def _s(t):
+        import torch
+        return torch.cuda.current_stream(t.device).cuda_stream
+
+    def shard_counts(self, key, has_key, shard_bits: int) -> np.ndarray:
+        import ctypes
+        ctx = self._c(key)
+        counts = (ctypes.c_uint64 * (1 << shard_bits))()
+        check(ctx.lib.sdgpu_shard_count_device(ctx.h, key.data_ptr(), has_key.data_ptr(),
+                                               key.numel(), shard_bits, counts, self._s(key)),
+              "sdgpu_shard_count_device")
+        return np.array(counts[:], dtype=np.int64)
+
+    def partition(self, key, has_key, rank, shard_bits: int, total: int):
+        import torch
+        ctx = self._c(key)
+        okey = torch.empty(total, dtype=torch.int64, device=key.device)
+        orank = torch.empty(total, dtype=torch.int32, device=key.device)
+        opos = torch.empty(total, dtype=torch.int32, device=key.device)
+        check(ctx.lib.sdgpu_shard_partition_device(
+            ctx.h, key.data_ptr(), has_key.data_ptr(), rank.data_ptr() if rank is not None else None,
+            key.numel(), shard_bits, okey.data_ptr(), orank.data_ptr(), opos.data_ptr(),
+            self._s(key)), "sdgpu_shard_partition_device")
+        return okey, orank, opos
+
+    def group(self, key, rank, chunk_rows: int, skip_bits: int):
+        import torch
+        ctx = self._c(key)
+        rep = torch.empty(key.numel(), dtype=torch.int32, device=key.device)
+        if key.numel():
+            check(ctx.lib.sdgpu_group_pairs_device(ctx.h, key.data_ptr(), rank.data_ptr(),
+                                                   key.numel(), chunk_rows, skip_bits,
+                                                   rep.data_ptr(), self._s(key)),
+                  "sdgpu_group_pairs_device")
+        return rep
+
+    def scatter(self, src, pos, n: int, init):
+        import torch
+        ctx = self._c(src)
+        out = torch.empty(n, dtype=torch.int32, device=src.device)
+        check(ctx.lib.sdgpu_scatter_rep_device(
+            ctx.h, src.data_ptr(), pos.data_ptr(), src.numel(), out.data_ptr(), n,
+            init.data_ptr() if init is not None else None, 1, self._s(src)),
+            "sdgpu_scatter_rep_device")
+        return out
+
+
+def shard_plan(world: int):
+    """(shard_bits, owner-of-shard array, skip_bits) for `world` ranks."""
+    if world <= 1:
+        return 0, np.zeros(1, np.int64), 0
+    bits = 8
+    owner = (np.arange(1 << bits, dtype=np.int64) * world) >> bits
+    skip = int(math.floor(math.log2(world)))
+    return bits, owner, skip
+
+
+def sharded_group_reps(key, has_key, rank, chunk_rows: int = CHUNK_SIZE, group=None, ops=None,
+                       timings: dict | None = None):
+    """Grouping of this rank's rows against the rows of every rank in `group`.
+
+    key: int64 tensor (u64 cas keys), has_key: uint8, rank: int32 (global
+    ranks, u32).  Returns int32 rep (global ranks) for this rank's rows.
+    Collective: every rank of `group` must call it."""
+    import torch
+    import torch.distributed as dist
+    ops = ops or HipOps()
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    n = key.numel()
+    bits, owner, skip = shard_plan(world)
+    counts = ops.shard_counts(key, has_key, bits)
+    send_counts = np.bincount(owner, weights=counts, minlength=world).astype(np.int64)
+    total = int(send_counts.sum())
+    skey, srank, spos = ops.partition(key, has_key, rank, bits, total)
+    if world == 1:
+        rep_sent = ops.group(skey, srank, chunk_rows, 0)
+        return ops.scatter(rep_sent, spos, n, rank)
+    dev = key.device
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = rc.cpu().numpy().astype(np.int64)
+    m = int(recv_counts.sum())
+    s_list, r_list = send_counts.tolist(), recv_counts.tolist()
+    rkey = torch.empty(m, dtype=torch.int64, device=dev)
+    rrank = torch.empty(m, dtype=torch.int32, device=dev)
+    dist.all_to_all_single(rkey, skey, r_list, s_list, group=group)
+    dist.all_to_all_single(rrank, srank, r_list, s_list, group=group)
+    rrep = ops.group(rkey, rrank, chunk_rows, skip)
+    rep_sent = torch.empty(total, dtype=torch.int32, device=dev)
+    dist.all_to_all_single(rep_sent, rrep, s_list, r_list, group=group)
+    return ops.scatter(rep_sent, spos, n, rank)
+
+
+def object_stats(rep: np.ndarray, has_key: np.ndarray, ok: np.ndarray | None = None):
+    """(created, linked) Object counts the reference's job would report
+    (identifier_job_step returns (total_created, updated_file_paths.len()),
+    mod.rs:335): a row whose rep is itself creates an Object; others link."""
+    rep = np.asarray(rep, np.int64)
+    r = np.arange(rep.size, dtype=np.int64)
+    valid = np.ones(rep.size, bool) if ok is None else np.asarray(ok, bool)
+    created = int(np.count_nonzero((rep == r) & valid))
+    linked = int(np.count_nonzero((rep != r) & valid))
+    return created, linked

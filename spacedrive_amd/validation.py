@@ -1,0 +1,72 @@
+"""Object validator checksum -- host mirror of core/src/object/validation/hash.rs.
+
+* ``file_checksum(path) -> str`` (hash.rs:10-24): 64 lowercase hex chars of the
+  full-file BLAKE3; raises OSError like the reference's io::Error.
+  The file is streamed in 64 MiB power-of-two slices (64 of the reference's
+  1 MiB BLOCK_LEN reads) through double-buffered pinned memory; every slice is
+  hashed by the tree kernels K2/K3 (csrc/b3_tree.hip) and the slice chaining
+  values are folded on the GPU.
+* ``checksum_bytes(buf)``, ``checksum_batch_device(tensors)`` for in-memory and
+  device-resident data (the object-validator bench, BASELINE config 3).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from ._native import SdgpuError, check, default_context
+
+BLOCK_LEN = 1048576  # hash.rs:8
+
+
+def file_checksum(path, ctx=None) -> str:
+    """Drop-in for `file_checksum(path)` (hash.rs:10)."""
+    ctx = ctx or default_context()
+    out = ctypes.create_string_buffer(65)
+    rc = ctx.lib.sdgpu_file_checksum(ctx.h, os.fsencode(os.fspath(path)), out)
+    if rc:
+        raise SdgpuError(rc, os.fspath(path))
+    return out.value.decode()
+
+
+def checksum_bytes(data, ctx=None) -> bytes:
+    """BLAKE3 digest (32 bytes) of a host buffer, computed on the GPU."""
+    ctx = ctx or default_context()
+    a = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else \
+        np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    out = np.zeros(32, np.uint8)
+    check(ctx.lib.sdgpu_checksum(ctx.h, a.ctypes.data if a.size else None, a.size, out.ctypes.data),
+          "sdgpu_checksum")
+    return out.tobytes()
+
+
+def checksum_batch_device(files, out=None, ctx=None, stream=None):
+    """Digests of device-resident files (list of 1-D uint8 torch tensors,
+    16-byte aligned) -> uint8 tensor [n, 32]; asynchronous on `stream`."""
+    import torch
+    n = len(files)
+    dev = files[0].device
+    ctx = ctx or default_context(dev.index)
+    if out is None:
+        out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    ptrs = (ctypes.c_uint64 * n)(*[f.data_ptr() for f in files])
+    lens = (ctypes.c_uint64 * n)(*[f.numel() for f in files])
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    check(ctx.lib.sdgpu_checksum_batch_device(ctx.h, ptrs, lens, n, out.data_ptr(), s),
+          "sdgpu_checksum_batch_device")
+    return out
+
+
+def subtree_device(data, chunk_offset: int, root: bool, out=None, ctx=None, stream=None):
+    """Chaining value (root=False) or digest (root=True) of an aligned slice."""
+    import torch
+    ctx = ctx or default_context(data.device.index)
+    if out is None:
+        out = torch.empty(32, dtype=torch.uint8, device=data.device)
+    s = stream if stream is not None else torch.cuda.current_stream(data.device).cuda_stream
+    check(ctx.lib.sdgpu_subtree_device(ctx.h, data.data_ptr(), data.numel(), int(chunk_offset),
+                                       1 if root else 0, out.data_ptr(), s),
+          "sdgpu_subtree_device")
+    return out

@@ -1,0 +1,56 @@
+"""CPU: the C-ABI library loads and exports every symbol include/sdgpu.h
+declares; no compute calls (there is no GPU here)."""
+import ctypes
+import subprocess
+
+from spacedrive_amd import _native
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.load()
+    declared = _native.declared_symbols()
+    assert len(declared) >= 25
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert set(declared) <= exported
+
+
+def test_abi_version_and_strerror():
+    lib = _native.load()
+    assert lib.sdgpu_abi_version() == 1
+    assert lib.sdgpu_strerror(0) == b"success"
+    assert lib.sdgpu_strerror(-22) == b"Invalid argument"
+
+
+def test_null_arguments_rejected_without_device():
+    lib = _native.load()
+    assert lib.sdgpu_open(0, None) == -22
+    assert lib.sdgpu_close(None) == -22
+    assert lib.sdgpu_cas_batch(None, None, None, None, 0, None, None) == -22
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list",
+                          "--type=o", f"--input={_native.LIB_PATH}"],
+                         capture_output=True, text=True)
+    # fall back to strings if the bundler cannot read a linked .so
+    text = out.stdout + subprocess.run(["strings", _native.LIB_PATH], capture_output=True,
+                                       text=True).stdout
+    assert "gfx950" in text
+
+
+def test_product_path_has_no_oracle_dependency():
+    """The product package must not import or link the CPU oracle."""
+    import pathlib
+    pkg = pathlib.Path(_native.__file__).parent
+    for f in list(pkg.glob("*.py")) + list(pkg.glob("csrc/*")):
+        text = f.read_text(errors="ignore")
+        assert "from oracle" not in text and "import oracle" not in text, f
+        assert "liboracle" not in text and "sd_oracle" not in text.replace(
+            "oracle/sd_oracle.c", ""), f
+    out = subprocess.run(["ldd", _native.LIB_PATH], capture_output=True, text=True).stdout
+    assert "liboracle" not in out
+    assert ctypes.CDLL(_native.LIB_PATH)

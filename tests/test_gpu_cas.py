@@ -1,0 +1,117 @@
+"""GPU parity: K1 (sampled cas_id) against the CPU oracle, bit-exact."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _host_batch(ctx, sizes, seeds):
+    from spacedrive_amd import cas
+    arena, off, ln = O.synth_arena(np.array(sizes, np.uint64), np.array(seeds, np.uint64))
+    out, st = cas.cas_batch(arena, off, ln, ctx)
+    return arena, off, ln, out, st
+
+
+def test_golden_cas_ids_host_api(ctx, golden):
+    from spacedrive_amd import cas
+    e = golden["cas_synthetic"]
+    _, _, _, out, st = _host_batch(ctx, [x["size"] for x in e], [x["seed"] for x in e])
+    assert np.all(st == 0)
+    assert cas.hex_ids(out) == [x["cas_id"] for x in e]
+
+
+def test_every_message_length_up_to_3_chunks(ctx):
+    """Arbitrary messages of every length 0..3100 (all block/chunk tails)."""
+    from spacedrive_amd import cas
+    lens = np.arange(0, 3101, dtype=np.uint32)
+    off = np.zeros(lens.size, np.uint64)
+    pos = 0
+    for i, n in enumerate(lens):
+        off[i] = pos
+        pos += (int(n) + 15) // 16 * 16
+    rng = np.random.default_rng(1)
+    arena = rng.integers(0, 256, pos + 16, dtype=np.uint8)
+    out, st = cas.cas_batch(arena, off, lens, ctx)
+    assert np.all(st == 0)
+    ref = O.cas_batch(arena, off, lens, threads=8)
+    np.testing.assert_array_equal(out, ref)
+
+
+def test_invalid_messages_rejected(ctx):
+    from spacedrive_amd import cas
+    arena = np.zeros(300_000, np.uint8)
+    off = np.array([0, 0, 16, 32], np.uint64)
+    ln = np.array([102408, 102409, 10, 200_000], np.uint32)
+    out, st = cas.cas_batch(arena, off, ln, ctx)
+    assert st.tolist() == [0, -22, 0, -22]
+    assert not out[1].any() and not out[3].any()
+    assert bytes(out[0]).hex() == O.cas_id_of_message(bytes(102408))
+
+
+def test_device_api_misaligned_offset_status(ctx):
+    import torch
+    from spacedrive_amd import cas
+    arena = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    off = torch.tensor([0, 8, 1024], dtype=torch.int64, device="cuda")
+    ln = torch.tensor([100, 100, 100], dtype=torch.int32, device="cuda")
+    out, st = cas.cas_batch_device(arena, off, ln, ctx=ctx)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [0, -22, 0]
+    assert bytes(out[0].cpu().numpy()).hex() == O.cas_id_of_message(bytes(100))
+
+
+def test_device_synth_arena_matches_oracle_bytes(ctx):
+    import torch
+    from spacedrive_amd import corpus
+    sizes, seeds = corpus.config2_files(3000, seed=9)
+    d_arena, d_off, d_len = corpus.synth_arena_device(sizes, seeds, ctx=ctx)
+    torch.cuda.synchronize()
+    arena, off, ln = O.synth_arena(sizes, seeds)
+    h = d_arena.cpu().numpy()
+    for i in range(sizes.size):
+        a, b = int(off[i]), int(off[i]) + int(ln[i])
+        assert np.array_equal(h[a:b], arena[a:b]), i
+
+
+def test_random_config2_subset_device_api(ctx):
+    import torch
+    from spacedrive_amd import cas, corpus
+    sizes, seeds = corpus.config2_files(50_000, seed=21)
+    d_arena, d_off, d_len = corpus.synth_arena_device(sizes, seeds, ctx=ctx)
+    out, st = cas.cas_batch_device(d_arena, d_off, d_len, ctx=ctx)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0
+    ref = O.cas_batch(d_arena.cpu().numpy(), d_off.cpu().numpy().view(np.uint64),
+                      d_len.cpu().numpy().view(np.uint32), threads=16)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+def test_full_config2_one_million_files_bit_exact(ctx):
+    """BASELINE config 2 at full size: 1 M files, every cas_id vs the oracle."""
+    import torch
+    from spacedrive_amd import cas, corpus
+    sizes, seeds = corpus.config2_files(1_000_000, seed=2)
+    d_arena, d_off, d_len = corpus.synth_arena_device(sizes, seeds, ctx=ctx)
+    out, st = cas.cas_batch_device(d_arena, d_off, d_len, ctx=ctx)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0
+    got = out.cpu().numpy()
+    host = d_arena.cpu().numpy()
+    del d_arena
+    ref = O.cas_batch(host, d_off.cpu().numpy().view(np.uint64),
+                      d_len.cpu().numpy().view(np.uint32), threads=16)
+    mism = np.flatnonzero(np.any(got != ref, axis=1))
+    assert mism.size == 0, f"{mism.size} mismatching cas ids, first rows {mism[:5]}"
+    # duplicates (same size+seed) must share a cas id, distinct content must not collide
+    keys = cas.keys_of(got)
+    pair = sizes * np.uint64(0x9E3779B97F4A7C15) ^ seeds
+    assert np.unique(keys).size == np.unique(pair).size
+
+
+def test_zero_files(ctx):
+    from spacedrive_amd import cas
+    out, st = cas.cas_batch(np.zeros(16, np.uint8), np.zeros(0, np.uint64),
+                            np.zeros(0, np.uint32), ctx)
+    assert out.shape == (0, 8)

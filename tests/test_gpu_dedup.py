@@ -1,0 +1,67 @@
+"""GPU parity: K4-K6 grouping against the oracle's canonical rule."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def test_golden_grouping_fixture(ctx):
+    from spacedrive_amd import dedup
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "grouping_10k.npz"))
+    rep = dedup.group_reps(z["key"], z["has_key"], int(z["chunk_rows"][0]), ctx)
+    np.testing.assert_array_equal(rep, z["rep"])
+
+
+@pytest.mark.parametrize("n,pool", [(0, 1), (1, 1), (2, 1), (1000, 10), (200_000, 150_000),
+                                    (1_000_000, 900_000), (300_000, 1), (500_000, 7)])
+def test_random_vs_oracle(ctx, n, pool):
+    """Includes buckets far beyond the LDS table (one key 300k times: the
+    global-table path) and a sentinel-valued key."""
+    from spacedrive_amd import dedup
+    rng = np.random.default_rng(n + pool)
+    keys = rng.integers(0, 2**64 - 1, max(pool, 1), dtype=np.uint64, endpoint=True)
+    keys[0] = np.uint64(2**64 - 1)
+    key = keys[rng.integers(0, keys.size, n)] if n else np.zeros(0, np.uint64)
+    has = (rng.random(n) > 0.01).astype(np.uint8)
+    for chunk in (100, 1, 7):
+        rep = dedup.group_reps(key, has, chunk, ctx)
+        np.testing.assert_array_equal(rep, O.group_reps(key, has, chunk))
+
+
+def test_skip_bits_shard(ctx):
+    """Keys of one shard of an 8-GPU partition (top 3 bits constant)."""
+    import torch
+    rng = np.random.default_rng(3)
+    n = 400_000
+    key = rng.integers(0, 2**61, n, dtype=np.uint64) | np.uint64(5 << 61)
+    key[rng.integers(0, n, n // 5)] = key[rng.integers(0, n, n // 5)]
+    rank = rng.permutation(n).astype(np.uint32)
+    from spacedrive_amd import dedup
+    ops = dedup.HipOps(ctx)
+    dk = torch.from_numpy(key.view(np.int64)).cuda()
+    dr = torch.from_numpy(rank.view(np.int32)).cuda()
+    rep = ops.group(dk, dr, 100, 3).cpu().numpy().view(np.uint32)
+    # oracle: rows in rank order
+    order = np.argsort(rank)
+    ref_rank_order = O.group_reps(key[order], np.ones(n, np.uint8), 100)
+    np.testing.assert_array_equal(rep[order], ref_rank_order)
+
+
+def test_config4_shape_single_gpu(ctx):
+    """12.5 M rows of the config-4 table (one GPU's share at 8 GPUs)."""
+    import torch
+    from spacedrive_amd import corpus, dedup
+    total = 12_500_000
+    key, has, rank = corpus.synth_dedup_rows_device(4, total, int(total * 0.8), 0, total, ctx=ctx)
+    rep = dedup.sharded_group_reps(key, has, rank, 100, ops=dedup.HipOps(ctx))
+    torch.cuda.synchronize()
+    hk = key.cpu().numpy().view(np.uint64)
+    hh = has.cpu().numpy()
+    k2, h2, _ = O.synth_dedup_rows(4, total, int(total * 0.8), 0, 200_000)
+    np.testing.assert_array_equal(hk[:200_000], k2)
+    np.testing.assert_array_equal(hh[:200_000], h2)
+    np.testing.assert_array_equal(rep.cpu().numpy().view(np.uint32), O.group_reps(hk, hh, 100))

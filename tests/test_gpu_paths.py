@@ -1,0 +1,95 @@
+"""GPU parity of the path-based drop-ins (generate_cas_id(path, size),
+file_checksum(path), the batched identifier) against the oracle's path-based
+restatement of the reference I/O pattern."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [0, 1, 57, 1024, 1025, 8192, 102399, 102400, 102401, 200_000, 1 << 20, 3_333_333]
+
+
+@pytest.fixture()
+def files(tmp_path):
+    paths = []
+    for i, s in enumerate(SIZES):
+        p = tmp_path / f"file_{i}.bin"
+        p.write_bytes(O.synth_file_bytes(900 + i, 0, s))
+        paths.append(str(p))
+    return paths
+
+
+def test_generate_cas_id_path(ctx, files):
+    from spacedrive_amd import cas
+    for p, s in zip(files, SIZES):
+        assert cas.generate_cas_id(p, s, ctx) == O.cas_id_path(p, s)
+
+
+def test_generate_cas_id_errors(ctx, tmp_path):
+    from spacedrive_amd import cas
+    with pytest.raises(OSError) as ei:
+        cas.generate_cas_id(tmp_path / "missing", 10, ctx)
+    assert ei.value.errno == 2
+    short = tmp_path / "short"
+    short.write_bytes(bytes(50_000))
+    with pytest.raises(OSError) as ei:  # read_exact past EOF: UnexpectedEof
+        cas.generate_cas_id(short, 400_000, ctx)
+    assert ei.value.errno == 61  # ENODATA
+    with pytest.raises(OSError):
+        O.cas_id_path(str(short), 400_000)
+
+
+def test_identify_batch_and_job(ctx, files, tmp_path):
+    from spacedrive_amd import file_identifier as fi
+    dup = tmp_path / "dup.bin"
+    dup.write_bytes(open(files[9], "rb").read())
+    paths = files + [str(dup), str(tmp_path / "gone"), files[9]]
+    res = fi.identify(paths, ctx=ctx)
+    for i, p in enumerate(paths):
+        if not os.path.exists(p):
+            assert res.status[i] == -2 and res.has_key[i] == 0
+            continue
+        s = os.path.getsize(p)
+        if s == 0:
+            assert res.has_key[i] == 0 and res.status[i] == 0
+        else:
+            assert res.has_key[i] == 1
+            assert bytes(res.cas8[i]).hex() == O.cas_id_path(p, s)
+    job = fi.identifier_job(paths, ctx=ctx)
+    ok = (job.identify.status == 0).astype(np.uint8)
+    from spacedrive_amd.cas import keys_of
+    ref = O.group_reps(keys_of(job.identify.cas8), job.identify.has_key & ok, 100)
+    np.testing.assert_array_equal(job.rep, ref)
+    assert job.rep[len(files)] == 9 and job.rep[-1] == 9  # duplicates link to row 9
+
+
+def test_identify_many_files_pipelined(ctx, tmp_path):
+    """More files than one staging slab's file budget is not needed; 3000
+    files of mixed sizes exercise the threaded pread + H2D pipeline."""
+    from spacedrive_amd import corpus
+    from spacedrive_amd import file_identifier as fi
+    sizes, seeds = corpus.config2_files(3000, seed=5)
+    sizes = np.minimum(sizes, 3_000_000)
+    paths = []
+    for i in range(sizes.size):
+        p = tmp_path / f"m{i}"
+        with open(p, "wb") as f:
+            f.write(O.synth_file_bytes(int(seeds[i]), 0, int(sizes[i])))
+        paths.append(str(p))
+    res = fi.identify(paths, sizes=sizes, ctx=ctx)
+    assert np.all(res.status == 0)
+    for i in range(0, sizes.size, 7):
+        if sizes[i]:
+            assert bytes(res.cas8[i]).hex() == O.cas_id_of_message(
+                O.synth_cas_message(int(sizes[i]), int(seeds[i])))
+
+
+def test_file_metadata(ctx, files):
+    from spacedrive_amd import file_identifier as fi
+    m = fi.file_metadata(os.path.dirname(files[5]), os.path.basename(files[5]), ctx)
+    assert m.cas_id == O.cas_id_path(files[5], SIZES[5]) and m.size == SIZES[5]
+    assert fi.file_metadata(os.path.dirname(files[0]), os.path.basename(files[0]), ctx).cas_id is None

@@ -1,0 +1,161 @@
+"""CPU: the oracle itself -- pinned by the reference KAT, two independent
+restatements agreeing, the cas.rs message semantics and the grouping rule."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import blake3_py as P
+from oracle import oracle as O
+from tests.golden.make_golden import KAT_CONTEXT, KAT_EXPECTED, KAT_MATERIAL, pattern
+
+
+def test_reference_derive_key_kat(golden):
+    # /root/reference/crates/crypto/src/keys/hashing.rs:324-327 (derive_b3)
+    assert golden["derive_key_kat"]["expected_hex"] == KAT_EXPECTED.hex()
+    assert O.derive_key(KAT_CONTEXT, KAT_MATERIAL) == KAT_EXPECTED
+    assert P.derive_key(KAT_CONTEXT, KAT_MATERIAL) == KAT_EXPECTED
+
+
+def test_empty_input_spec_value():
+    h = "af1349b9f5f9a1a6a0404dea36dcc9499bcb25c9adc112b7cc9a93cae41f3262"
+    assert O.blake3(b"").hex() == h
+    assert P.blake3(b"").hex() == h
+
+
+def test_golden_pattern_hashes(golden):
+    for n, h in golden["blake3_pattern"].items():
+        d = pattern(int(n))
+        assert O.blake3(d).hex() == h
+        if int(n) <= 8192:
+            assert P.blake3(d).hex() == h
+
+
+@pytest.mark.parametrize("n", [0, 1, 64, 1024, 1025, 2048, 3 * 1024 + 1, 17 * 1024, 33 * 1024 + 7,
+                               100 * 1024 + 8, 131072, 300_001])
+def test_tree_shapes_agree(n):
+    """Recursive (C), incremental stack (C, odd update sizes), multi-threaded
+    subtree split (C) and incremental (python) must agree."""
+    rng = np.random.default_rng(n)
+    d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    ref = O.blake3(d)
+    assert O.blake3_incremental(d, 777) == ref
+    assert O.blake3_incremental(d, 1 << 20) == ref
+    assert O.blake3(d, threads=4) == ref
+    if n <= 40_000:
+        assert P.blake3(d) == ref
+
+
+def test_keyed_hash_agrees():
+    key = bytes(range(32))
+    d = pattern(5000)
+    assert O.keyed_hash(key, d) == P.keyed_hash(key, d)
+
+
+def test_cas_message_layout_small_and_sampled():
+    size = 250_000
+    fb = O.synth_file_bytes(7, 0, size)
+    msg = O.cas_build_message(fb, size)
+    assert len(msg) == 57352
+    assert msg[:8] == size.to_bytes(8, "little")
+    jump = (size - 16384) // 4
+    assert msg[8:8 + 8192] == fb[:8192]
+    for k in range(4):
+        o = 8192 + k * jump
+        assert msg[8 + 8192 + k * 10240: 8 + 8192 + (k + 1) * 10240] == fb[o:o + 10240]
+    assert msg[-8192:] == fb[-8192:]
+    # synthetic message builder == message built from the whole file
+    assert O.synth_cas_message(size, 7) == msg
+    small = O.synth_file_bytes(9, 0, 5000)
+    assert O.cas_build_message(small) == (5000).to_bytes(8, "little") + small
+
+
+def test_cas_size_argument_semantics():
+    """The samples use the passed size (cas.rs:41) but the footer the ACTUAL
+    end (SeekFrom::End, cas.rs:54); a file shorter than a sample read fails
+    with UnexpectedEof (read_exact)."""
+    fb = O.synth_file_bytes(11, 0, 300_000)
+    a = O.cas_id_of_file_bytes(fb, 300_000)
+    b = O.cas_id_of_file_bytes(fb, 290_000)  # stale stat size: different samples
+    assert a != b
+    assert P.cas_id_of_file_bytes(fb, 290_000) == b
+    with pytest.raises(EOFError):
+        O.cas_id_of_file_bytes(fb[:120_000], 400_000)
+
+
+def test_golden_cas_ids(golden):
+    for e in golden["cas_synthetic"]:
+        msg = O.synth_cas_message(e["size"], e["seed"])
+        assert len(msg) == e["msg_len"]
+        assert O.cas_id_of_message(msg) == e["cas_id"]
+
+
+def test_path_oracle_matches_memory_oracle(tmp_path):
+    for i, size in enumerate([0, 1, 1024, 102400, 102401, 250_000, 1_000_003]):
+        p = tmp_path / f"f{i}"
+        data = O.synth_file_bytes(100 + i, 0, size)
+        p.write_bytes(data)
+        assert O.cas_id_path(str(p), size) == O.cas_id_of_file_bytes(data, size)
+        assert O.file_checksum_path(str(p)) == O.blake3(data).hex()
+    with pytest.raises(FileNotFoundError):
+        O.cas_id_path(str(tmp_path / "missing"), 10)
+
+
+def test_golden_checksums(golden):
+    for e in golden["checksum_synthetic"]:
+        data = O.synth_file_bytes(e["seed"], 0, e["len"])
+        assert O.blake3(data).hex() == e["checksum"]
+
+
+def test_grouping_fixture():
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "grouping_10k.npz"))
+    rep = O.group_reps(z["key"], z["has_key"], int(z["chunk_rows"][0]))
+    np.testing.assert_array_equal(rep, z["rep"])
+    # k0 > 1 cases exist: a key first seen several times inside one chunk
+    key, has = z["key"], z["has_key"]
+    assert np.count_nonzero((z["rep"] == np.arange(key.size)) & (has == 1)) > 1500
+
+
+def test_grouping_rule_properties():
+    rng = np.random.default_rng(5)
+    n = 50_000
+    key = rng.integers(0, 3000, n).astype(np.uint64)
+    has = (rng.random(n) > 0.05).astype(np.uint8)
+    rep = O.group_reps(key, has, 100).astype(np.int64)
+    r = np.arange(n)
+    assert np.all(rep <= r)                      # representative never later
+    assert np.all(rep[rep] == rep)               # idempotent
+    assert np.all(key[rep] == key)               # same key
+    assert np.all(rep[has == 0] == r[has == 0])  # keyless rows are singletons
+
+
+def test_synth_arena_layout_matches_corpus_layout():
+    from spacedrive_amd import corpus
+    sizes, seeds = corpus.config2_files(2000, seed=3)
+    arena, off, ln = O.synth_arena(sizes, seeds)
+    off2, ln2, total = corpus.arena_layout(sizes)
+    np.testing.assert_array_equal(off, off2)
+    np.testing.assert_array_equal(ln, ln2)
+    for i in range(0, 2000, 97):
+        m = O.synth_cas_message(int(sizes[i]), int(seeds[i]))
+        assert arena[int(off[i]):int(off[i]) + len(m)].tobytes() == m
+
+
+def test_config2_distribution():
+    from spacedrive_amd import corpus
+    sizes, seeds = corpus.config2_files(200_000, seed=2)
+    small = np.count_nonzero(sizes <= 102400) / sizes.size
+    assert 0.55 < small < 0.62                   # ~58.7% <= 100 KiB
+    assert np.count_nonzero(sizes == 0) == 200
+    pairs = sizes.astype(np.uint64) * np.uint64(1_000_003) ^ seeds
+    uniq = np.unique(pairs).size
+    assert 0.78 < uniq / sizes.size < 0.82        # ~20% exact duplicates
+
+
+def test_dedup_corpus_rows():
+    key, has, rank = O.synth_dedup_rows(4, 100_000, 80_000, 0, 100_000)
+    np.testing.assert_array_equal(rank, np.arange(100_000, dtype=np.uint32))
+    assert np.unique(key).size == 80_000
+    assert 60 < np.count_nonzero(has == 0) < 150
+    k2, h2, r2 = O.synth_dedup_rows(4, 100_000, 80_000, 50_000, 1000)
+    np.testing.assert_array_equal(k2, key[50_000:51_000])
