@@ -83,6 +83,15 @@ def load():
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()); "
                 "there is no CPU fallback for the content-identification path")
+        # One HIP/HSA runtime per process: torch bundles its own libamdhip64
+        # (SONAME libamdhip64.so.7).  Loading torch first lets the dynamic
+        # linker bind libsdgpu's libamdhip64.so.7 dependency to that same copy;
+        # loading libsdgpu first would pull /opt/rocm's runtime and torch would
+        # then start a second HSA runtime that cannot open the device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         _proto(L)
         _lib = L
