@@ -17,7 +17,8 @@
  *    the same encoding, so a Rust caller maps them with
  *    io::Error::from_raw_os_error(-status) (FileIOError, core/src/util/error.rs:5-20).
  *  - "_device" entry points take device pointers and a hipStream_t passed as
- *    `void* stream` (NULL = the context's own stream) and return without
+ *    `void* stream` (NULL = the context's own stream, a blocking stream ordered
+ *    with the null stream) and return without
  *    synchronising; all others take host pointers and return when done.
  *  - A context is used by one host thread at a time (the reference runs one
  *    job at a time, core/src/job/manager.rs:32); its device workspace is

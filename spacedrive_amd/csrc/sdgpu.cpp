@@ -498,7 +498,9 @@ int sdgpu_open(int device, sdgpu_ctx** out) {
   sdgpu_ctx* c = new (std::nothrow) sdgpu_ctx;
   if (!c) return -ENOMEM;
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+  // A BLOCKING stream: callers that pass NULL (e.g. torch's legacy default
+  // stream, whose handle is 0) get work ordered with the null stream both ways.
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess ||
       hipEventCreateWithFlags(&c->plan_evt, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return -EIO;
