@@ -16,6 +16,7 @@
 //            (left-complete tree = BLAKE3 tree), ROOT on the last parent.
 // Every compression is done by exactly one lane: no log-depth idle tree phase.
 #include <errno.h>
+#include <stdlib.h>
 
 #include "b3_device.hpp"
 #include "internal.hpp"
@@ -56,6 +57,13 @@ __global__ __launch_bounds__(kThreads) void k_fill_map(const uint32_t* __restric
 }
 
 // One lane per chunk (grid-stride over the flattened chunk list).
+// K1 variant for A/B runs in one process (SDGPU_K1_VARIANT: 0 plain, 1 pipelined).
+int k1_variant() {
+  const char* v = getenv("SDGPU_K1_VARIANT");
+  return v ? atoi(v) : 0;
+}
+
+template <bool kPipelined>
 __global__ __launch_bounds__(kThreads) void k_chunks(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ chunk_msg,
@@ -70,8 +78,12 @@ __global__ __launch_bounds__(kThreads) void k_chunks(
     const bool single = l <= B3_CHUNK_LEN;
     const uint32_t clen = min(B3_CHUNK_LEN, l - j * B3_CHUNK_LEN);
     uint32_t cv[8];
-    b3_chunk(arena + off[m] + static_cast<uint64_t>(j) * B3_CHUNK_LEN, clen, j,
-             single ? B3_ROOT : 0u, cv);
+    if (kPipelined)
+      b3_chunk_pipelined(arena + off[m] + static_cast<uint64_t>(j) * B3_CHUNK_LEN, clen, j,
+                         single ? B3_ROOT : 0u, cv);
+    else
+      b3_chunk(arena + off[m] + static_cast<uint64_t>(j) * B3_CHUNK_LEN, clen, j,
+               single ? B3_ROOT : 0u, cv);
     if (single) {
       for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = cv[w];
     } else {
@@ -145,8 +157,12 @@ hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
   const uint32_t grid = static_cast<uint32_t>(want < 8192 ? (want ? want : 1) : 8192);
   {
     KScope k(timer, "cas_chunks", s);
-    k_chunks<<<grid, kThreads, 0, s>>>(arena, off, len, w.chunk_msg, w.chunk_base, w.total, w.cvs,
-                                       out_words, o);
+    if (k1_variant() == 1)
+      k_chunks<true><<<grid, kThreads, 0, s>>>(arena, off, len, w.chunk_msg, w.chunk_base, w.total,
+                                               w.cvs, out_words, o);
+    else
+      k_chunks<false><<<grid, kThreads, 0, s>>>(arena, off, len, w.chunk_msg, w.chunk_base,
+                                                w.total, w.cvs, out_words, o);
   }
   {
     KScope k(timer, "cas_parents", s);

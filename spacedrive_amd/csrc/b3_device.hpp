@@ -157,4 +157,28 @@ __device__ __forceinline__ void b3_chunk(const uint8_t* __restrict__ p, uint32_t
               B3_CHUNK_END | (nb == 1 ? B3_CHUNK_START : 0u) | root_flag);
 }
 
+// Same as b3_chunk, software-pipelined: the next block's 64 bytes are loaded
+// before the current block is compressed, so one wave keeps a load in flight
+// under every compression.
+__device__ __forceinline__ void b3_chunk_pipelined(const uint8_t* __restrict__ p, uint32_t clen,
+                                                   uint64_t ctr, uint32_t root_flag,
+                                                   uint32_t cv[8]) {
+  b3_iv(cv);
+  const uint32_t nb = clen == 0 ? 1u : (clen + 63u) >> 6;
+  const uint32_t last = clen - 64u * (nb - 1);
+  const uint32_t lo = static_cast<uint32_t>(ctr), hi = static_cast<uint32_t>(ctr >> 32);
+  uint32_t m[16], mn[16];
+  if (nb > 1) b3_load_block(p, m);
+  else b3_load_block_partial(p, last, m);
+  for (uint32_t b = 0; b + 1 < nb; ++b) {
+    if (b + 2 < nb) b3_load_block(p + 64u * (b + 1), mn);
+    else b3_load_block_partial(p + 64u * (b + 1), last, mn);
+    b3_compress(cv, m, lo, hi, B3_BLOCK_LEN, b == 0 ? B3_CHUNK_START : 0u);
+#pragma unroll
+    for (int w = 0; w < 16; ++w) m[w] = mn[w];
+  }
+  b3_compress(cv, m, root_flag ? 0u : lo, root_flag ? 0u : hi, last,
+              B3_CHUNK_END | (nb == 1 ? B3_CHUNK_START : 0u) | root_flag);
+}
+
 }  // namespace sdgpu
