@@ -64,7 +64,12 @@ def test_identify_batch_and_job(ctx, files, tmp_path):
     from spacedrive_amd.cas import keys_of
     ref = O.group_reps(keys_of(job.identify.cas8), job.identify.has_key & ok, 100)
     np.testing.assert_array_equal(job.rep, ref)
-    assert job.rep[len(files)] == 9 and job.rep[-1] == 9  # duplicates link to row 9
+    # all rows sit in the first 100-row chunk: each duplicate gets its own Object
+    assert job.rep[len(files)] == len(files) and job.rep[-1] == len(paths) - 1
+    # with 10-row chunks the later duplicates (rows 12, 14) link to row 9's Object
+    job10 = fi.identifier_job(paths, chunk_size=10, ctx=ctx)
+    assert job10.rep[len(files)] == 9 and job10.rep[-1] == 9
+    assert job10.linked == 2
 
 
 def test_identify_many_files_pipelined(ctx, tmp_path):
