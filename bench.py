@@ -33,7 +33,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-VALU_PEAK_SPEC = 256 * 4 * 32 * 2.4e9  # 256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz (lane-ops/s)
+# int32 VALU peak: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz.  The 32-bit integer
+# ops BLAKE3 uses (v_add3_u32, v_alignbit_b32, v_xor_b32, v_add_u32) issue a
+# wave64 in 4 cycles on gfx950 (measured: sdgpu_valu_probe ~ 33 T/s under load,
+# DESIGN.md §4); the 157 TFLOP/s FP32 figure counts packed-FMA lanes instead.
+VALU_PEAK_SPEC = 256 * 4 * 16 * 2.4e9
 HBM_PEAK = 8.0e12                       # B/s (MI355X spec)
 ISA_PER_COMPRESSION = 680               # fused VALU instructions per BLAKE3 compression
 METRIC = "cas_id files/sec + full-file BLAKE3 GB/s + dedup rows/sec at 1/2/4/8 MI355X"
@@ -240,8 +244,10 @@ def main():
     R = Runner(args)
     torch = R.torch
     valu_peak = R.ctx.valu_peak()
+    classes = {name: R.ctx.valu_peak(k) / 1e12 for k, name in
+               [(1, "v_xor_b32"), (2, "v_add3_u32"), (3, "v_alignbit_b32"), (4, "v_add_u32")]}
     log(f"measured int32 VALU peak: {valu_peak / 1e12:.1f} T lane-ops/s "
-        f"(spec {VALU_PEAK_SPEC / 1e12:.1f})")
+        f"(spec {VALU_PEAK_SPEC / 1e12:.1f}); per class {json.dumps(classes)}")
     c = R.run_cas(args.steps, args.warmup)
     log("cas:", json.dumps(c["cas"]), json.dumps(c["kernels"]))
     cpu = None
@@ -268,7 +274,7 @@ def main():
     roof = {"bound": "valu", "kernel": "cas_chunks (K1)",
             "achieved": achieved / 1e12, "peak": VALU_PEAK_SPEC / 1e12, "unit": "Tops/s",
             "frac": achieved / VALU_PEAK_SPEC, "traffic": None,
-            "peak_measured": valu_peak / 1e12,
+            "peak_measured": valu_peak / 1e12, "peak_by_class_measured": classes,
             "frac_of_measured": achieved / valu_peak if valu_peak else None,
             "algorithmic_per_launch": {"compressions": ri["chunk_blocks"],
                                        "int32_ops": ops, "window_bytes": ri["bytes"]},

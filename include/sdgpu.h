@@ -190,6 +190,9 @@ int sdgpu_timing_read(sdgpu_ctx *ctx, uint32_t idx, char name[32], double *total
 /* Measured int32 VALU issue rate (lane-ops/s) of a BLAKE3-G-shaped
  * add3/xor/alignbit stream at full occupancy: the VALU roofline's peak. */
 int sdgpu_valu_probe(sdgpu_ctx *ctx, double *lane_ops_per_s);
+/* Same for one instruction class: 0 the G mix above, 1 v_xor_b32, 2 v_add3_u32,
+ * 3 v_alignbit_b32, 4 v_add_u32. */
+int sdgpu_valu_probe_kind(sdgpu_ctx *ctx, int kind, double *lane_ops_per_s);
 
 #ifdef __cplusplus
 }

@@ -68,6 +68,7 @@ def _proto(L):
         "sdgpu_timing_read": (i32, [ctx, u32, ctypes.c_char_p, P(ctypes.c_double),
                                     P(ctypes.c_uint64)]),
         "sdgpu_valu_probe": (i32, [ctx, P(ctypes.c_double)]),
+        "sdgpu_valu_probe_kind": (i32, [ctx, i32, P(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -163,10 +164,11 @@ class Context:
             i += 1
         return res
 
-    def valu_peak(self) -> float:
-        """Measured int32 VALU lane-ops/s (BLAKE3-shaped instruction mix)."""
+    def valu_peak(self, kind: int = 0) -> float:
+        """Measured int32 VALU lane-ops/s: kind 0 = BLAKE3-G instruction mix,
+        1 v_xor_b32, 2 v_add3_u32, 3 v_alignbit_b32, 4 v_add_u32."""
         v = ctypes.c_double()
-        check(self.lib.sdgpu_valu_probe(self.h, ctypes.byref(v)), "sdgpu_valu_probe")
+        check(self.lib.sdgpu_valu_probe_kind(self.h, kind, ctypes.byref(v)), "sdgpu_valu_probe")
         return v.value
 
 

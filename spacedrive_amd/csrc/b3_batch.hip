@@ -106,27 +106,96 @@ __device__ __forceinline__ void store_cv(uint32_t* p, const uint32_t cv[8]) {
   reinterpret_cast<uint4*>(p)[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
 }
 
+// Parent lanes are ordered by chunk count (descending) so that the 64 lanes of
+// a wave fold equally long trees: bin = 127 - min(n_chunks, 127), messages
+// with fewer than 2 chunks are left out.  Block-aggregated counting sort.
+constexpr uint32_t kBins = 128;
+
+__device__ __forceinline__ uint32_t parent_bin(uint32_t nch) {
+  return kBins - 1 - min(nch, kBins - 1);
+}
+
+__global__ __launch_bounds__(kThreads) void k_bin_hist(const uint32_t* __restrict__ n_chunks,
+                                                       uint32_t n, uint32_t* __restrict__ bins) {
+  __shared__ uint32_t h[kBins];
+  if (threadIdx.x < kBins) h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+    const uint32_t c = n_chunks[i];
+    if (c >= 2) atomicAdd(&h[parent_bin(c)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kBins && h[threadIdx.x]) atomicAdd(&bins[threadIdx.x], h[threadIdx.x]);
+}
+
+// bins[0..kBins) -> exclusive offsets (used as cursors), bins[kBins] = total.
+__global__ void k_bin_scan(uint32_t* __restrict__ bins) {
+  if (threadIdx.x != 0) return;
+  uint32_t run = 0;
+  for (uint32_t b = 0; b < kBins; ++b) {
+    const uint32_t v = bins[b];
+    bins[b] = run;
+    run += v;
+  }
+  bins[kBins] = run;
+}
+
+__global__ __launch_bounds__(kThreads) void k_bin_scatter(const uint32_t* __restrict__ n_chunks,
+                                                          uint32_t n, uint32_t* __restrict__ bins,
+                                                          uint32_t* __restrict__ order) {
+  __shared__ uint32_t h[kBins], base[kBins];
+  for (uint32_t i0 = blockIdx.x * kThreads; i0 < n; i0 += gridDim.x * kThreads) {
+    if (threadIdx.x < kBins) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = i0 + threadIdx.x;
+    const uint32_t c = i < n ? n_chunks[i] : 0u;
+    uint32_t local = 0, b = 0;
+    if (c >= 2) {
+      b = parent_bin(c);
+      local = atomicAdd(&h[b], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < kBins && h[threadIdx.x])
+      base[threadIdx.x] = atomicAdd(&bins[threadIdx.x], h[threadIdx.x]);
+    __syncthreads();
+    if (c >= 2) order[base[b] + local] = i;
+    __syncthreads();
+  }
+}
+
 // One lane per multi-chunk message: pairwise fold of its chunk CVs, in place.
 // Pairwise merging with the odd node carried up builds exactly BLAKE3's
-// left-complete tree; the last merge (two nodes left) carries ROOT.
+// left-complete tree; the last merge (two nodes left) carries ROOT.  The next
+// pair is loaded before the current one is compressed.
 __global__ __launch_bounds__(kThreads) void k_parents(const uint32_t* __restrict__ n_chunks,
                                                       const uint32_t* __restrict__ chunk_base,
+                                                      const uint32_t* __restrict__ order,
+                                                      const uint32_t* __restrict__ bins,
                                                       uint32_t n, uint32_t* __restrict__ cvs,
                                                       uint32_t out_words,
                                                       uint32_t* __restrict__ out) {
-  const uint32_t m = blockIdx.x * kThreads + threadIdx.x;
-  if (m >= n) return;
+  const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= bins[kBins]) return;
+  const uint32_t m = order[i];
   uint32_t cnt = n_chunks[m];
-  if (cnt < 2) return;
   uint32_t* c = cvs + static_cast<uint64_t>(chunk_base[m]) * 8;
-  uint32_t l[8], r[8], p[8];
+  uint32_t l[8], r[8], p[8], ln[8], rn[8];
   while (cnt > 2) {
     const uint32_t half = cnt >> 1;
+    load_cv(c, l);
+    load_cv(c + 8, r);
     for (uint32_t k = 0; k < half; ++k) {
-      load_cv(c + 16 * k, l);
-      load_cv(c + 16 * k + 8, r);
+      if (k + 1 < half) {
+        load_cv(c + 16 * (k + 1), ln);
+        load_cv(c + 16 * (k + 1) + 8, rn);
+      }
       b3_parent(p, l, r, 0u);
       store_cv(c + 8 * k, p);
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        l[w] = ln[w];
+        r[w] = rn[w];
+      }
     }
     if (cnt & 1u) {
       load_cv(c + 8 * (cnt - 1), l);
@@ -166,7 +235,13 @@ hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
   }
   {
     KScope k(timer, "cas_parents", s);
-    k_parents<<<blocks, kThreads, 0, s>>>(w.n_chunks, w.chunk_base, n, w.cvs, out_words, o);
+    (void)hipMemsetAsync(w.bins, 0, sizeof(uint32_t) * (kBins + 1), s);
+    const uint32_t g = blocks < 1024 ? blocks : 1024;
+    k_bin_hist<<<g, kThreads, 0, s>>>(w.n_chunks, n, w.bins);
+    k_bin_scan<<<1, 64, 0, s>>>(w.bins);
+    k_bin_scatter<<<g, kThreads, 0, s>>>(w.n_chunks, n, w.bins, w.order);
+    k_parents<<<blocks, kThreads, 0, s>>>(w.n_chunks, w.chunk_base, w.order, w.bins, n, w.cvs,
+                                          out_words, o);
   }
   return hipGetLastError();
 }

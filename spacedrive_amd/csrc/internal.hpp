@@ -35,6 +35,8 @@ struct BatchWork {
   uint32_t* chunk_msg = nullptr;   // [max_chunks]
   uint32_t* cvs = nullptr;         // [max_chunks][8]
   uint32_t* total = nullptr;       // [1]   == chunk_base[n]
+  uint32_t* order = nullptr;       // [n]   parent-lane order (by chunk count)
+  uint32_t* bins = nullptr;        // [129] chunk-count bins (counting sort)
   uint64_t max_chunks = 0;
 };
 
@@ -78,7 +80,9 @@ hipError_t synth_cas_arena_launch(const uint64_t* sizes, const uint64_t* seeds,
 hipError_t synth_file_launch(uint64_t seed, uint64_t offset, uint64_t len, uint8_t* out,
                              hipStream_t s);
 // Integer VALU throughput microbenchmark (add3/xor/alignbit mix of BLAKE3's G).
-hipError_t valu_probe_launch(uint32_t* sink, uint32_t iters, uint32_t blocks, hipStream_t s);
+// kind 0: BLAKE3-G mix; 1 v_xor_b32; 2 v_add3_u32; 3 v_alignbit_b32; 4 v_add_u32.
+hipError_t valu_probe_launch(int kind, uint32_t* sink, uint32_t iters, uint32_t blocks,
+                             hipStream_t s);
 hipError_t synth_dedup_rows_launch(uint64_t seed, uint64_t total_rows, uint64_t distinct,
                                    uint64_t first_rank, uint64_t n, uint64_t* key,
                                    uint8_t* has_key, uint32_t* rank, hipStream_t s);

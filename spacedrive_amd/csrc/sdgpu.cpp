@@ -207,7 +207,9 @@ int batch_work(sdgpu_ctx* c, uint32_t n, uint64_t max_chunks, BatchWork& w) {
   const size_t o_base = align_up(o_nch + 4ull * n, 256);
   const size_t o_sums = align_up(o_base + 4ull * (n + 1), 256);
   const size_t o_tot = align_up(o_sums + 4ull * (scan::tiles_for(n) + 1), 256);
-  const size_t o_map = align_up(o_tot + 4, 256);
+  const size_t o_order = align_up(o_tot + 4, 256);
+  const size_t o_bins = align_up(o_order + 4ull * n, 256);
+  const size_t o_map = align_up(o_bins + 4ull * 129, 256);
   const size_t o_cvs = align_up(o_map + 4ull * max_chunks, 256);
   const size_t total = align_up(o_cvs + 32ull * max_chunks, 256);
   SD_TRY_RC(ensure_dev(c, c->batch_ws, total));
@@ -216,6 +218,8 @@ int batch_work(sdgpu_ctx* c, uint32_t n, uint64_t max_chunks, BatchWork& w) {
   w.chunk_base = reinterpret_cast<uint32_t*>(b + o_base);
   w.block_sums = reinterpret_cast<uint32_t*>(b + o_sums);
   w.total = reinterpret_cast<uint32_t*>(b + o_tot);
+  w.order = reinterpret_cast<uint32_t*>(b + o_order);
+  w.bins = reinterpret_cast<uint32_t*>(b + o_bins);
   w.chunk_msg = reinterpret_cast<uint32_t*>(b + o_map);
   w.cvs = reinterpret_cast<uint32_t*>(b + o_cvs);
   w.max_chunks = max_chunks;
@@ -965,7 +969,11 @@ int sdgpu_timing_read(sdgpu_ctx* c, uint32_t idx, char name[32], double* total_m
 }
 
 int sdgpu_valu_probe(sdgpu_ctx* c, double* lane_ops_per_s) {
-  if (!c || !lane_ops_per_s) return -EINVAL;
+  return sdgpu_valu_probe_kind(c, 0, lane_ops_per_s);
+}
+
+int sdgpu_valu_probe_kind(sdgpu_ctx* c, int kind, double* lane_ops_per_s) {
+  if (!c || !lane_ops_per_s || kind < 0 || kind > 4) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
   SD_TRY_RC(ensure_dev(c, c->io_b, 1 << 20));
@@ -974,9 +982,9 @@ int sdgpu_valu_probe(sdgpu_ctx* c, double* lane_ops_per_s) {
   SD_TRY(hipEventCreate(&b));
   const uint32_t iters = 4096, blocks = 256 * 8 * 4;  // 32 waves per CU
   uint32_t* sink = static_cast<uint32_t*>(c->io_b.p);
-  SD_TRY(valu_probe_launch(sink, 64, blocks, c->stream));  // warm
+  SD_TRY(valu_probe_launch(kind, sink, 64, blocks, c->stream));  // warm
   SD_TRY(hipEventRecord(a, c->stream));
-  SD_TRY(valu_probe_launch(sink, iters, blocks, c->stream));
+  SD_TRY(valu_probe_launch(kind, sink, iters, blocks, c->stream));
   SD_TRY(hipEventRecord(b, c->stream));
   SD_TRY(hipEventSynchronize(b));
   float ms = 0;

@@ -160,10 +160,43 @@ __global__ __launch_bounds__(256) void k_valu_probe(uint32_t* __restrict__ sink,
   if (x == 0x12345678u) sink[blockIdx.x] = x;
 }
 
+// One instruction class only, forced by inline asm (8 independent chains per
+// lane, 6 instructions per chain per iteration): prices VOP2 vs VOP3 issue.
+template <int kKind>
+__global__ __launch_bounds__(256) void k_valu_class(uint32_t* __restrict__ sink, uint32_t iters) {
+  uint32_t a[8];
+  const uint32_t b = blockIdx.x * 0x85EBCA6Bu, c = threadIdx.x * 0x9E3779B9u;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = c + k;
+  for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (kKind == 1) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(a[k]) : "v"(b));
+        if (kKind == 2) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(b), "v"(c));
+        if (kKind == 3) asm volatile("v_alignbit_b32 %0, %0, %0, 16" : "+v"(a[k]));
+        if (kKind == 4) asm volatile("v_add_u32 %0, %1, %0" : "+v"(a[k]) : "v"(b));
+      }
+    }
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x ^= a[k];
+  if (x == 0x12345678u) sink[blockIdx.x] = x;
+}
+
 }  // namespace
 
-hipError_t valu_probe_launch(uint32_t* sink, uint32_t iters, uint32_t blocks, hipStream_t s) {
-  k_valu_probe<<<blocks, 256, 0, s>>>(sink, iters);
+hipError_t valu_probe_launch(int kind, uint32_t* sink, uint32_t iters, uint32_t blocks,
+                             hipStream_t s) {
+  switch (kind) {
+    case 1: k_valu_class<1><<<blocks, 256, 0, s>>>(sink, iters); break;
+    case 2: k_valu_class<2><<<blocks, 256, 0, s>>>(sink, iters); break;
+    case 3: k_valu_class<3><<<blocks, 256, 0, s>>>(sink, iters); break;
+    case 4: k_valu_class<4><<<blocks, 256, 0, s>>>(sink, iters); break;
+    default: k_valu_probe<<<blocks, 256, 0, s>>>(sink, iters); break;
+  }
   return hipGetLastError();
 }
 
