@@ -145,6 +145,12 @@ int sdgpu_dedup(sdgpu_ctx *ctx, const uint64_t *key, const uint8_t *has_key, uin
 int sdgpu_group_pairs_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint32_t *d_rank,
                              uint64_t n, uint32_t chunk_rows, uint32_t skip_bits, uint32_t *d_rep,
                              void *stream);
+/* Device-resident, one GPU, whole rows: rep[i] for every row i; rows with
+ * d_has_key[i] == 0 get rep[i] = rank[i].  d_has_key NULL = every row keyed;
+ * d_rank NULL = rank i (rows already in id order). */
+int sdgpu_group_rows_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t *d_has_key,
+                            const uint32_t *d_rank, uint64_t n, uint32_t chunk_rows,
+                            uint32_t skip_bits, uint32_t *d_rep, void *stream);
 /* Sharding helpers for the multi-GPU dedup (one process per GPU, RCCL
  * all-to-all between them): shard of a key = its top shard_bits bits.
  * count: h_counts[s] = rows with has_key destined to shard s (host array of

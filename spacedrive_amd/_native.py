@@ -55,6 +55,7 @@ def _proto(L):
         "sdgpu_file_checksum": (i32, [ctx, ctypes.c_char_p, ctypes.c_char_p]),
         "sdgpu_dedup": (i32, [ctx, c_vp, c_vp, u32, u32, c_vp]),
         "sdgpu_group_pairs_device": (i32, [ctx, c_vp, c_vp, u64, u32, u32, c_vp, c_vp]),
+        "sdgpu_group_rows_device": (i32, [ctx, c_vp, c_vp, c_vp, u64, u32, u32, c_vp, c_vp]),
         "sdgpu_shard_count_device": (i32, [ctx, c_vp, c_vp, u64, u32, c_vp, c_vp]),
         "sdgpu_shard_partition_device": (i32, [ctx, c_vp, c_vp, c_vp, u64, u32, c_vp, c_vp, c_vp,
                                                c_vp]),

@@ -98,14 +98,40 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
   }
 }
 
+// Bucket partition writing ONE 16-byte record {key lo, key hi, rank, row} per
+// row (a single scattered store instead of three).  Rows without a key are
+// not partitioned; their rep (= their own rank) is written here directly.
+__global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
+    const uint64_t* __restrict__ key, const uint32_t* __restrict__ rank,
+    const uint8_t* __restrict__ valid, uint64_t n, uint32_t skip, uint32_t bits,
+    const uint32_t* __restrict__ offs, uint4* __restrict__ rec, uint32_t* __restrict__ rep) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
+  const uint32_t nbins = 1u << bits;
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
+    cur[b] = offs[static_cast<uint64_t>(b) * kPartBlocks + blockIdx.x];
+  __syncthreads();
+  uint64_t t0, t1;
+  tile_of(n, t0, t1);
+  for (uint64_t i = t0 + threadIdx.x; i < t1; i += kPartThreads) {
+    const uint32_t r = rank ? rank[i] : static_cast<uint32_t>(i);
+    if (valid && !valid[i]) {
+      rep[i] = r;
+      continue;
+    }
+    const uint64_t k = key[i];
+    const uint32_t p = atomicAdd(&cur[digit_of(k, skip, bits)], 1u);
+    rec[p] = make_uint4(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32), r,
+                        static_cast<uint32_t>(i));
+  }
+}
+
 __device__ __forceinline__ uint32_t slot_hash(uint64_t k) {
   return static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> 32);
 }
 
 // One workgroup per bucket.  Rows of bucket b: [offs[b*P], offs[(b+1)*P]).
 __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
-    const uint64_t* __restrict__ skey, const uint32_t* __restrict__ srank,
-    const uint32_t* __restrict__ spos, const uint32_t* __restrict__ offs, uint32_t nbuckets,
+    const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t nbuckets,
     uint32_t chunk_rows, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
     uint32_t* __restrict__ rep) {
   __shared__ uint64_t lkey[kLdsSlots];
@@ -134,8 +160,9 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
   __syncthreads();
   const uint32_t mask = tsize - 1;
   for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
-    const uint64_t k = skey[i];
-    const uint32_t r = srank[i];
+    const uint4 q = rec[i];
+    const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
+    const uint32_t r = q.z;
     if (k == kEmpty) {
       atomicMin(&special_min, r);
       continue;
@@ -154,8 +181,9 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
   }
   __syncthreads();
   for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
-    const uint64_t k = skey[i];
-    const uint32_t r = srank[i];
+    const uint4 q = rec[i];
+    const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
+    const uint32_t r = q.z;
     uint32_t f;
     if (k == kEmpty) {
       f = special_min;
@@ -170,7 +198,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
       }
       f = in_lds ? tm[h] : __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    rep[spos[i]] = (r / chunk_rows == f / chunk_rows) ? r : f;
+    rep[q.w] = (r / chunk_rows == f / chunk_rows) ? r : f;
   }
 }
 
@@ -207,7 +235,7 @@ uint32_t bucket_bits_for(uint64_t n) {
 
 struct GroupLayout {
   uint32_t bits;
-  size_t hist, tiles, skey, srank, spos, gkey, gmin, total;
+  size_t hist, tiles, rec, gkey, gmin, total;
 };
 
 GroupLayout group_layout(uint64_t n) {
@@ -217,9 +245,7 @@ GroupLayout group_layout(uint64_t n) {
   size_t o = 0;
   L.hist = o; o = align_up(o + 4 * (nh + 1), 256);
   L.tiles = o; o = align_up(o + 4 * (scan::tiles_for(nh) + 1), 256);
-  L.skey = o; o = align_up(o + 8 * n, 256);
-  L.srank = o; o = align_up(o + 4 * n, 256);
-  L.spos = o; o = align_up(o + 4 * n, 256);
+  L.rec = o; o = align_up(o + 16 * n, 256);
   L.gkey = o; o = align_up(o + 8 * 4 * n, 256);
   L.gmin = o; o = align_up(o + 4 * 4 * n, 256);
   L.total = o;
@@ -249,26 +275,33 @@ hipError_t partition(const uint64_t* key, const uint8_t* valid, const uint32_t* 
 
 size_t dedup_workspace_bytes(uint64_t n) { return group_layout(n).total; }
 
-hipError_t dedup_local_launch(const uint64_t* key, const uint32_t* rank, uint64_t n,
-                              uint32_t chunk_rows, uint32_t shard_bits, uint32_t* rep, void* ws,
-                              hipStream_t s, KTimer* timer) {
+hipError_t dedup_local_launch(const uint64_t* key, const uint8_t* has_key, const uint32_t* rank,
+                              uint64_t n, uint32_t chunk_rows, uint32_t shard_bits, uint32_t* rep,
+                              void* ws, hipStream_t s, KTimer* timer) {
   if (n == 0) return hipSuccess;
   const GroupLayout L = group_layout(n);
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(w + L.hist);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(w + L.tiles);
-  uint64_t* skey = reinterpret_cast<uint64_t*>(w + L.skey);
-  uint32_t* srank = reinterpret_cast<uint32_t*>(w + L.srank);
-  uint32_t* spos = reinterpret_cast<uint32_t*>(w + L.spos);
+  uint4* rec = reinterpret_cast<uint4*>(w + L.rec);
   uint64_t* gkey = reinterpret_cast<uint64_t*>(w + L.gkey);
   uint32_t* gmin = reinterpret_cast<uint32_t*>(w + L.gmin);
   const uint32_t bits = std::min<uint32_t>(L.bits, 64u - shard_bits);
-  hipError_t e = partition(key, nullptr, rank, n, shard_bits, bits, hist, tiles, skey, srank,
-                           spos, s, timer, "bucket_hist", "bucket_scatter");
-  if (e != hipSuccess) return e;
+  const uint64_t nh = (static_cast<uint64_t>(1) << bits) * kPartBlocks;
+  const size_t lds = sizeof(uint32_t) << bits;
+  {
+    KScope k(timer, "bucket_hist", s);
+    k_part_hist<<<kPartBlocks, kPartThreads, lds, s>>>(key, has_key, n, shard_bits, bits, hist);
+  }
+  scan::exclusive(hist, nh, hist, tiles, nullptr, s);
+  {
+    KScope k(timer, "bucket_scatter", s);
+    k_part_scatter_rec<<<kPartBlocks, kPartThreads, lds, s>>>(key, rank, has_key, n, shard_bits,
+                                                              bits, hist, rec, rep);
+  }
   KScope k(timer, "bucket_group", s);
-  k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(skey, srank, spos, hist, 1u << bits,
-                                                      chunk_rows, gkey, gmin, rep);
+  k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, 1u << bits, chunk_rows, gkey,
+                                                      gmin, rep);
   return hipGetLastError();
 }
 

@@ -91,9 +91,11 @@ hipError_t synth_dedup_rows_launch(uint64_t seed, uint64_t total_rows, uint64_t 
 size_t dedup_workspace_bytes(uint64_t n);
 // Group (key, rank) pairs; rep[i] for pair i.  Keys' top shard_bits bits are
 // constant on this shard (skipped by the bucket digit).
-hipError_t dedup_local_launch(const uint64_t* key, const uint32_t* rank, uint64_t n,
-                              uint32_t chunk_rows, uint32_t shard_bits, uint32_t* rep, void* ws,
-                              hipStream_t s, KTimer* timer = nullptr);
+// has_key may be null (all rows keyed); rank may be null (rank = row index).
+// Rows without a key get rep = their own rank.
+hipError_t dedup_local_launch(const uint64_t* key, const uint8_t* has_key, const uint32_t* rank,
+                              uint64_t n, uint32_t chunk_rows, uint32_t shard_bits, uint32_t* rep,
+                              void* ws, hipStream_t s, KTimer* timer = nullptr);
 size_t shard_workspace_bytes(uint32_t shard_bits);
 hipError_t shard_count_launch(const uint64_t* key, const uint8_t* has_key, uint64_t n,
                               uint32_t shard_bits, uint64_t* d_counts, void* ws, hipStream_t s);

@@ -826,8 +826,23 @@ int sdgpu_group_pairs_device(sdgpu_ctx* c, const uint64_t* d_key, const uint32_t
   hipStream_t s = pick(c, stream);
   if (n == 0) return 0;
   SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(n)));
-  SD_TRY(dedup_local_launch(d_key, d_rank, n, chunk_rows, skip_bits, d_rep, c->dedup_ws.p, s,
-                            c->kt()));
+  SD_TRY(dedup_local_launch(d_key, nullptr, d_rank, n, chunk_rows, skip_bits, d_rep,
+                            c->dedup_ws.p, s, c->kt()));
+  return 0;
+}
+
+int sdgpu_group_rows_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8_t* d_has_key,
+                            const uint32_t* d_rank, uint64_t n, uint32_t chunk_rows,
+                            uint32_t skip_bits, uint32_t* d_rep, void* stream) {
+  if (!c || chunk_rows == 0 || skip_bits > 32 || (n && (!d_key || !d_rep))) return -EINVAL;
+  if (n >= (1ull << 32)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  if (n == 0) return 0;
+  SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(n)));
+  SD_TRY(dedup_local_launch(d_key, d_has_key, d_rank, n, chunk_rows, skip_bits, d_rep,
+                            c->dedup_ws.p, s, c->kt()));
   return 0;
 }
 
@@ -882,10 +897,8 @@ int sdgpu_dedup(sdgpu_ctx* c, const uint64_t* key, const uint8_t* has_key, uint3
     std::lock_guard<std::mutex> g(c->mu);
     SD_TRY(hipSetDevice(c->device));
   }
-  // [key n*8 | has n | pkey n*8 | prank n*4 | ppos n*4 | prep n*4 | rep n*4]
-  const size_t o_key = 0, o_has = align_up(8ull * n, 256), o_pkey = align_up(o_has + n, 256);
-  const size_t o_prank = align_up(o_pkey + 8ull * n, 256), o_ppos = align_up(o_prank + 4ull * n, 256);
-  const size_t o_prep = align_up(o_ppos + 4ull * n, 256), o_rep = align_up(o_prep + 4ull * n, 256);
+  // [key n*8 | has n | rep n*4]
+  const size_t o_key = 0, o_has = align_up(8ull * n, 256), o_rep = align_up(o_has + n, 256);
   const size_t total = align_up(o_rep + 4ull * n, 256);
   if (hipMalloc(&d, total) != hipSuccess) return -ENOMEM;
   hipStream_t s = c->stream;
@@ -895,18 +908,10 @@ int sdgpu_dedup(sdgpu_ctx* c, const uint64_t* key, const uint8_t* has_key, uint3
       rc = -EIO;
       break;
     }
-    uint64_t cnt = 0;
     const uint64_t* dk = reinterpret_cast<const uint64_t*>(d + o_key);
-    if ((rc = sdgpu_shard_count_device(c, dk, d + o_has, n, 0, &cnt, s))) break;
-    uint64_t* pkey = reinterpret_cast<uint64_t*>(d + o_pkey);
-    uint32_t* prank = reinterpret_cast<uint32_t*>(d + o_prank);
-    uint32_t* ppos = reinterpret_cast<uint32_t*>(d + o_ppos);
-    uint32_t* prep = reinterpret_cast<uint32_t*>(d + o_prep);
     uint32_t* drep = reinterpret_cast<uint32_t*>(d + o_rep);
-    if ((rc = sdgpu_shard_partition_device(c, dk, d + o_has, nullptr, n, 0, pkey, prank, ppos, s)))
+    if ((rc = sdgpu_group_rows_device(c, dk, d + o_has, nullptr, n, chunk_rows, 0, drep, s)))
       break;
-    if ((rc = sdgpu_group_pairs_device(c, pkey, prank, cnt, chunk_rows, 0, prep, s))) break;
-    if ((rc = sdgpu_scatter_rep_device(c, prep, ppos, cnt, drep, n, nullptr, 1, s))) break;
     if (hipMemcpyAsync(rep, drep, 4ull * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
       rc = -EIO;

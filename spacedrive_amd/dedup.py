@@ -82,6 +82,18 @@ class HipOps:
                   "sdgpu_group_pairs_device")
         return rep
 
+    def group_rows(self, key, has_key, rank, chunk_rows: int, skip_bits: int):
+        """rep for every row (rows without a key keep their own rank)."""
+        import torch
+        ctx = self._c(key)
+        rep = torch.empty(key.numel(), dtype=torch.int32, device=key.device)
+        if key.numel():
+            check(ctx.lib.sdgpu_group_rows_device(
+                ctx.h, key.data_ptr(), has_key.data_ptr() if has_key is not None else None,
+                rank.data_ptr() if rank is not None else None, key.numel(), chunk_rows,
+                skip_bits, rep.data_ptr(), self._s(key)), "sdgpu_group_rows_device")
+        return rep
+
     def scatter(self, src, pos, n: int, init):
         import torch
         ctx = self._c(src)
@@ -115,14 +127,13 @@ def sharded_group_reps(key, has_key, rank, chunk_rows: int = CHUNK_SIZE, group=N
     ops = ops or HipOps()
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     n = key.numel()
+    if world == 1:  # no exchange: group the rows in place (no compaction pass)
+        return ops.group_rows(key, has_key, rank, chunk_rows, 0)
     bits, owner, skip = shard_plan(world)
     counts = ops.shard_counts(key, has_key, bits)
     send_counts = np.bincount(owner, weights=counts, minlength=world).astype(np.int64)
     total = int(send_counts.sum())
     skey, srank, spos = ops.partition(key, has_key, rank, bits, total)
-    if world == 1:
-        rep_sent = ops.group(skey, srank, chunk_rows, 0)
-        return ops.scatter(rep_sent, spos, n, rank)
     dev = key.device
     sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
     rc = torch.empty_like(sc)

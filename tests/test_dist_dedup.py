@@ -51,6 +51,16 @@ class NumpyOps:
             rep[order] = np.where(rr // chunk_rows == first // chunk_rows, rr, first)
         return torch.from_numpy(rep.astype(np.uint32).view(np.int32))
 
+    def group_rows(self, key, has_key, rank, chunk_rows, skip):
+        h = has_key.numpy().astype(bool)
+        r = rank.numpy() if rank is not None else np.arange(key.numel(), dtype=np.int32)
+        out = torch.from_numpy(np.ascontiguousarray(r, np.int32).copy())
+        idx = np.flatnonzero(h)
+        g = self.group(torch.from_numpy(key.numpy()[idx].copy()),
+                       torch.from_numpy(np.ascontiguousarray(r[idx], np.int32)), chunk_rows, skip)
+        out[torch.from_numpy(idx)] = g
+        return out
+
     def scatter(self, src, pos, n, init):
         out = init.clone() if init is not None else torch.arange(n, dtype=torch.int32)
         out[pos.long()] = src
