@@ -63,7 +63,7 @@ int k1_variant() {
   return v ? atoi(v) : 0;
 }
 
-template <bool kPipelined, bool kSdwa>
+template <bool kPipelined>
 __global__ __launch_bounds__(kThreads) void k_chunks(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ chunk_msg,
@@ -79,10 +79,10 @@ __global__ __launch_bounds__(kThreads) void k_chunks(
     const uint32_t clen = min(B3_CHUNK_LEN, l - j * B3_CHUNK_LEN);
     uint32_t cv[8];
     if (kPipelined)
-      b3_chunk_pipelined<kSdwa>(arena + off[m] + static_cast<uint64_t>(j) * B3_CHUNK_LEN, clen,
+      b3_chunk_pipelined(arena + off[m] + static_cast<uint64_t>(j) * B3_CHUNK_LEN, clen,
                                 j, single ? B3_ROOT : 0u, cv);
     else
-      b3_chunk<kSdwa>(arena + off[m] + static_cast<uint64_t>(j) * B3_CHUNK_LEN, clen, j,
+      b3_chunk(arena + off[m] + static_cast<uint64_t>(j) * B3_CHUNK_LEN, clen, j,
                       single ? B3_ROOT : 0u, cv);
     if (single) {
       for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = cv[w];
@@ -226,16 +226,12 @@ hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
   const uint32_t grid = static_cast<uint32_t>(want < 8192 ? (want ? want : 1) : 8192);
   {
     KScope k(timer, "cas_chunks", s);
-#define SDGPU_K1(P, S)                                                                  \
-  k_chunks<P, S><<<grid, kThreads, 0, s>>>(arena, off, len, w.chunk_msg, w.chunk_base, \
-                                           w.total, w.cvs, out_words, o)
-    switch (k1_variant()) {
-      case 1: SDGPU_K1(true, false); break;
-      case 2: SDGPU_K1(false, true); break;
-      case 3: SDGPU_K1(true, true); break;
-      default: SDGPU_K1(false, false); break;
-    }
-#undef SDGPU_K1
+    if (k1_variant() == 1)
+      k_chunks<true><<<grid, kThreads, 0, s>>>(arena, off, len, w.chunk_msg, w.chunk_base,
+                                               w.total, w.cvs, out_words, o);
+    else
+      k_chunks<false><<<grid, kThreads, 0, s>>>(arena, off, len, w.chunk_msg, w.chunk_base,
+                                                w.total, w.cvs, out_words, o);
   }
   {
     KScope k(timer, "cas_parents", s);

@@ -35,32 +35,10 @@ __device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t n) {
   return __builtin_amdgcn_alignbit(x, x, n);
 }
 
-// rotr(d ^ a, 16).  The plain form is v_xor_b32 (VOP2) + v_alignbit_b32
-// (VOP3).  On gfx950 a VOP3 integer op issues at half the VOP2 rate (measured:
-// v_xor/v_add ~70 T lane-ops/s, v_add3/v_alignbit ~38.5 T), so the SDWA form
-// builds the half-swapped xor with two VOP2 SDWA xors, each writing one 16-bit
-// half of the result: 2 VOP2 issues instead of VOP2 + VOP3.
-template <bool kSdwa>
-__device__ __forceinline__ uint32_t xor_rotr16(uint32_t d, uint32_t a) {
-  if constexpr (kSdwa) {
-    uint32_t t;
-    asm volatile(
-        "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 "
-        "src1_sel:WORD_0\n\t"
-        "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 "
-        "src1_sel:WORD_1"
-        : "=&v"(t)
-        : "v"(d), "v"(a));
-    return t;
-  } else {
-    return rotr32(d ^ a, 16);
-  }
-}
-
 #define SDGPU_G(a, b, c, d, x, y)    \
   do {                               \
     a = a + b + (x);                 \
-    d = xor_rotr16<kSdwa>(d, a);     \
+    d = rotr32(d ^ a, 16);           \
     c = c + d;                       \
     b = rotr32(b ^ c, 12);           \
     a = a + b + (y);                 \
@@ -82,12 +60,8 @@ __device__ __forceinline__ uint32_t xor_rotr16(uint32_t d, uint32_t a) {
     SDGPU_G(v3, v4, v9, v14, M[s14], M[s15]);                                              \
   } while (0)
 
-// Default rotate-16 form for every kernel (A/B-able through K1's variant bit 1).
-constexpr bool kSdwaDefault = false;
-
 // cv <- first 8 output words of compress(cv, m, counter, block_len, flags).
 // For a ROOT compression this is the first 32 bytes of the digest.
-template <bool kSdwa = kSdwaDefault>
 __device__ __forceinline__ void b3_compress(uint32_t cv[8], const uint32_t m[16],
                                             uint32_t counter_lo, uint32_t counter_hi,
                                             uint32_t block_len, uint32_t flags) {
@@ -119,7 +93,6 @@ __device__ __forceinline__ void b3_iv(uint32_t cv[8]) {
 }
 
 // Parent node: cv <- compress(IV, left || right, 0, 64, PARENT | extra).
-template <bool kSdwa = kSdwaDefault>
 __device__ __forceinline__ void b3_parent(uint32_t out[8], const uint32_t l[8],
                                           const uint32_t r[8], uint32_t extra_flags) {
   uint32_t m[16];
@@ -129,7 +102,7 @@ __device__ __forceinline__ void b3_parent(uint32_t out[8], const uint32_t l[8],
     m[8 + i] = r[i];
   }
   b3_iv(out);
-  b3_compress<kSdwa>(out, m, 0u, 0u, B3_BLOCK_LEN, B3_PARENT | extra_flags);
+  b3_compress(out, m, 0u, 0u, B3_BLOCK_LEN, B3_PARENT | extra_flags);
 }
 
 // 64 bytes at a 16-byte aligned address -> 16 little-endian words.
@@ -167,7 +140,6 @@ __device__ __forceinline__ void b3_load_block_partial(const uint8_t* __restrict_
 
 // Chaining value (or, with ROOT in `root_flag`, the digest words) of one chunk
 // of `clen` (0..1024) bytes at 16-byte aligned `p`, chunk counter `ctr`.
-template <bool kSdwa = kSdwaDefault>
 __device__ __forceinline__ void b3_chunk(const uint8_t* __restrict__ p, uint32_t clen,
                                          uint64_t ctr, uint32_t root_flag, uint32_t cv[8]) {
   b3_iv(cv);
@@ -177,18 +149,17 @@ __device__ __forceinline__ void b3_chunk(const uint8_t* __restrict__ p, uint32_t
   uint32_t b = 0;
   for (; b + 1 < nb; ++b) {
     b3_load_block(p + 64u * b, m);
-    b3_compress<kSdwa>(cv, m, lo, hi, B3_BLOCK_LEN, b == 0 ? B3_CHUNK_START : 0u);
+    b3_compress(cv, m, lo, hi, B3_BLOCK_LEN, b == 0 ? B3_CHUNK_START : 0u);
   }
   const uint32_t last = clen - 64u * b;
   b3_load_block_partial(p + 64u * b, last, m);
-  b3_compress<kSdwa>(cv, m, root_flag ? 0u : lo, root_flag ? 0u : hi, last,
+  b3_compress(cv, m, root_flag ? 0u : lo, root_flag ? 0u : hi, last,
               B3_CHUNK_END | (nb == 1 ? B3_CHUNK_START : 0u) | root_flag);
 }
 
 // Same as b3_chunk, software-pipelined: the next block's 64 bytes are loaded
 // before the current block is compressed, so one wave keeps a load in flight
 // under every compression.
-template <bool kSdwa = kSdwaDefault>
 __device__ __forceinline__ void b3_chunk_pipelined(const uint8_t* __restrict__ p, uint32_t clen,
                                                    uint64_t ctr, uint32_t root_flag,
                                                    uint32_t cv[8]) {
@@ -202,11 +173,11 @@ __device__ __forceinline__ void b3_chunk_pipelined(const uint8_t* __restrict__ p
   for (uint32_t b = 0; b + 1 < nb; ++b) {
     if (b + 2 < nb) b3_load_block(p + 64u * (b + 1), mn);
     else b3_load_block_partial(p + 64u * (b + 1), last, mn);
-    b3_compress<kSdwa>(cv, m, lo, hi, B3_BLOCK_LEN, b == 0 ? B3_CHUNK_START : 0u);
+    b3_compress(cv, m, lo, hi, B3_BLOCK_LEN, b == 0 ? B3_CHUNK_START : 0u);
 #pragma unroll
     for (int w = 0; w < 16; ++w) m[w] = mn[w];
   }
-  b3_compress<kSdwa>(cv, m, root_flag ? 0u : lo, root_flag ? 0u : hi, last,
+  b3_compress(cv, m, root_flag ? 0u : lo, root_flag ? 0u : hi, last,
               B3_CHUNK_END | (nb == 1 ? B3_CHUNK_START : 0u) | root_flag);
 }
 
