@@ -209,6 +209,260 @@ __global__ __launch_bounds__(kThreads) void k_parents(const uint32_t* __restrict
   for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = p[w];
 }
 
+// ============================================================================
+// K1 v2: 4-chunk units + one lane per message for the ragged rest.
+//
+// A message of n > 4 chunks has q = floor(full_chunks / 4) aligned units of 4
+// FULL chunks.  UNIT lanes (grid-stride over all units of the batch) hash the
+// 4 chunks and merge them in-lane: P(P(c0,c1), P(c2,c3)) -- 67 compressions,
+// identical for every lane, no ragged chunk anywhere.  A unit is a complete
+// level-2 subtree of BLAKE3's tree.  MESSAGE lanes (one per message, ordered
+// by remaining work so waves are uniform) hash the 0..4 remaining chunks
+// [4q, n) into one level-2 node and fold the q + 1 level-2 nodes pairwise
+// (ROOT on the last compression).  Messages of <= 4 chunks are done entirely
+// by their message lane.  For a sampled cas message (56 full chunks + 8 bytes)
+// that is 14 unit lanes and 15 compressions on the message lane instead of
+// 56 serial parents.
+// ============================================================================
+
+__device__ __forceinline__ uint32_t n_chunks_of(uint32_t len) {
+  return len <= B3_CHUNK_LEN ? 1u : (len + B3_CHUNK_LEN - 1) / B3_CHUNK_LEN;
+}
+
+__device__ __forceinline__ uint32_t units_of(uint32_t len) {
+  return n_chunks_of(len) > 4 ? (len / B3_CHUNK_LEN) / 4 : 0u;
+}
+
+// Remaining work of a message lane, in compressions (for ordering only).
+__device__ __forceinline__ uint32_t msg_work(uint32_t len) {
+  const uint32_t nch = n_chunks_of(len), q = units_of(len);
+  const uint32_t first = 4 * q * B3_CHUNK_LEN;
+  const uint32_t rem_bytes = len - first;
+  const uint32_t rem_blocks = rem_bytes == 0 ? (q ? 0u : 1u) : (rem_bytes + 63) / 64;
+  const uint32_t rem = nch - 4 * q;
+  return 1 + rem_blocks + (rem > 1 ? rem - 1 : 0) + (q ? q + (rem ? 1 : 0) - 1 : 0);
+}
+
+__global__ __launch_bounds__(kThreads) void k_plan2(const uint64_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ len, uint32_t n,
+                                                    uint32_t max_len,
+                                                    uint32_t* __restrict__ units,
+                                                    uint32_t* __restrict__ slots,
+                                                    uint32_t* __restrict__ work,
+                                                    int32_t* __restrict__ status,
+                                                    uint32_t out_words, uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t l = len[i];
+  const bool ok = l <= max_len && (off[i] & 15u) == 0;
+  const uint32_t q = ok ? units_of(l) : 0u;
+  units[i] = q;
+  slots[i] = q ? q + 1 : 0u;
+  work[i] = ok ? msg_work(l) : 0u;
+  if (status) status[i] = ok ? 0 : -EINVAL;
+  if (!ok)
+    for (uint32_t w = 0; w < out_words; ++w) out[i * out_words + w] = 0u;
+}
+
+// One chunk of 1024 bytes (16 full blocks).
+__device__ __forceinline__ void full_chunk(const uint8_t* __restrict__ p, uint32_t ctr,
+                                           uint32_t cv[8]) {
+  b3_iv(cv);
+  uint32_t m[16];
+  for (uint32_t b = 0; b < 16; ++b) {
+    b3_load_block(p + 64u * b, m);
+    b3_compress(cv, m, ctr, 0u, B3_BLOCK_LEN,
+                (b == 0 ? B3_CHUNK_START : 0u) | (b == 15 ? B3_CHUNK_END : 0u));
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_units(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ unit_msg, const uint32_t* __restrict__ unit_base,
+    const uint32_t* __restrict__ slot_base, const uint32_t* __restrict__ d_total,
+    uint32_t* __restrict__ cvs) {
+  const uint32_t total = *d_total;
+  const uint32_t stride = gridDim.x * kThreads;
+  for (uint32_t u = blockIdx.x * kThreads + threadIdx.x; u < total; u += stride) {
+    const uint32_t m = unit_msg[u];
+    const uint32_t g = u - unit_base[m];
+    const uint32_t j0 = 4 * g;
+    const uint8_t* p = arena + off[m] + static_cast<uint64_t>(j0) * B3_CHUNK_LEN;
+    uint32_t a[8], b[8];
+    full_chunk(p, j0, a);
+    full_chunk(p + 1024, j0 + 1, b);
+    b3_parent(a, a, b, 0u);
+    full_chunk(p + 2048, j0 + 2, b);
+    uint32_t c[8];
+    full_chunk(p + 3072, j0 + 3, c);
+    b3_parent(b, b, c, 0u);
+    b3_parent(c, a, b, 0u);
+    store_cv(cvs + static_cast<uint64_t>(slot_base[m] + g) * 8, c);
+  }
+}
+
+// In-place pairwise fold of cnt >= 2 CVs at c; ROOT on the last merge.
+__device__ __forceinline__ void fold_root(uint32_t* c, uint32_t cnt, uint32_t p[8]) {
+  uint32_t l[8], r[8], ln[8], rn[8];
+  while (cnt > 2) {
+    const uint32_t half = cnt >> 1;
+    load_cv(c, l);
+    load_cv(c + 8, r);
+    for (uint32_t k = 0; k < half; ++k) {
+      if (k + 1 < half) {
+        load_cv(c + 16 * (k + 1), ln);
+        load_cv(c + 16 * (k + 1) + 8, rn);
+      }
+      b3_parent(p, l, r, 0u);
+      store_cv(c + 8 * k, p);
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        l[w] = ln[w];
+        r[w] = rn[w];
+      }
+    }
+    if (cnt & 1u) {
+      load_cv(c + 8 * (cnt - 1), l);
+      store_cv(c + 8 * half, l);
+    }
+    cnt = half + (cnt & 1u);
+  }
+  load_cv(c, l);
+  load_cv(c + 8, r);
+  b3_parent(p, l, r, B3_ROOT);
+}
+
+__global__ __launch_bounds__(kThreads) void k_msgs(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ slot_base,
+    const uint32_t* __restrict__ order, const uint32_t* __restrict__ bins,
+    uint32_t* __restrict__ cvs, uint32_t out_words, uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= bins[kBins]) return;
+  const uint32_t m = order[i];
+  const uint32_t l = len[m];
+  const uint32_t nch = n_chunks_of(l), q = units_of(l);
+  const uint32_t rem = nch - 4 * q;  // 0..4 (1..4 when q == 0)
+  const uint8_t* p = arena + off[m];
+  const uint32_t rootf = q == 0 ? B3_ROOT : 0u;
+  // level-2 node of the remaining chunks [4q, nch): pairwise fold of <= 4
+  // chunk CVs with a 2-entry register stack (s0, s1).
+  uint32_t cv[8], s0[8], s1[8];
+  uint32_t sp = 0;
+  for (uint32_t k = 0; k < rem; ++k) {
+    const uint32_t j = 4 * q + k;
+    const uint32_t clen = min(B3_CHUNK_LEN, l - j * B3_CHUNK_LEN);
+    b3_chunk(p + static_cast<uint64_t>(j) * B3_CHUNK_LEN, clen, j, rem == 1 ? rootf : 0u, cv);
+    if (k + 1 == rem) break;
+    if (((k + 1) & 1u) == 0) {  // two nodes of the pair are complete: merge
+      uint32_t t[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) t[w] = sp == 2 ? s1[w] : s0[w];
+      b3_parent(cv, t, cv, 0u);
+      --sp;
+    }
+    if (sp == 0) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) s0[w] = cv[w];
+    } else {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) s1[w] = cv[w];
+    }
+    ++sp;
+  }
+  while (sp > 0) {
+    uint32_t t[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) t[w] = sp == 2 ? s1[w] : s0[w];
+    b3_parent(cv, t, cv, sp == 1 ? rootf : 0u);
+    --sp;
+  }
+  if (q == 0) {
+    for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = cv[w];
+    return;
+  }
+  uint32_t* c = cvs + static_cast<uint64_t>(slot_base[m]) * 8;
+  if (rem) store_cv(c + 8 * q, cv);
+  uint32_t r[8];
+  fold_root(c, q + (rem ? 1u : 0u), r);
+  for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = r[w];
+}
+
+// order = messages with key >= kmin sorted by descending key (capped at 127).
+__global__ __launch_bounds__(kThreads) void k_kbin_hist(const uint32_t* __restrict__ key,
+                                                        uint32_t n, uint32_t kmin,
+                                                        uint32_t* __restrict__ bins) {
+  __shared__ uint32_t h[kBins];
+  if (threadIdx.x < kBins) h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+    const uint32_t c = key[i];
+    if (c >= kmin) atomicAdd(&h[parent_bin(c)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kBins && h[threadIdx.x]) atomicAdd(&bins[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kThreads) void k_kbin_scatter(const uint32_t* __restrict__ key,
+                                                           uint32_t n, uint32_t kmin,
+                                                           uint32_t* __restrict__ bins,
+                                                           uint32_t* __restrict__ order) {
+  __shared__ uint32_t h[kBins], base[kBins];
+  for (uint32_t i0 = blockIdx.x * kThreads; i0 < n; i0 += gridDim.x * kThreads) {
+    if (threadIdx.x < kBins) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = i0 + threadIdx.x;
+    const uint32_t c = i < n ? key[i] : 0u;
+    uint32_t local = 0, b = 0;
+    if (c >= kmin) {
+      b = parent_bin(c);
+      local = atomicAdd(&h[b], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < kBins && h[threadIdx.x])
+      base[threadIdx.x] = atomicAdd(&bins[threadIdx.x], h[threadIdx.x]);
+    __syncthreads();
+    if (c >= kmin) order[base[b] + local] = i;
+    __syncthreads();
+  }
+}
+
+hipError_t batch_hash_launch_v2(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                                uint32_t n, uint32_t max_len, uint32_t out_words, uint8_t* out,
+                                int32_t* status, const BatchWork& w, hipStream_t s,
+                                KTimer* timer) {
+  const uint32_t blocks = (n + kThreads - 1) / kThreads;
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  // n_chunks <- units per message; the per-message work estimate is parked in
+  // the head of the CV buffer, which k_units only writes after the sort.
+  uint32_t* units = w.n_chunks;
+  uint32_t* slots = w.slot_base;
+  k_plan2<<<blocks, kThreads, 0, s>>>(off, len, n, max_len, units, slots, w.cvs, status,
+                                      out_words, o);
+  scan::exclusive(units, n, w.chunk_base, w.block_sums, w.total, s);
+  scan::exclusive(slots, n, w.slot_base, w.slot_sums, nullptr, s);
+  k_fill_map<<<(n + 3) / 4, kThreads, 0, s>>>(units, w.chunk_base, n, w.chunk_msg);
+  // sort message lanes by work (the estimate sits in w.cvs[0..n) until k_units)
+  (void)hipMemsetAsync(w.bins, 0, sizeof(uint32_t) * (kBins + 1), s);
+  const uint32_t g = blocks < 1024 ? blocks : 1024;
+  k_kbin_hist<<<g, kThreads, 0, s>>>(w.cvs, n, 1, w.bins);
+  k_bin_scan<<<1, 64, 0, s>>>(w.bins);
+  k_kbin_scatter<<<g, kThreads, 0, s>>>(w.cvs, n, 1, w.bins, w.order);
+  uint64_t want = (w.max_chunks / 4 + kThreads - 1) / kThreads;
+  const uint32_t grid = static_cast<uint32_t>(want < 8192 ? (want ? want : 1) : 8192);
+  {
+    KScope k(timer, "cas_units", s);
+    k_units<<<grid, kThreads, 0, s>>>(arena, off, w.chunk_msg, w.chunk_base, w.slot_base, w.total,
+                                      w.cvs);
+  }
+  {
+    KScope k(timer, "cas_msgs", s);
+    k_msgs<<<blocks, kThreads, 0, s>>>(arena, off, len, w.slot_base, w.order, w.bins, w.cvs,
+                                       out_words, o);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
@@ -216,6 +470,8 @@ hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
                              int32_t* status, const BatchWork& w, hipStream_t s,
                              KTimer* timer) {
   if (n == 0) return hipSuccess;
+  if (k1_variant() == 2)
+    return batch_hash_launch_v2(arena, off, len, n, max_len, out_words, out, status, w, s, timer);
   const uint32_t blocks = (n + kThreads - 1) / kThreads;
   uint32_t* o = reinterpret_cast<uint32_t*>(out);
   k_plan<<<blocks, kThreads, 0, s>>>(off, len, n, max_len, w.n_chunks, status, out_words, o);

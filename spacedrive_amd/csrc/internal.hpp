@@ -37,6 +37,8 @@ struct BatchWork {
   uint32_t* total = nullptr;       // [1]   == chunk_base[n]
   uint32_t* order = nullptr;       // [n]   parent-lane order (by chunk count)
   uint32_t* bins = nullptr;        // [129] chunk-count bins (counting sort)
+  uint32_t* slot_base = nullptr;   // [n + 1] v2: CV slot prefix (units + 1 per unit-bearing msg)
+  uint32_t* slot_sums = nullptr;   // [scan tiles of n]
   uint64_t max_chunks = 0;
 };
 

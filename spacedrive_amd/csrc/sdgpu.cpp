@@ -209,7 +209,9 @@ int batch_work(sdgpu_ctx* c, uint32_t n, uint64_t max_chunks, BatchWork& w) {
   const size_t o_tot = align_up(o_sums + 4ull * (scan::tiles_for(n) + 1), 256);
   const size_t o_order = align_up(o_tot + 4, 256);
   const size_t o_bins = align_up(o_order + 4ull * n, 256);
-  const size_t o_map = align_up(o_bins + 4ull * 129, 256);
+  const size_t o_slot = align_up(o_bins + 4ull * 129, 256);
+  const size_t o_ssum = align_up(o_slot + 4ull * (n + 1), 256);
+  const size_t o_map = align_up(o_ssum + 4ull * (scan::tiles_for(n) + 1), 256);
   const size_t o_cvs = align_up(o_map + 4ull * max_chunks, 256);
   const size_t total = align_up(o_cvs + 32ull * max_chunks, 256);
   SD_TRY_RC(ensure_dev(c, c->batch_ws, total));
@@ -220,6 +222,8 @@ int batch_work(sdgpu_ctx* c, uint32_t n, uint64_t max_chunks, BatchWork& w) {
   w.total = reinterpret_cast<uint32_t*>(b + o_tot);
   w.order = reinterpret_cast<uint32_t*>(b + o_order);
   w.bins = reinterpret_cast<uint32_t*>(b + o_bins);
+  w.slot_base = reinterpret_cast<uint32_t*>(b + o_slot);
+  w.slot_sums = reinterpret_cast<uint32_t*>(b + o_ssum);
   w.chunk_msg = reinterpret_cast<uint32_t*>(b + o_map);
   w.cvs = reinterpret_cast<uint32_t*>(b + o_cvs);
   w.max_chunks = max_chunks;
