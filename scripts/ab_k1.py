@@ -41,12 +41,15 @@ def main():
             if ref is None:
                 ref = got
             assert np.array_equal(got, ref), f"variant {v} differs"
-            res[v].append((wall * 1e3, kt["cas_chunks"][0] / 3, kt["cas_parents"][0] / 3))
+            res[v].append((wall * 1e3, {k: t[0] / 3 for k, t in kt.items()}))
     for v in variants:
-        a = np.array(res[v])
-        print(f"K1 variant {v}: wall ms median {np.median(a[:, 0]):.3f} min {a[:, 0].min():.3f} | "
-              f"cas_chunks ms median {np.median(a[:, 1]):.3f} | cas_parents {np.median(a[:, 2]):.3f}"
-              f" | files/s {n / np.median(a[:, 0]) * 1e3:.3e}")
+        walls = np.array([w for w, _ in res[v]])
+        names = sorted(res[v][0][1])
+        per = {k: np.median([d[k] for _, d in res[v]]) for k in names}
+        ks = " | ".join(f"{k} {per[k]:.3f}" for k in names)
+        print(f"K1 variant {v}: wall ms median {np.median(walls):.3f} min {walls.min():.3f} | "
+              f"{ks} | files/s {n / np.median(walls) * 1e3:.3e}  (bit-identical to variant "
+              f"{variants[0]})")
 
 
 if __name__ == "__main__":

@@ -1,5 +1,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 300 python -u scripts/ab_k1.py ${VARIANTS:-0,1} 5 > gpurun_out/${TAG}_ab.log 2>&1
+timeout -k 10 300 python -u scripts/ab_k1.py ${AB:-0,2} 5 > gpurun_out/${TAG}_ab.log 2>&1
 echo "exit $?"

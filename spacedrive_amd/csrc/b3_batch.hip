@@ -57,10 +57,12 @@ __global__ __launch_bounds__(kThreads) void k_fill_map(const uint32_t* __restric
 }
 
 // One lane per chunk (grid-stride over the flattened chunk list).
-// K1 variant for A/B runs in one process (SDGPU_K1_VARIANT: 0 plain, 1 pipelined).
+// K1 variant for A/B runs in one process.  SDGPU_K1_VARIANT unset or 2: the
+// unit/message scheme (default); 0: chunk-lane + parent-lane scheme; 1: the
+// same with software-pipelined block loads.
 int k1_variant() {
   const char* v = getenv("SDGPU_K1_VARIANT");
-  return v ? atoi(v) : 0;
+  return v ? atoi(v) : 2;
 }
 
 template <bool kPipelined>
@@ -264,18 +266,6 @@ __global__ __launch_bounds__(kThreads) void k_plan2(const uint64_t* __restrict__
     for (uint32_t w = 0; w < out_words; ++w) out[i * out_words + w] = 0u;
 }
 
-// One chunk of 1024 bytes (16 full blocks).
-__device__ __forceinline__ void full_chunk(const uint8_t* __restrict__ p, uint32_t ctr,
-                                           uint32_t cv[8]) {
-  b3_iv(cv);
-  uint32_t m[16];
-  for (uint32_t b = 0; b < 16; ++b) {
-    b3_load_block(p + 64u * b, m);
-    b3_compress(cv, m, ctr, 0u, B3_BLOCK_LEN,
-                (b == 0 ? B3_CHUNK_START : 0u) | (b == 15 ? B3_CHUNK_END : 0u));
-  }
-}
-
 __global__ __launch_bounds__(kThreads) void k_units(
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ unit_msg, const uint32_t* __restrict__ unit_base,
@@ -289,12 +279,12 @@ __global__ __launch_bounds__(kThreads) void k_units(
     const uint32_t j0 = 4 * g;
     const uint8_t* p = arena + off[m] + static_cast<uint64_t>(j0) * B3_CHUNK_LEN;
     uint32_t a[8], b[8];
-    full_chunk(p, j0, a);
-    full_chunk(p + 1024, j0 + 1, b);
+    b3_chunk_full(p, j0, a);
+    b3_chunk_full(p + 1024, j0 + 1, b);
     b3_parent(a, a, b, 0u);
-    full_chunk(p + 2048, j0 + 2, b);
+    b3_chunk_full(p + 2048, j0 + 2, b);
     uint32_t c[8];
-    full_chunk(p + 3072, j0 + 3, c);
+    b3_chunk_full(p + 3072, j0 + 3, c);
     b3_parent(b, b, c, 0u);
     b3_parent(c, a, b, 0u);
     store_cv(cvs + static_cast<uint64_t>(slot_base[m] + g) * 8, c);

@@ -95,8 +95,11 @@ __global__ __launch_bounds__(kThreads) void k_tree_level(const LevelSeg* __restr
         const uint32_t clen = static_cast<uint32_t>(min<uint64_t>(B3_CHUNK_LEN, d.len - off));
         // a single-chunk root segment puts ROOT on the chunk's last block
         const uint32_t rf = (fin && d.root && d.in_count == 1) ? B3_ROOT : 0u;
-        b3_chunk(reinterpret_cast<const uint8_t*>(d.src) + off, clen, d.chunk_offset + node, rf,
-                 cv);
+        const uint8_t* cp = reinterpret_cast<const uint8_t*>(d.src) + off;
+        if (clen == B3_CHUNK_LEN && rf == 0)
+          b3_chunk_full(cp, d.chunk_offset + node, cv);
+        else
+          b3_chunk(cp, clen, d.chunk_offset + node, rf, cv);
       } else {
         const uint4* p = reinterpret_cast<const uint4*>(in_cvs + (d.src + node) * 8);
         const uint4 a = p[0], b = p[1];
