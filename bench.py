@@ -16,7 +16,7 @@ warm-up, barrier + synchronize on both sides, max over ranks):
   cas      K1 alone over config 2                              files/s
   dedup    config 4: 12.5 M rows per GPU (100 M at 8 GPUs)     rows/s
   checksum config 3: 64 x 4 GiB files per GPU, device-resident GB/s
-`roofline` is for the dominant kernel (K1 "cas_chunks"), timed live with HIP
+`roofline` is for the dominant kernel (K1 "cas_leaves"), timed live with HIP
 events on its launch stream; `cpu_baseline` times the scalar C oracle port of
 generate_cas_id's hashing on this host's cores over a bounded sample.
 """
@@ -57,6 +57,38 @@ def compressions(lens: np.ndarray):
     blocks = np.where(L == 0, 1, blocks)
     chunks = np.maximum(1, (L + 1023) // 1024)
     return int(blocks.sum()), int((chunks - 1).sum())
+
+
+def k1_split(lens: np.ndarray):
+    """Compressions done by K1 v3's two kernels (b3_batch.hip k_leaves3 / k_fold3):
+    leaves = every chunk block + the parents inside 4-chunk units (3 each) and
+    inside the 1..4-chunk ragged tail of a message (rem - 1); fold = the
+    (q + [rem > 0] - 1) parents above the level-2 nodes of a message."""
+    L = lens.astype(np.int64)
+    blk, par = compressions(L)
+    nch = np.maximum(1, (L + 1023) // 1024)
+    q = np.where(nch > 4, (L // 1024) // 4, 0)
+    rem = nch - 4 * q
+    leaves = blk + int(3 * q.sum()) + int(np.maximum(rem - 1, 0).sum())
+    return leaves, blk + par - leaves
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/<round>/pmc_traffic.json, written by scripts/pmc_summary.py from
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench's workload)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")),
+                   key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in d.get("kernels", {}):
+            k = d["kernels"][kernel]
+            return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
 
 
 class Runner:
@@ -137,16 +169,15 @@ class Runner:
                       "ms_per_step": 1e3 * t_cas / steps,
                       "config": {"workload": "config2: 1M log-normal files/GPU, 20% dup, 0.1% empty",
                                  "files_per_gpu": n, "window_bytes_per_gpu": int(lens.sum())}}
-        ms_chunks, nl = kt.get("cas_chunks", (0.0, 1))
-        ms_par, _ = kt.get("cas_parents", (0.0, 1))
-        avg_chunks = ms_chunks / max(nl, 1) * 1e-3
-        avg_par = ms_par / max(nl, 1) * 1e-3
+        ms_leaves, nl = kt.get("cas_leaves", (0.0, 1))
+        avg_leaves = ms_leaves / max(nl, 1) * 1e-3
         res["kernels"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in kt.items()}
         # identifier job step: K1 + sharded grouping (RCCL all-to-all at N > 1)
         t_job = self.timed(job, steps, warmup)
         res["job"] = {"value": self.world * n * steps / t_job, "ms_per_step": 1e3 * t_job / steps}
-        res["roofline_inputs"] = {"chunk_blocks": blk, "parents": par,
-                                  "avg_chunks_s": avg_chunks, "avg_parents_s": avg_par,
+        leaves, fold = k1_split(lens)
+        res["roofline_inputs"] = {"chunk_blocks": blk, "parents": par, "leaf_compressions": leaves,
+                                  "fold_compressions": fold, "avg_leaves_s": avg_leaves,
                                   "bytes": int(lens.sum())}
         self._cpu_sample = (arena, off, ln, min(n, self.args.cpu_files))
         return res
@@ -217,13 +248,19 @@ class Runner:
         host = arena[:end].cpu().numpy()
         threads = min(16, os.cpu_count() or 1)
         O.cas_batch(host, h_off[:100], h_len[:100], threads)  # warm
+        # repeat the sample until about 10 s of CPU work has been timed
         t0 = time.perf_counter()
         O.cas_batch(host, h_off, h_len, threads)
+        t1 = time.perf_counter() - t0
+        reps = int(min(60, max(1, np.ceil(self.args.cpu_seconds / max(t1, 1e-3)))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            O.cas_batch(host, h_off, h_len, threads)
         dt = time.perf_counter() - t0
-        return {"value": m / dt, "unit": "files/s", "cores": threads, "kind": "port",
+        return {"value": reps * m / dt, "unit": "files/s", "cores": threads, "kind": "port",
                 "sample": f"first {m} files of config 2 (their {int(h_len.sum())} window bytes "
-                          f"in host RAM), scalar C BLAKE3 oracle, {threads} threads, "
-                          f"{dt:.2f} s wall"}
+                          f"in host RAM) hashed {reps}x, scalar C BLAKE3 oracle "
+                          f"(oracle/sd_oracle.c), {threads} threads, {dt:.1f} s wall"}
 
 
 def main():
@@ -237,6 +274,7 @@ def main():
     ap.add_argument("--checksum-bytes", type=int, default=1 << 32)
     ap.add_argument("--cpu-files", type=int, default=100_000)
     ap.add_argument("--components", default="cas,dedup,checksum")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
     comps = set(args.components.split(","))
@@ -269,17 +307,21 @@ def main():
         torch.cuda.empty_cache()
 
     ri = c["roofline_inputs"]
-    ops = ri["chunk_blocks"] * ISA_PER_COMPRESSION
-    achieved = ops / ri["avg_chunks_s"] if ri["avg_chunks_s"] > 0 else 0.0
-    roof = {"bound": "valu", "kernel": "cas_chunks (K1)",
+    ops = ri["leaf_compressions"] * ISA_PER_COMPRESSION
+    t_leaf = ri["avg_leaves_s"]
+    achieved = ops / t_leaf if t_leaf > 0 else 0.0
+    traffic, traffic_src = pmc_traffic("k_leaves3")
+    roof = {"bound": "valu", "kernel": "cas_leaves (K1 k_leaves3)",
             "achieved": achieved / 1e12, "peak": VALU_PEAK_SPEC / 1e12, "unit": "Tops/s",
-            "frac": achieved / VALU_PEAK_SPEC, "traffic": None,
+            "frac": achieved / VALU_PEAK_SPEC, "traffic": traffic,
+            "traffic_source": traffic_src,
             "peak_measured": valu_peak / 1e12, "peak_by_class_measured": classes,
             "frac_of_measured": achieved / valu_peak if valu_peak else None,
-            "algorithmic_per_launch": {"compressions": ri["chunk_blocks"],
+            "algorithmic_per_launch": {"compressions": ri["leaf_compressions"],
                                        "int32_ops": ops, "window_bytes": ri["bytes"]},
-            "hbm_GBps": ri["bytes"] / ri["avg_chunks_s"] / 1e9 if ri["avg_chunks_s"] else None,
-            "hbm_frac": ri["bytes"] / ri["avg_chunks_s"] / HBM_PEAK if ri["avg_chunks_s"] else None}
+            "compressions_per_s": ri["leaf_compressions"] / t_leaf if t_leaf else None,
+            "hbm_GBps": ri["bytes"] / t_leaf / 1e9 if t_leaf else None,
+            "hbm_frac": ri["bytes"] / t_leaf / HBM_PEAK if t_leaf else None}
     job = c["job"]
     line = {"metric": METRIC, "value": job["value"], "unit": "files/s", "n_gpus": R.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": job["ms_per_step"],

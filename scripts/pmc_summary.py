@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-kernel HBM bytes
+per launch (profiles/<round>/pmc_traffic.json, read by bench.py's roofline).
+
+Units and gfx950 corrections follow /opt/skills/guides/MI355X_MICROARCH.md
+(HBM section): both counters are in KiB; FETCH_SIZE of wide (16 B/lane)
+streaming reads is exactly half the bytes on gfx950, so it is doubled;
+WRITE_SIZE is exact for 16-B-per-lane stores.
+
+Usage: python scripts/pmc_summary.py <prof_dir> <out.json> [kernel-substring ...]
+"""
+import collections
+import csv
+import json
+import os
+import re
+import sys
+
+
+def load(path, counter):
+    agg = collections.defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"]
+            m = re.search(r"(k_\w+)", name)
+            agg[m.group(1) if m else name[:80]].append(float(r["Counter_Value"]))
+    return agg
+
+
+def main():
+    prof, out = sys.argv[1], sys.argv[2]
+    want = sys.argv[3:]
+    fetch = load(os.path.join(prof, "pmc_FETCH_SIZE", "pmc_counter_collection.csv"), "FETCH_SIZE")
+    write = load(os.path.join(prof, "pmc_WRITE_SIZE", "pmc_counter_collection.csv"), "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        if want and not any(w in k for w in want):
+            continue
+        f = fetch.get(k, [])
+        w = write.get(k, [])
+        fb = 2 * 1024 * sum(f) / len(f) if f else None
+        wb = 1024 * sum(w) / len(w) if w else None
+        res[k] = {"fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+                  "hbm_bytes_per_launch": (fb or 0) + (wb or 0), "launches": max(len(f), len(w))}
+    doc = {"source": prof, "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count of "
+           "16-B/lane streaming reads), WRITE_SIZE KiB x 1024", "kernels": res}
+    with open(out, "w") as fo:
+        json.dump(doc, fo, indent=1)
+    for k, v in res.items():
+        print(f"{k:32s} fetch {v['fetch_bytes_per_launch'] or 0:.4g} B  write "
+              f"{v['write_bytes_per_launch'] or 0:.4g} B")
+
+
+if __name__ == "__main__":
+    main()

@@ -21,5 +21,6 @@ if [ -n "$PMC" ]; then
     timeout -s KILL 240 rocprofv3 --pmc $C -d "$OUT/pmc_$N" -o pmc --output-format csv \
       -- python3 bench.py $PARGS > "$OUT/pmc_$N.log" 2>&1 || { echo "pmc $C failed: $?"; exit 1; }
   done
+  python3 scripts/pmc_summary.py "$OUT" "$OUT/pmc_traffic.json" > "$OUT/pmc_traffic.txt" || exit 1
 fi
 echo done

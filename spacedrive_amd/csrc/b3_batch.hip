@@ -18,6 +18,8 @@
 #include <errno.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "b3_device.hpp"
 #include "internal.hpp"
 #include "scan_device.hpp"
@@ -57,12 +59,14 @@ __global__ __launch_bounds__(kThreads) void k_fill_map(const uint32_t* __restric
 }
 
 // One lane per chunk (grid-stride over the flattened chunk list).
-// K1 variant for A/B runs in one process.  SDGPU_K1_VARIANT unset or 2: the
-// unit/message scheme (default); 0: chunk-lane + parent-lane scheme; 1: the
-// same with software-pipelined block loads.
+// K1 variant for A/B runs in one process.  SDGPU_K1_VARIANT unset or 3: the
+// persistent longest-first queue (default; 5 waves/SIMD, 4: the same pinned
+// to 6 waves/SIMD with a few bytes of spill); 2: unit/message lanes over a
+// fixed grid; 0: chunk-lane + parent-lane scheme; 1: the same with
+// software-pipelined block loads.
 int k1_variant() {
   const char* v = getenv("SDGPU_K1_VARIANT");
-  return v ? atoi(v) : 2;
+  return v ? atoi(v) : 3;
 }
 
 template <bool kPipelined>
@@ -453,6 +457,295 @@ hipError_t batch_hash_launch_v2(const uint8_t* arena, const uint64_t* off, const
   return hipGetLastError();
 }
 
+// ============================================================================
+// K1 v3: persistent, longest-first work queue over units and message items.
+//
+// v2 launched one lane per unit over a fixed grid of 8192 blocks: with 6
+// resident blocks per CU that is 5.3 "rounds" of blocks, and the last third of
+// a round ran on a third of the machine (~11 % of K1 lost to the tail).  v3:
+//   leaves: a grid of exactly the resident capacity; each wave grabs the next
+//           64 items from one global counter.  Items are the U units (67
+//           compressions each, the heaviest items) followed by the R message
+//           items (the 1..4 ragged chunks of each message, or the whole
+//           message when it has <= 4 chunks) sorted by descending work, so
+//           the queue drains heaviest-first (LPT) and the tail is made of the
+//           lightest items.
+//   fold  : one lane per unit-bearing message (sorted by node count) folds
+//           its q (+1) level-2 nodes pairwise, ROOT on the last parent.
+// CV slots: message m owns slots [unit_base[m] + m, + q + 1): its units'
+// nodes, then the node of its ragged chunks.  sum(q + 1) <= total chunks.
+// Both lane orders come from one counting sort (per-block histograms in
+// bin-major order + one exclusive scan: no global atomics on hot bins).
+// ============================================================================
+
+constexpr uint32_t kSortBlocks = 256;
+
+// Leaf work of message m (compressions of its message item; 0 = no item).
+__device__ __forceinline__ uint32_t leaf_work3(uint32_t len) {
+  const uint32_t nch = n_chunks_of(len), q = units_of(len);
+  const uint32_t rem = nch - 4 * q;
+  if (rem == 0) return 0u;
+  const uint32_t rem_bytes = len - 4 * q * B3_CHUNK_LEN;
+  const uint32_t rem_blocks = rem_bytes == 0 ? 1u : (rem_bytes + 63) / 64;
+  return rem_blocks + (rem - 1);
+}
+
+// Sort bins of message (len, ok): key 0 = message item by leaf work, key 1 =
+// fold lane by node count.  kBins means "not in this list".
+__device__ __forceinline__ void bins3(uint32_t len, bool ok, uint32_t& b0, uint32_t& b1) {
+  b0 = b1 = kBins;
+  if (!ok) return;
+  const uint32_t lw = leaf_work3(len);
+  if (lw) b0 = parent_bin(lw);
+  const uint32_t q = units_of(len);
+  if (q) b1 = parent_bin(q + (n_chunks_of(len) > 4 * q ? 1u : 0u));
+}
+
+struct Range3 {
+  uint32_t lo, hi;
+};
+__device__ __forceinline__ Range3 block_range3(uint32_t n) {
+  const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+  const uint32_t lo = min(n, blockIdx.x * per);
+  return {lo, min(n, lo + per)};
+}
+
+// Per message: unit count, status, zeroed output of invalid messages; per
+// block: histograms of both sort keys -> hist[(key * kBins + bin) * NB + blk].
+__global__ __launch_bounds__(kThreads) void k_plan3(const uint64_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ len, uint32_t n,
+                                                    uint32_t max_len, uint32_t* __restrict__ units,
+                                                    uint32_t* __restrict__ hist,
+                                                    uint32_t* __restrict__ grab,
+                                                    int32_t* __restrict__ status,
+                                                    uint32_t out_words, uint32_t* __restrict__ out) {
+  __shared__ uint32_t h[2][kBins];
+  for (uint32_t t = threadIdx.x; t < 2 * kBins; t += kThreads) (&h[0][0])[t] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *grab = 0;
+  __syncthreads();
+  const Range3 r = block_range3(n);
+  for (uint32_t i = r.lo + threadIdx.x; i < r.hi; i += kThreads) {
+    const uint32_t l = len[i];
+    const bool ok = l <= max_len && (off[i] & 15u) == 0;
+    units[i] = ok ? units_of(l) : 0u;
+    if (status) status[i] = ok ? 0 : -EINVAL;
+    if (!ok)
+      for (uint32_t w = 0; w < out_words; ++w) out[i * out_words + w] = 0u;
+    uint32_t b0, b1;
+    bins3(l, ok, b0, b1);
+    if (b0 < kBins) atomicAdd(&h[0][b0], 1u);
+    if (b1 < kBins) atomicAdd(&h[1][b1], 1u);
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < 2 * kBins; t += kThreads)
+    hist[static_cast<size_t>(t) * gridDim.x + blockIdx.x] = (&h[0][0])[t];
+}
+
+// Scatter both lane orders (positions from the scanned histograms: key 0 lands
+// in [0, R), key 1 in [R, R + F)) and fill the unit -> message map.
+__global__ __launch_bounds__(kThreads) void k_scatter3(const uint64_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ len, uint32_t n,
+                                                       uint32_t max_len,
+                                                       const uint32_t* __restrict__ unit_base,
+                                                       const uint32_t* __restrict__ hist_scan,
+                                                       uint32_t* __restrict__ order,
+                                                       uint32_t* __restrict__ unit_msg) {
+  __shared__ uint32_t cur[2][kBins], cnt[2][kBins];
+  for (uint32_t t = threadIdx.x; t < 2 * kBins; t += kThreads) {
+    (&cur[0][0])[t] = hist_scan[static_cast<size_t>(t) * gridDim.x + blockIdx.x];
+    (&cnt[0][0])[t] = 0;
+  }
+  __syncthreads();
+  const Range3 r = block_range3(n);
+  for (uint32_t i0 = r.lo; i0 < r.hi; i0 += kThreads) {
+    const uint32_t i = i0 + threadIdx.x;
+    uint32_t b0 = kBins, b1 = kBins, l0 = 0, l1 = 0;
+    if (i < r.hi) {
+      const uint32_t l = len[i];
+      const bool ok = l <= max_len && (off[i] & 15u) == 0;
+      bins3(l, ok, b0, b1);
+      if (b0 < kBins) l0 = atomicAdd(&cnt[0][b0], 1u);
+      if (b1 < kBins) l1 = atomicAdd(&cnt[1][b1], 1u);
+      const uint32_t q = ok ? units_of(l) : 0u;
+      const uint32_t ub = unit_base[i];
+      for (uint32_t g = 0; g < q; ++g) unit_msg[ub + g] = i;
+    }
+    __syncthreads();
+    if (b0 < kBins) order[cur[0][b0] + l0] = i;
+    if (b1 < kBins) order[cur[1][b1] + l1] = i;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < 2 * kBins; t += kThreads) {
+      (&cur[0][0])[t] += (&cnt[0][0])[t];
+      (&cnt[0][0])[t] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// One 4-chunk unit: level-2 node of chunks [4g, 4g + 4) of message m.
+__device__ __forceinline__ void unit_item(const uint8_t* __restrict__ arena,
+                                          const uint64_t* __restrict__ off,
+                                          const uint32_t* __restrict__ unit_msg,
+                                          const uint32_t* __restrict__ unit_base, uint32_t u,
+                                          uint32_t* __restrict__ cvs) {
+  const uint32_t m = unit_msg[u];
+  const uint32_t ub = unit_base[m];
+  const uint32_t g = u - ub;
+  const uint32_t j0 = 4 * g;
+  const uint8_t* p = arena + off[m] + static_cast<uint64_t>(j0) * B3_CHUNK_LEN;
+  uint32_t a[8], b[8], c[8];
+  b3_chunk_full(p, j0, a);
+  b3_chunk_full(p + 1024, j0 + 1, b);
+  b3_parent(a, a, b, 0u);
+  b3_chunk_full(p + 2048, j0 + 2, b);
+  b3_chunk_full(p + 3072, j0 + 3, c);
+  b3_parent(b, b, c, 0u);
+  b3_parent(c, a, b, 0u);
+  store_cv(cvs + static_cast<uint64_t>(ub + m + g) * 8, c);
+}
+
+// Chunk j of a message (full chunks take the 128-byte-line path).
+__device__ __forceinline__ void chunk_any(const uint8_t* __restrict__ p, uint32_t l, uint32_t j,
+                                          uint32_t root_flag, uint32_t cv[8]) {
+  const uint32_t clen = min(B3_CHUNK_LEN, l - j * B3_CHUNK_LEN);
+  const uint8_t* cp = p + static_cast<uint64_t>(j) * B3_CHUNK_LEN;
+  if (clen == B3_CHUNK_LEN && root_flag == 0)
+    b3_chunk_full(cp, j, cv);
+  else
+    b3_chunk(cp, clen, j, root_flag, cv);
+}
+
+// Message item: the node of chunks [4q, nch) (the whole message, with ROOT,
+// when q == 0).  1..4 chunks form the left-complete subtree
+// c0 | P(c0,c1) | P(P(c0,c1),c2) | P(P(c0,c1),P(c2,c3)), built with the
+// same three CV registers as a unit.
+__device__ __forceinline__ void msg_item(const uint8_t* __restrict__ arena,
+                                         const uint64_t* __restrict__ off,
+                                         const uint32_t* __restrict__ len,
+                                         const uint32_t* __restrict__ unit_base, uint32_t m,
+                                         uint32_t* __restrict__ cvs, uint32_t out_words,
+                                         uint32_t* __restrict__ out) {
+  const uint32_t l = len[m];
+  const uint32_t nch = n_chunks_of(l), q = units_of(l);
+  const uint32_t rem = nch - 4 * q;  // 1..4
+  const uint8_t* p = arena + off[m];
+  const uint32_t rootf = q == 0 ? B3_ROOT : 0u;
+  const uint32_t j0 = 4 * q;
+  uint32_t a[8], b[8], c[8];
+  chunk_any(p, l, j0, rem == 1 ? rootf : 0u, a);
+  if (rem >= 2) {
+    chunk_any(p, l, j0 + 1, 0u, b);
+    b3_parent(a, a, b, rem == 2 ? rootf : 0u);
+  }
+  if (rem >= 3) {
+    chunk_any(p, l, j0 + 2, 0u, b);
+    if (rem == 4) {
+      chunk_any(p, l, j0 + 3, 0u, c);
+      b3_parent(b, b, c, 0u);
+    }
+    b3_parent(a, a, b, rootf);
+  }
+  if (q == 0) {
+    for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = a[w];
+  } else {
+    store_cv(cvs + static_cast<uint64_t>(unit_base[m] + m + q) * 8, a);
+  }
+}
+
+template <int kMinBlocks>
+__global__ __launch_bounds__(kThreads, kMinBlocks) void k_leaves3(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ unit_msg,
+    const uint32_t* __restrict__ unit_base, const uint32_t* __restrict__ d_units,
+    const uint32_t* __restrict__ order, const uint32_t* __restrict__ d_r,
+    uint32_t* __restrict__ grab, uint32_t* __restrict__ cvs, uint32_t out_words,
+    uint32_t* __restrict__ out) {
+  const uint32_t U = *d_units;
+  const uint32_t total = U + *d_r;
+  const uint32_t lane = threadIdx.x & 63u;
+  for (;;) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(grab, 64u);
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+    if (base >= total) break;  // uniform: every wave reaches this exit
+    const uint32_t i = base + lane;
+    if (i < U)
+      unit_item(arena, off, unit_msg, unit_base, i, cvs);
+    else if (i < total)
+      msg_item(arena, off, len, unit_base, order[i - U], cvs, out_words, out);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_fold3(const uint32_t* __restrict__ len,
+                                                    const uint32_t* __restrict__ unit_base,
+                                                    const uint32_t* __restrict__ order,
+                                                    const uint32_t* __restrict__ d_r,
+                                                    const uint32_t* __restrict__ d_end,
+                                                    uint32_t* __restrict__ cvs, uint32_t out_words,
+                                                    uint32_t* __restrict__ out) {
+  const uint32_t R = *d_r;
+  const uint32_t i = R + blockIdx.x * kThreads + threadIdx.x;
+  if (i >= *d_end) return;
+  const uint32_t m = order[i];
+  const uint32_t l = len[m];
+  const uint32_t q = units_of(l);
+  const uint32_t cnt = q + (n_chunks_of(l) > 4 * q ? 1u : 0u);
+  uint32_t r[8];
+  fold_root(cvs + static_cast<uint64_t>(unit_base[m] + m) * 8, cnt, r);
+  for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = r[w];
+}
+
+// Resident-capacity grid of k_leaves3<kMinBlocks> on the current device.
+template <int kMinBlocks>
+uint32_t leaves3_grid() {
+  static int cached_dev = -1;
+  static uint32_t cached = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev != cached_dev) {
+    int cus = 0, per = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_leaves3<kMinBlocks>, kThreads, 0);
+    cached = static_cast<uint32_t>(std::max(1, cus) * std::max(1, per));
+    cached_dev = dev;
+  }
+  return cached;
+}
+
+hipError_t batch_hash_launch_v3(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                                uint32_t n, uint32_t max_len, uint32_t out_words, uint8_t* out,
+                                int32_t* status, const BatchWork& w, hipStream_t s,
+                                KTimer* timer, bool occ6) {
+  uint32_t* o = reinterpret_cast<uint32_t*>(out);
+  const uint32_t nb = std::min<uint32_t>(kSortBlocks, (n + kThreads - 1) / kThreads);
+  const uint32_t nh = 2 * kBins * nb;
+  // hist_scan[kBins * nb] = R (start of the fold list), hist_scan[nh] = R + F
+  k_plan3<<<nb, kThreads, 0, s>>>(off, len, n, max_len, w.n_chunks, w.hist, w.grab, status,
+                                  out_words, o);
+  scan::exclusive(w.n_chunks, n, w.chunk_base, w.block_sums, w.total, s);
+  scan::exclusive(w.hist, nh, w.hist, w.hist_sums, nullptr, s);
+  k_scatter3<<<nb, kThreads, 0, s>>>(off, len, n, max_len, w.chunk_base, w.hist, w.order,
+                                     w.chunk_msg);
+  const uint32_t* d_r = w.hist + static_cast<size_t>(kBins) * nb;
+  {
+    KScope k(timer, "cas_leaves", s);
+    if (occ6)
+      k_leaves3<6><<<leaves3_grid<6>(), kThreads, 0, s>>>(arena, off, len, w.chunk_msg,
+                                                          w.chunk_base, w.total, w.order, d_r,
+                                                          w.grab, w.cvs, out_words, o);
+    else
+      k_leaves3<5><<<leaves3_grid<5>(), kThreads, 0, s>>>(arena, off, len, w.chunk_msg,
+                                                          w.chunk_base, w.total, w.order, d_r,
+                                                          w.grab, w.cvs, out_words, o);
+  }
+  {
+    KScope k(timer, "cas_fold", s);
+    k_fold3<<<(n + kThreads - 1) / kThreads, kThreads, 0, s>>>(len, w.chunk_base, w.order, d_r,
+                                                               w.hist + nh, w.cvs, out_words, o);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
@@ -460,6 +753,10 @@ hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
                              int32_t* status, const BatchWork& w, hipStream_t s,
                              KTimer* timer) {
   if (n == 0) return hipSuccess;
+  const int variant = k1_variant();
+  if (variant == 3 || variant == 4)
+    return batch_hash_launch_v3(arena, off, len, n, max_len, out_words, out, status, w, s, timer,
+                                variant == 4);
   if (k1_variant() == 2)
     return batch_hash_launch_v2(arena, off, len, n, max_len, out_words, out, status, w, s, timer);
   const uint32_t blocks = (n + kThreads - 1) / kThreads;

@@ -35,10 +35,13 @@ struct BatchWork {
   uint32_t* chunk_msg = nullptr;   // [max_chunks]
   uint32_t* cvs = nullptr;         // [max_chunks][8]
   uint32_t* total = nullptr;       // [1]   == chunk_base[n]
-  uint32_t* order = nullptr;       // [n]   parent-lane order (by chunk count)
+  uint32_t* order = nullptr;       // [2n]  lane orders (v0/v2: [n]; v3: items then folds)
   uint32_t* bins = nullptr;        // [129] chunk-count bins (counting sort)
   uint32_t* slot_base = nullptr;   // [n + 1] v2: CV slot prefix (units + 1 per unit-bearing msg)
   uint32_t* slot_sums = nullptr;   // [scan tiles of n]
+  uint32_t* hist = nullptr;        // [2 * 128 * 256 + 1] v3: per-block sort histograms
+  uint32_t* hist_sums = nullptr;   // [scan tiles of hist]
+  uint32_t* grab = nullptr;        // [1] v3: work-queue counter
   uint64_t max_chunks = 0;
 };
 

@@ -208,10 +208,14 @@ int batch_work(sdgpu_ctx* c, uint32_t n, uint64_t max_chunks, BatchWork& w) {
   const size_t o_sums = align_up(o_base + 4ull * (n + 1), 256);
   const size_t o_tot = align_up(o_sums + 4ull * (scan::tiles_for(n) + 1), 256);
   const size_t o_order = align_up(o_tot + 4, 256);
-  const size_t o_bins = align_up(o_order + 4ull * n, 256);
+  const size_t o_bins = align_up(o_order + 8ull * n, 256);
   const size_t o_slot = align_up(o_bins + 4ull * 129, 256);
   const size_t o_ssum = align_up(o_slot + 4ull * (n + 1), 256);
-  const size_t o_map = align_up(o_ssum + 4ull * (scan::tiles_for(n) + 1), 256);
+  const size_t n_hist = 2ull * 128 * 256;
+  const size_t o_hist = align_up(o_ssum + 4ull * (scan::tiles_for(n) + 1), 256);
+  const size_t o_hsum = align_up(o_hist + 4ull * (n_hist + 1), 256);
+  const size_t o_grab = align_up(o_hsum + 4ull * (scan::tiles_for(n_hist) + 1), 256);
+  const size_t o_map = align_up(o_grab + 4, 256);
   const size_t o_cvs = align_up(o_map + 4ull * max_chunks, 256);
   const size_t total = align_up(o_cvs + 32ull * max_chunks, 256);
   SD_TRY_RC(ensure_dev(c, c->batch_ws, total));
@@ -224,6 +228,9 @@ int batch_work(sdgpu_ctx* c, uint32_t n, uint64_t max_chunks, BatchWork& w) {
   w.bins = reinterpret_cast<uint32_t*>(b + o_bins);
   w.slot_base = reinterpret_cast<uint32_t*>(b + o_slot);
   w.slot_sums = reinterpret_cast<uint32_t*>(b + o_ssum);
+  w.hist = reinterpret_cast<uint32_t*>(b + o_hist);
+  w.hist_sums = reinterpret_cast<uint32_t*>(b + o_hsum);
+  w.grab = reinterpret_cast<uint32_t*>(b + o_grab);
   w.chunk_msg = reinterpret_cast<uint32_t*>(b + o_map);
   w.cvs = reinterpret_cast<uint32_t*>(b + o_cvs);
   w.max_chunks = max_chunks;

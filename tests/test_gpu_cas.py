@@ -118,3 +118,36 @@ def test_zero_files(ctx):
     out, st = cas.cas_batch(np.zeros(16, np.uint8), np.zeros(0, np.uint64),
                             np.zeros(0, np.uint32), ctx)
     assert out.shape == (0, 8)
+
+
+def _tree_edge_lengths():
+    """Message lengths at every chunk-count / unit boundary up to 102 408 B:
+    n*1024 + {-64, -1, 0, 1, 8, 65} for n = 1..100, plus 57 352 (sampled)."""
+    ls = {57352, 102408, 102407}
+    for n in range(1, 101):
+        for d in (-64, -1, 0, 1, 8, 65):
+            v = n * 1024 + d
+            if 0 <= v <= 102408:
+                ls.add(v)
+    return np.array(sorted(ls), np.uint32)
+
+
+@pytest.mark.parametrize("variant", ["0", "2", "3", "4"])
+def test_k1_variants_tree_edges_bit_exact(ctx, variant, monkeypatch):
+    """Every K1 scheduling variant (SDGPU_K1_VARIANT) on every unit/ragged-tail
+    shape: q = 0..25 four-chunk units with 0..4 trailing chunks."""
+    from spacedrive_amd import cas
+    monkeypatch.setenv("SDGPU_K1_VARIANT", variant)
+    lens = _tree_edge_lengths()
+    lens = np.concatenate([lens, lens[::-1]])  # both orders in one batch
+    off = np.zeros(lens.size, np.uint64)
+    pos = 0
+    for i, n in enumerate(lens):
+        off[i] = pos
+        pos += (int(n) + 127) // 128 * 128
+    rng = np.random.default_rng(int(variant) + 7)
+    arena = rng.integers(0, 256, pos + 16, dtype=np.uint8)
+    out, st = cas.cas_batch(arena, off, lens, ctx)
+    assert np.all(st == 0)
+    ref = O.cas_batch(arena, off, lens, threads=8)
+    np.testing.assert_array_equal(out, ref)
