@@ -7,15 +7,17 @@
 Headline `value` (files/s, whole job): one STEP = one identifier pass over a
 batch resident in HBM -- BASELINE config 2 per GPU (1 M synthetic files,
 log-normal sizes, 20 % duplicates, 0.1 % empty; only the cas windows exist) --
-consisting of K1 (sampled cas_id of every file) followed by the cas_id ->
-Object grouping of all files of all GPUs (hash-sharded, RCCL all-to-all at
-N > 1).  Weak scaling: every GPU brings its own 1 M files.
+consisting of K1 (sampled cas_id of every file), the cas_id -> Object
+grouping of all files of all GPUs (hash-sharded, RCCL all-to-all at N > 1) and
+the Object link batch (K7: create / connect lists).  Weak scaling: every GPU brings its own 1 M files.
 
 Components reported on the same line (each timed the same way, K steps after W
 warm-up, barrier + synchronize on both sides, max over ranks):
   cas      K1 alone over config 2                              files/s
   dedup    config 4: 12.5 M rows per GPU (100 M at 8 GPUs)     rows/s
   checksum config 3: 64 x 4 GiB files per GPU, device-resident GB/s
+  staged   config 5 shape: 250 k config-2 files per GPU whose windows sit in
+           pinned host memory, streamed H2D + K1 + grouping + link batch files/s
 `roofline` is for the dominant kernel (K1 "cas_leaves"), timed live with HIP
 events on its launch stream; `cpu_baseline` times the scalar C oracle port of
 generate_cas_id's hashing on this host's cores over a bounded sample.
@@ -157,7 +159,8 @@ class Runner:
         def job():
             k1()
             key = out.view(torch.int64).view(-1)
-            dedup.sharded_group_reps(key, has, grank, 100, ops=ops)
+            rep = dedup.sharded_group_reps(key, has, grank, 100, ops=ops)
+            dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx)
 
         # K1 alone, with live per-kernel event timing on its launch stream
         self.ctx.set_timing(True)
@@ -181,6 +184,67 @@ class Runner:
                                   "bytes": int(lens.sum())}
         self._cpu_sample = (arena, off, ln, min(n, self.args.cpu_files))
         return res
+
+    # ---------------------------------------------------------------- config 5
+    def h2d_peak(self, nbytes=1 << 30, reps=5):
+        """Measured pinned host -> device copy rate (B/s) on this GPU's link."""
+        torch = self.torch
+        h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+        d = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+        d.copy_(h, non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            d.copy_(h, non_blocking=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        del h, d
+        return nbytes * reps / dt
+
+    def run_staged(self, steps, warmup):
+        """Config 5 shape: identifier job whose cas windows sit in PINNED host
+        memory (where the preads land): staged H2D through the slab ring
+        overlapped with K1, then the sharded grouping and the Object link batch."""
+        torch = self.torch
+        from spacedrive_amd import cas, corpus, dedup
+        n = self.args.staged_files
+        sizes, seeds = corpus.config2_files(n, seed=5 + 1000 * self.rank)
+        d_arena, d_off, d_len = corpus.synth_arena_device(sizes, seeds, device=self.local,
+                                                          ctx=self.ctx)
+        torch.cuda.synchronize()
+        h_arena = torch.empty(d_arena.numel(), dtype=torch.uint8).pin_memory()
+        h_arena.copy_(d_arena)
+        off = d_off.cpu().numpy().view(np.uint64).copy()
+        ln = d_len.cpu().numpy().view(np.uint32).copy()
+        del d_arena, d_off, d_len
+        torch.cuda.empty_cache()
+        window_bytes = int(ln.astype(np.int64).sum())
+        out = torch.empty((n, 8), dtype=torch.uint8, device=self.dev)
+        st = torch.empty(n, dtype=torch.int32, device=self.dev)
+        has = torch.from_numpy((sizes != 0).astype(np.uint8)).to(self.dev)
+        grank = torch.arange(self.rank * n, (self.rank + 1) * n, dtype=torch.int64,
+                             device=self.dev).to(torch.int32)
+        ops = dedup.HipOps(self.ctx)
+        peak = self.h2d_peak()
+
+        def step():
+            cas.cas_stage_pinned(h_arena, off, ln, out, st, ctx=self.ctx)
+            key = out.view(torch.int64).view(-1)
+            rep = dedup.sharded_group_reps(key, has, grank, 100, ops=ops)
+            dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx)
+
+        t = self.timed(step, steps, warmup)
+        assert int(st.abs().sum()) == 0
+        per_gpu_Bps = window_bytes * steps / t
+        del h_arena
+        return {"value": self.world * n * steps / t, "unit": "files/s",
+                "ms_per_step": 1e3 * t / steps,
+                "window_GBps_per_gpu": per_gpu_Bps / 1e9,
+                "h2d_peak_GBps": peak / 1e9, "h2d_frac": per_gpu_Bps / peak,
+                "config": {"workload": "config5 shape: config2 files/GPU, windows in pinned host "
+                                       "memory, staged H2D (3-slab ring) + K1 + sharded grouping "
+                                       "+ Object link batch",
+                           "files_per_gpu": n, "window_bytes_per_gpu": window_bytes}}
 
     # ---------------------------------------------------------------- config 4
     def run_dedup(self, steps, warmup):
@@ -273,7 +337,8 @@ def main():
     ap.add_argument("--checksum-files", type=int, default=64)
     ap.add_argument("--checksum-bytes", type=int, default=1 << 32)
     ap.add_argument("--cpu-files", type=int, default=100_000)
-    ap.add_argument("--components", default="cas,dedup,checksum")
+    ap.add_argument("--staged-files", type=int, default=250_000)
+    ap.add_argument("--components", default="cas,dedup,checksum,staged")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -299,6 +364,11 @@ def main():
         d = R.run_dedup(args.steps, args.warmup)
         log("dedup:", json.dumps(d))
         comp["dedup"] = d
+        torch.cuda.empty_cache()
+    if "staged" in comps:
+        g = R.run_staged(max(1, min(args.steps, 5)), 1)
+        log("staged:", json.dumps(g))
+        comp["staged"] = g
         torch.cuda.empty_cache()
     if "checksum" in comps:
         k = R.run_checksum(args.steps, args.warmup)
@@ -328,7 +398,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (BASELINE configs 2/3/4 shapes, generated in HBM)",
             "config": {"workload": "identifier job step: config2 (1M files/GPU) cas_id + "
-                                   "sharded cas_id->Object grouping",
+                                   "sharded cas_id->Object grouping + Object link batch",
                        "files_per_gpu": args.files, "global_files": args.files * R.world,
                        "parallelism": f"dp{R.world} (files) + hash-sharded dedup, RCCL all-to-all"},
             "components": comp, "kernels": c["kernels"], "roofline": roof, "cpu_baseline": cpu}

@@ -91,6 +91,18 @@ int sdgpu_cas_batch_device(sdgpu_ctx *ctx, const uint8_t *d_arena, uint64_t aren
                            const uint64_t *d_off, const uint32_t *d_len, uint32_t n,
                            uint8_t *d_out8, int32_t *d_status, void *stream);
 
+/* Pinned-host staged variant (the identifier's "pinned async staging", BASELINE
+ * config 5): the messages live in caller-owned PINNED host memory (e.g. where
+ * the pread of the cas windows landed, sdgpu_alloc_pinned), in file order
+ * (h_off ascending, 16-B aligned).  The library streams the arena through a
+ * ring of device slabs -- H2D on its own copy stream overlapped with K1 on
+ * `stream` -- and leaves the cas bytes in device memory (d_out8 [n][8],
+ * d_status [n] or NULL) for the grouping step.  Asynchronous: h_arena must
+ * stay untouched until sdgpu_sync; h_off/h_len are consumed before return. */
+int sdgpu_cas_stage_pinned(sdgpu_ctx *ctx, const uint8_t *h_arena, const uint64_t *h_off,
+                           const uint32_t *h_len, uint32_t n, uint8_t *d_out8, int32_t *d_status,
+                           void *stream);
+
 /* Path-based drop-in for generate_cas_id(path, size) (cas.rs:23): same reads
  * as the reference (open, header, 4 samples by seek, footer from the actual
  * end), hash on the GPU, out_hex = 16 lowercase hex chars + NUL. */
@@ -169,6 +181,20 @@ int sdgpu_shard_partition_device(sdgpu_ctx *ctx, const uint64_t *d_key, const ui
 int sdgpu_scatter_rep_device(sdgpu_ctx *ctx, const uint32_t *d_src, const uint32_t *d_pos,
                              uint64_t n, uint32_t *d_dst, uint64_t n_dst, const uint32_t *d_init,
                              int init, void *stream);
+
+/* ---- K7: Object link batch ------------------------------------------------------
+ * The write set of identifier_job_step (file_identifier/mod.rs:189-333) for a
+ * whole batch of rows, from the grouping's rep[]: rows with rep == own rank
+ * create an Object (object::create_many, mod.rs:243-297), the others connect
+ * to the Object of row rep (mod.rs:189-225); rows with d_valid[i] == 0 (I/O
+ * error, mod.rs:113,127) are in neither list.  Row i has rank d_rank[i]
+ * (d_rank NULL: first_rank + i).  Outputs (device): d_create[0..C) creator
+ * ranks, d_link_row/d_link_obj[0..L) (row rank, creator rank), both in row
+ * order; d_counts[0] = C, d_counts[1] = L.  Each output holds n entries. */
+int sdgpu_link_batch_device(sdgpu_ctx *ctx, const uint32_t *d_rep, const uint32_t *d_rank,
+                            const uint8_t *d_valid, uint32_t first_rank, uint64_t n,
+                            uint32_t *d_create, uint32_t *d_link_row, uint32_t *d_link_obj,
+                            uint32_t *d_counts, void *stream);
 
 /* ---- synthetic corpora (bench / tests; same content function as oracle/) ---- */
 int sdgpu_synth_cas_arena_device(sdgpu_ctx *ctx, const uint64_t *d_sizes, const uint64_t *d_seeds,

@@ -196,6 +196,23 @@ def group_reps(key: np.ndarray, has_key: np.ndarray, chunk_rows: int = 100) -> n
     return rep
 
 
+def link_batch(rep: np.ndarray, rank: np.ndarray | None = None, valid: np.ndarray | None = None,
+               first_rank: int = 0):
+    """Object write set of identifier_job_step for a batch of rows
+    (/root/reference/core/src/object/file_identifier/mod.rs:189-333): rows whose
+    grouping rep is their own rank get a new Object (create_many, :243-297),
+    the others connect to the Object of row rep (:189-225); rows whose metadata
+    failed (valid == 0, :113,127) stay orphans.  Returns (create, link_row,
+    link_obj) in row order."""
+    rep = np.asarray(rep, np.uint32)
+    r = (np.arange(rep.size, dtype=np.uint64) + first_rank).astype(np.uint32) if rank is None \
+        else np.asarray(rank, np.uint32)
+    v = np.ones(rep.size, bool) if valid is None else np.asarray(valid) != 0
+    create = r[v & (rep == r)]
+    lk = v & (rep != r)
+    return create, r[lk], rep[lk]
+
+
 def synth_dedup_rows(seed: int, total: int, distinct: int, first: int, n: int):
     key = np.zeros(n, np.uint64)
     has = np.zeros(n, np.uint8)

@@ -88,6 +88,31 @@ def cas_batch_device(arena, off, length, out=None, status=None, ctx=None, stream
     return out, status
 
 
+def cas_stage_pinned(h_arena, off, length, out=None, status=None, ctx=None, device=None,
+                     stream=None):
+    """K1 over messages in PINNED host memory (torch pinned uint8 tensor), in
+    file order, streamed H2D through device slabs overlapped with hashing
+    (sdgpu_cas_stage_pinned).  Returns device (out[n,8] uint8, status[n] int32);
+    asynchronous on `stream` -- keep h_arena alive until it has completed."""
+    import torch
+    if not h_arena.is_pinned():
+        raise ValueError("h_arena must be pinned host memory (pin_memory=True)")
+    dev = torch.device("cuda", device if device is not None else torch.cuda.current_device())
+    ctx = ctx or default_context(dev.index)
+    off = np.ascontiguousarray(off, np.uint64)
+    length = np.ascontiguousarray(length, np.uint32)
+    n = off.size
+    if out is None:
+        out = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+    if status is None:
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    check(ctx.lib.sdgpu_cas_stage_pinned(ctx.h, h_arena.data_ptr(), _ptr(off), _ptr(length), n,
+                                         out.data_ptr(), status.data_ptr(), s),
+          "sdgpu_cas_stage_pinned")
+    return out, status
+
+
 def hex_ids(out8: np.ndarray) -> list[str]:
     """`to_hex()[..16]` of each 8-byte cas digest prefix (cas.rs:61)."""
     return [bytes(r).hex() for r in np.asarray(out8, np.uint8).reshape(-1, 8)]

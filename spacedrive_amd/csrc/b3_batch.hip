@@ -676,6 +676,11 @@ __global__ __launch_bounds__(kThreads, kMinBlocks) void k_leaves3(
   }
 }
 
+// Fold lanes keep a CV stack of depth 5 in LDS (lane-minor, conflict-free):
+// enough for the <= 26 level-2 nodes of any cas message (<= 100 KiB); longer
+// staged messages fall back to the in-place pairwise fold.
+constexpr uint32_t kFoldStack = 5;
+
 __global__ __launch_bounds__(kThreads) void k_fold3(const uint32_t* __restrict__ len,
                                                     const uint32_t* __restrict__ unit_base,
                                                     const uint32_t* __restrict__ order,
@@ -683,6 +688,7 @@ __global__ __launch_bounds__(kThreads) void k_fold3(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ d_end,
                                                     uint32_t* __restrict__ cvs, uint32_t out_words,
                                                     uint32_t* __restrict__ out) {
+  __shared__ uint32_t stk[kFoldStack][8][kThreads];
   const uint32_t R = *d_r;
   const uint32_t i = R + blockIdx.x * kThreads + threadIdx.x;
   if (i >= *d_end) return;
@@ -690,8 +696,37 @@ __global__ __launch_bounds__(kThreads) void k_fold3(const uint32_t* __restrict__
   const uint32_t l = len[m];
   const uint32_t q = units_of(l);
   const uint32_t cnt = q + (n_chunks_of(l) > 4 * q ? 1u : 0u);
+  uint32_t* c = cvs + static_cast<uint64_t>(unit_base[m] + m) * 8;
   uint32_t r[8];
-  fold_root(cvs + static_cast<uint64_t>(unit_base[m] + m) * 8, cnt, r);
+  if (cnt > (1u << kFoldStack)) {
+    fold_root(c, cnt, r);
+  } else {
+    // BLAKE3's lazy-merge stack over the level-2 nodes: merge while the count
+    // of completed nodes is even, never merge the last node before the end.
+    uint32_t lf[8], nx[8];
+    uint32_t sp = 0;
+    load_cv(c, r);
+    for (uint32_t k = 0; k + 1 < cnt; ++k) {
+      load_cv(c + 8 * (k + 1), nx);  // next node, loaded ahead of the merges
+      for (uint32_t tot = k + 1; (tot & 1u) == 0; tot >>= 1) {
+        --sp;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) lf[w] = stk[sp][w][threadIdx.x];
+        b3_parent(r, lf, r, 0u);
+      }
+#pragma unroll
+      for (int w = 0; w < 8; ++w) stk[sp][w][threadIdx.x] = r[w];
+      ++sp;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) r[w] = nx[w];
+    }
+    while (sp > 0) {
+      --sp;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) lf[w] = stk[sp][w][threadIdx.x];
+      b3_parent(r, lf, r, sp == 0 ? B3_ROOT : 0u);
+    }
+  }
   for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = r[w];
 }
 

@@ -111,4 +111,13 @@ hipError_t shard_partition_launch(const uint64_t* key, const uint8_t* has_key,
 hipError_t scatter_rep_launch(const uint32_t* src, const uint32_t* pos, uint64_t n, uint32_t* dst,
                               uint64_t n_dst, const uint32_t* init, bool do_init, hipStream_t s);
 
+// ---- Object link batch (K7) ----------------------------------------------------
+size_t link_workspace_bytes(uint64_t n);
+// rank may be null (rank = first_rank + i), valid may be null (all rows valid).
+// d_counts[0] = rows creating an Object, d_counts[1] = rows linking to one.
+hipError_t link_batch_launch(const uint32_t* rep, const uint32_t* rank, const uint8_t* valid,
+                             uint32_t first_rank, uint64_t n, uint32_t* create, uint32_t* link_row,
+                             uint32_t* link_obj, uint32_t* d_counts, void* ws, hipStream_t s,
+                             KTimer* timer = nullptr);
+
 }  // namespace sdgpu

@@ -74,6 +74,7 @@ constexpr size_t kSlabBytes = size_t(256) << 20;   // pinned staging per slab
 constexpr uint32_t kSlabFiles = 1u << 16;          // files per slab
 constexpr size_t kSliceBytes = size_t(64) << 20;   // file_checksum slice = 2^16 chunks
 constexpr uint32_t kStageMaxMsg = 8u + (64u << 20);  // largest staged cas message
+constexpr size_t kStageSlabBytes = size_t(256) << 20;  // sdgpu_cas_stage_pinned device slab
 
 // Brackets kernels with HIP events on their own stream; elapsed times are
 // resolved (one sync per event pair) only when read.
@@ -140,7 +141,10 @@ struct sdgpu_ctx {
   hipStream_t stream = nullptr;
   hipStream_t last = nullptr;
   std::mutex mu;
-  DevBuf batch_ws, tree_ws, dedup_ws, shard_ws, io_a, io_b;
+  DevBuf batch_ws, tree_ws, dedup_ws, shard_ws, io_a, io_b, link_ws, stage_meta;
+  DevBuf stage_slab[3];
+  hipStream_t copy_stream = nullptr;  // H2D of staged slabs (SDMA), created on first use
+  hipEvent_t stage_copied[3] = {}, stage_freed[3] = {};
   PinBuf plan_pin;
   hipEvent_t plan_evt = nullptr;
   bool plan_pending = false;
@@ -530,8 +534,16 @@ int sdgpu_close(sdgpu_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   if (c->last && c->last != c->stream) (void)hipStreamSynchronize(c->last);
-  for (DevBuf* b : {&c->batch_ws, &c->tree_ws, &c->dedup_ws, &c->shard_ws, &c->io_a, &c->io_b})
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  for (DevBuf* b : {&c->batch_ws, &c->tree_ws, &c->dedup_ws, &c->shard_ws, &c->io_a, &c->io_b,
+                    &c->link_ws, &c->stage_meta, &c->stage_slab[0], &c->stage_slab[1],
+                    &c->stage_slab[2]})
     if (b->p) (void)hipFree(b->p);
+  for (int k = 0; k < 3; ++k) {
+    if (c->stage_copied[k]) (void)hipEventDestroy(c->stage_copied[k]);
+    if (c->stage_freed[k]) (void)hipEventDestroy(c->stage_freed[k]);
+  }
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->plan_pin.p) (void)hipHostFree(c->plan_pin.p);
   (void)hipEventDestroy(c->plan_evt);
   (void)hipStreamDestroy(c->stream);
@@ -598,6 +610,107 @@ int sdgpu_cas_batch_device(sdgpu_ctx* c, const uint8_t* d_arena, uint64_t arena_
   SD_TRY_RC(batch_work(c, n, arena_bytes / kChunkLen + n, w));
   SD_TRY(batch_hash_launch(d_arena, d_off, d_len, n, CAS_MAX_MSG_LEN, 2, d_out8, d_status, w, s,
                            c->kt()));
+  return 0;
+}
+
+// Pinned-host staged K1 (config 5): slabs of the caller's pinned arena are
+// copied H2D on the context's copy stream (SDMA) into a ring of three device
+// slabs while K1 hashes the previous slab on the compute stream; events order
+// copy k after the hash of slab k-3 and hash k after copy k.  No host packing:
+// the arena is the pinned buffer the file reads landed in.
+int sdgpu_cas_stage_pinned(sdgpu_ctx* c, const uint8_t* h_arena, const uint64_t* h_off,
+                           const uint32_t* h_len, uint32_t n, uint8_t* d_out8, int32_t* d_status,
+                           void* stream) {
+  if (!c || (n && (!h_arena || !h_off || !h_len || !d_out8))) return -EINVAL;
+  if (reinterpret_cast<uintptr_t>(h_arena) % 16 || reinterpret_cast<uintptr_t>(d_out8) % 4)
+    return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  if (n == 0) return 0;
+  // slab plan: consecutive files whose byte extent fits one slab
+  struct Piece {
+    uint32_t first, count;
+    uint64_t base, bytes;
+  };
+  std::vector<Piece> pieces;
+  uint64_t max_chunks = 0;
+  uint32_t max_count = 0;
+  {
+    uint32_t i = 0;
+    while (i < n) {
+      if (i && h_off[i] < h_off[i - 1]) return -EINVAL;  // arena must be in file order
+      const uint64_t base = h_off[i];
+      uint64_t end = base;
+      uint32_t j = i;
+      while (j < n && j - i < kSlabFiles) {
+        if (j > i && h_off[j] < h_off[j - 1]) return -EINVAL;
+        const uint64_t ext = h_len[j] <= CAS_MAX_MSG_LEN ? h_len[j] : 0;  // invalid: not read
+        const uint64_t e = std::max(end, h_off[j] + ext);
+        if (e - base > kStageSlabBytes && j > i) break;
+        end = e;
+        ++j;
+      }
+      pieces.push_back(Piece{i, j - i, base, end - base});
+      max_chunks = std::max<uint64_t>(max_chunks, (end - base) / kChunkLen + (j - i));
+      max_count = std::max(max_count, j - i);
+      i = j;
+    }
+  }
+  // device copies of the file table, slabs, events, copy stream
+  const size_t meta_off = align_up(8ull * n, 256);
+  SD_TRY_RC(ensure_dev(c, c->stage_meta, meta_off + 4ull * n));
+  uint64_t* d_off = static_cast<uint64_t*>(c->stage_meta.p);
+  uint32_t* d_len = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->stage_meta.p) + meta_off);
+  SD_TRY(hipMemcpyAsync(d_off, h_off, 8ull * n, hipMemcpyHostToDevice, s));
+  SD_TRY(hipMemcpyAsync(d_len, h_len, 4ull * n, hipMemcpyHostToDevice, s));
+  if (!c->copy_stream) {
+    SD_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (int k = 0; k < 3; ++k) {
+      SD_TRY(hipEventCreateWithFlags(&c->stage_copied[k], hipEventDisableTiming));
+      SD_TRY(hipEventCreateWithFlags(&c->stage_freed[k], hipEventDisableTiming));
+    }
+  }
+  for (int k = 0; k < 3; ++k) SD_TRY_RC(ensure_dev(c, c->stage_slab[k], kStageSlabBytes + 256));
+  BatchWork w;
+  SD_TRY_RC(batch_work(c, max_count, max_chunks, w));
+  // the copy stream starts after everything issued on s so far (slab reuse
+  // across calls, the file table copies above)
+  SD_TRY(hipEventRecord(c->stage_freed[0], s));
+  SD_TRY(hipStreamWaitEvent(c->copy_stream, c->stage_freed[0], 0));
+  for (size_t k = 0; k < pieces.size(); ++k) {
+    const Piece& pc = pieces[k];
+    const int r = static_cast<int>(k % 3);
+    uint8_t* slab = static_cast<uint8_t*>(c->stage_slab[r].p);
+    if (k >= 3) SD_TRY(hipStreamWaitEvent(c->copy_stream, c->stage_freed[r], 0));
+    SD_TRY(hipMemcpyAsync(slab, h_arena + pc.base, pc.bytes, hipMemcpyHostToDevice,
+                          c->copy_stream));
+    SD_TRY(hipEventRecord(c->stage_copied[r], c->copy_stream));
+    SD_TRY(hipStreamWaitEvent(s, c->stage_copied[r], 0));
+    // message i of the piece sits at slab + (off[i] - base): hand K1 an arena
+    // origin of slab - base (16-B aligned: slab and off are)
+    const uint8_t* origin = slab - pc.base;
+    SD_TRY(batch_hash_launch(origin, d_off + pc.first, d_len + pc.first, pc.count,
+                             CAS_MAX_MSG_LEN, 2, d_out8 + 8ull * pc.first,
+                             d_status ? d_status + pc.first : nullptr, w, s, c->kt()));
+    SD_TRY(hipEventRecord(c->stage_freed[r], s));
+  }
+  return 0;
+}
+
+int sdgpu_link_batch_device(sdgpu_ctx* c, const uint32_t* d_rep, const uint32_t* d_rank,
+                            const uint8_t* d_valid, uint32_t first_rank, uint64_t n,
+                            uint32_t* d_create, uint32_t* d_link_row, uint32_t* d_link_obj,
+                            uint32_t* d_counts, void* stream) {
+  if (!c || !d_counts || (n && (!d_rep || !d_create || !d_link_row || !d_link_obj)))
+    return -EINVAL;
+  if (n > 0xffffffffull) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  SD_TRY_RC(ensure_dev(c, c->link_ws, link_workspace_bytes(n)));
+  SD_TRY(link_batch_launch(d_rep, d_rank, d_valid, first_rank, n, d_create, d_link_row,
+                           d_link_obj, d_counts, c->link_ws.p, s, c->kt()));
   return 0;
 }
 

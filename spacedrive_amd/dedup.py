@@ -151,6 +151,30 @@ def sharded_group_reps(key, has_key, rank, chunk_rows: int = CHUNK_SIZE, group=N
     return ops.scatter(rep_sent, spos, n, rank)
 
 
+def link_batch_device(rep, rank=None, valid=None, first_rank: int = 0, ctx=None):
+    """K7 (sdgpu_link_batch_device): the Object write set of a batch of rows.
+
+    rep int32 (u32 ranks), rank int32 or None (= first_rank + i), valid uint8 or
+    None.  Returns device tensors (create, link_row, link_obj) trimmed to their
+    counts: creator ranks (object::create_many, file_identifier/mod.rs:243-297)
+    and (row, creator) connect pairs (mod.rs:189-225), both in row order."""
+    import torch
+    dev = rep.device
+    ctx = ctx or default_context(dev.index)
+    n = rep.numel()
+    create = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    lrow = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    lobj = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    counts = torch.zeros(2, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    check(ctx.lib.sdgpu_link_batch_device(
+        ctx.h, rep.data_ptr(), rank.data_ptr() if rank is not None else None,
+        valid.data_ptr() if valid is not None else None, first_rank, n, create.data_ptr(),
+        lrow.data_ptr(), lobj.data_ptr(), counts.data_ptr(), s), "sdgpu_link_batch_device")
+    c, l = (int(x) for x in counts.cpu().tolist())
+    return create[:c], lrow[:l], lobj[:l]
+
+
 def object_stats(rep: np.ndarray, has_key: np.ndarray, ok: np.ndarray | None = None):
     """(created, linked) Object counts the reference's job would report
     (identifier_job_step returns (total_created, updated_file_paths.len()),

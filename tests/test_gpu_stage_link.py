@@ -1,0 +1,90 @@
+"""GPU parity: pinned-host staged K1 (config 5 path) and the K7 Object link
+batch, both bit-exact against the oracle."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _pinned_arena(sizes, seeds):
+    import torch
+    arena, off, ln = O.synth_arena(sizes, seeds)
+    h = torch.empty(arena.size, dtype=torch.uint8).pin_memory()
+    h.numpy()[:] = arena
+    return h, arena, off, ln
+
+
+def test_stage_pinned_matches_oracle_across_many_slabs(ctx):
+    """~40k config-2 files (~1.7 GB of windows): several 256 MiB slabs cycle
+    through the 3-slab ring; every cas id vs the oracle."""
+    import torch
+    from spacedrive_amd import cas, corpus
+    sizes, seeds = corpus.config2_files(40_000, seed=31)
+    h, arena, off, ln = _pinned_arena(sizes, seeds)
+    out, st = cas.cas_stage_pinned(h, off, ln, ctx=ctx)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0
+    ref = O.cas_batch(arena, off, ln, threads=16)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    # a second call reuses the slab ring
+    out2, _ = cas.cas_stage_pinned(h, off, ln, ctx=ctx)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out2.cpu().numpy(), ref)
+
+
+def test_stage_pinned_edge_messages(ctx):
+    """Invalid lengths / misaligned offsets get -EINVAL; empty and tiny messages."""
+    import torch
+    from spacedrive_amd import cas
+    lens = np.array([0, 1, 1024, 1025, 4096, 4097, 57352, 102408, 102409, 64], np.uint32)
+    off = np.zeros(lens.size, np.uint64)
+    pos = 0
+    for i, n in enumerate(lens):
+        off[i] = pos
+        pos += (min(int(n), 102408) + 127) // 128 * 128
+    off[-1] = off[-2] + 8  # misaligned
+    rng = np.random.default_rng(5)
+    arena = rng.integers(0, 256, pos + 256, dtype=np.uint8)
+    h = torch.empty(arena.size, dtype=torch.uint8).pin_memory()
+    h.numpy()[:] = arena
+    out, st = cas.cas_stage_pinned(h, off, lens, ctx=ctx)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert st.tolist() == [0] * 8 + [-22, -22]
+    ref = O.cas_batch(arena, off[:8], lens[:8], threads=4)
+    np.testing.assert_array_equal(out.cpu().numpy()[:8], ref)
+    assert not out.cpu().numpy()[8:].any()
+
+
+def test_stage_pinned_rejects_unordered_arena(ctx):
+    import torch
+    from spacedrive_amd import cas
+    from spacedrive_amd._native import SdgpuError
+    h = torch.zeros(4096, dtype=torch.uint8).pin_memory()
+    with pytest.raises(SdgpuError):
+        cas.cas_stage_pinned(h, np.array([1024, 0], np.uint64), np.array([10, 10], np.uint32),
+                             ctx=ctx)
+
+
+@pytest.mark.parametrize("n,first_rank,with_valid", [(0, 0, False), (1, 0, False),
+                                                     (100_000, 0, True), (2_000_000, 7_000, True)])
+def test_link_batch_vs_oracle(ctx, n, first_rank, with_valid):
+    import torch
+    from spacedrive_amd import dedup
+    key, has, rank = O.synth_dedup_rows(4, max(n, 1) * 2, max(n, 1), 0, n)
+    rep_h = O.group_reps(key, has, 100) + np.uint32(first_rank)
+    valid = (np.random.default_rng(n).random(n) > 0.02).astype(np.uint8) if with_valid else None
+    d_rep = torch.from_numpy(rep_h.view(np.int32)).cuda()
+    d_valid = torch.from_numpy(valid).cuda() if valid is not None else None
+    c, lr, lo = dedup.link_batch_device(d_rep, None, d_valid, first_rank, ctx=ctx)
+    rc, rlr, rlo = O.link_batch(rep_h, None, valid, first_rank)
+    np.testing.assert_array_equal(c.cpu().numpy().view(np.uint32), rc)
+    np.testing.assert_array_equal(lr.cpu().numpy().view(np.uint32), rlr)
+    np.testing.assert_array_equal(lo.cpu().numpy().view(np.uint32), rlo)
+    # explicit ranks give the same lists
+    if n:
+        d_rank = torch.arange(first_rank, first_rank + n, dtype=torch.int64).to(torch.int32).cuda()
+        c2, lr2, lo2 = dedup.link_batch_device(d_rep, d_rank, d_valid, 0, ctx=ctx)
+        assert torch.equal(c2, c) and torch.equal(lr2, lr) and torch.equal(lo2, lo)
