@@ -18,6 +18,8 @@ warm-up, barrier + synchronize on both sides, max over ranks):
   checksum config 3: 64 x 4 GiB files per GPU, device-resident GB/s
   staged   config 5 shape: 250 k config-2 files per GPU whose windows sit in
            pinned host memory, streamed H2D + K1 + grouping + link batch files/s
+  dir      config 1: a real 10 k-file directory (sparse files, warm cache)
+           through sdgpu_identify_files (pread -> pinned -> K1)         files/s
 `roofline` is for the dominant kernel (K1 "cas_leaves"), timed live with HIP
 events on its launch stream; `cpu_baseline` times the scalar C oracle port of
 generate_cas_id's hashing on this host's cores over a bounded sample.
@@ -160,7 +162,7 @@ class Runner:
             k1()
             key = out.view(torch.int64).view(-1)
             rep = dedup.sharded_group_reps(key, has, grank, 100, ops=ops)
-            dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx)
+            dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx, trim=False)
 
         # K1 alone, with live per-kernel event timing on its launch stream
         self.ctx.set_timing(True)
@@ -231,7 +233,7 @@ class Runner:
             cas.cas_stage_pinned(h_arena, off, ln, out, st, ctx=self.ctx)
             key = out.view(torch.int64).view(-1)
             rep = dedup.sharded_group_reps(key, has, grank, 100, ops=ops)
-            dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx)
+            dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx, trim=False)
 
         t = self.timed(step, steps, warmup)
         assert int(st.abs().sum()) == 0
@@ -245,6 +247,35 @@ class Runner:
                                        "memory, staged H2D (3-slab ring) + K1 + sharded grouping "
                                        "+ Object link batch",
                            "files_per_gpu": n, "window_bytes_per_gpu": window_bytes}}
+
+    # ---------------------------------------------------------------- config 1
+    def run_dir(self, steps):
+        """Config 1: the reference's CPU-runnable case -- identify a synthetic
+        10 k-file directory (mixed 1 KiB-10 MiB, sparse) from real files:
+        stat sizes given, pread of the cas windows into pinned slabs by a thread
+        pool, H2D + K1 (sdgpu_identify_files).  Warm page cache (one untimed pass)."""
+        import shutil
+        import tempfile
+        from spacedrive_amd import corpus, file_identifier as fi
+        root = tempfile.mkdtemp(prefix=f"sd_cfg1_r{self.rank}_")
+        try:
+            paths, sizes = corpus.write_config1_dir(root, self.args.dir_files, seed=1)
+            fi.identify(paths, sizes=sizes, ctx=self.ctx)  # warm page cache
+            self.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                res = fi.identify(paths, sizes=sizes, ctx=self.ctx)
+            dt = self.max_over_ranks(time.perf_counter() - t0)
+            assert np.all(res.status == 0)
+            self._dir_sample = (paths, sizes, root)
+            return {"value": self.world * len(paths) * steps / dt, "unit": "files/s",
+                    "ms_per_step": 1e3 * dt / steps,
+                    "config": {"workload": "config1: 10k-file directory, log-uniform 1 KiB-10 MiB, "
+                                           "sparse files, warm page cache, real pread I/O",
+                               "files_per_gpu": len(paths)}}
+        except BaseException:
+            shutil.rmtree(root, ignore_errors=True)
+            raise
 
     # ---------------------------------------------------------------- config 4
     def run_dedup(self, steps, warmup):
@@ -321,7 +352,23 @@ class Runner:
         for _ in range(reps):
             O.cas_batch(host, h_off, h_len, threads)
         dt = time.perf_counter() - t0
+        dir_res = None
+        if getattr(self, "_dir_sample", None):
+            import shutil
+            from concurrent.futures import ThreadPoolExecutor
+            paths, sizes, root = self._dir_sample
+            with ThreadPoolExecutor(threads) as ex:  # the C oracle releases the GIL
+                list(ex.map(O.cas_id_path, paths[:200], sizes[:200].tolist()))
+                t0 = time.perf_counter()
+                list(ex.map(O.cas_id_path, paths, sizes.tolist()))
+                ddt = time.perf_counter() - t0
+            dir_res = {"value": len(paths) / ddt, "unit": "files/s", "threads": threads,
+                       "sample": f"config 1: {len(paths)} files, oracle cas_id_path (open, "
+                                 f"header/sample/footer reads, scalar BLAKE3), warm cache"}
+            shutil.rmtree(root, ignore_errors=True)
+            self._dir_sample = None
         return {"value": reps * m / dt, "unit": "files/s", "cores": threads, "kind": "port",
+                "config1_dir": dir_res,
                 "sample": f"first {m} files of config 2 (their {int(h_len.sum())} window bytes "
                           f"in host RAM) hashed {reps}x, scalar C BLAKE3 oracle "
                           f"(oracle/sd_oracle.c), {threads} threads, {dt:.1f} s wall"}
@@ -338,7 +385,8 @@ def main():
     ap.add_argument("--checksum-bytes", type=int, default=1 << 32)
     ap.add_argument("--cpu-files", type=int, default=100_000)
     ap.add_argument("--staged-files", type=int, default=250_000)
-    ap.add_argument("--components", default="cas,dedup,checksum,staged")
+    ap.add_argument("--dir-files", type=int, default=10_000)
+    ap.add_argument("--components", default="cas,dedup,checksum,staged,dir")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -353,6 +401,10 @@ def main():
         f"(spec {VALU_PEAK_SPEC / 1e12:.1f}); per class {json.dumps(classes)}")
     c = R.run_cas(args.steps, args.warmup)
     log("cas:", json.dumps(c["cas"]), json.dumps(c["kernels"]))
+    dir_comp = None
+    if "dir" in comps:
+        dir_comp = R.run_dir(max(1, min(args.steps, 3)))
+        log("dir:", json.dumps(dir_comp))
     cpu = None
     if R.rank == 0 and not args.no_cpu:
         cpu = R.cpu_baseline()
@@ -360,6 +412,8 @@ def main():
     R._cpu_sample = None
     torch.cuda.empty_cache()
     comp = {"cas": c["cas"], "identifier_job": c["job"]}
+    if dir_comp:
+        comp["dir"] = dir_comp
     if "dedup" in comps:
         d = R.run_dedup(args.steps, args.warmup)
         log("dedup:", json.dumps(d))

@@ -136,6 +136,15 @@ int sdgpu_subtree_device(sdgpu_ctx *ctx, const uint8_t *d_bytes, uint64_t len,
  * lowercase hex chars + NUL. */
 int sdgpu_file_checksum(sdgpu_ctx *ctx, const char *path, char out_hex[65]);
 
+/* Batched object validator: file_checksum of n files (validator_job.rs:126-169
+ * checksums one file per job step).  Files up to 16 MiB are read whole by a
+ * thread pool into pinned slabs and each slab is hashed by one tree launch;
+ * larger files are streamed like sdgpu_file_checksum.  out32[i] = BLAKE3 of
+ * file i (lowercase hex of it = the reference's integrity_checksum);
+ * status[i] = 0 or -errno (out32 zeroed), status may be NULL. */
+int sdgpu_checksum_files(sdgpu_ctx *ctx, const char *const *paths, uint32_t n,
+                         uint8_t (*out32)[32], int32_t *status);
+
 /* ---- K4-K6: cas_id -> Object grouping ------------------------------------------
  * Replaces the Object link/create decisions of identifier_job_step
  * (file_identifier/mod.rs:167-333) over the orphan rows in ascending id order

@@ -116,3 +116,40 @@ def synth_dedup_rows_device(seed: int, total_rows: int, distinct: int, first: in
                                                 key.data_ptr(), has.data_ptr(), rank.data_ptr(),
                                                 s), "sdgpu_synth_dedup_rows_device")
     return key, has, rank
+
+
+def config1_sizes(n: int = 10_000, seed: int = 1) -> np.ndarray:
+    """Config 1: sizes log-uniform in [1 KiB, 10 MiB] (seed 1)."""
+    rng = np.random.default_rng(seed)
+    return np.rint(np.exp(rng.uniform(np.log(1024.0), np.log(10.0 * (1 << 20)), n))).astype(
+        np.uint64)
+
+
+def write_config1_dir(root: str, n: int = 10_000, seed: int = 1) -> tuple[list[str], np.ndarray]:
+    """Writes BASELINE config 1 (a synthetic n-file directory, mixed 1 KiB-10 MiB)
+    under `root`.  Files are SPARSE: only the bytes generate_cas_id reads
+    (cas.rs:27-58: the whole file up to 100 KiB, else header, the 4 samples and
+    the footer) hold random data; the rest is a hole (ftruncate), so 10 k files
+    cost ~0.4 GB of disk.  Returns (paths, sizes)."""
+    import os
+    sizes = config1_sizes(n, seed)
+    rng = np.random.default_rng(seed + 1)
+    os.makedirs(root, exist_ok=True)
+    paths = []
+    hf, ss = 8192, 10240
+    for i, sz in enumerate(sizes.tolist()):
+        p = os.path.join(root, f"f{i:05d}.bin")
+        fd = os.open(p, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        try:
+            if sz <= 100 * 1024:
+                os.pwrite(fd, rng.integers(0, 256, sz, dtype=np.uint8).tobytes(), 0)
+            else:
+                jump = (sz - 2 * hf) // 4
+                spans = [(0, hf)] + [(hf + k * jump, ss) for k in range(4)] + [(sz - hf, hf)]
+                for o, ln in spans:
+                    os.pwrite(fd, rng.integers(0, 256, ln, dtype=np.uint8).tobytes(), o)
+                os.ftruncate(fd, sz)
+        finally:
+            os.close(fd)
+        paths.append(p)
+    return paths, sizes

@@ -75,6 +75,7 @@ constexpr uint32_t kSlabFiles = 1u << 16;          // files per slab
 constexpr size_t kSliceBytes = size_t(64) << 20;   // file_checksum slice = 2^16 chunks
 constexpr uint32_t kStageMaxMsg = 8u + (64u << 20);  // largest staged cas message
 constexpr size_t kStageSlabBytes = size_t(256) << 20;  // sdgpu_cas_stage_pinned device slab
+constexpr uint64_t kValidateBatchMax = uint64_t(16) << 20;  // larger files are streamed
 
 // Brackets kernels with HIP events on their own stream; elapsed times are
 // resolved (one sync per event pair) only when read.
@@ -838,10 +839,10 @@ int sdgpu_checksum(sdgpu_ctx* c, const void* bytes, uint64_t len, uint8_t out32[
   return 0;
 }
 
-int sdgpu_file_checksum(sdgpu_ctx* c, const char* path, char out_hex[65]) {
-  if (!c || !path || !out_hex) return -EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  SD_TRY(hipSetDevice(c->device));
+namespace {
+
+// file_checksum of one file, streamed in slices (context lock held).
+int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
   const int fd = open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return -errno;
   hipStream_t s = c->stream;
@@ -933,7 +934,180 @@ int sdgpu_file_checksum(sdgpu_ctx* c, const char* path, char out_hex[65]) {
   }
   close(fd);
   if (rc) return rc;
-  to_hex(out.data(), 32, out_hex);
+  memcpy(digest, out.data(), 32);
+  return 0;
+}
+
+// Reads the whole file into dst (capacity cap).  Returns its length, -errno,
+// or -EFBIG when it holds more than cap bytes (grown since stat).
+int64_t read_whole(const char* path, uint8_t* dst, size_t cap) {
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  size_t len = 0;
+  int64_t rc = 0;
+  for (;;) {
+    if (len == cap) {
+      uint8_t probe;
+      const ssize_t r = read(fd, &probe, 1);
+      rc = r == 0 ? 0 : (r < 0 ? -errno : -EFBIG);
+      break;
+    }
+    const ssize_t r = read(fd, dst + len, cap - len);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      rc = -errno;
+      break;
+    }
+    if (r == 0) break;
+    len += static_cast<size_t>(r);
+  }
+  close(fd);
+  return rc ? rc : static_cast<int64_t>(len);
+}
+
+}  // namespace
+
+int sdgpu_file_checksum(sdgpu_ctx* c, const char* path, char out_hex[65]) {
+  if (!c || !path || !out_hex) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  uint8_t d[32];
+  SD_TRY_RC(file_checksum_locked(c, path, d));
+  to_hex(d, 32, out_hex);
+  return 0;
+}
+
+// Batched object validator (validator_job.rs:126-169 runs file_checksum one
+// file per step): files up to kValidateBatchMax are read whole by a thread
+// pool into pinned slabs; each slab is hashed by ONE tree launch (a segment
+// per file, K2/K3) while the next slab is read.  Larger files -- and files
+// that grew past their reserved room -- take the streamed single-file path.
+int sdgpu_checksum_files(sdgpu_ctx* c, const char* const* paths, uint32_t n, uint8_t (*out32)[32],
+                         int32_t* status) {
+  if (!c || (n && (!paths || !out32))) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  c->last = s;
+  std::vector<int64_t> size(n);
+  parallel_for(n, [&](uint32_t i) {
+    struct stat st;
+    if (stat(paths[i], &st) != 0) size[i] = -errno;
+    else if (S_ISDIR(st.st_mode)) size[i] = -EISDIR;
+    else size[i] = st.st_size;
+  });
+  std::vector<int32_t> st(n, 0);
+  std::vector<uint8_t> deferred(n, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (size[i] < 0) st[i] = static_cast<int32_t>(size[i]);
+    else if (static_cast<uint64_t>(size[i]) > kValidateBatchMax) deferred[i] = 1;
+  }
+  struct VSlab {
+    PinBuf h;
+    DevBuf d;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+    std::vector<uint32_t> files;
+  };
+  const size_t out_off = kSlabBytes;  // [arena | digests]
+  const size_t slab_total = out_off + 32ull * kSlabFiles;
+  VSlab slabs[2];
+  int rc = 0;
+  for (auto& sl : slabs) {
+    if ((rc = ensure_pin(sl.h, slab_total)) != 0) break;
+    if ((rc = ensure_dev(c, sl.d, slab_total)) != 0) break;
+    if (hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+  }
+  auto drain = [&](VSlab& sl) -> int {
+    if (!sl.busy) return 0;
+    if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
+    sl.busy = false;
+    const uint8_t* dg = static_cast<const uint8_t*>(sl.h.p) + out_off;
+    for (size_t j = 0; j < sl.files.size(); ++j) memcpy(out32[sl.files[j]], dg + 32 * j, 32);
+    return 0;
+  };
+  uint32_t i = 0, k = 0;
+  std::vector<uint64_t> off, cap;
+  std::vector<int64_t> got;
+  while (rc == 0) {
+    while (i < n && (st[i] != 0 || deferred[i])) ++i;
+    if (i >= n) break;
+    VSlab& sl = slabs[k & 1];
+    if ((rc = drain(sl)) != 0) break;
+    sl.files.clear();
+    off.clear();
+    cap.clear();
+    uint64_t pos = 0;
+    for (; i < n && sl.files.size() < kSlabFiles; ++i) {
+      if (st[i] != 0 || deferred[i]) continue;
+      const uint64_t room = align_up(static_cast<uint64_t>(size[i]) + 4096, 256);
+      if (pos + room > kSlabBytes) break;
+      sl.files.push_back(i);
+      off.push_back(pos);
+      cap.push_back(room);
+      pos += room;
+    }
+    const uint32_t cnt = static_cast<uint32_t>(sl.files.size());
+    got.assign(cnt, 0);
+    uint8_t* hb = static_cast<uint8_t*>(sl.h.p);
+    parallel_for(cnt, [&](uint32_t j) {
+      got[j] = read_whole(paths[sl.files[j]], hb + off[j], static_cast<size_t>(cap[j]));
+    });
+    uint8_t* db = static_cast<uint8_t*>(sl.d.p);
+    std::vector<TreeSeg> segs;
+    std::vector<uint32_t> kept;
+    segs.reserve(cnt);
+    for (uint32_t j = 0; j < cnt; ++j) {
+      const uint32_t f = sl.files[j];
+      if (got[j] == -EFBIG) {
+        deferred[f] = 1;  // grew since stat: stream it
+        continue;
+      }
+      if (got[j] < 0) {
+        st[f] = static_cast<int32_t>(got[j]);
+        continue;
+      }
+      segs.push_back(TreeSeg{db + off[j], static_cast<uint64_t>(got[j]), 0, 1, 0});
+      kept.push_back(f);
+    }
+    sl.files = kept;
+    if (segs.empty()) continue;
+    if (hipMemcpyAsync(db, hb, pos, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+    if ((rc = tree_launch(c, segs.data(), static_cast<uint32_t>(segs.size()), false, db + out_off,
+                          s)) != 0)
+      break;
+    if (hipMemcpyAsync(hb + out_off, db + out_off, 32 * segs.size(), hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipEventRecord(sl.done, s) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+    sl.busy = true;
+    ++k;
+  }
+  for (auto& sl : slabs) {
+    const int r2 = drain(sl);
+    if (rc == 0) rc = r2;
+  }
+  (void)hipStreamSynchronize(s);
+  for (auto& sl : slabs) {
+    if (sl.done) (void)hipEventDestroy(sl.done);
+    if (sl.h.p) (void)hipHostFree(sl.h.p);
+    if (sl.d.p) (void)hipFree(sl.d.p);
+  }
+  if (rc) return rc;
+  for (uint32_t j = 0; j < n; ++j)
+    if (deferred[j] && st[j] == 0) st[j] = file_checksum_locked(c, paths[j], out32[j]);
+  for (uint32_t j = 0; j < n; ++j) {
+    if (st[j] != 0) memset(out32[j], 0, 32);
+    if (status) status[j] = st[j];
+  }
   return 0;
 }
 

@@ -151,13 +151,16 @@ def sharded_group_reps(key, has_key, rank, chunk_rows: int = CHUNK_SIZE, group=N
     return ops.scatter(rep_sent, spos, n, rank)
 
 
-def link_batch_device(rep, rank=None, valid=None, first_rank: int = 0, ctx=None):
+def link_batch_device(rep, rank=None, valid=None, first_rank: int = 0, ctx=None,
+                      trim: bool = True):
     """K7 (sdgpu_link_batch_device): the Object write set of a batch of rows.
 
     rep int32 (u32 ranks), rank int32 or None (= first_rank + i), valid uint8 or
     None.  Returns device tensors (create, link_row, link_obj) trimmed to their
     counts: creator ranks (object::create_many, file_identifier/mod.rs:243-297)
-    and (row, creator) connect pairs (mod.rs:189-225), both in row order."""
+    and (row, creator) connect pairs (mod.rs:189-225), both in row order.
+    trim=False skips the host read of the counts (no synchronisation) and
+    returns the full-length lists plus the device counts tensor [C, L]."""
     import torch
     dev = rep.device
     ctx = ctx or default_context(dev.index)
@@ -171,6 +174,8 @@ def link_batch_device(rep, rank=None, valid=None, first_rank: int = 0, ctx=None)
         ctx.h, rep.data_ptr(), rank.data_ptr() if rank is not None else None,
         valid.data_ptr() if valid is not None else None, first_rank, n, create.data_ptr(),
         lrow.data_ptr(), lobj.data_ptr(), counts.data_ptr(), s), "sdgpu_link_batch_device")
+    if not trim:
+        return create, lrow, lobj, counts
     c, l = (int(x) for x in counts.cpu().tolist())
     return create[:c], lrow[:l], lobj[:l]
 

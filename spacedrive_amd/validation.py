@@ -8,6 +8,10 @@
   values are folded on the GPU.
 * ``checksum_bytes(buf)``, ``checksum_batch_device(tensors)`` for in-memory and
   device-resident data (the object-validator bench, BASELINE config 3).
+* ``checksum_files(paths)`` / ``validator_job(paths)``: the object validator
+  job (core/src/object/validation/validator_job.rs:35-171) over many rows at
+  once -- small files are read whole into pinned slabs and hashed one tree
+  launch per slab (sdgpu_checksum_files) instead of one file per job step.
 """
 from __future__ import annotations
 
@@ -29,6 +33,30 @@ def file_checksum(path, ctx=None) -> str:
     if rc:
         raise SdgpuError(rc, os.fspath(path))
     return out.value.decode()
+
+
+def checksum_files(paths, ctx=None):
+    """(digests [n, 32] uint8, status [n] int32) of many files in one call."""
+    ctx = ctx or default_context()
+    n = len(paths)
+    enc = [os.fsencode(os.fspath(p)) for p in paths]
+    arr = (ctypes.c_char_p * max(n, 1))(*enc)
+    out = np.zeros((n, 32), np.uint8)
+    status = np.zeros(n, np.int32)
+    check(ctx.lib.sdgpu_checksum_files(ctx.h, arr, n, out.ctypes.data, status.ctypes.data),
+          "sdgpu_checksum_files")
+    return out, status
+
+
+def validator_job(paths, ctx=None):
+    """ObjectValidatorJob (validator_job.rs:126-169) over the rows whose
+    integrity_checksum is NULL: {path: checksum hex} for the rows written;
+    like the reference, the first I/O error fails the job (FileIOError)."""
+    out, status = checksum_files(paths, ctx)
+    for i, p in enumerate(paths):
+        if status[i]:
+            raise SdgpuError(int(status[i]), os.fspath(p))
+    return {os.fspath(p): bytes(out[i]).hex() for i, p in enumerate(paths)}
 
 
 def checksum_bytes(data, ctx=None) -> bytes:

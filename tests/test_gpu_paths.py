@@ -98,3 +98,29 @@ def test_file_metadata(ctx, files):
     m = fi.file_metadata(os.path.dirname(files[5]), os.path.basename(files[5]), ctx)
     assert m.cas_id == O.cas_id_path(files[5], SIZES[5]) and m.size == SIZES[5]
     assert fi.file_metadata(os.path.dirname(files[0]), os.path.basename(files[0]), ctx).cas_id is None
+
+
+def test_checksum_files_batched_validator(ctx, tmp_path):
+    """sdgpu_checksum_files over a directory of mixed files: tiny, chunk
+    boundaries, > 1 slab in total, one streamed (> 16 MiB) file, and errors."""
+    from spacedrive_amd import validation
+    sizes = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 16 * 1024 + 1, 1 << 20, (1 << 20) + 1,
+             5_000_000, 17 << 20]
+    rng = np.random.default_rng(3)
+    sizes += [int(x) for x in rng.integers(0, 3_000_000, 150)]  # ~225 MB: crosses a slab
+    paths = []
+    for i, s in enumerate(sizes):
+        p = tmp_path / f"v{i}"
+        p.write_bytes(O.synth_file_bytes(4000 + i, 0, s))
+        paths.append(str(p))
+    paths += [str(tmp_path / "missing"), str(tmp_path)]
+    out, st = validation.checksum_files(paths, ctx)
+    assert st[-2] == -2 and st[-1] == -21  # ENOENT, EISDIR
+    for i, p in enumerate(paths[:-2]):
+        assert st[i] == 0, (i, st[i])
+        assert bytes(out[i]).hex() == O.file_checksum_path(p), (i, sizes[i])
+    assert not out[-2:].any()
+    job = validation.validator_job(paths[:20], ctx)
+    assert job[paths[5]] == O.file_checksum_path(paths[5])
+    with pytest.raises(OSError):
+        validation.validator_job(paths, ctx)
