@@ -410,6 +410,10 @@ def main():
         cpu = R.cpu_baseline()
         log("cpu:", json.dumps(cpu))
     R._cpu_sample = None
+    if getattr(R, "_dir_sample", None):  # ranks > 0, or --no-cpu: drop the config-1 files
+        import shutil
+        shutil.rmtree(R._dir_sample[2], ignore_errors=True)
+        R._dir_sample = None
     torch.cuda.empty_cache()
     comp = {"cas": c["cas"], "identifier_job": c["job"]}
     if dir_comp:

@@ -41,9 +41,10 @@ namespace {
 
 constexpr int kPartThreads = 1024;
 constexpr uint32_t kPartBlocks = 256;  // one per CU
-constexpr int kGroupThreads = 256;
-constexpr uint32_t kLdsSlots = 4096;   // table slots in LDS
-constexpr uint32_t kLdsCap = 3072;     // rows per bucket handled in LDS (load <= 75%)
+constexpr int kGroupThreads = 1024;
+constexpr uint32_t kLdsSlots = 8192;   // table slots in LDS (96 KiB: one bucket per CU)
+constexpr uint32_t kLdsCap = 6144;     // rows per bucket handled in LDS (load <= 75%)
+constexpr uint64_t kBucketRows = 3072; // target mean rows per bucket (bucket_bits_for)
 constexpr uint64_t kEmpty = ~0ull;
 
 __device__ __forceinline__ uint32_t digit_of(uint64_t key, uint32_t skip, uint32_t bits) {
@@ -56,6 +57,10 @@ __device__ __forceinline__ void tile_of(uint64_t n, uint64_t& t0, uint64_t& t1) 
   t1 = min<uint64_t>(n, t0 + per);
 }
 
+// Rows per thread per step of the partition kernels: the loads of a step are
+// issued back to back, so one tile costs a few memory latencies, not one per row.
+constexpr int kUnroll = 8;
+
 __global__ __launch_bounds__(kPartThreads) void k_part_hist(const uint64_t* __restrict__ key,
                                                             const uint8_t* __restrict__ valid,
                                                             uint64_t n, uint32_t skip,
@@ -67,9 +72,19 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(const uint64_t* __re
   __syncthreads();
   uint64_t t0, t1;
   tile_of(n, t0, t1);
-  for (uint64_t i = t0 + threadIdx.x; i < t1; i += kPartThreads) {
-    if (valid && !valid[i]) continue;
-    atomicAdd(&cnt[digit_of(key[i], skip, bits)], 1u);
+  for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += kUnroll * kPartThreads) {
+    uint64_t k[kUnroll];
+    bool v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
+      v[u] = i < t1;
+      k[u] = v[u] ? key[i] : 0;
+      if (valid && v[u]) v[u] = valid[i] != 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+      if (v[u]) atomicAdd(&cnt[digit_of(k[u], skip, bits)], 1u);
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
@@ -88,19 +103,35 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
   __syncthreads();
   uint64_t t0, t1;
   tile_of(n, t0, t1);
-  for (uint64_t i = t0 + threadIdx.x; i < t1; i += kPartThreads) {
-    if (valid && !valid[i]) continue;
-    const uint64_t k = key[i];
-    const uint32_t p = atomicAdd(&cur[digit_of(k, skip, bits)], 1u);
-    out_key[p] = k;
-    out_rank[p] = rank ? rank[i] : static_cast<uint32_t>(i);
-    out_pos[p] = static_cast<uint32_t>(i);
+  constexpr int U = kUnroll / 2;
+  for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += U * kPartThreads) {
+    uint64_t k[U];
+    uint32_t r[U];
+    bool v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
+      v[u] = i < t1;
+      k[u] = v[u] ? key[i] : 0;
+      r[u] = v[u] ? (rank ? rank[i] : static_cast<uint32_t>(i)) : 0u;
+      if (valid && v[u]) v[u] = valid[i] != 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!v[u]) continue;
+      const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
+      const uint32_t p = atomicAdd(&cur[digit_of(k[u], skip, bits)], 1u);
+      out_key[p] = k[u];
+      out_rank[p] = r[u];
+      out_pos[p] = static_cast<uint32_t>(i);
+    }
   }
 }
 
 // Bucket partition writing ONE 16-byte record {key lo, key hi, rank, row} per
-// row (a single scattered store instead of three).  Rows without a key are
-// not partitioned; their rep (= their own rank) is written here directly.
+// row (a single scattered store instead of three).  Every row's rep is first
+// set to its own rank here (one coalesced store); rows without a key are not
+// partitioned, and K5 rewrites only the rows that link to an earlier chunk.
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
     const uint64_t* __restrict__ key, const uint32_t* __restrict__ rank,
     const uint8_t* __restrict__ valid, uint64_t n, uint32_t skip, uint32_t bits,
@@ -112,16 +143,30 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
   __syncthreads();
   uint64_t t0, t1;
   tile_of(n, t0, t1);
-  for (uint64_t i = t0 + threadIdx.x; i < t1; i += kPartThreads) {
-    const uint32_t r = rank ? rank[i] : static_cast<uint32_t>(i);
-    if (valid && !valid[i]) {
-      rep[i] = r;
-      continue;
+  constexpr int U = kUnroll / 2;
+  for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += U * kPartThreads) {
+    uint64_t k[U];
+    uint32_t r[U];
+    bool in[U], v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
+      in[u] = i < t1;
+      k[u] = in[u] ? key[i] : 0;
+      r[u] = in[u] ? (rank ? rank[i] : static_cast<uint32_t>(i)) : 0u;
+      v[u] = in[u] && (!valid || valid[i] != 0);
     }
-    const uint64_t k = key[i];
-    const uint32_t p = atomicAdd(&cur[digit_of(k, skip, bits)], 1u);
-    rec[p] = make_uint4(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32), r,
-                        static_cast<uint32_t>(i));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
+      // every row starts as its own Object (coalesced store): rows without a
+      // key stay so (mod.rs:238-239); K5 overwrites only the rows that link
+      if (in[u]) rep[i] = r[u];
+      if (!v[u]) continue;
+      const uint32_t p = atomicAdd(&cur[digit_of(k[u], skip, bits)], 1u);
+      rec[p] = make_uint4(static_cast<uint32_t>(k[u]), static_cast<uint32_t>(k[u] >> 32), r[u],
+                          static_cast<uint32_t>(i));
+    }
   }
 }
 
@@ -152,6 +197,17 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
     tk = gkey + 4ull * start;
     tm = gmin + 4ull * start;
   }
+  // LDS-sized bucket: every thread loads its (at most kPer) records at once
+  // and keeps them in registers for both phases.
+  constexpr int kPer = (kLdsCap + kGroupThreads - 1) / kGroupThreads;
+  uint4 q_reg[kPer];
+  if (in_lds) {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const uint32_t i = start + threadIdx.x + j * kGroupThreads;
+      q_reg[j] = i < end ? rec[i] : make_uint4(0, 0, 0, 0);
+    }
+  }
   for (uint32_t s = threadIdx.x; s < tsize; s += kGroupThreads) {
     tk[s] = kEmpty;
     tm[s] = 0xFFFFFFFFu;
@@ -159,6 +215,46 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
   if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
   __syncthreads();
   const uint32_t mask = tsize - 1;
+  if (in_lds) {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (start + threadIdx.x + j * kGroupThreads >= end) break;
+      const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
+      const uint32_t r = q_reg[j].z;
+      if (k == kEmpty) {
+        atomicMin(&special_min, r);
+        continue;
+      }
+      uint32_t h = slot_hash(k) & mask;
+      for (;;) {
+        const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tk[h]),
+                                        static_cast<unsigned long long>(kEmpty),
+                                        static_cast<unsigned long long>(k));
+        if (prev == kEmpty || prev == k) {
+          atomicMin(&tm[h], r);
+          break;
+        }
+        h = (h + 1) & mask;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (start + threadIdx.x + j * kGroupThreads >= end) break;
+      const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
+      const uint32_t r = q_reg[j].z;
+      uint32_t f;
+      if (k == kEmpty) {
+        f = special_min;
+      } else {
+        uint32_t h = slot_hash(k) & mask;
+        while (tk[h] != k) h = (h + 1) & mask;
+        f = tm[h];
+      }
+      if (r / chunk_rows != f / chunk_rows) rep[q_reg[j].w] = f;  // others keep rank
+    }
+    return;
+  }
   for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
     const uint4 q = rec[i];
     const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
@@ -198,7 +294,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
       }
       f = in_lds ? tm[h] : __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    rep[q.w] = (r / chunk_rows == f / chunk_rows) ? r : f;
+    if (r / chunk_rows != f / chunk_rows) rep[q.w] = f;
   }
 }
 
@@ -229,7 +325,7 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 uint32_t bucket_bits_for(uint64_t n) {
   uint32_t bits = 1;
-  while (bits < 13 && (n >> bits) > 1024) ++bits;
+  while (bits < 13 && (n >> bits) > kBucketRows) ++bits;
   return bits;
 }
 
