@@ -277,6 +277,39 @@ class Runner:
             shutil.rmtree(root, ignore_errors=True)
             raise
 
+    # ------------------------------------------------ single-file latency
+    def run_single(self, calls=200):
+        """Latency of the single-file drop-ins the watcher / non-indexed
+        callers use (watcher/utils.rs:236,411,467; non_indexed.rs:161):
+        generate_cas_id(path, size) and file_checksum(path), one call at a time,
+        warm page cache.  Median microseconds per call."""
+        import tempfile
+        from spacedrive_amd import cas, validation
+        root = tempfile.mkdtemp(prefix=f"sd_single_r{self.rank}_")
+        rng = np.random.default_rng(7)
+        res = {}
+        try:
+            for name, size in (("4KiB", 4096), ("1MiB", 1 << 20)):
+                p = os.path.join(root, name)
+                rng.integers(0, 256, size, dtype=np.uint8).tofile(p)
+                for fn_name, fn in (("generate_cas_id", lambda: cas.generate_cas_id(p, size,
+                                                                                   self.ctx)),
+                                    ("file_checksum", lambda: validation.file_checksum(p,
+                                                                                       self.ctx))):
+                    for _ in range(10):
+                        fn()
+                    ts = []
+                    for _ in range(calls):
+                        t0 = time.perf_counter()
+                        fn()
+                        ts.append(time.perf_counter() - t0)
+                    res[f"{fn_name}_{name}_us"] = float(np.median(ts) * 1e6)
+            self._single_sample = [(os.path.join(root, n), s) for n, s in
+                                   (("4KiB", 4096), ("1MiB", 1 << 20))]
+        finally:
+            self._single_root = root
+        return res
+
     # ---------------------------------------------------------------- config 4
     def run_dedup(self, steps, warmup):
         torch = self.torch
@@ -367,8 +400,23 @@ class Runner:
                                  f"header/sample/footer reads, scalar BLAKE3), warm cache"}
             shutil.rmtree(root, ignore_errors=True)
             self._dir_sample = None
+        single = None
+        if getattr(self, "_single_sample", None):
+            single = {}
+            for p, size in self._single_sample:
+                name = os.path.basename(p)
+                for fn_name, fn in (("generate_cas_id", lambda: O.cas_id_path(p, size)),
+                                    ("file_checksum", lambda: O.file_checksum_path(p))):
+                    for _ in range(10):
+                        fn()
+                    ts = []
+                    for _ in range(200):
+                        t0 = time.perf_counter()
+                        fn()
+                        ts.append(time.perf_counter() - t0)
+                    single[f"{fn_name}_{name}_us"] = float(np.median(ts) * 1e6)
         return {"value": reps * m / dt, "unit": "files/s", "cores": threads, "kind": "port",
-                "config1_dir": dir_res,
+                "config1_dir": dir_res, "single_file_1thread": single,
                 "sample": f"first {m} files of config 2 (their {int(h_len.sum())} window bytes "
                           f"in host RAM) hashed {reps}x, scalar C BLAKE3 oracle "
                           f"(oracle/sd_oracle.c), {threads} threads, {dt:.1f} s wall"}
@@ -386,7 +434,7 @@ def main():
     ap.add_argument("--cpu-files", type=int, default=100_000)
     ap.add_argument("--staged-files", type=int, default=250_000)
     ap.add_argument("--dir-files", type=int, default=10_000)
-    ap.add_argument("--components", default="cas,dedup,checksum,staged,dir")
+    ap.add_argument("--components", default="cas,dedup,checksum,staged,dir,single")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -401,6 +449,10 @@ def main():
         f"(spec {VALU_PEAK_SPEC / 1e12:.1f}); per class {json.dumps(classes)}")
     c = R.run_cas(args.steps, args.warmup)
     log("cas:", json.dumps(c["cas"]), json.dumps(c["kernels"]))
+    single = None
+    if "single" in comps:
+        single = R.run_single()
+        log("single:", json.dumps(single))
     dir_comp = None
     if "dir" in comps:
         dir_comp = R.run_dir(max(1, min(args.steps, 3)))
@@ -410,6 +462,10 @@ def main():
         cpu = R.cpu_baseline()
         log("cpu:", json.dumps(cpu))
     R._cpu_sample = None
+    if getattr(R, "_single_root", None):
+        import shutil
+        shutil.rmtree(R._single_root, ignore_errors=True)
+        R._single_root = R._single_sample = None
     if getattr(R, "_dir_sample", None):  # ranks > 0, or --no-cpu: drop the config-1 files
         import shutil
         shutil.rmtree(R._dir_sample[2], ignore_errors=True)
@@ -418,6 +474,8 @@ def main():
     comp = {"cas": c["cas"], "identifier_job": c["job"]}
     if dir_comp:
         comp["dir"] = dir_comp
+    if single:
+        comp["single_file_latency"] = single
     if "dedup" in comps:
         d = R.run_dedup(args.steps, args.warmup)
         log("dedup:", json.dumps(d))

@@ -44,13 +44,33 @@ def main():
         wb = 1024 * sum(w) / len(w) if w else None
         res[k] = {"fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                   "hbm_bytes_per_launch": (fb or 0) + (wb or 0), "launches": max(len(f), len(w))}
+    # effective clock per kernel (MI355X_MICROARCH.md 'DVFS give-back'):
+    # GRBM_GUI_ACTIVE summed over the 8 XCDs / 8 / dispatch wall time
+    clk = {}
+    gpath = os.path.join(prof, "pmc_GRBM_GUI_ACTIVE_GRBM_COUNT", "pmc_counter_collection.csv")
+    if os.path.exists(gpath):
+        acc = collections.defaultdict(list)
+        with open(gpath) as f:
+            for r in csv.DictReader(f):
+                if r["Counter_Name"] != "GRBM_GUI_ACTIVE":
+                    continue
+                m = re.search(r"(k_\w+)", r["Kernel_Name"])
+                k = m.group(1) if m else r["Kernel_Name"][:80]
+                dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+                if dur > 0:
+                    acc[k].append(float(r["Counter_Value"]) / 8 / dur / 1e9)
+        clk = {k: sum(v) / len(v) for k, v in acc.items()}
+        for k, v in res.items():
+            if k in clk:
+                v["effective_clock_GHz"] = clk[k]
     doc = {"source": prof, "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count of "
            "16-B/lane streaming reads), WRITE_SIZE KiB x 1024", "kernels": res}
     with open(out, "w") as fo:
         json.dump(doc, fo, indent=1)
     for k, v in res.items():
         print(f"{k:32s} fetch {v['fetch_bytes_per_launch'] or 0:.4g} B  write "
-              f"{v['write_bytes_per_launch'] or 0:.4g} B")
+              f"{v['write_bytes_per_launch'] or 0:.4g} B  clock "
+              f"{v.get('effective_clock_GHz', 0):.3f} GHz")
 
 
 if __name__ == "__main__":

@@ -16,7 +16,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --outp
 if [ -n "$PMC" ]; then
   rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
   PARGS="--steps 1 --warmup 0 --no-cpu ${PMC_ARGS:---components cas}"
-  for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES"; do
+  for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
     N=$(echo $C | tr ' ' '_')
     timeout -s KILL 240 rocprofv3 --pmc $C -d "$OUT/pmc_$N" -o pmc --output-format csv \
       -- python3 bench.py $PARGS > "$OUT/pmc_$N.log" 2>&1 || { echo "pmc $C failed: $?"; exit 1; }

@@ -144,6 +144,13 @@ struct sdgpu_ctx {
   std::mutex mu;
   DevBuf batch_ws, tree_ws, dedup_ws, shard_ws, io_a, io_b, link_ws, stage_meta;
   DevBuf stage_slab[3];
+  // host staging of the path / host-buffer entry points (identify_files,
+  // cas_batch, generate_cas_id, checksum_files, file_checksum): two pinned and
+  // two device slabs kept for the context's lifetime, grown on demand, so a
+  // call pays no pinned allocation (a 256 MiB hipHostMalloc costs ~10^5 us)
+  PinBuf pipe_h[2];
+  DevBuf pipe_d[2];
+  hipEvent_t pipe_evt[2] = {};
   hipStream_t copy_stream = nullptr;  // H2D of staged slabs (SDMA), created on first use
   hipEvent_t stage_copied[3] = {}, stage_freed[3] = {};
   PinBuf plan_pin;
@@ -369,50 +376,65 @@ void parallel_for(uint32_t n, F&& f) {
 // ---------------------------------------------------------------------------
 
 struct Slab {
-  PinBuf h;          // [arena | off | len | out | status]
-  DevBuf d;          // same layout on the device
+  uint8_t* h = nullptr;  // pinned [arena | off | len | out | status]
+  uint8_t* d = nullptr;  // same layout on the device
   hipEvent_t done = nullptr;
   bool busy = false;
   uint32_t first = 0, count = 0;
 };
 
 struct SlabLayout {
-  size_t arena, off, len, out, status, total;
+  size_t arena_cap, off, len, out, status, total;
+  uint32_t files_cap;
 };
 
-SlabLayout slab_layout() {
+SlabLayout slab_layout(size_t arena_cap, uint32_t files_cap) {
   SlabLayout L;
-  L.arena = 0;
-  L.off = align_up(kSlabBytes, 256);
-  L.len = align_up(L.off + 8ull * kSlabFiles, 256);
-  L.out = align_up(L.len + 4ull * kSlabFiles, 256);
-  L.status = align_up(L.out + 8ull * kSlabFiles, 256);
-  L.total = align_up(L.status + 4ull * kSlabFiles, 256);
+  L.arena_cap = arena_cap;
+  L.files_cap = files_cap;
+  L.off = align_up(arena_cap, 256);
+  L.len = align_up(L.off + 8ull * files_cap, 256);
+  L.out = align_up(L.len + 4ull * files_cap, 256);
+  L.status = align_up(L.out + 8ull * files_cap, 256);
+  L.total = align_up(L.status + 4ull * files_cap, 256);
   return L;
+}
+
+// Pinned + device staging slot k of the context (grown on demand, kept).  Only
+// called when no work of the context is in flight.
+int pipe_slot(sdgpu_ctx* c, int k, size_t bytes) {
+  SD_TRY_RC(ensure_pin(c->pipe_h[k], bytes));
+  SD_TRY_RC(ensure_dev(c, c->pipe_d[k], bytes));
+  if (!c->pipe_evt[k]) SD_TRY(hipEventCreateWithFlags(&c->pipe_evt[k], hipEventDisableTiming));
+  return 0;
 }
 
 // producer(i, dst, cap) -> message length (>= 0), or -errno, or 0x7fffffff
 // meaning "no message for this file" (size 0).  est(i) = bytes to reserve.
+// Slabs are sized for this call (at most kSlabBytes / kSlabFiles): a single
+// file costs one ~60 KiB slab, not 256 MiB.
 template <typename Est, typename Produce, typename Finish>
 int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&& finish) {
-  const SlabLayout L = slab_layout();
+  uint64_t want = 0;
+  for (uint32_t i = 0; i < n && want < kSlabBytes; ++i) want += align_up(est(i), 16);
+  const SlabLayout L = slab_layout(static_cast<size_t>(std::clamp<uint64_t>(want, 4096, kSlabBytes)),
+                                   std::clamp<uint32_t>(n, 1, kSlabFiles));
   Slab slabs[2];
   int rc = 0;
-  for (auto& sl : slabs) {
-    if ((rc = ensure_pin(sl.h, L.total)) != 0) break;
-    if ((rc = ensure_dev(c, sl.d, L.total)) != 0) break;
-    if (hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
-      rc = -EIO;
-      break;
-    }
+  for (int k = 0; k < 2 && rc == 0; ++k) {
+    if ((rc = pipe_slot(c, k, L.total)) != 0) break;
+    slabs[k].h = static_cast<uint8_t*>(c->pipe_h[k].p);
+    slabs[k].d = static_cast<uint8_t*>(c->pipe_d[k].p);
+    slabs[k].done = c->pipe_evt[k];
   }
+  BatchWork w;
+  if (rc == 0) rc = batch_work(c, L.files_cap, L.arena_cap / kChunkLen + L.files_cap, w);
   auto drain = [&](Slab& sl) -> int {
     if (!sl.busy) return 0;
     if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
     sl.busy = false;
-    uint8_t* hb = static_cast<uint8_t*>(sl.h.p);
-    finish(sl.first, sl.count, reinterpret_cast<const uint8_t(*)[8]>(hb + L.out),
-           reinterpret_cast<const int32_t*>(hb + L.status));
+    finish(sl.first, sl.count, reinterpret_cast<const uint8_t(*)[8]>(sl.h + L.out),
+           reinterpret_cast<const int32_t*>(sl.h + L.status));
     return 0;
   };
   uint32_t i = 0, k = 0;
@@ -420,24 +442,25 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     Slab& sl = slabs[k & 1];
     if ((rc = drain(sl)) != 0) break;
     // assign files to this slab
-    uint8_t* hb = static_cast<uint8_t*>(sl.h.p);
+    uint8_t* hb = sl.h;
     uint64_t* off = reinterpret_cast<uint64_t*>(hb + L.off);
     uint32_t* len = reinterpret_cast<uint32_t*>(hb + L.len);
     int32_t* pst = reinterpret_cast<int32_t*>(hb + L.status);
     sl.first = i;
     uint64_t pos = 0;
     uint32_t cnt = 0;
-    while (i + cnt < n && cnt < kSlabFiles) {
+    while (i + cnt < n && cnt < L.files_cap) {
       const uint64_t need = align_up(est(i + cnt), 16);
-      if (pos + need > kSlabBytes && cnt > 0) break;
+      if (pos + need > L.arena_cap && cnt > 0) break;
       off[cnt] = pos;
-      pos += std::min<uint64_t>(need, kSlabBytes);
+      pos += std::min<uint64_t>(need, L.arena_cap);
       ++cnt;
     }
     sl.count = cnt;
     // fill (threads): message bytes + per-file pre-status
     parallel_for(cnt, [&](uint32_t j) {
-      const uint64_t cap = (j + 1 < cnt ? off[j + 1] : std::min<uint64_t>(pos, kSlabBytes)) - off[j];
+      const uint64_t cap =
+          (j + 1 < cnt ? off[j + 1] : std::min<uint64_t>(pos, L.arena_cap)) - off[j];
       const int64_t r = produce(sl.first + j, hb + off[j], static_cast<size_t>(cap));
       if (r >= 0 && r != 0x7fffffff) {
         len[j] = static_cast<uint32_t>(r);
@@ -449,9 +472,7 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     });
     // device: copy, hash, copy back
     hipStream_t s = c->stream;
-    uint8_t* db = static_cast<uint8_t*>(sl.d.p);
-    BatchWork w;
-    if ((rc = batch_work(c, cnt, pos / kChunkLen + cnt, w)) != 0) break;
+    uint8_t* db = sl.d;
     if (hipMemcpyAsync(db, hb, pos, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(db + L.off, hb + L.off, 8ull * cnt, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(db + L.len, hb + L.len, 4ull * cnt, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -472,11 +493,6 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     if (rc == 0) rc = r2;
   }
   (void)hipStreamSynchronize(c->stream);
-  for (auto& sl : slabs) {
-    if (sl.done) (void)hipEventDestroy(sl.done);
-    if (sl.h.p) (void)hipHostFree(sl.h.p);
-    if (sl.d.p) (void)hipFree(sl.d.p);
-  }
   return rc;
 }
 
@@ -538,8 +554,12 @@ int sdgpu_close(sdgpu_ctx* c) {
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   for (DevBuf* b : {&c->batch_ws, &c->tree_ws, &c->dedup_ws, &c->shard_ws, &c->io_a, &c->io_b,
                     &c->link_ws, &c->stage_meta, &c->stage_slab[0], &c->stage_slab[1],
-                    &c->stage_slab[2]})
+                    &c->stage_slab[2], &c->pipe_d[0], &c->pipe_d[1]})
     if (b->p) (void)hipFree(b->p);
+  for (int k = 0; k < 2; ++k) {
+    if (c->pipe_h[k].p) (void)hipHostFree(c->pipe_h[k].p);
+    if (c->pipe_evt[k]) (void)hipEventDestroy(c->pipe_evt[k]);
+  }
   for (int k = 0; k < 3; ++k) {
     if (c->stage_copied[k]) (void)hipEventDestroy(c->stage_copied[k]);
     if (c->stage_freed[k]) (void)hipEventDestroy(c->stage_freed[k]);
@@ -848,25 +868,20 @@ int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
   hipStream_t s = c->stream;
   c->last = s;
   // two pinned + two device slices; slice k's subtree CV lands in cvs[k]
-  PinBuf hp[2];
+  PinBuf* hp = c->pipe_h;  // the context's two staging slots
   int rc = 0;
   uint64_t nslices = 0;
   uint64_t total = 0;
-  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipEvent_t* ev = c->pipe_evt;
   bool inflight[2] = {false, false};
   std::vector<uint8_t> out(32);
   do {
-    if ((rc = ensure_pin(hp[0], kSliceBytes)) || (rc = ensure_pin(hp[1], kSliceBytes))) break;
+    if ((rc = pipe_slot(c, 0, kSliceBytes)) || (rc = pipe_slot(c, 1, kSliceBytes))) break;
     struct stat st;
     if (fstat(fd, &st) == 0 && st.st_size > 0 &&
         (rc = grow_dev_keep(c, c->io_b, 32 * (static_cast<uint64_t>(st.st_size) / kSliceBytes + 2) + 256, 0)))
       break;
     if ((rc = ensure_dev(c, c->io_a, 2 * kSliceBytes + 4096))) break;
-    if (hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) {
-      rc = -EIO;
-      break;
-    }
     uint8_t* dslice[2] = {static_cast<uint8_t*>(c->io_a.p),
                           static_cast<uint8_t*>(c->io_a.p) + kSliceBytes};
     uint8_t* droot = static_cast<uint8_t*>(c->io_a.p) + 2 * kSliceBytes;
@@ -928,10 +943,6 @@ int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
       rc = -EIO;
   } while (false);
   (void)hipStreamSynchronize(s);
-  for (int k = 0; k < 2; ++k) {
-    if (ev[k]) (void)hipEventDestroy(ev[k]);
-    if (hp[k].p) (void)hipHostFree(hp[k].p);
-  }
   close(fd);
   if (rc) return rc;
   memcpy(digest, out.data(), 32);
@@ -1003,29 +1014,32 @@ int sdgpu_checksum_files(sdgpu_ctx* c, const char* const* paths, uint32_t n, uin
     else if (static_cast<uint64_t>(size[i]) > kValidateBatchMax) deferred[i] = 1;
   }
   struct VSlab {
-    PinBuf h;
-    DevBuf d;
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
     hipEvent_t done = nullptr;
     bool busy = false;
     std::vector<uint32_t> files;
   };
-  const size_t out_off = kSlabBytes;  // [arena | digests]
+  // [arena | digests], the arena sized for this call's batched files
+  uint64_t want = 0;
+  for (uint32_t j = 0; j < n && want < kSlabBytes; ++j)
+    if (st[j] == 0 && !deferred[j]) want += align_up(static_cast<uint64_t>(size[j]) + 4096, 256);
+  const uint64_t arena_cap = std::clamp<uint64_t>(want, 4096, kSlabBytes);
+  const size_t out_off = align_up(arena_cap, 256);
   const size_t slab_total = out_off + 32ull * kSlabFiles;
   VSlab slabs[2];
   int rc = 0;
-  for (auto& sl : slabs) {
-    if ((rc = ensure_pin(sl.h, slab_total)) != 0) break;
-    if ((rc = ensure_dev(c, sl.d, slab_total)) != 0) break;
-    if (hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
-      rc = -EIO;
-      break;
-    }
+  for (int k = 0; k < 2 && rc == 0; ++k) {
+    if ((rc = pipe_slot(c, k, slab_total)) != 0) break;
+    slabs[k].h = static_cast<uint8_t*>(c->pipe_h[k].p);
+    slabs[k].d = static_cast<uint8_t*>(c->pipe_d[k].p);
+    slabs[k].done = c->pipe_evt[k];
   }
   auto drain = [&](VSlab& sl) -> int {
     if (!sl.busy) return 0;
     if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
     sl.busy = false;
-    const uint8_t* dg = static_cast<const uint8_t*>(sl.h.p) + out_off;
+    const uint8_t* dg = sl.h + out_off;
     for (size_t j = 0; j < sl.files.size(); ++j) memcpy(out32[sl.files[j]], dg + 32 * j, 32);
     return 0;
   };
@@ -1044,7 +1058,7 @@ int sdgpu_checksum_files(sdgpu_ctx* c, const char* const* paths, uint32_t n, uin
     for (; i < n && sl.files.size() < kSlabFiles; ++i) {
       if (st[i] != 0 || deferred[i]) continue;
       const uint64_t room = align_up(static_cast<uint64_t>(size[i]) + 4096, 256);
-      if (pos + room > kSlabBytes) break;
+      if (pos + room > arena_cap) break;
       sl.files.push_back(i);
       off.push_back(pos);
       cap.push_back(room);
@@ -1052,11 +1066,11 @@ int sdgpu_checksum_files(sdgpu_ctx* c, const char* const* paths, uint32_t n, uin
     }
     const uint32_t cnt = static_cast<uint32_t>(sl.files.size());
     got.assign(cnt, 0);
-    uint8_t* hb = static_cast<uint8_t*>(sl.h.p);
+    uint8_t* hb = sl.h;
     parallel_for(cnt, [&](uint32_t j) {
       got[j] = read_whole(paths[sl.files[j]], hb + off[j], static_cast<size_t>(cap[j]));
     });
-    uint8_t* db = static_cast<uint8_t*>(sl.d.p);
+    uint8_t* db = sl.d;
     std::vector<TreeSeg> segs;
     std::vector<uint32_t> kept;
     segs.reserve(cnt);
@@ -1096,11 +1110,6 @@ int sdgpu_checksum_files(sdgpu_ctx* c, const char* const* paths, uint32_t n, uin
     if (rc == 0) rc = r2;
   }
   (void)hipStreamSynchronize(s);
-  for (auto& sl : slabs) {
-    if (sl.done) (void)hipEventDestroy(sl.done);
-    if (sl.h.p) (void)hipHostFree(sl.h.p);
-    if (sl.d.p) (void)hipFree(sl.d.p);
-  }
   if (rc) return rc;
   for (uint32_t j = 0; j < n; ++j)
     if (deferred[j] && st[j] == 0) st[j] = file_checksum_locked(c, paths[j], out32[j]);
