@@ -781,6 +781,87 @@ hipError_t batch_hash_launch_v3(const uint8_t* arena, const uint64_t* off, const
   return hipGetLastError();
 }
 
+// ============================================================================
+// Latency path: one workgroup per message of at most 1024 chunks (1 MiB).
+// Thread t hashes chunk t (16 compressions), then the CVs are folded level by
+// level in LDS (pairwise, odd node carried up: BLAKE3's left-complete tree),
+// one compression per level, ROOT on the last.  A 57-chunk cas message is one
+// pass of 57 lanes + 6 levels: ~22 compression latencies in ONE launch, for
+// the single-file callers (watcher/utils.rs:236,411,467, non_indexed.rs:161)
+// where K1's planning launches would dominate.
+// ============================================================================
+
+constexpr uint32_t kSmallMaxChunks = 1024;
+
+__global__ __launch_bounds__(1024) void k_small(const uint8_t* __restrict__ arena,
+                                                const uint64_t* __restrict__ off,
+                                                const uint32_t* __restrict__ len,
+                                                uint32_t max_len, uint32_t out_words,
+                                                uint32_t* __restrict__ out,
+                                                int32_t* __restrict__ status) {
+  __shared__ uint32_t cv[8][kSmallMaxChunks];  // word-major: lane-indexed access is conflict-free
+  const uint32_t m = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  const uint32_t l = len[m];
+  const bool ok = l <= max_len && (off[m] & 15u) == 0 && l <= kSmallMaxChunks * B3_CHUNK_LEN;
+  if (t == 0 && status) status[m] = ok ? 0 : -EINVAL;
+  if (!ok) {
+    if (t < out_words) out[m * out_words + t] = 0u;
+    return;
+  }
+  const uint32_t nch = n_chunks_of(l);
+  const uint8_t* p = arena + off[m];
+  uint32_t c[8];
+  if (nch == 1) {
+    if (t == 0) {
+      b3_chunk(p, l, 0, B3_ROOT, c);
+      for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = c[w];
+    }
+    return;
+  }
+  if (t < nch) {
+    chunk_any(p, l, t, 0u, c);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
+  }
+  __syncthreads();
+  uint32_t cnt = nch;
+  while (cnt > 2) {
+    const uint32_t half = cnt >> 1;
+    uint32_t a[8], b[8];
+    const bool merge = t < half;
+    const bool carry = (cnt & 1u) && t == half;
+    if (merge) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        a[w] = cv[w][2 * t];
+        b[w] = cv[w][2 * t + 1];
+      }
+      b3_parent(c, a, b, 0u);
+    } else if (carry) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) c[w] = cv[w][cnt - 1];
+    }
+    __syncthreads();
+    if (merge || carry) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
+    }
+    __syncthreads();
+    cnt = half + (cnt & 1u);
+  }
+  if (t == 0) {
+    uint32_t a[8], b[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      a[w] = cv[w][0];
+      b[w] = cv[w][1];
+    }
+    b3_parent(c, a, b, B3_ROOT);
+    for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = c[w];
+  }
+}
+
 }  // namespace
 
 hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
@@ -821,6 +902,25 @@ hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
     k_parents<<<blocks, kThreads, 0, s>>>(w.n_chunks, w.chunk_base, w.order, w.bins, n, w.cvs,
                                           out_words, o);
   }
+  return hipGetLastError();
+}
+
+}  // namespace sdgpu
+
+namespace sdgpu {
+
+// One workgroup per message; max_chunks = the largest chunk count of the batch
+// (host-known), which sizes the workgroup.  Messages must be <= 1 MiB.
+hipError_t small_hash_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                             uint32_t n, uint32_t max_len, uint32_t max_chunks,
+                             uint32_t out_words, uint8_t* out, int32_t* status, hipStream_t s,
+                             KTimer* timer) {
+  if (n == 0) return hipSuccess;
+  if (max_chunks > kSmallMaxChunks) return hipErrorInvalidValue;
+  const uint32_t threads = std::max<uint32_t>(64, (max_chunks + 63) / 64 * 64);
+  KScope k(timer, "cas_small", s);
+  k_small<<<n, threads, 0, s>>>(arena, off, len, max_len, out_words,
+                                reinterpret_cast<uint32_t*>(out), status);
   return hipGetLastError();
 }
 

@@ -57,6 +57,15 @@ hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
                              int32_t* status, const BatchWork& w, hipStream_t s,
                              KTimer* timer = nullptr);
 
+// Latency path for a few messages of at most 1 MiB each: ONE launch, one
+// workgroup per message (thread per chunk, LDS tree).  max_chunks = largest
+// chunk count in the batch.  Same status / out semantics as batch_hash_launch.
+constexpr uint32_t SMALL_MAX_BYTES = 1024u * 1024u;
+hipError_t small_hash_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                             uint32_t n, uint32_t max_len, uint32_t max_chunks,
+                             uint32_t out_words, uint8_t* out, int32_t* status, hipStream_t s,
+                             KTimer* timer = nullptr);
+
 // ---- tree BLAKE3 of large segments (file_checksum, K2/K3) -------------------
 struct TreeSeg {
   const uint8_t* data;    // device pointer, 16-B aligned (bytes, or CVs when cv_input)

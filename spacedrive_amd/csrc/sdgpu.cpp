@@ -76,6 +76,7 @@ constexpr size_t kSliceBytes = size_t(64) << 20;   // file_checksum slice = 2^16
 constexpr uint32_t kStageMaxMsg = 8u + (64u << 20);  // largest staged cas message
 constexpr size_t kStageSlabBytes = size_t(256) << 20;  // sdgpu_cas_stage_pinned device slab
 constexpr uint64_t kValidateBatchMax = uint64_t(16) << 20;  // larger files are streamed
+constexpr uint32_t kSmallBatch = 64;  // up to this many messages take the latency kernel
 
 // Brackets kernels with HIP events on their own stream; elapsed times are
 // resolved (one sync per event pair) only when read.
@@ -470,15 +471,33 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
         pst[j] = r == 0x7fffffff ? 1 : static_cast<int32_t>(r);
       }
     });
-    // device: copy, hash, copy back
+    // device: copy, hash, copy back.  A few messages of <= 1 MiB take the
+    // one-launch latency kernel and one H2D copy of the whole slab prefix.
     hipStream_t s = c->stream;
     uint8_t* db = sl.d;
-    if (hipMemcpyAsync(db, hb, pos, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(db + L.off, hb + L.off, 8ull * cnt, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(db + L.len, hb + L.len, 4ull * cnt, hipMemcpyHostToDevice, s) != hipSuccess ||
-        batch_hash_launch(db, reinterpret_cast<const uint64_t*>(db + L.off),
-                          reinterpret_cast<const uint32_t*>(db + L.len), cnt, kStageMaxMsg, 2,
-                          db + L.out, nullptr, w, s) != hipSuccess ||
+    uint32_t max_msg = 0;
+    for (uint32_t j = 0; j < cnt; ++j) max_msg = std::max(max_msg, len[j]);
+    const bool small = cnt <= kSmallBatch && max_msg <= SMALL_MAX_BYTES;
+    const size_t prefix = L.len + 4ull * cnt;
+    bool ok;
+    if (small && prefix <= (size_t(8) << 20)) {
+      ok = hipMemcpyAsync(db, hb, prefix, hipMemcpyHostToDevice, s) == hipSuccess;
+    } else {
+      ok = hipMemcpyAsync(db, hb, pos, hipMemcpyHostToDevice, s) == hipSuccess &&
+           hipMemcpyAsync(db + L.off, hb + L.off, 8ull * cnt, hipMemcpyHostToDevice, s) ==
+               hipSuccess &&
+           hipMemcpyAsync(db + L.len, hb + L.len, 4ull * cnt, hipMemcpyHostToDevice, s) ==
+               hipSuccess;
+    }
+    const uint64_t* d_off = reinterpret_cast<const uint64_t*>(db + L.off);
+    const uint32_t* d_len = reinterpret_cast<const uint32_t*>(db + L.len);
+    if (ok)
+      ok = (small ? small_hash_launch(db, d_off, d_len, cnt, kStageMaxMsg,
+                                      max_msg <= kChunkLen ? 1u : (max_msg + kChunkLen - 1) / kChunkLen,
+                                      2, db + L.out, nullptr, s, c->kt())
+                  : batch_hash_launch(db, d_off, d_len, cnt, kStageMaxMsg, 2, db + L.out, nullptr,
+                                      w, s, c->kt())) == hipSuccess;
+    if (!ok ||
         hipMemcpyAsync(hb + L.out, db + L.out, 8ull * cnt, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipEventRecord(sl.done, s) != hipSuccess) {
       rc = -EIO;
@@ -861,6 +880,25 @@ int sdgpu_checksum(sdgpu_ctx* c, const void* bytes, uint64_t len, uint8_t out32[
 
 namespace {
 
+// Reads all of fd (from its current offset) into dst; -EFBIG past cap bytes.
+int64_t read_whole_fd(int fd, uint8_t* dst, size_t cap) {
+  size_t len = 0;
+  for (;;) {
+    if (len == cap) {
+      uint8_t probe;
+      const ssize_t r = read(fd, &probe, 1);
+      return r == 0 ? static_cast<int64_t>(len) : (r < 0 ? -errno : -EFBIG);
+    }
+    const ssize_t r = read(fd, dst + len, cap - len);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return -errno;
+    }
+    if (r == 0) return static_cast<int64_t>(len);
+    len += static_cast<size_t>(r);
+  }
+}
+
 // file_checksum of one file, streamed in slices (context lock held).
 int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
   const int fd = open(path, O_RDONLY | O_CLOEXEC);
@@ -876,8 +914,40 @@ int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
   bool inflight[2] = {false, false};
   std::vector<uint8_t> out(32);
   do {
-    if ((rc = pipe_slot(c, 0, kSliceBytes)) || (rc = pipe_slot(c, 1, kSliceBytes))) break;
     struct stat st;
+    if (fstat(fd, &st) == 0 && static_cast<uint64_t>(st.st_size) <= SMALL_MAX_BYTES) {
+      // latency path: the whole file in one read, one copy, one launch (the
+      // reference's 1 MiB read loop, hash.rs:14-20, ends on the short read)
+      const size_t cap = SMALL_MAX_BYTES;  // room for growth up to 1 MiB
+      if ((rc = pipe_slot(c, 0, cap + 256))) break;
+      uint8_t* hb = static_cast<uint8_t*>(hp[0].p);
+      const int64_t got = read_whole_fd(fd, hb, cap);
+      if (got >= 0) {
+        uint8_t* db = static_cast<uint8_t*>(c->pipe_d[0].p);
+        uint64_t* meta = reinterpret_cast<uint64_t*>(hb + cap);  // {off = 0, len}
+        meta[0] = 0;
+        meta[1] = static_cast<uint64_t>(got);
+        const uint32_t nch = got <= 1024 ? 1u : static_cast<uint32_t>((got + 1023) / 1024);
+        if (hipMemcpyAsync(db, hb, static_cast<size_t>(got), hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(db + cap, hb + cap, 16, hipMemcpyHostToDevice, s) != hipSuccess ||
+            small_hash_launch(db, reinterpret_cast<const uint64_t*>(db + cap),
+                              reinterpret_cast<const uint32_t*>(db + cap + 8), 1, SMALL_MAX_BYTES,
+                              nch, 8, db + cap + 64, nullptr, s, c->kt()) != hipSuccess ||
+            hipMemcpyAsync(out.data(), db + cap + 64, 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+          rc = -EIO;
+        break;
+      }
+      if (got != -EFBIG) {
+        rc = static_cast<int>(got);
+        break;
+      }
+      if (lseek(fd, 0, SEEK_SET) < 0) {  // grew past 1 MiB since fstat: stream it
+        rc = -errno;
+        break;
+      }
+    }
+    if ((rc = pipe_slot(c, 0, kSliceBytes)) || (rc = pipe_slot(c, 1, kSliceBytes))) break;
     if (fstat(fd, &st) == 0 && st.st_size > 0 &&
         (rc = grow_dev_keep(c, c->io_b, 32 * (static_cast<uint64_t>(st.st_size) / kSliceBytes + 2) + 256, 0)))
       break;

@@ -151,3 +151,23 @@ def test_k1_variants_tree_edges_bit_exact(ctx, variant, monkeypatch):
     assert np.all(st == 0)
     ref = O.cas_batch(arena, off, lens, threads=8)
     np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("n", [1, 3, 64])
+def test_small_batch_latency_kernel_bit_exact(ctx, n, tmp_path):
+    """Batches of <= 64 messages take the one-launch latency kernel (k_small):
+    every chunk-count shape up to 101 chunks, through sdgpu_cas_batch."""
+    from spacedrive_amd import cas
+    lens = _tree_edge_lengths()
+    rng = np.random.default_rng(n)
+    for start in range(0, lens.size, n):
+        ln = lens[start:start + n]
+        off = np.zeros(ln.size, np.uint64)
+        pos = 0
+        for i, m in enumerate(ln):
+            off[i] = pos
+            pos += (int(m) + 127) // 128 * 128
+        arena = rng.integers(0, 256, pos + 16, dtype=np.uint8)
+        out, st = cas.cas_batch(arena, off, ln, ctx)
+        assert np.all(st == 0)
+        np.testing.assert_array_equal(out, O.cas_batch(arena, off, ln, threads=4))
