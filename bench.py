@@ -385,6 +385,12 @@ class Runner:
         for _ in range(reps):
             O.cas_batch(host, h_off, h_len, threads)
         dt = time.perf_counter() - t0
+        # one thread (the reference hashes a 100-file chunk on ONE runtime
+        # thread, file_identifier/mod.rs:107-134): a 1/16 slice of the sample
+        m1 = max(1, m // 16)
+        t0 = time.perf_counter()
+        O.cas_batch(host, h_off[:m1], h_len[:m1], 1)
+        one = m1 / (time.perf_counter() - t0)
         dir_res = None
         if getattr(self, "_dir_sample", None):
             import shutil
@@ -416,6 +422,7 @@ class Runner:
                         ts.append(time.perf_counter() - t0)
                     single[f"{fn_name}_{name}_us"] = float(np.median(ts) * 1e6)
         return {"value": reps * m / dt, "unit": "files/s", "cores": threads, "kind": "port",
+                "value_1thread": one,
                 "config1_dir": dir_res, "single_file_1thread": single,
                 "sample": f"first {m} files of config 2 (their {int(h_len.sum())} window bytes "
                           f"in host RAM) hashed {reps}x, scalar C BLAKE3 oracle "
