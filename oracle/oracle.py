@@ -49,6 +49,8 @@ def lib():
         L.orc_file_checksum_path.restype = ctypes.c_int
         L.orc_cas_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
+        L.orc_cas_batch_simd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
         L.orc_synth_file_bytes.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                            ctypes.c_void_p]
         L.orc_synth_cas_message.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
@@ -159,6 +161,18 @@ def cas_batch(arena: np.ndarray, off: np.ndarray, length: np.ndarray, threads: i
     length = np.ascontiguousarray(length, np.uint32)
     out = np.zeros((off.size, 8), np.uint8)
     lib().orc_cas_batch(_ptr(arena), _ptr(off), _ptr(length), off.size, _ptr(out), threads)
+    return out
+
+
+def cas_batch_simd(arena: np.ndarray, off: np.ndarray, length: np.ndarray,
+                   threads: int = 1) -> np.ndarray:
+    """cas bytes (n x 8) with the AVX2 8-way chunk/parent hashing (CPU baseline:
+    the reference crate's multi-chunk SIMD idea, restated)."""
+    arena = np.ascontiguousarray(arena, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
+    length = np.ascontiguousarray(length, np.uint32)
+    out = np.zeros((off.size, 8), np.uint8)
+    lib().orc_cas_batch_simd(_ptr(arena), _ptr(off), _ptr(length), off.size, _ptr(out), threads)
     return out
 
 

@@ -20,6 +20,10 @@ uint32_t orc_synth_cas_message(uint64_t size, uint64_t seed, uint8_t *out);
 void orc_cas_id_of_message(const uint8_t *msg, size_t len, char out_hex[17]);
 int orc_group_reps(const uint64_t *key, const uint8_t *has_key, uint32_t n, uint32_t chunk_rows,
                    uint32_t *rep);
+void orc_cas_batch(const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t n,
+                   uint8_t *out8, int threads);
+void orc_cas_batch_simd(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                        uint64_t n, uint8_t *out8, int threads);
 
 static int fails = 0;
 #define CHECK(c, ...)                 \
@@ -75,6 +79,26 @@ int main(void) {
           (unsigned long long)sizes[i]);
   }
   free(msg);
+
+  /* AVX2 8-way baseline == scalar on every chunk count 1..101 with ragged tails */
+  {
+    enum { M = 101 * 3 };
+    uint64_t off[M];
+    uint32_t len[M];
+    uint64_t pos = 0;
+    for (int i = 0; i < M; ++i) {
+      len[i] = (uint32_t)((i / 3 + 1) * 1024 - (i % 3 == 0 ? 0 : (i % 3 == 1 ? 1 : 1000)));
+      off[i] = pos;
+      pos += (len[i] + 127) / 128 * 128;
+    }
+    uint8_t *arena = malloc(pos + 64);
+    for (uint64_t i = 0; i < pos + 64; ++i) arena[i] = (uint8_t)(i * 2654435761u >> 13);
+    uint8_t a[M][8], b[M][8];
+    orc_cas_batch(arena, off, len, M, &a[0][0], 2);
+    orc_cas_batch_simd(arena, off, len, M, &b[0][0], 2);
+    CHECK(memcmp(a, b, sizeof a) == 0, "simd baseline differs from scalar");
+    free(arena);
+  }
 
   const uint32_t n = 50000;
   uint64_t *key = malloc(n * sizeof *key);

@@ -39,6 +39,10 @@
  *
  *  - the synthetic corpus content function shared with the device generator
  *    (spacedrive_amd/csrc/synth.hip); see DESIGN.md "Synthetic corpora".
+ *
+ *  - (end of file) an AVX2 8-way chunk/parent hasher used ONLY as bench.py's
+ *    timed CPU baseline (the crate hashes chunks with SIMD too), checked
+ *    bit-exact against the scalar restatement above.
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -822,4 +826,251 @@ int orc_group_reps(const uint64_t *key, const uint8_t *has_key, uint32_t n,
   }
   free(v);
   return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* AVX2 8-way chunk hashing (CPU BASELINE ONLY: bench.py cpu_baseline leg).  */
+/* ------------------------------------------------------------------------- */
+/*
+ * The reference's blake3 1.4.1 crate hashes a message's full chunks several at
+ * a time with SIMD (hash_many; AVX2 = 8 lanes).  This is the same idea written
+ * from the spec: 8 chunks' states live transposed in 16 __m256i registers,
+ * their message blocks are transposed 8x8 on load, and the parent levels are
+ * hashed 8 at a time the same way (a parent block = two adjacent CVs).  The
+ * tree is folded level by level, odd node carried up (BLAKE3's left-complete
+ * tree).  tests/test_oracle.py checks it bit-exact against the scalar oracle.
+ */
+#include <immintrin.h>
+
+typedef __m256i v8u;
+
+static inline v8u v_add(v8u a, v8u b) { return _mm256_add_epi32(a, b); }
+static inline v8u v_xor(v8u a, v8u b) { return _mm256_xor_si256(a, b); }
+static inline v8u v_set1(uint32_t x) { return _mm256_set1_epi32((int)x); }
+static inline v8u v_rot16(v8u x) {
+  const v8u m = _mm256_setr_epi8(2, 3, 0, 1, 6, 7, 4, 5, 10, 11, 8, 9, 14, 15, 12, 13, 2, 3, 0,
+                                 1, 6, 7, 4, 5, 10, 11, 8, 9, 14, 15, 12, 13);
+  return _mm256_shuffle_epi8(x, m);
+}
+static inline v8u v_rot8(v8u x) {
+  const v8u m = _mm256_setr_epi8(1, 2, 3, 0, 5, 6, 7, 4, 9, 10, 11, 8, 13, 14, 15, 12, 1, 2, 3,
+                                 0, 5, 6, 7, 4, 9, 10, 11, 8, 13, 14, 15, 12);
+  return _mm256_shuffle_epi8(x, m);
+}
+static inline v8u v_rot12(v8u x) {
+  return _mm256_or_si256(_mm256_srli_epi32(x, 12), _mm256_slli_epi32(x, 20));
+}
+static inline v8u v_rot7(v8u x) {
+  return _mm256_or_si256(_mm256_srli_epi32(x, 7), _mm256_slli_epi32(x, 25));
+}
+
+#define VG(a, b, c, d, x, y)      \
+  do {                            \
+    a = v_add(v_add(a, b), x);    \
+    d = v_rot16(v_xor(d, a));     \
+    c = v_add(c, d);              \
+    b = v_rot12(v_xor(b, c));     \
+    a = v_add(v_add(a, b), y);    \
+    d = v_rot8(v_xor(d, a));      \
+    c = v_add(c, d);              \
+    b = v_rot7(v_xor(b, c));      \
+  } while (0)
+
+/* 8 compressions: h[8] in/out (transposed CVs), m[16] transposed words. */
+static inline void v_compress(v8u h[8], const v8u m[16], v8u ctr_lo, v8u ctr_hi, uint32_t blen,
+                              uint32_t flags) {
+  static const uint8_t S[7][16] = {
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8},
+      {3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1},
+      {10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6},
+      {12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4},
+      {9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7},
+      {11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13}};
+  v8u v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3], v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
+  v8u v8 = v_set1(B3_IV[0]), v9 = v_set1(B3_IV[1]), v10 = v_set1(B3_IV[2]),
+      v11 = v_set1(B3_IV[3]);
+  v8u v12 = ctr_lo, v13 = ctr_hi, v14 = v_set1(blen), v15 = v_set1(flags);
+  for (int r = 0; r < 7; ++r) {
+    const uint8_t *s = S[r];
+    VG(v0, v4, v8, v12, m[s[0]], m[s[1]]);
+    VG(v1, v5, v9, v13, m[s[2]], m[s[3]]);
+    VG(v2, v6, v10, v14, m[s[4]], m[s[5]]);
+    VG(v3, v7, v11, v15, m[s[6]], m[s[7]]);
+    VG(v0, v5, v10, v15, m[s[8]], m[s[9]]);
+    VG(v1, v6, v11, v12, m[s[10]], m[s[11]]);
+    VG(v2, v7, v8, v13, m[s[12]], m[s[13]]);
+    VG(v3, v4, v9, v14, m[s[14]], m[s[15]]);
+  }
+  h[0] = v_xor(v0, v8);
+  h[1] = v_xor(v1, v9);
+  h[2] = v_xor(v2, v10);
+  h[3] = v_xor(v3, v11);
+  h[4] = v_xor(v4, v12);
+  h[5] = v_xor(v5, v13);
+  h[6] = v_xor(v6, v14);
+  h[7] = v_xor(v7, v15);
+}
+
+/* r[j] = 8 words (32 B) of lane j -> out[w] = word w of every lane. */
+static inline void v_transpose8(const v8u r[8], v8u out[8]) {
+  const v8u t0 = _mm256_unpacklo_epi32(r[0], r[1]), t1 = _mm256_unpackhi_epi32(r[0], r[1]);
+  const v8u t2 = _mm256_unpacklo_epi32(r[2], r[3]), t3 = _mm256_unpackhi_epi32(r[2], r[3]);
+  const v8u t4 = _mm256_unpacklo_epi32(r[4], r[5]), t5 = _mm256_unpackhi_epi32(r[4], r[5]);
+  const v8u t6 = _mm256_unpacklo_epi32(r[6], r[7]), t7 = _mm256_unpackhi_epi32(r[6], r[7]);
+  const v8u u0 = _mm256_unpacklo_epi64(t0, t2), u1 = _mm256_unpackhi_epi64(t0, t2);
+  const v8u u2 = _mm256_unpacklo_epi64(t1, t3), u3 = _mm256_unpackhi_epi64(t1, t3);
+  const v8u u4 = _mm256_unpacklo_epi64(t4, t6), u5 = _mm256_unpackhi_epi64(t4, t6);
+  const v8u u6 = _mm256_unpacklo_epi64(t5, t7), u7 = _mm256_unpackhi_epi64(t5, t7);
+  out[0] = _mm256_permute2x128_si256(u0, u4, 0x20);
+  out[1] = _mm256_permute2x128_si256(u1, u5, 0x20);
+  out[2] = _mm256_permute2x128_si256(u2, u6, 0x20);
+  out[3] = _mm256_permute2x128_si256(u3, u7, 0x20);
+  out[4] = _mm256_permute2x128_si256(u0, u4, 0x31);
+  out[5] = _mm256_permute2x128_si256(u1, u5, 0x31);
+  out[6] = _mm256_permute2x128_si256(u2, u6, 0x31);
+  out[7] = _mm256_permute2x128_si256(u3, u7, 0x31);
+}
+
+/* Words of 64-byte block b of the 8 inputs p[j] (+ 64 b), transposed. */
+static inline void v_load_block(const uint8_t *const p[8], size_t boff, v8u m[16]) {
+  v8u r[8];
+  for (int j = 0; j < 8; ++j) r[j] = _mm256_loadu_si256((const v8u *)(p[j] + boff));
+  v_transpose8(r, m);
+  for (int j = 0; j < 8; ++j) r[j] = _mm256_loadu_si256((const v8u *)(p[j] + boff + 32));
+  v_transpose8(r, m + 8);
+}
+
+static inline void v_store_cvs(const v8u h[8], uint32_t *out[8]) {
+  v8u t[8];
+  v_transpose8(h, t); /* t[j] = CV of lane j (the transpose is an involution) */
+  for (int j = 0; j < 8; ++j) _mm256_storeu_si256((v8u *)out[j], t[j]);
+}
+
+/* CVs of 8 FULL non-root chunks p[j] with chunk counters ctr0 + j. */
+static void v_chunks8(const uint8_t *const p[8], uint64_t ctr0, uint32_t *out[8]) {
+  v8u h[8], m[16];
+  for (int w = 0; w < 8; ++w) h[w] = v_set1(B3_IV[w]);
+  uint32_t lo[8], hi[8];
+  for (int j = 0; j < 8; ++j) {
+    lo[j] = (uint32_t)(ctr0 + j);
+    hi[j] = (uint32_t)((ctr0 + j) >> 32);
+  }
+  const v8u clo = _mm256_loadu_si256((const v8u *)lo), chi = _mm256_loadu_si256((const v8u *)hi);
+  for (int b = 0; b < 16; ++b) {
+    v_load_block(p, (size_t)64 * b, m);
+    v_compress(h, m, clo, chi, 64, (b == 0 ? B3_CHUNK_START : 0) | (b == 15 ? B3_CHUNK_END : 0));
+  }
+  v_store_cvs(h, out);
+}
+
+/* 8 parents: out[j] = P(cvs[2k], cvs[2k+1]) for pair k = k0 + j (8 words each). */
+static void v_parents8(const uint32_t *pairs[8], uint32_t *out[8]) {
+  v8u h[8], m[16];
+  for (int w = 0; w < 8; ++w) h[w] = v_set1(B3_IV[w]);
+  const uint8_t *p[8];
+  for (int j = 0; j < 8; ++j) p[j] = (const uint8_t *)pairs[j];
+  v_load_block(p, 0, m);
+  const v8u z = _mm256_setzero_si256();
+  v_compress(h, m, z, z, 64, B3_PARENT);
+  v_store_cvs(h, out);
+}
+
+static void s_chunk_cv(const uint8_t *p, size_t clen, uint64_t ctr, uint32_t cv[8]) {
+  b3_output o;
+  b3_chunk_output(B3_IV, 0, p, clen, ctr, &o);
+  b3_output_cv(&o, cv);
+}
+
+static void s_parent_cv(const uint32_t l[8], const uint32_t r[8], uint32_t flags,
+                        uint32_t cv[8]) {
+  b3_output o;
+  b3_parent_output(B3_IV, 0, l, r, &o);
+  uint32_t w[16];
+  b3_compress(o.cv, o.block, 0, 64, o.flags | flags, w);
+  memcpy(cv, w, 32);
+}
+
+/* BLAKE3 (hash mode, first 8 digest bytes) of one message <= 128 chunks. */
+static void simd_hash8(const uint8_t *msg, size_t len, uint8_t out8[8]) {
+  const size_t nch = len <= B3_CHUNK ? 1 : (len + B3_CHUNK - 1) / B3_CHUNK;
+  if (nch == 1 || nch > 128) {
+    uint8_t d[32];
+    orc_blake3(msg, len, d);
+    memcpy(out8, d, 8);
+    return;
+  }
+  uint32_t cvs[128][8] __attribute__((aligned(32)));
+  size_t c = 0;
+  /* full chunks 8 at a time (the last chunk is never ROOT here: nch >= 2) */
+  const size_t full = len / B3_CHUNK;
+  for (; c + 8 <= full; c += 8) {
+    const uint8_t *p[8];
+    uint32_t *o[8];
+    for (int j = 0; j < 8; ++j) {
+      p[j] = msg + (c + j) * B3_CHUNK;
+      o[j] = cvs[c + j];
+    }
+    v_chunks8(p, c, o);
+  }
+  for (; c < nch; ++c) {
+    const size_t clen = len - c * B3_CHUNK < B3_CHUNK ? len - c * B3_CHUNK : B3_CHUNK;
+    s_chunk_cv(msg + c * B3_CHUNK, clen, c, cvs[c]);
+  }
+  size_t cnt = nch;
+  while (cnt > 2) {
+    const size_t half = cnt / 2;
+    size_t k = 0;
+    for (; k + 8 <= half; k += 8) {
+      const uint32_t *pr[8];
+      uint32_t *o[8];
+      uint32_t tmp[8][8] __attribute__((aligned(32)));
+      for (int j = 0; j < 8; ++j) {
+        pr[j] = cvs[2 * (k + j)];
+        o[j] = tmp[j];
+      }
+      v_parents8(pr, o);
+      for (int j = 0; j < 8; ++j) memcpy(cvs[k + j], tmp[j], 32);
+    }
+    for (; k < half; ++k) {
+      uint32_t t[8];
+      s_parent_cv(cvs[2 * k], cvs[2 * k + 1], 0, t);
+      memcpy(cvs[k], t, 32);
+    }
+    if (cnt & 1) memcpy(cvs[half], cvs[cnt - 1], 32);
+    cnt = half + (cnt & 1);
+  }
+  uint32_t root[8];
+  s_parent_cv(cvs[0], cvs[1], B3_ROOT, root);
+  for (int i = 0; i < 2; ++i) store32le(out8 + 4 * i, root[i]);
+}
+
+typedef struct {
+  const uint8_t *arena;
+  const uint64_t *off;
+  const uint32_t *len;
+  uint8_t *out8;
+  uint64_t begin, end;
+} simd_job;
+
+static void *simd_worker(void *arg) {
+  simd_job *j = (simd_job *)arg;
+  for (uint64_t i = j->begin; i < j->end; i++)
+    simd_hash8(j->arena + j->off[i], j->len[i], j->out8 + 8 * i);
+  return NULL;
+}
+
+/* cas bytes of n messages, AVX2 8-way per message, `threads` threads. */
+void orc_cas_batch_simd(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                        uint64_t n, uint8_t *out8, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  simd_job jobs[256];
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (simd_job){arena, off, len, out8, n * (uint64_t)t / (uint64_t)threads,
+                         n * (uint64_t)(t + 1) / (uint64_t)threads};
+    pthread_create(&th[t], NULL, simd_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
 }

@@ -176,3 +176,22 @@ def test_link_batch_oracle_matches_object_stats():
     assert np.isin(lobj, create).all()
     assert np.all(rep[create] == create)
     assert np.all(rep[lrow] == lobj)
+
+
+def test_simd_cpu_baseline_matches_scalar_oracle():
+    """The AVX2 8-way CPU-baseline hashing is bit-exact with the scalar oracle on
+    every chunk-count / tail shape and on a config-2 sample."""
+    from spacedrive_amd import corpus
+    lens = np.array(sorted({n * 1024 + d for n in range(0, 101) for d in (-64, -1, 0, 1, 8, 65)
+                            if 0 <= n * 1024 + d <= 102408} | {57352}), np.uint32)
+    off = np.zeros(lens.size, np.uint64)
+    pos = 0
+    for i, n in enumerate(lens):
+        off[i] = pos
+        pos += (int(n) + 127) // 128 * 128
+    arena = np.random.default_rng(3).integers(0, 256, pos + 16, dtype=np.uint8)
+    np.testing.assert_array_equal(O.cas_batch_simd(arena, off, lens, 4),
+                                  O.cas_batch(arena, off, lens, 4))
+    sizes, seeds = corpus.config2_files(3000, seed=8)
+    ar, of, ln = O.synth_arena(sizes, seeds)
+    np.testing.assert_array_equal(O.cas_batch_simd(ar, of, ln, 4), O.cas_batch(ar, of, ln, 4))

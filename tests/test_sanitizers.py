@@ -14,7 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not available")
 def test_oracle_clean_under_asan_ubsan(tmp_path):
     exe = tmp_path / "oracle_san"
-    cmd = ["gcc", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+    cmd = ["gcc", "-O1", "-g", "-march=x86-64-v3", "-fno-omit-frame-pointer",
+           "-fsanitize=address,undefined",
            "-fno-sanitize-recover=all", "-pthread",
            os.path.join(ROOT, "oracle", "sd_oracle.c"),
            os.path.join(ROOT, "oracle", "sanitize_main.c"), "-o", str(exe)]
