@@ -115,17 +115,36 @@ def shard_plan(world: int):
     return bits, owner, skip
 
 
+class TorchDistExchange:
+    """The exchange of the sharded grouping over torch.distributed (RCCL on
+    ROCm, gloo in the CPU tests)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def world_size(self) -> int:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(self.group)
+        return 1
+
+    def all_to_all(self, out, inp, out_splits=None, in_splits=None):
+        import torch.distributed as dist
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
+
 def sharded_group_reps(key, has_key, rank, chunk_rows: int = CHUNK_SIZE, group=None, ops=None,
-                       timings: dict | None = None):
+                       timings: dict | None = None, exchange=None):
     """Grouping of this rank's rows against the rows of every rank in `group`.
 
     key: int64 tensor (u64 cas keys), has_key: uint8, rank: int32 (global
     ranks, u32).  Returns int32 rep (global ranks) for this rank's rows.
-    Collective: every rank of `group` must call it."""
+    Collective: every rank of `group` must call it.  `exchange` replaces the
+    torch.distributed all-to-alls (default TorchDistExchange(group))."""
     import torch
-    import torch.distributed as dist
     ops = ops or HipOps()
-    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    exchange = exchange or TorchDistExchange(group)
+    world = exchange.world_size()
     n = key.numel()
     if world == 1:  # no exchange: group the rows in place (no compaction pass)
         return ops.group_rows(key, has_key, rank, chunk_rows, 0)
@@ -137,17 +156,17 @@ def sharded_group_reps(key, has_key, rank, chunk_rows: int = CHUNK_SIZE, group=N
     dev = key.device
     sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
     rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
+    exchange.all_to_all(rc, sc)
     recv_counts = rc.cpu().numpy().astype(np.int64)
     m = int(recv_counts.sum())
     s_list, r_list = send_counts.tolist(), recv_counts.tolist()
     rkey = torch.empty(m, dtype=torch.int64, device=dev)
     rrank = torch.empty(m, dtype=torch.int32, device=dev)
-    dist.all_to_all_single(rkey, skey, r_list, s_list, group=group)
-    dist.all_to_all_single(rrank, srank, r_list, s_list, group=group)
+    exchange.all_to_all(rkey, skey, r_list, s_list)
+    exchange.all_to_all(rrank, srank, r_list, s_list)
     rrep = ops.group(rkey, rrank, chunk_rows, skip)
     rep_sent = torch.empty(total, dtype=torch.int32, device=dev)
-    dist.all_to_all_single(rep_sent, rrep, s_list, r_list, group=group)
+    exchange.all_to_all(rep_sent, rrep, s_list, r_list)
     return ops.scatter(rep_sent, spos, n, rank)
 
 

@@ -65,3 +65,67 @@ def test_config4_shape_single_gpu(ctx):
     np.testing.assert_array_equal(hk[:200_000], k2)
     np.testing.assert_array_equal(hh[:200_000], h2)
     np.testing.assert_array_equal(rep.cpu().numpy().view(np.uint32), O.group_reps(hk, hh, 100))
+
+
+class ThreadExchange:
+    """W 'ranks' as threads of one process on one GPU: all_to_all moves the
+    device tensors between them through shared slots (a test stand-in for
+    RCCL that exercises every HipOps step of the N > 1 path on the GPU)."""
+
+    def __init__(self, rank, world, shared):
+        self.rank, self.world, self.shared = rank, world, shared
+
+    def world_size(self):
+        return self.world
+
+    def all_to_all(self, out, inp, out_splits=None, in_splits=None):
+        import torch
+        W = self.world
+        ins = in_splits or [inp.numel() // W] * W
+        outs = out_splits or [out.numel() // W] * W
+        torch.cuda.synchronize()
+        self.shared["slots"][self.rank] = list(torch.split(inp, ins))
+        self.shared["barrier"].wait()
+        parts = [self.shared["slots"][src][self.rank] for src in range(W)]
+        assert [p.numel() for p in parts] == outs
+        torch.cat(parts, out=out) if out.numel() else None
+        torch.cuda.synchronize()
+        self.shared["barrier"].wait()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sharded_path_all_hip_ops_on_gpu(ctx, world):
+    """The N-GPU grouping (partition -> exchange -> group -> return ->
+    scatter) with the HIP kernels, W ranks emulated in one process."""
+    import threading
+    import torch
+    from spacedrive_amd import dedup
+    total, distinct = 300_000, 200_000
+    shared = {"slots": [None] * world, "barrier": threading.Barrier(world)}
+    results, errors = {}, []
+
+    def run(r):
+        try:
+            per = total // world
+            first = r * per
+            n = per if r < world - 1 else total - first
+            k, h, rk = O.synth_dedup_rows(11, total, distinct, first, n)
+            rep = dedup.sharded_group_reps(
+                torch.from_numpy(k.view(np.int64)).cuda(), torch.from_numpy(h).cuda(),
+                torch.from_numpy(rk.view(np.int32)).cuda(), 100, ops=dedup.HipOps(ctx),
+                exchange=ThreadExchange(r, world, shared))
+            torch.cuda.synchronize()
+            results[r] = rep.cpu().numpy().view(np.uint32)
+        except Exception as e:  # surface thread failures
+            errors.append(e)
+            shared["barrier"].abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errors, errors
+    rep = np.concatenate([results[r] for r in range(world)])
+    k, h, _ = O.synth_dedup_rows(11, total, distinct, 0, total)
+    np.testing.assert_array_equal(rep, O.group_reps(k, h, 100))
