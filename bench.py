@@ -458,6 +458,7 @@ def main():
     R = Runner(args)
     torch = R.torch
     valu_peak = R.ctx.valu_peak()
+    compress_peak = R.ctx.valu_peak(5)  # register-only compressions, 680 VALU each
     classes = {name: R.ctx.valu_peak(k) / 1e12 for k, name in
                [(1, "v_xor_b32"), (2, "v_add3_u32"), (3, "v_alignbit_b32"), (4, "v_add_u32")]}
     log(f"measured int32 VALU peak: {valu_peak / 1e12:.1f} T lane-ops/s "
@@ -516,8 +517,11 @@ def main():
             "achieved": achieved / 1e12, "peak": VALU_PEAK_SPEC / 1e12, "unit": "Tops/s",
             "frac": achieved / VALU_PEAK_SPEC, "traffic": traffic,
             "traffic_source": traffic_src,
-            "peak_measured": valu_peak / 1e12, "peak_by_class_measured": classes,
-            "frac_of_measured": achieved / valu_peak if valu_peak else None,
+            "peak_measured": compress_peak / 1e12,
+            "peak_measured_note": "register-only BLAKE3 compressions (same 680-VALU stream, no "
+                                  "memory traffic): the attainable issue roof of this mix",
+            "peak_g_mix_probe": valu_peak / 1e12, "peak_by_class_measured": classes,
+            "frac_of_measured": achieved / compress_peak if compress_peak else None,
             "algorithmic_per_launch": {"compressions": ri["leaf_compressions"],
                                        "int32_ops": ops, "window_bytes": ri["bytes"]},
             "compressions_per_s": ri["leaf_compressions"] / t_leaf if t_leaf else None,

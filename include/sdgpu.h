@@ -232,7 +232,8 @@ int sdgpu_timing_read(sdgpu_ctx *ctx, uint32_t idx, char name[32], double *total
  * add3/xor/alignbit stream at full occupancy: the VALU roofline's peak. */
 int sdgpu_valu_probe(sdgpu_ctx *ctx, double *lane_ops_per_s);
 /* Same for one instruction class: 0 the G mix above, 1 v_xor_b32, 2 v_add3_u32,
- * 3 v_alignbit_b32, 4 v_add_u32. */
+ * 3 v_alignbit_b32, 4 v_add_u32; 5 = whole BLAKE3 compressions with everything
+ * in registers (680 VALU each): the attainable roof of K1/K2's stream. */
 int sdgpu_valu_probe_kind(sdgpu_ctx *ctx, int kind, double *lane_ops_per_s);
 
 #ifdef __cplusplus

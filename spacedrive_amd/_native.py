@@ -171,7 +171,8 @@ class Context:
 
     def valu_peak(self, kind: int = 0) -> float:
         """Measured int32 VALU lane-ops/s: kind 0 = BLAKE3-G instruction mix,
-        1 v_xor_b32, 2 v_add3_u32, 3 v_alignbit_b32, 4 v_add_u32."""
+        1 v_xor_b32, 2 v_add3_u32, 3 v_alignbit_b32, 4 v_add_u32, 5 register-only
+        BLAKE3 compressions (680 VALU each: the attainable roof of K1/K2)."""
         v = ctypes.c_double()
         check(self.lib.sdgpu_valu_probe_kind(self.h, kind, ctypes.byref(v)), "sdgpu_valu_probe")
         return v.value

@@ -1355,14 +1355,15 @@ int sdgpu_valu_probe(sdgpu_ctx* c, double* lane_ops_per_s) {
 }
 
 int sdgpu_valu_probe_kind(sdgpu_ctx* c, int kind, double* lane_ops_per_s) {
-  if (!c || !lane_ops_per_s || kind < 0 || kind > 4) return -EINVAL;
+  if (!c || !lane_ops_per_s || kind < 0 || kind > 5) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
   SD_TRY_RC(ensure_dev(c, c->io_b, 1 << 20));
   hipEvent_t a, b;
   SD_TRY(hipEventCreate(&a));
   SD_TRY(hipEventCreate(&b));
-  const uint32_t iters = 4096, blocks = 256 * 8 * 4;  // 32 waves per CU
+  // kind 5 (register-only compressions): 16 waves per CU, 2000 compressions each
+  const uint32_t iters = kind == 5 ? 2000 : 4096, blocks = kind == 5 ? 256 * 16 : 256 * 8 * 4;
   uint32_t* sink = static_cast<uint32_t*>(c->io_b.p);
   SD_TRY(valu_probe_launch(kind, sink, 64, blocks, c->stream));  // warm
   SD_TRY(hipEventRecord(a, c->stream));
@@ -1373,8 +1374,10 @@ int sdgpu_valu_probe_kind(sdgpu_ctx* c, int kind, double* lane_ops_per_s) {
   SD_TRY(hipEventElapsedTime(&ms, a, b));
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
-  // per iteration per chain: add3, xor, alignbit, add3, xor, alignbit = 6 VALU
-  const double ops = double(iters) * 8 * 6 * blocks * 256;
+  // kind 5: 680 VALU per compression; others: per iteration per chain add3,
+  // xor, alignbit, add3, xor, alignbit = 6 VALU (kinds 1-4: 6 of one class)
+  const double ops = kind == 5 ? double(iters) * 680 * blocks * 256
+                               : double(iters) * 8 * 6 * blocks * 256;
   *lane_ops_per_s = ops / (ms * 1e-3);
   return 0;
 }

@@ -6,6 +6,7 @@
 // A cas message for a file (size, seed) is laid out as generate_cas_id reads it
 // (/root/reference/core/src/object/cas.rs:24-58): size_le || whole file (size <=
 // 100 KiB) or size_le || header || 4 samples at 8192 + k*((size-16384)/4) || footer.
+#include "b3_device.hpp"
 #include "internal.hpp"
 
 namespace sdgpu {
@@ -188,9 +189,29 @@ __global__ __launch_bounds__(256) void k_valu_class(uint32_t* __restrict__ sink,
 
 }  // namespace
 
+// BLAKE3 compressions with everything in registers (no memory): the
+// attainable roof of the exact instruction stream K1/K2 issue (680 VALU per
+// compression, BLAKE3's add3/xor/alignbit mix).
+__global__ __launch_bounds__(256) void k_compress_probe(uint32_t* __restrict__ sink,
+                                                        uint32_t iters) {
+  uint32_t cv[8], m[16];
+  b3_iv(cv);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) m[i] = threadIdx.x * 0x9E3779B9u + blockIdx.x * 7u + i;
+  for (uint32_t it = 0; it < iters; ++it) {
+    b3_compress(cv, m, it, 0u, 64u, 0u);
+    m[it & 15] ^= cv[it & 7];
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x ^= cv[i];
+  if (x == 0x12345u) sink[blockIdx.x] = x;
+}
+
 hipError_t valu_probe_launch(int kind, uint32_t* sink, uint32_t iters, uint32_t blocks,
                              hipStream_t s) {
   switch (kind) {
+    case 5: k_compress_probe<<<blocks, 256, 0, s>>>(sink, iters); break;
     case 1: k_valu_class<1><<<blocks, 256, 0, s>>>(sink, iters); break;
     case 2: k_valu_class<2><<<blocks, 256, 0, s>>>(sink, iters); break;
     case 3: k_valu_class<3><<<blocks, 256, 0, s>>>(sink, iters); break;
