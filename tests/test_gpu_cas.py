@@ -171,3 +171,33 @@ def test_small_batch_latency_kernel_bit_exact(ctx, n, tmp_path):
         out, st = cas.cas_batch(arena, off, ln, ctx)
         assert np.all(st == 0)
         np.testing.assert_array_equal(out, O.cas_batch(arena, off, ln, threads=4))
+
+
+def test_host_pipeline_many_slabs_by_file_count(ctx):
+    """sdgpu_cas_batch with more messages than one staging slab holds
+    (65 536 files per slab): the double-buffered pipeline drains and refills."""
+    from spacedrive_amd import cas
+    n = 150_000
+    rng = np.random.default_rng(11)
+    lens = rng.integers(0, 1500, n).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum((lens[:-1].astype(np.uint64) + 15) // 16 * 16)
+    arena = rng.integers(0, 256, int(off[-1]) + int(lens[-1]) + 16, dtype=np.uint8)
+    out, st = cas.cas_batch(arena, off, lens, ctx)
+    assert np.all(st == 0)
+    np.testing.assert_array_equal(out, O.cas_batch(arena, off, lens, threads=16))
+
+
+def test_host_pipeline_many_slabs_by_bytes(ctx):
+    """~700 MB of maximal messages: the 256 MiB slab fills by bytes first."""
+    from spacedrive_amd import cas
+    n = 7000
+    lens = np.full(n, 102408, np.uint32)
+    lens[::7] = 57352
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum((lens[:-1].astype(np.uint64) + 127) // 128 * 128)
+    arena = np.random.default_rng(12).integers(0, 256, int(off[-1]) + 102408 + 16,
+                                                dtype=np.uint8)
+    out, st = cas.cas_batch(arena, off, lens, ctx)
+    assert np.all(st == 0)
+    np.testing.assert_array_equal(out, O.cas_batch(arena, off, lens, threads=16))

@@ -88,3 +88,23 @@ def test_link_batch_vs_oracle(ctx, n, first_rank, with_valid):
         d_rank = torch.arange(first_rank, first_rank + n, dtype=torch.int64).to(torch.int32).cuda()
         c2, lr2, lo2 = dedup.link_batch_device(d_rep, d_rank, d_valid, 0, ctx=ctx)
         assert torch.equal(c2, c) and torch.equal(lr2, lr) and torch.equal(lo2, lo)
+
+
+def test_stage_pinned_piece_split_by_file_count(ctx):
+    """More than 65 536 tiny messages: the staged path splits pieces by file
+    count, not bytes."""
+    import torch
+    from spacedrive_amd import cas
+    n = 140_000
+    rng = np.random.default_rng(13)
+    lens = rng.integers(0, 300, n).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum((lens[:-1].astype(np.uint64) + 15) // 16 * 16)
+    total = int(off[-1]) + int(lens[-1]) + 16
+    arena = rng.integers(0, 256, total, dtype=np.uint8)
+    h = torch.empty(total, dtype=torch.uint8).pin_memory()
+    h.numpy()[:] = arena
+    out, st = cas.cas_stage_pinned(h, off, lens, ctx=ctx)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0
+    np.testing.assert_array_equal(out.cpu().numpy(), O.cas_batch(arena, off, lens, threads=16))
