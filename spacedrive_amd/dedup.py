@@ -187,7 +187,9 @@ def link_batch_device(rep, rank=None, valid=None, first_rank: int = 0, ctx=None,
     create = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     lrow = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     lobj = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-    counts = torch.zeros(2, dtype=torch.int32, device=dev)
+    # no fill kernel: the K7 scans write both counts (a null-stream fill here would
+    # order the host behind the whole queued step on the context stream)
+    counts = torch.empty(2, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream(dev).cuda_stream
     check(ctx.lib.sdgpu_link_batch_device(
         ctx.h, rep.data_ptr(), rank.data_ptr() if rank is not None else None,
