@@ -103,11 +103,17 @@ class Runner:
         self.torch, self.dist = torch, dist
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
-        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # one process per GPU; LOCAL_RANK wraps only in the 1-GPU rehearsal
+        # (SD_BENCH_BACKEND=gloo: N ranks sharing one card, exchange via host)
+        self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(self.local)
         self.dev = torch.device("cuda", self.local)
+        backend = os.environ.get("SD_BENCH_BACKEND", "nccl")  # nccl = RCCL over xGMI
         if self.world > 1:
-            dist.init_process_group("nccl", device_id=self.dev)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(backend)
         from spacedrive_amd._native import default_context
         self.ctx = default_context(self.local)
         self.args = args
@@ -173,7 +179,7 @@ class Runner:
         assert int(st.abs().sum()) == 0
         res["cas"] = {"value": self.world * n * steps / t_cas, "unit": "files/s",
                       "ms_per_step": 1e3 * t_cas / steps,
-                      "config": {"workload": "config2: 1M log-normal files/GPU, 20% dup, 0.1% empty",
+                      "config": {"workload": f"config2: {n} log-normal files/GPU, 20% dup, 0.1% empty",
                                  "files_per_gpu": n, "window_bytes_per_gpu": int(lens.sum())}}
         ms_leaves, nl = kt.get("cas_leaves", (0.0, 1))
         avg_leaves = ms_leaves / max(nl, 1) * 1e-3
@@ -321,6 +327,8 @@ class Runner:
                                                         self.rank * per, per,
                                                         device=self.local, ctx=self.ctx)
         ops = dedup.HipOps(self.ctx)
+        if self.args.verify:
+            self.verify_sharded(key, has, rank, ops)
         self.ctx.set_timing(True)
         t = self.timed(lambda: dedup.sharded_group_reps(key, has, rank, 100, ops=ops), steps,
                        warmup)
@@ -331,6 +339,25 @@ class Runner:
                            "rows_per_gpu": per, "rows_total": total},
                 "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
                             for k, v in kt.items()}}
+
+    def verify_sharded(self, key, has, rank, ops):
+        """--verify: the sharded grouping over all ranks (the exchange path the
+        timed steps use) equals the one-GPU grouping of the gathered table."""
+        torch, dist = self.torch, self.dist
+        from spacedrive_amd import dedup
+        rep = dedup.sharded_group_reps(key, has, rank, 100, ops=ops)
+        if self.world > 1:
+            parts = [[torch.empty_like(t) for _ in range(self.world)] for t in (key, has, rank, rep)]
+            for p, t in zip(parts, (key, has, rank, rep)):
+                dist.all_gather(p, t)
+            key, has, rank, rep = (torch.cat(p) for p in parts)
+        if self.rank == 0:
+            ref = ops.group_rows(key, has, rank, 100, 0)
+            bad = int((ref != rep).sum())
+            log(f"verify: sharded grouping of {key.numel()} rows over {self.world} ranks: "
+                f"{bad} mismatches vs the one-GPU grouping")
+            assert bad == 0, "sharded grouping differs from the one-GPU grouping"
+        self.barrier()
 
     # ---------------------------------------------------------------- config 3
     def run_checksum(self, steps, warmup):
@@ -452,6 +479,8 @@ def main():
     ap.add_argument("--components", default="cas,dedup,checksum,staged,dir,single")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verify", action="store_true",
+                    help="check the sharded grouping against the one-GPU grouping first")
     args = ap.parse_args()
     comps = set(args.components.split(","))
 
