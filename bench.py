@@ -334,7 +334,22 @@ class Runner:
                        warmup)
         kt = self.ctx.kernel_times()
         self.ctx.set_timing(False)
+        xinfo = {}
+        dedup.sharded_group_reps(key, has, rank, 100, ops=ops, timings=xinfo)
+        xchg = None
+        if self.world > 1:
+            # payload of one step on this rank: (key u64, rank u32) out, rep u32 back;
+            # a 1/W share of it stays on the GPU (its own shards)
+            fwd = 12 * (xinfo["sent_rows"] + xinfo["recv_rows"])
+            back = 4 * (xinfo["sent_rows"] + xinfo["recv_rows"])
+            remote = (self.world - 1) / self.world
+            xchg = {"payload_bytes_per_gpu": fwd + back,
+                    "remote_bytes_per_gpu_est": int((fwd + back) * remote),
+                    "remote_GBps_per_gpu_over_step": (fwd + back) * remote / (t / steps) / 1e9,
+                    "note": "bytes sent + received per GPU per step over xGMI (RCCL all-to-all); "
+                            "rate is over the whole step, a lower bound on the link rate"}
         return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
+                "exchange": xchg,
                 "config": {"workload": "config4: 80% distinct u64 keys + 20% dups, 0.1% keyless",
                            "rows_per_gpu": per, "rows_total": total},
                 "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}

@@ -184,6 +184,16 @@ int sdgpu_shard_partition_device(sdgpu_ctx *ctx, const uint64_t *d_key, const ui
                                  const uint32_t *d_rank, uint64_t n, uint32_t shard_bits,
                                  uint64_t *d_out_key, uint32_t *d_out_rank, uint32_t *d_out_pos,
                                  void *stream);
+/* The send side of the sharded grouping's exchange in one call, with no host
+ * synchronisation: the partition of sdgpu_shard_partition_device (one
+ * histogram pass) plus d_dest_counts[d] (int64, device) = packed rows destined
+ * to rank d, where shard s belongs to rank (s * world) >> shard_bits.  Ranks'
+ * segments are contiguous and in rank order in d_out_*; sized n rows (keyless
+ * rows are dropped, so the tail is unused).  world <= 64, world <= 2^shard_bits. */
+int sdgpu_shard_exchange_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t *d_has_key,
+                                const uint32_t *d_rank, uint64_t n, uint32_t shard_bits,
+                                uint32_t world, uint64_t *d_out_key, uint32_t *d_out_rank,
+                                uint32_t *d_out_pos, int64_t *d_dest_counts, void *stream);
 /* d_dst[d_pos[i]] = d_src[i] for i < n.  With init != 0 every row of d_dst is
  * first set to d_init[r] (or to r when d_init is NULL), so rows without a key
  * keep their own rank (mod.rs:238-239). */

@@ -63,6 +63,8 @@ def _proto(L):
         "sdgpu_shard_count_device": (i32, [ctx, c_vp, c_vp, u64, u32, c_vp, c_vp]),
         "sdgpu_shard_partition_device": (i32, [ctx, c_vp, c_vp, c_vp, u64, u32, c_vp, c_vp, c_vp,
                                                c_vp]),
+        "sdgpu_shard_exchange_device": (i32, [ctx, c_vp, c_vp, c_vp, u64, u32, u32, c_vp, c_vp,
+                                              c_vp, c_vp, c_vp]),
         "sdgpu_scatter_rep_device": (i32, [ctx, c_vp, c_vp, u64, c_vp, u64, c_vp, i32, c_vp]),
         "sdgpu_synth_cas_arena_device": (i32, [ctx, c_vp, c_vp, c_vp, u32, c_vp, c_vp]),
         "sdgpu_synth_file_device": (i32, [ctx, u64, u64, u64, c_vp, c_vp]),

@@ -321,6 +321,20 @@ __global__ void k_copy_counts(const uint32_t* __restrict__ offs, uint32_t nbins,
                 offs[static_cast<uint64_t>(b) * kPartBlocks];
 }
 
+// Rows per destination rank of the exchange, from the scanned shard offsets
+// (owner of shard s = s * world >> bits, shard_plan in spacedrive_amd/dedup.py).
+__global__ void k_dest_counts(const uint32_t* __restrict__ offs, uint32_t bits, uint32_t world,
+                              int64_t* __restrict__ counts) {
+  const uint32_t d = threadIdx.x;
+  if (d >= world) return;
+  int64_t c = 0;
+  for (uint32_t b = 0; b < (1u << bits); ++b)
+    if (((static_cast<uint64_t>(b) * world) >> bits) == d)
+      c += offs[static_cast<uint64_t>(b + 1) * kPartBlocks] -
+           offs[static_cast<uint64_t>(b) * kPartBlocks];
+  counts[d] = c;
+}
+
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 uint32_t bucket_bits_for(uint64_t n) {
@@ -430,6 +444,22 @@ hipError_t shard_partition_launch(const uint64_t* key, const uint8_t* has_key,
   uint32_t* tiles = reinterpret_cast<uint32_t*>(w + align_up(4 * (nh + 1), 256));
   return partition(key, has_key, rank, n, 0, shard_bits, hist, tiles, out_key, out_rank, out_pos,
                    s, timer, "shard_hist", "shard_scatter");
+}
+
+hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
+                                 const uint32_t* rank, uint64_t n, uint32_t shard_bits,
+                                 uint32_t world, uint64_t* out_key, uint32_t* out_rank,
+                                 uint32_t* out_pos, int64_t* d_dest_counts, void* ws,
+                                 hipStream_t s, KTimer* timer) {
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + align_up(4 * (nh + 1), 256));
+  hipError_t e = partition(key, has_key, rank, n, 0, shard_bits, hist, tiles, out_key, out_rank,
+                           out_pos, s, timer, "shard_hist", "shard_scatter");
+  if (e != hipSuccess) return e;
+  k_dest_counts<<<1, 64, 0, s>>>(hist, shard_bits, world, d_dest_counts);
+  return hipGetLastError();
 }
 
 hipError_t scatter_rep_launch(const uint32_t* src, const uint32_t* pos, uint64_t n, uint32_t* dst,

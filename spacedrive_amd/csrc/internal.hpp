@@ -117,6 +117,13 @@ hipError_t shard_partition_launch(const uint64_t* key, const uint8_t* has_key,
                                   const uint32_t* rank, uint64_t n, uint32_t shard_bits,
                                   uint64_t* out_key, uint32_t* out_rank, uint32_t* out_pos,
                                   void* ws, hipStream_t s, KTimer* timer = nullptr);
+// partition by shard (one hist + scan + scatter) and, on device, the rows per
+// destination rank (int64[world]); no host synchronisation.
+hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
+                                 const uint32_t* rank, uint64_t n, uint32_t shard_bits,
+                                 uint32_t world, uint64_t* out_key, uint32_t* out_rank,
+                                 uint32_t* out_pos, int64_t* d_dest_counts, void* ws,
+                                 hipStream_t s, KTimer* timer = nullptr);
 hipError_t scatter_rep_launch(const uint32_t* src, const uint32_t* pos, uint64_t n, uint32_t* dst,
                               uint64_t n_dst, const uint32_t* init, bool do_init, hipStream_t s);
 

@@ -1254,6 +1254,23 @@ int sdgpu_shard_partition_device(sdgpu_ctx* c, const uint64_t* d_key, const uint
   return 0;
 }
 
+int sdgpu_shard_exchange_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8_t* d_has_key,
+                                const uint32_t* d_rank, uint64_t n, uint32_t shard_bits,
+                                uint32_t world, uint64_t* d_out_key, uint32_t* d_out_rank,
+                                uint32_t* d_out_pos, int64_t* d_dest_counts, void* stream) {
+  if (!c || shard_bits == 0 || shard_bits > 8 || world == 0 || world > 64 ||
+      world > (1u << shard_bits) || !d_dest_counts ||
+      (n && (!d_key || !d_out_key || !d_out_rank || !d_out_pos)))
+    return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  SD_TRY_RC(ensure_dev(c, c->shard_ws, shard_workspace_bytes(shard_bits)));
+  SD_TRY(shard_exchange_launch(d_key, d_has_key, d_rank, n, shard_bits, world, d_out_key,
+                               d_out_rank, d_out_pos, d_dest_counts, c->shard_ws.p, s, c->kt()));
+  return 0;
+}
+
 int sdgpu_scatter_rep_device(sdgpu_ctx* c, const uint32_t* d_src, const uint32_t* d_pos,
                              uint64_t n, uint32_t* d_dst, uint64_t n_dst, const uint32_t* d_init,
                              int init, void* stream) {

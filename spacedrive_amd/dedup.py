@@ -8,7 +8,7 @@ lowest-rank row f; rep[r] = f otherwise.
 
 Multi-GPU (one process per GPU, torch.distributed over RCCL/xGMI): rows are
 hash-partitioned by the top 8 bits of the cas key (256 shards, shard s owned
-by rank s*W//256), exchanged with ONE all-to-all of (key, rank), grouped locally
+by rank s*W//256), exchanged by all-to-all of (key, rank), grouped locally
 (the chunk rule only needs the global rank carried in the payload) and the
 representatives return with a second all-to-all.  The exchange logic below is
 backend-agnostic (`ops`), so it is tested with gloo on CPU; the product ops are
@@ -70,6 +70,23 @@ class HipOps:
             key.numel(), shard_bits, okey.data_ptr(), orank.data_ptr(), opos.data_ptr(),
             self._s(key)), "sdgpu_shard_partition_device")
         return okey, orank, opos
+
+    def exchange_partition(self, key, has_key, rank, shard_bits: int, world: int):
+        """Send side in one pass, no host sync: rows packed by destination rank
+        (n-row buffers, keyless rows dropped) + int64 rows per destination on
+        the device (sdgpu_shard_exchange_device)."""
+        import torch
+        ctx = self._c(key)
+        n = key.numel()
+        okey = torch.empty(max(n, 1), dtype=torch.int64, device=key.device)
+        orank = torch.empty(max(n, 1), dtype=torch.int32, device=key.device)
+        opos = torch.empty(max(n, 1), dtype=torch.int32, device=key.device)
+        dest = torch.empty(world, dtype=torch.int64, device=key.device)
+        check(ctx.lib.sdgpu_shard_exchange_device(
+            ctx.h, key.data_ptr(), has_key.data_ptr(), rank.data_ptr() if rank is not None else None,
+            n, shard_bits, world, okey.data_ptr(), orank.data_ptr(), opos.data_ptr(),
+            dest.data_ptr(), self._s(key)), "sdgpu_shard_exchange_device")
+        return okey, orank, opos, dest
 
     def group(self, key, rank, chunk_rows: int, skip_bits: int):
         import torch
@@ -149,17 +166,20 @@ def sharded_group_reps(key, has_key, rank, chunk_rows: int = CHUNK_SIZE, group=N
     if world == 1:  # no exchange: group the rows in place (no compaction pass)
         return ops.group_rows(key, has_key, rank, chunk_rows, 0)
     bits, owner, skip = shard_plan(world)
-    counts = ops.shard_counts(key, has_key, bits)
-    send_counts = np.bincount(owner, weights=counts, minlength=world).astype(np.int64)
-    total = int(send_counts.sum())
-    skey, srank, spos = ops.partition(key, has_key, rank, bits, total)
+    # partition + per-destination counts on the device, counts exchanged
+    # device to device: the step's ONE host synchronisation is the read of the
+    # send and receive counts that size the payload all-to-alls
+    skey, srank, spos, sc = ops.exchange_partition(key, has_key, rank, bits, world)
     dev = key.device
-    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
     rc = torch.empty_like(sc)
     exchange.all_to_all(rc, sc)
-    recv_counts = rc.cpu().numpy().astype(np.int64)
-    m = int(recv_counts.sum())
-    s_list, r_list = send_counts.tolist(), recv_counts.tolist()
+    both = torch.cat([sc, rc]).cpu().numpy().astype(np.int64)
+    s_list, r_list = both[:world].tolist(), both[world:].tolist()
+    total, m = int(sum(s_list)), int(sum(r_list))
+    if timings is not None:  # exchange volume of this call (payload bytes sent / received)
+        timings["sent_rows"] = total
+        timings["recv_rows"] = m
+    skey, srank, spos = skey[:total], srank[:total], spos[:total]
     rkey = torch.empty(m, dtype=torch.int64, device=dev)
     rrank = torch.empty(m, dtype=torch.int32, device=dev)
     exchange.all_to_all(rkey, skey, r_list, s_list)

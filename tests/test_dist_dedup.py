@@ -36,6 +36,16 @@ class NumpyOps:
                 torch.from_numpy(np.ascontiguousarray(r[sel], np.int32)),
                 torch.from_numpy(sel.astype(np.int32)))
 
+    def exchange_partition(self, key, has_key, rank, bits, world):
+        counts = self.shard_counts(key, has_key, bits)
+        owner = (np.arange(1 << bits, dtype=np.int64) * world) >> bits
+        dest = np.bincount(owner, weights=counts, minlength=world).astype(np.int64)
+        okey, orank, opos = self.partition(key, has_key, rank, bits, int(dest.sum()))
+        pad = key.numel() - okey.numel()  # n-row buffers, as the HIP op returns
+        z64, z32 = torch.zeros(pad, dtype=torch.int64), torch.zeros(pad, dtype=torch.int32)
+        return (torch.cat([okey, z64]), torch.cat([orank, z32]), torch.cat([opos, z32]),
+                torch.from_numpy(dest))
+
     def group(self, key, rank, chunk_rows, skip):
         k = key.numpy().view(np.uint64)
         r = rank.numpy().view(np.uint32).astype(np.int64)

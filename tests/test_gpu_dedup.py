@@ -129,3 +129,29 @@ def test_sharded_path_all_hip_ops_on_gpu(ctx, world):
     rep = np.concatenate([results[r] for r in range(world)])
     k, h, _ = O.synth_dedup_rows(11, total, distinct, 0, total)
     np.testing.assert_array_equal(rep, O.group_reps(k, h, 100))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_exchange_partition_matches_count_and_partition(ctx, world):
+    """sdgpu_shard_exchange_device (one pass, device counts) packs exactly what
+    sdgpu_shard_count_device + sdgpu_shard_partition_device do."""
+    import torch
+    from spacedrive_amd import dedup
+    k, h, rk = O.synth_dedup_rows(13, 500_000, 350_000, 0, 500_000)
+    key = torch.from_numpy(k.view(np.int64)).cuda()
+    has = torch.from_numpy(h).cuda()
+    rank = torch.from_numpy(rk.view(np.int32)).cuda()
+    ops = dedup.HipOps(ctx)
+    bits, owner, _ = dedup.shard_plan(world)
+    counts = ops.shard_counts(key, has, bits)
+    dest_ref = np.bincount(owner, weights=counts, minlength=world).astype(np.int64)
+    total = int(dest_ref.sum())
+    rk_, rr_, rp_ = ops.partition(key, has, rank, bits, total)
+    ok, orr, op, dest = ops.exchange_partition(key, has, rank, bits, world)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dest.cpu().numpy(), dest_ref)
+    assert total == int(h.sum())
+    np.testing.assert_array_equal(ok[:total].cpu().numpy(), rk_.cpu().numpy())
+    np.testing.assert_array_equal(orr[:total].cpu().numpy(), rr_.cpu().numpy())
+    np.testing.assert_array_equal(op[:total].cpu().numpy(), rp_.cpu().numpy())
