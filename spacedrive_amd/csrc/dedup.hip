@@ -42,8 +42,11 @@ namespace {
 constexpr int kPartThreads = 1024;
 constexpr uint32_t kPartBlocks = 256;  // one per CU
 constexpr int kGroupThreads = 1024;
-constexpr uint32_t kLdsSlots = 8192;   // table slots in LDS (96 KiB: one bucket per CU)
-constexpr uint32_t kLdsCap = 6144;     // rows per bucket handled in LDS (load <= 75%)
+// 6144 slots x 12 B = 72 KiB of LDS, so two buckets share a CU (8 waves/SIMD)
+// and one bucket's loads overlap the other's LDS atomics.  The slot count is
+// not a power of two: slots are indexed by the high half of hash * tsize.
+constexpr uint32_t kLdsSlots = 6144;
+constexpr uint32_t kLdsCap = 4608;     // rows per bucket handled in LDS (load <= 75%)
 constexpr uint64_t kBucketRows = 3072; // target mean rows per bucket (bucket_bits_for)
 constexpr uint64_t kEmpty = ~0ull;
 
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
   __syncthreads();
   uint64_t t0, t1;
   tile_of(n, t0, t1);
-  constexpr int U = kUnroll / 2;
+  constexpr int U = kUnroll;
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += U * kPartThreads) {
     uint64_t k[U];
     uint32_t r[U];
@@ -170,12 +173,18 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
   }
 }
 
-__device__ __forceinline__ uint32_t slot_hash(uint64_t k) {
-  return static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> 32);
+// First probe slot of key k in a table of tsize slots (any tsize).
+__device__ __forceinline__ uint32_t slot_of(uint64_t k, uint32_t tsize) {
+  const uint32_t h = static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> 32);
+  return static_cast<uint32_t>((static_cast<uint64_t>(h) * tsize) >> 32);
+}
+
+__device__ __forceinline__ uint32_t next_slot(uint32_t h, uint32_t tsize) {
+  return h + 1 == tsize ? 0u : h + 1;
 }
 
 // One workgroup per bucket.  Rows of bucket b: [offs[b*P], offs[(b+1)*P]).
-__global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
+__global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
     const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t nbuckets,
     uint32_t chunk_rows, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
     uint32_t* __restrict__ rep) {
@@ -214,7 +223,6 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
   }
   if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
   __syncthreads();
-  const uint32_t mask = tsize - 1;
   if (in_lds) {
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
         atomicMin(&special_min, r);
         continue;
       }
-      uint32_t h = slot_hash(k) & mask;
+      uint32_t h = slot_of(k, tsize);
       for (;;) {
         const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tk[h]),
                                         static_cast<unsigned long long>(kEmpty),
@@ -234,7 +242,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
           atomicMin(&tm[h], r);
           break;
         }
-        h = (h + 1) & mask;
+        h = next_slot(h, tsize);
       }
     }
     __syncthreads();
@@ -247,8 +255,8 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
       if (k == kEmpty) {
         f = special_min;
       } else {
-        uint32_t h = slot_hash(k) & mask;
-        while (tk[h] != k) h = (h + 1) & mask;
+        uint32_t h = slot_of(k, tsize);
+        while (tk[h] != k) h = next_slot(h, tsize);
         f = tm[h];
       }
       if (r / chunk_rows != f / chunk_rows) rep[q_reg[j].w] = f;  // others keep rank
@@ -263,7 +271,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
       atomicMin(&special_min, r);
       continue;
     }
-    uint32_t h = slot_hash(k) & mask;
+    uint32_t h = slot_of(k, tsize);
     for (;;) {
       const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tk[h]),
                                       static_cast<unsigned long long>(kEmpty),
@@ -272,7 +280,7 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
         atomicMin(&tm[h], r);
         break;
       }
-      h = (h + 1) & mask;
+      h = next_slot(h, tsize);
     }
   }
   __syncthreads();
@@ -284,13 +292,13 @@ __global__ __launch_bounds__(kGroupThreads) void k_bucket_group(
     if (k == kEmpty) {
       f = special_min;
     } else {
-      uint32_t h = slot_hash(k) & mask;
+      uint32_t h = slot_of(k, tsize);
       for (;;) {
         const uint64_t kk = in_lds ? tk[h]
                                    : __hip_atomic_load(&tk[h], __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT);
         if (kk == k) break;
-        h = (h + 1) & mask;
+        h = next_slot(h, tsize);
       }
       f = in_lds ? tm[h] : __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
