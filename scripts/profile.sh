@@ -13,6 +13,7 @@ mkdir -p "$OUT"
 ARGS="--steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
   -- python3 bench.py $ARGS > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err" || exit $?
+python3 scripts/trace_summary.py "$OUT/trace/run_kernel_trace.csv" "$OUT/trace_summary.txt" > /dev/null || exit 1
 if [ -n "$PMC" ]; then
   rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
   PARGS="--steps 1 --warmup 0 --no-cpu ${PMC_ARGS:---components cas}"

@@ -164,3 +164,20 @@ def test_exchange_partition_matches_count_and_partition(ctx, world):
         seg = slice(bounds[d], bounds[d + 1])
         np.testing.assert_array_equal(np.sort(op[seg]), np.sort(ref_pos[seg]))
         assert np.all(owner[(k[op[seg]] >> np.uint64(64 - bits)).astype(np.int64)] == d)
+
+
+@pytest.mark.parametrize("n", [4607, 4608, 4609, 6144, 6145, 9000])
+def test_single_bucket_at_lds_capacity(ctx, n):
+    """Every key in one bucket (top bit clear): rows just under, at and over the
+    LDS table's capacity (4608 rows of 6144 slots) take the LDS path or the
+    global-table path, with a sentinel-valued key and ~30% duplicates."""
+    from spacedrive_amd import dedup
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, 2**63 - 1, n, dtype=np.uint64)
+    key = keys[rng.integers(0, int(n * 0.7), n)]
+    key[rng.integers(0, n, 5)] = np.uint64(2**63 - 1)
+    key[rng.integers(0, n, 3)] = np.uint64(2**64 - 1)  # the empty-slot sentinel
+    has = (rng.random(n) > 0.01).astype(np.uint8)
+    for chunk in (100, 1):
+        rep = dedup.group_reps(key, has, chunk, ctx)
+        np.testing.assert_array_equal(rep, O.group_reps(key, has, chunk))
