@@ -518,7 +518,7 @@ def main():
         dir_comp = R.run_dir(max(1, min(args.steps, 3)))
         log("dir:", json.dumps(dir_comp))
     cpu = None
-    if R.rank == 0 and not args.no_cpu:
+    if R.rank == 0 and R.world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N = 1 only
         cpu = R.cpu_baseline()
         log("cpu:", json.dumps(cpu))
     R._cpu_sample = None
