@@ -181,3 +181,52 @@ def test_single_bucket_at_lds_capacity(ctx, n):
     for chunk in (100, 1):
         rep = dedup.group_reps(key, has, chunk, ctx)
         np.testing.assert_array_equal(rep, O.group_reps(key, has, chunk))
+
+
+@pytest.mark.timeout(400)
+def test_config4_full_100m_rows_eight_ranks(ctx):
+    """BASELINE config 4 at its full size: 100 M rows (80 M distinct keys, 20 M
+    duplicates, 0.1 % keyless) as 8 ranks of 12.5 M rows, the whole N = 8
+    sharded path (partition -> exchange -> group -> return -> scatter) on the
+    HIP kernels, against the oracle's grouping of the whole table."""
+    import threading
+    import torch
+    from spacedrive_amd import corpus, dedup
+    world, total = 8, 100_000_000
+    per = total // world
+    shared = {"slots": [None] * world, "barrier": threading.Barrier(world)}
+    inputs, results, errors = {}, {}, []
+    for r in range(world):
+        inputs[r] = corpus.synth_dedup_rows_device(4, total, int(total * 0.8), r * per, per,
+                                                   ctx=ctx)
+    torch.cuda.synchronize()
+
+    def run(r):
+        try:
+            k, h, rk = inputs[r]
+            rep = dedup.sharded_group_reps(k, h, rk, 100, ops=dedup.HipOps(ctx),
+                                           exchange=ThreadExchange(r, world, shared))
+            torch.cuda.synchronize()
+            results[r] = rep.cpu().numpy().view(np.uint32)
+        except Exception as e:  # surface thread failures
+            errors.append(e)
+            shared["barrier"].abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors
+    rep = np.concatenate([results[r] for r in range(world)])
+    key = np.concatenate([inputs[r][0].cpu().numpy().view(np.uint64) for r in range(world)])
+    has = np.concatenate([inputs[r][1].cpu().numpy() for r in range(world)])
+    rank = np.concatenate([inputs[r][2].cpu().numpy().view(np.uint32) for r in range(world)])
+    del inputs
+    np.testing.assert_array_equal(rank, np.arange(total, dtype=np.uint32))
+    assert abs(int(total - has.sum()) - total // 1000) < total // 5000  # ~0.1 % keyless
+    ref = O.group_reps(key, has, 100)
+    np.testing.assert_array_equal(rep, ref)
+    # the config's shape: 20 % of the keyed rows link to an earlier row's Object
+    linked = np.count_nonzero(rep != rank)
+    assert 0.15 * total < linked < 0.21 * total
