@@ -34,6 +34,7 @@
 #include "scan_device.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace sdgpu {
 
@@ -41,6 +42,7 @@ namespace {
 
 constexpr int kPartThreads = 1024;
 constexpr uint32_t kPartBlocks = 256;  // one per CU
+constexpr uint32_t kMaxPartBlocks = 1024;  // bucket partition: sizes the workspace
 constexpr int kGroupThreads = 1024;
 // 6144 slots x 12 B = 72 KiB of LDS, so two buckets share a CU (8 waves/SIMD)
 // and one bucket's loads overlap the other's LDS atomics.  The slot count is
@@ -54,9 +56,19 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t key, uint32_t skip, uint32
   return bits == 0 ? 0u : static_cast<uint32_t>((key << skip) >> (64u - bits));
 }
 
-__device__ __forceinline__ void tile_of(uint64_t n, uint64_t& t0, uint64_t& t1) {
-  const uint64_t per = (n + kPartBlocks - 1) / kPartBlocks;
-  t0 = min<uint64_t>(n, per * blockIdx.x);
+// XCD-aware block numbering: workgroups are dispatched round-robin over the 8
+// XCDs, so physical block i runs on XCD i % 8.  Logical block (i % 8) * P/8 +
+// i / 8 gives each XCD a contiguous run of logical blocks; the 16 per-block
+// counters of one digit that share a 64-B line of the digit-major histogram
+// (and the offsets the scatter reads back) then come from one XCD's L2.
+__device__ __forceinline__ uint32_t part_block() {
+  const uint32_t P = gridDim.x;
+  return (P & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (P >> 3) + (blockIdx.x >> 3);
+}
+
+__device__ __forceinline__ void tile_of(uint64_t n, uint32_t P, uint64_t& t0, uint64_t& t1) {
+  const uint64_t per = (n + P - 1) / P;
+  t0 = min<uint64_t>(n, per * part_block());
   t1 = min<uint64_t>(n, t0 + per);
 }
 
@@ -74,7 +86,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(const uint64_t* __re
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) cnt[b] = 0;
   __syncthreads();
   uint64_t t0, t1;
-  tile_of(n, t0, t1);
+  tile_of(n, gridDim.x, t0, t1);
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += kUnroll * kPartThreads) {
     uint64_t k[kUnroll];
     bool v[kUnroll];
@@ -91,7 +103,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(const uint64_t* __re
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
-    hist[static_cast<uint64_t>(b) * kPartBlocks + blockIdx.x] = cnt[b];
+    hist[static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
 }
 
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
@@ -102,10 +114,10 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
   extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
   const uint32_t nbins = 1u << bits;
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
-    cur[b] = offs[static_cast<uint64_t>(b) * kPartBlocks + blockIdx.x];
+    cur[b] = offs[static_cast<uint64_t>(b) * gridDim.x + part_block()];
   __syncthreads();
   uint64_t t0, t1;
-  tile_of(n, t0, t1);
+  tile_of(n, gridDim.x, t0, t1);
   constexpr int U = kUnroll / 2;
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += U * kPartThreads) {
     uint64_t k[U];
@@ -142,10 +154,10 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
   extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
   const uint32_t nbins = 1u << bits;
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
-    cur[b] = offs[static_cast<uint64_t>(b) * kPartBlocks + blockIdx.x];
+    cur[b] = offs[static_cast<uint64_t>(b) * gridDim.x + part_block()];
   __syncthreads();
   uint64_t t0, t1;
-  tile_of(n, t0, t1);
+  tile_of(n, gridDim.x, t0, t1);
   constexpr int U = kUnroll;
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += U * kPartThreads) {
     uint64_t k[U];
@@ -185,15 +197,15 @@ __device__ __forceinline__ uint32_t next_slot(uint32_t h, uint32_t tsize) {
 
 // One workgroup per bucket.  Rows of bucket b: [offs[b*P], offs[(b+1)*P]).
 __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
-    const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t nbuckets,
+    const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P,
     uint32_t chunk_rows, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
     uint32_t* __restrict__ rep) {
   __shared__ uint64_t lkey[kLdsSlots];
   __shared__ uint32_t lmin[kLdsSlots];
   __shared__ uint32_t special_min;  // min rank of key == kEmpty (sentinel clash)
   const uint32_t b = blockIdx.x;
-  const uint32_t start = offs[static_cast<uint64_t>(b) * kPartBlocks];
-  const uint32_t end = offs[static_cast<uint64_t>(b + 1) * kPartBlocks];  // offs[nb*P] = total
+  const uint32_t start = offs[static_cast<uint64_t>(b) * P];
+  const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];  // offs[nb*P] = total
   const uint32_t m = end - start;
   if (m == 0) return;
   const bool in_lds = m <= kLdsCap;
@@ -345,6 +357,19 @@ __global__ void k_dest_counts(const uint32_t* __restrict__ offs, uint32_t bits, 
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Blocks of the bucket partition (<= kMaxPartBlocks, which sizes the workspace).
+// Each block keeps one open output line per bucket, so the blocks resident on
+// one XCD hold blocks/8 x buckets x 128 B of partially written lines in its
+// 4 MB L2; fewer blocks trade parallelism for fewer evicted partial lines.
+uint32_t bucket_part_blocks() {
+  static const uint32_t P = [] {
+    const char* e = getenv("SDGPU_BUCKET_PART_BLOCKS");
+    const long v = e ? strtol(e, nullptr, 10) : 0;
+    return (v >= 8 && v <= static_cast<long>(kMaxPartBlocks)) ? static_cast<uint32_t>(v) : kPartBlocks;
+  }();
+  return P;
+}
+
 uint32_t bucket_bits_for(uint64_t n) {
   uint32_t bits = 1;
   while (bits < 13 && (n >> bits) > kBucketRows) ++bits;
@@ -359,7 +384,7 @@ struct GroupLayout {
 GroupLayout group_layout(uint64_t n) {
   GroupLayout L;
   L.bits = bucket_bits_for(n);
-  const uint64_t nh = (static_cast<uint64_t>(1) << L.bits) * kPartBlocks;
+  const uint64_t nh = (static_cast<uint64_t>(1) << L.bits) * kMaxPartBlocks;
   size_t o = 0;
   L.hist = o; o = align_up(o + 4 * (nh + 1), 256);
   L.tiles = o; o = align_up(o + 4 * (scan::tiles_for(nh) + 1), 256);
@@ -405,21 +430,21 @@ hipError_t dedup_local_launch(const uint64_t* key, const uint8_t* has_key, const
   uint64_t* gkey = reinterpret_cast<uint64_t*>(w + L.gkey);
   uint32_t* gmin = reinterpret_cast<uint32_t*>(w + L.gmin);
   const uint32_t bits = std::min<uint32_t>(L.bits, 64u - shard_bits);
-  const uint64_t nh = (static_cast<uint64_t>(1) << bits) * kPartBlocks;
+  const uint32_t P = bucket_part_blocks();
+  const uint64_t nh = (static_cast<uint64_t>(1) << bits) * P;
   const size_t lds = sizeof(uint32_t) << bits;
   {
     KScope k(timer, "bucket_hist", s);
-    k_part_hist<<<kPartBlocks, kPartThreads, lds, s>>>(key, has_key, n, shard_bits, bits, hist);
+    k_part_hist<<<P, kPartThreads, lds, s>>>(key, has_key, n, shard_bits, bits, hist);
   }
   scan::exclusive(hist, nh, hist, tiles, nullptr, s);
   {
     KScope k(timer, "bucket_scatter", s);
-    k_part_scatter_rec<<<kPartBlocks, kPartThreads, lds, s>>>(key, rank, has_key, n, shard_bits,
-                                                              bits, hist, rec, rep);
+    k_part_scatter_rec<<<P, kPartThreads, lds, s>>>(key, rank, has_key, n, shard_bits, bits, hist,
+                                                    rec, rep);
   }
   KScope k(timer, "bucket_group", s);
-  k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, 1u << bits, chunk_rows, gkey,
-                                                      gmin, rep);
+  k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, chunk_rows, gkey, gmin, rep);
   return hipGetLastError();
 }
 
