@@ -6,7 +6,7 @@ T=${TAG:-pab}
 for P in 256 100; do
   SDGPU_BUCKET_PART_BLOCKS=$P timeout -k 10 300 python -u -m pytest tests/test_gpu_dedup.py -x -q --timeout 200 --timeout-method thread > gpurun_out/${T}_pytest_P$P.log 2>&1 || { echo "pytest P=$P failed"; exit 1; }
 done
-for P in 256 512 128; do
+for P in ${PLIST:-256 128 512}; do
   SDGPU_BUCKET_PART_BLOCKS=$P timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --components dedup --no-cpu --files 100000 > gpurun_out/${T}_bench_P$P.json 2> gpurun_out/${T}_bench_P$P.err || { echo "bench P=$P failed"; exit 1; }
 done
 echo "exit 0"

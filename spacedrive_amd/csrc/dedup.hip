@@ -195,17 +195,28 @@ __device__ __forceinline__ uint32_t next_slot(uint32_t h, uint32_t tsize) {
   return h + 1 == tsize ? 0u : h + 1;
 }
 
-// One workgroup per bucket.  Rows of bucket b: [offs[b*P], offs[(b+1)*P]).
-__global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
-    const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P,
-    uint32_t chunk_rows, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
-    uint32_t* __restrict__ rep) {
-  __shared__ uint64_t lkey[kLdsSlots];
-  __shared__ uint32_t lmin[kLdsSlots];
-  __shared__ uint32_t special_min;  // min rank of key == kEmpty (sentinel clash)
-  const uint32_t b = blockIdx.x;
-  const uint32_t start = offs[static_cast<uint64_t>(b) * P];
-  const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];  // offs[nb*P] = total
+constexpr int kPer = (kLdsCap + kGroupThreads - 1) / kGroupThreads;
+
+// LDS-sized bucket: every thread loads its (at most kPer) records at once and
+// keeps them in registers for both phases.
+__device__ __forceinline__ void load_bucket(const uint4* __restrict__ rec, uint32_t start,
+                                            uint32_t end, uint4 (&q_reg)[kPer]) {
+  if (end - start > kLdsCap) return;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint32_t i = start + threadIdx.x + j * kGroupThreads;
+    q_reg[j] = i < end ? rec[i] : make_uint4(0, 0, 0, 0);
+  }
+}
+
+// Group-by of one bucket, rows [start, end) of rec (q_reg preloaded by
+// load_bucket when the bucket fits the LDS table).
+__device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint32_t start,
+                                             uint32_t end, const uint4 (&q_reg)[kPer],
+                                             uint32_t chunk_rows, uint64_t* __restrict__ gkey,
+                                             uint32_t* __restrict__ gmin,
+                                             uint32_t* __restrict__ rep, uint64_t* lkey,
+                                             uint32_t* lmin, uint32_t& special_min) {
   const uint32_t m = end - start;
   if (m == 0) return;
   const bool in_lds = m <= kLdsCap;
@@ -218,17 +229,6 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
     tk = gkey + 4ull * start;
     tm = gmin + 4ull * start;
   }
-  // LDS-sized bucket: every thread loads its (at most kPer) records at once
-  // and keeps them in registers for both phases.
-  constexpr int kPer = (kLdsCap + kGroupThreads - 1) / kGroupThreads;
-  uint4 q_reg[kPer];
-  if (in_lds) {
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const uint32_t i = start + threadIdx.x + j * kGroupThreads;
-      q_reg[j] = i < end ? rec[i] : make_uint4(0, 0, 0, 0);
-    }
-  }
   for (uint32_t s = threadIdx.x; s < tsize; s += kGroupThreads) {
     tk[s] = kEmpty;
     tm[s] = 0xFFFFFFFFu;
@@ -236,41 +236,56 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
   if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
   __syncthreads();
   if (in_lds) {
+    // A thread's records probe in lock step: every pass issues the LDS
+    // round trips of all its pending records back to back and only then
+    // inspects the results, so their latencies overlap (the probe loops are
+    // latency-bound, not LDS-bandwidth-bound).
+    uint32_t h[kPer];
+    uint32_t live = 0, pend = 0;  // bit j: record j exists / is still probing
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      if (start + threadIdx.x + j * kGroupThreads >= end) break;
       const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
-      const uint32_t r = q_reg[j].z;
-      if (k == kEmpty) {
-        atomicMin(&special_min, r);
-        continue;
+      h[j] = slot_of(k, tsize);
+      if (start + threadIdx.x + j * kGroupThreads < end) {
+        live |= 1u << j;
+        if (k == kEmpty)
+          atomicMin(&special_min, q_reg[j].z);
+        else
+          pend |= 1u << j;
       }
-      uint32_t h = slot_of(k, tsize);
-      for (;;) {
-        const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tk[h]),
-                                        static_cast<unsigned long long>(kEmpty),
-                                        static_cast<unsigned long long>(k));
-        if (prev == kEmpty || prev == k) {
-          atomicMin(&tm[h], r);
-          break;
+    }
+    const uint32_t keyed = pend;
+    while (pend) {
+      uint64_t prev[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
+        prev[j] = (pend >> j & 1u)
+                      ? atomicCAS(reinterpret_cast<unsigned long long*>(&tk[h[j]]),
+                                  static_cast<unsigned long long>(kEmpty),
+                                  static_cast<unsigned long long>(k))
+                      : 0ull;
+      }
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        if (!(pend >> j & 1u)) continue;
+        const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
+        if (prev[j] == kEmpty || prev[j] == k) {
+          atomicMin(&tm[h[j]], q_reg[j].z);
+          pend &= ~(1u << j);
+        } else {
+          h[j] = next_slot(h[j], tsize);
         }
-        h = next_slot(h, tsize);
       }
     }
     __syncthreads();
+    // every keyed record's final probe slot h[j] holds its key: read the
+    // group minimum there (no second probe sequence needed)
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      if (start + threadIdx.x + j * kGroupThreads >= end) break;
-      const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
+      if (!(live >> j & 1u)) continue;
       const uint32_t r = q_reg[j].z;
-      uint32_t f;
-      if (k == kEmpty) {
-        f = special_min;
-      } else {
-        uint32_t h = slot_of(k, tsize);
-        while (tk[h] != k) h = next_slot(h, tsize);
-        f = tm[h];
-      }
+      const uint32_t f = (keyed >> j & 1u) ? tm[h[j]] : special_min;
       if (r / chunk_rows != f / chunk_rows) rep[q_reg[j].w] = f;  // others keep rank
     }
     return;
@@ -316,6 +331,23 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
     }
     if (r / chunk_rows != f / chunk_rows) rep[q.w] = f;
   }
+}
+
+
+// One workgroup per bucket.  Rows of bucket b: [offs[b*P], offs[(b+1)*P]).
+__global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
+    const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P,
+    uint32_t chunk_rows, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
+    uint32_t* __restrict__ rep) {
+  __shared__ uint64_t lkey[kLdsSlots];
+  __shared__ uint32_t lmin[kLdsSlots];
+  __shared__ uint32_t special_min;  // min rank of key == kEmpty (sentinel clash)
+  const uint32_t b = blockIdx.x;
+  const uint32_t start = offs[static_cast<uint64_t>(b) * P];
+  const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];  // offs[nb*P] = total
+  uint4 q_reg[kPer];
+  load_bucket(rec, start, end, q_reg);
+  group_bucket(rec, start, end, q_reg, chunk_rows, gkey, gmin, rep, lkey, lmin, special_min);
 }
 
 __global__ __launch_bounds__(256) void k_fill_init(uint32_t* __restrict__ dst, uint64_t n,
