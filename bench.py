@@ -348,12 +348,32 @@ class Runner:
                     "remote_GBps_per_gpu_over_step": (fwd + back) * remote / (t / steps) / 1e9,
                     "note": "bytes sent + received per GPU per step over xGMI (RCCL all-to-all); "
                             "rate is over the whole step, a lower bound on the link rate"}
+        kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in kt.items()}
+        roof = None
+        if self.world == 1:
+            # algorithmic HBM bytes per launch of the one-GPU grouping:
+            # hist reads key + has_key; the scatter reads key, rank, has_key and writes one
+            # 16-B record per keyed row plus every row's initial rep; the group-by reads
+            # the records and writes rep for the rows that link to an earlier chunk
+            rep = dedup.sharded_group_reps(key, has, rank, 100, ops=ops)
+            nk = int(has.sum())
+            linked = int((rep != rank).sum())
+            alg = {"bucket_hist": 9 * per, "bucket_scatter": 17 * per + 16 * nk,
+                   "bucket_group": 16 * nk + 4 * linked}
+            roof = {"bound": "hbm", "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                    "linked_rows": linked,
+                    "kernels": {k: {"algorithmic_bytes": b,
+                                    "achieved": b / (kernels[k]["avg_ms"] * 1e-3) / 1e9,
+                                    "frac": b / (kernels[k]["avg_ms"] * 1e-3) / HBM_PEAK}
+                                for k, b in alg.items() if kernels.get(k, {}).get("avg_ms")},
+                    "note": "algorithmic bytes of this partition + group-by design; the "
+                            "scatter's PMC traffic is ~3x its algorithmic write (16-B records "
+                            "scattered into 4096 buckets, DESIGN.md section 4)"}
         return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
-                "exchange": xchg,
+                "exchange": xchg, "roofline": roof,
                 "config": {"workload": "config4: 80% distinct u64 keys + 20% dups, 0.1% keyless",
                            "rows_per_gpu": per, "rows_total": total},
-                "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
-                            for k, v in kt.items()}}
+                "kernels": kernels}
 
     def verify_sharded(self, key, has, rank, ops):
         """--verify: the sharded grouping over all ranks (the exchange path the
