@@ -185,6 +185,63 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
   }
 }
 
+// Bucket partition with LDS pair staging (12-bit digits only): a keyed row is
+// parked in its bucket's 2-record LDS slot and leaves as a 32-B pair, so the
+// scattered writes are half as many and twice as wide.  Rows arriving at a full
+// slot are written directly.  Rows are taken 2 per thread per round; each
+// round ends with a flush of the full pairs; the odd rows go out at the end.
+constexpr uint32_t kStageBits = 12;
+__global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
+    const uint64_t* __restrict__ key, const uint32_t* __restrict__ rank,
+    const uint8_t* __restrict__ valid, uint64_t n, uint32_t skip,
+    const uint32_t* __restrict__ offs, uint4* __restrict__ rec, uint32_t* __restrict__ rep) {
+  constexpr uint32_t nbins = 1u << kStageBits;
+  __shared__ uint4 stage[nbins][2];
+  __shared__ uint32_t fill[nbins];
+  __shared__ uint32_t cur[nbins];
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) {
+    cur[b] = offs[static_cast<uint64_t>(b) * gridDim.x + part_block()];
+    fill[b] = 0;
+  }
+  __syncthreads();
+  uint64_t t0, t1;
+  tile_of(n, gridDim.x, t0, t1);
+  constexpr int U = 2;
+  for (uint64_t i0 = t0; i0 < t1; i0 += U * kPartThreads) {  // uniform trip count
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads;
+      if (i >= t1) continue;
+      const uint64_t k = key[i];
+      const uint32_t r = rank ? rank[i] : static_cast<uint32_t>(i);
+      rep[i] = r;
+      if (valid && valid[i] == 0) continue;
+      const uint32_t b = digit_of(k, skip, kStageBits);
+      const uint4 q = make_uint4(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32), r,
+                                 static_cast<uint32_t>(i));
+      const uint32_t sl = atomicAdd(&fill[b], 1u);
+      if (sl < 2) {
+        stage[b][sl] = q;
+      } else {
+        rec[atomicAdd(&cur[b], 1u)] = q;
+      }
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) {
+      if (fill[b] >= 2) {
+        const uint32_t p = cur[b];
+        cur[b] = p + 2;
+        rec[p] = stage[b][0];
+        rec[p + 1] = stage[b][1];
+        fill[b] = 0;
+      }
+    }
+    __syncthreads();
+  }
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
+    if (fill[b] == 1) rec[cur[b]] = stage[b][0];
+}
+
 // First probe slot of key k in a table of tsize slots (any tsize).
 __device__ __forceinline__ uint32_t slot_of(uint64_t k, uint32_t tsize) {
   const uint32_t h = static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> 32);
@@ -472,8 +529,12 @@ hipError_t dedup_local_launch(const uint64_t* key, const uint8_t* has_key, const
   scan::exclusive(hist, nh, hist, tiles, nullptr, s);
   {
     KScope k(timer, "bucket_scatter", s);
-    k_part_scatter_rec<<<P, kPartThreads, lds, s>>>(key, rank, has_key, n, shard_bits, bits, hist,
-                                                    rec, rep);
+    if (bits == kStageBits && !getenv("SDGPU_SCATTER_UNSTAGED"))
+      k_part_scatter_rec_staged<<<P, kPartThreads, 0, s>>>(key, rank, has_key, n, shard_bits, hist,
+                                                           rec, rep);
+    else
+      k_part_scatter_rec<<<P, kPartThreads, lds, s>>>(key, rank, has_key, n, shard_bits, bits,
+                                                      hist, rec, rep);
   }
   KScope k(timer, "bucket_group", s);
   k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, chunk_rows, gkey, gmin, rep);
