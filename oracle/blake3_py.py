@@ -184,6 +184,38 @@ def keyed_hash(key32: bytes, data: bytes) -> bytes:
     return Hasher.new_keyed(key32).update(data).finalize(32)
 
 
+# --- Balloon over BLAKE3 hash mode (the reference's hash-mode KATs) ---
+
+def balloon(pwd: bytes, salt: bytes, secret: bytes, s_cost: int, t_cost: int,
+            h=blake3) -> bytes:
+    """balloon-hash 0.4.0 Algorithm::Balloon with digest `h` (default: this
+    module's BLAKE3), as /root/reference/crates/crypto/src/keys/hashing.rs:95-114
+    calls it (p_cost 1; `secret` b"" when the caller passes None, :101).
+    Independent of orc_balloon_blake3 in oracle/sd_oracle.c; same algorithm
+    (eprint 2016/027 §3.1, delta 3).  Pure Python: small s_cost only unless `h`
+    is a fast hash."""
+    def u64(x):
+        return x.to_bytes(8, "little")
+    cnt = 0
+    buf = [b""] * s_cost
+    buf[0] = h(u64(cnt) + pwd + salt + secret)
+    cnt += 1
+    for m in range(1, s_cost):
+        buf[m] = h(u64(cnt) + buf[m - 1])
+        cnt += 1
+    for t in range(t_cost):
+        for m in range(s_cost):
+            buf[m] = h(u64(cnt) + buf[m - 1] + buf[m])  # buf[-1] = buf[s_cost - 1]
+            cnt += 1
+            for i in range(3):
+                idx = h(u64(t) + u64(m) + u64(i))
+                other = int.from_bytes(h(u64(cnt) + salt + secret + idx), "little") % s_cost
+                cnt += 1
+                buf[m] = h(u64(cnt) + buf[m] + buf[other])
+                cnt += 1
+    return buf[s_cost - 1]
+
+
 # --- cas.rs restated over in-memory file bytes (independent of the C oracle) ---
 
 SAMPLE_COUNT = 4            # cas.rs:10

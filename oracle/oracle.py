@@ -64,6 +64,13 @@ def lib():
                                      ctypes.c_uint32, ctypes.c_void_p]
         L.orc_group_reps.restype = ctypes.c_int
         L.orc_synth_dedup_rows.argtypes = [ctypes.c_uint64] * 5 + [ctypes.c_void_p] * 3
+        L.orc_balloon_blake3.argtypes = [ctypes.c_void_p, ctypes.c_size_t] * 3 + [
+            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+        L.orc_balloon_blake3.restype = ctypes.c_int
+        L.orc_balloon_blake3_trace.argtypes = [ctypes.c_void_p, ctypes.c_size_t] * 3 + [
+            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_balloon_blake3_trace.restype = ctypes.c_int64
         del u8p
         _lib = L
     return _lib
@@ -103,6 +110,34 @@ def derive_key(context: str, material: bytes) -> bytes:
     c = context.encode()
     lib().orc_blake3_derive_key(c, len(c), _ptr(a), a.size, _ptr(out))
     return out.tobytes()
+
+
+def balloon_blake3(pwd: bytes, salt: bytes, secret: bytes, s_cost: int, t_cost: int) -> bytes:
+    """Balloon (balloon-hash 0.4.0) over BLAKE3 hash mode, orc_balloon_blake3."""
+    bufs = [_buf(x if x else b"\0") for x in (pwd, salt, secret)]
+    out = np.zeros(32, np.uint8)
+    rc = lib().orc_balloon_blake3(_ptr(bufs[0]), len(pwd), _ptr(bufs[1]), len(salt),
+                                  _ptr(bufs[2]), len(secret), s_cost, t_cost, _ptr(out))
+    if rc:
+        raise OSError(-rc, os.strerror(-rc))
+    return out.tobytes()
+
+
+def balloon_blake3_trace(pwd: bytes, salt: bytes, secret: bytes, s_cost: int, t_cost: int,
+                         stride: int, cap: int):
+    """(digest, [(message, blake3 digest)...]) recording every stride-th BLAKE3
+    message the Balloon run hashes (replayable through another hasher)."""
+    bufs = [_buf(x if x else b"\0") for x in (pwd, salt, secret)]
+    out = np.zeros(32, np.uint8)
+    msg = np.zeros((cap, 128), np.uint8)
+    ln = np.zeros(cap, np.uint32)
+    dig = np.zeros((cap, 32), np.uint8)
+    k = lib().orc_balloon_blake3_trace(_ptr(bufs[0]), len(pwd), _ptr(bufs[1]), len(salt),
+                                       _ptr(bufs[2]), len(secret), s_cost, t_cost, _ptr(out),
+                                       stride, cap, _ptr(msg), _ptr(ln), _ptr(dig))
+    if k < 0:
+        raise OSError(-k, os.strerror(-k))
+    return out.tobytes(), [(msg[i, :ln[i]].tobytes(), dig[i].tobytes()) for i in range(k)]
 
 
 def keyed_hash(key32: bytes, data) -> bytes:

@@ -19,11 +19,14 @@
  *    strictly below the chunk count), deliberately unlike the incremental
  *    CV-stack formulation of oracle/blake3_py.py, so the two restatements
  *    cross-check each other's tree shape.
- *    Pinned by the reference's only BLAKE3 known-answer test,
- *    /root/reference/crates/crypto/src/keys/hashing.rs:324-327 (derive_b3,
+ *    Pinned by the reference's BLAKE3 known-answer tests in
+ *    /root/reference/crates/crypto/src/keys/hashing.rs: derive_b3 (:324-327,
  *    expected bytes :210-213, inputs :121,132-141, concatenation order
- *    /root/reference/crates/crypto/src/types.rs:163-170), and by the spec's
- *    hash of the empty input.
+ *    /root/reference/crates/crypto/src/types.rs:163-170; derive-key mode) and
+ *    the six Balloon-BLAKE3 vectors (:180-208, tests :269-321), which run
+ *    BLAKE3 in HASH mode -- the mode of cas.rs / hash.rs -- over ~2.7-11 M
+ *    messages of 24-74 bytes each (orc_balloon_blake3 below); and by the
+ *    spec's hash of the empty input.
  *
  *  - generate_cas_id  (/root/reference/core/src/object/cas.rs:23-62), incl. the
  *    exact file-I/O pattern (open, read_exact header, 4 x {read_exact 10 KiB,
@@ -267,6 +270,144 @@ void orc_blake3_keyed(const uint8_t key32[32], const uint8_t *in, size_t len,
   uint32_t kw[8];
   for (int i = 0; i < 8; i++) kw[i] = load32le(key32 + 4 * i);
   b3_hash_keyed_flags(kw, B3_KEYED_HASH, in, len, out32);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Balloon hashing over BLAKE3 hash mode: the reference's only known-answer  */
+/* tests that run BLAKE3 in hash mode (the mode cas.rs and hash.rs use).     */
+/* ------------------------------------------------------------------------- */
+/*
+ * Restates `Algorithm::Balloon` of the third-party crate balloon-hash 0.4.0
+ * (/root/reference/Cargo.lock:492-500; not vendored) as the reference calls
+ * it: Balloon::<blake3::Hasher>::new(Algorithm::Balloon, params, Some(secret))
+ * .hash_into(password, salt, key) (crates/crypto/src/keys/hashing.rs:95-114;
+ * params (s_cost, t_cost, p_cost) = (131072|262144|524288, 2, 1), :58-63;
+ * with no secret the crate still receives Some(&[]), :101).  The algorithm is
+ * Boneh, Corrigan-Gibbs and Schechter's Balloon (eprint 2016/027 §3.1) with
+ * delta = 3, every hash H = BLAKE3 of the concatenation of its arguments:
+ *   cnt = 0
+ *   buf[0] = H(cnt++ u64le, pwd, salt, secret)
+ *   buf[m] = H(cnt++, buf[m-1])                          m = 1 .. s-1
+ *   for t < t_cost, m < s:
+ *     buf[m] = H(cnt++, buf[(m-1) mod s], buf[m])
+ *     for i < 3:
+ *       idx   = H(t u64le, m u64le, i u64le)
+ *       other = H(cnt++, salt, secret, idx) as a 256-bit LE integer mod s
+ *       buf[m] = H(cnt++, buf[m], buf[other])
+ *   key = buf[s-1]
+ * Pinned by the six HASH_B3BALLOON_* vectors (hashing.rs:180-208, tests
+ * :269-321; password :130, salt :138-141, secret :143-146). */
+/* Optional transcript: every stride-th hashed message (<= 128 B kept) and its
+ * digest, so a test can replay the KAT's own messages through another hasher. */
+typedef struct {
+  uint64_t stride, seen, kept, cap;
+  uint8_t *msg;  /* [cap][128] */
+  uint32_t *len; /* [cap] */
+  uint8_t *dig;  /* [cap][32] */
+} bal_trace;
+
+static void b3_cat(bal_trace *tr, uint8_t out32[32], int nparts,
+                   const uint8_t *const *p, const size_t *l) {
+  uint8_t msg[1024];
+  size_t n = 0;
+  for (int i = 0; i < nparts; i++) {
+    memcpy(msg + n, p[i], l[i]);
+    n += l[i];
+  }
+  orc_blake3(msg, n, out32);
+  if (tr && tr->seen++ % tr->stride == 0 && tr->kept < tr->cap && n <= 128) {
+    memcpy(tr->msg + 128 * tr->kept, msg, n);
+    tr->len[tr->kept] = (uint32_t)n;
+    memcpy(tr->dig + 32 * tr->kept, out32, 32);
+    tr->kept++;
+  }
+}
+
+static void le64(uint8_t b[8], uint64_t x) {
+  for (int i = 0; i < 8; i++) b[i] = (uint8_t)(x >> (8 * i));
+}
+
+static int balloon_run(bal_trace *tr, const uint8_t *pwd, size_t pwd_len,
+                       const uint8_t *salt, size_t salt_len, const uint8_t *secret,
+                       size_t secret_len, uint32_t s_cost, uint32_t t_cost,
+                       uint8_t out32[32]) {
+  if (s_cost == 0 || t_cost == 0 || pwd_len + salt_len + secret_len > 900 ||
+      salt_len + secret_len > 900)
+    return -EINVAL;
+  uint8_t (*buf)[32] = malloc((size_t)32 * s_cost);
+  if (!buf) return -ENOMEM;
+  uint64_t cnt = 0;
+  uint8_t c8[8], t8[8], m8[8], i8[8], idx[32], oth[32];
+  le64(c8, cnt++);
+  {
+    const uint8_t *p[4] = {c8, pwd, salt, secret};
+    const size_t l[4] = {8, pwd_len, salt_len, secret_len};
+    b3_cat(tr, buf[0], 4, p, l);
+  }
+  for (uint32_t m = 1; m < s_cost; m++) {
+    le64(c8, cnt++);
+    const uint8_t *p[2] = {c8, buf[m - 1]};
+    const size_t l[2] = {8, 32};
+    b3_cat(tr, buf[m], 2, p, l);
+  }
+  for (uint64_t t = 0; t < t_cost; t++) {
+    for (uint32_t m = 0; m < s_cost; m++) {
+      const uint8_t *prev = buf[m == 0 ? s_cost - 1 : m - 1];
+      le64(c8, cnt++);
+      {
+        const uint8_t *p[3] = {c8, prev, buf[m]};
+        const size_t l[3] = {8, 32, 32};
+        b3_cat(tr, buf[m], 3, p, l);
+      }
+      for (uint64_t i = 0; i < 3; i++) {
+        le64(t8, t);
+        le64(m8, m);
+        le64(i8, i);
+        {
+          const uint8_t *p[3] = {t8, m8, i8};
+          const size_t l[3] = {8, 8, 8};
+          b3_cat(tr, idx, 3, p, l);
+        }
+        le64(c8, cnt++);
+        {
+          const uint8_t *p[4] = {c8, salt, secret, idx};
+          const size_t l[4] = {8, salt_len, secret_len, 32};
+          b3_cat(tr, oth, 4, p, l);
+        }
+        uint64_t r = 0; /* (digest as little-endian 256-bit integer) mod s_cost */
+        for (int k = 31; k >= 0; k--) r = ((r << 8) | oth[k]) % s_cost;
+        le64(c8, cnt++);
+        {
+          const uint8_t *p[3] = {c8, buf[m], buf[r]};
+          const size_t l[3] = {8, 32, 32};
+          b3_cat(tr, buf[m], 3, p, l);
+        }
+      }
+    }
+  }
+  memcpy(out32, buf[s_cost - 1], 32);
+  free(buf);
+  return 0;
+}
+
+int orc_balloon_blake3(const uint8_t *pwd, size_t pwd_len, const uint8_t *salt,
+                       size_t salt_len, const uint8_t *secret, size_t secret_len,
+                       uint32_t s_cost, uint32_t t_cost, uint8_t out32[32]) {
+  return balloon_run(NULL, pwd, pwd_len, salt, salt_len, secret, secret_len, s_cost,
+                     t_cost, out32);
+}
+
+/* Same, recording every `stride`-th hashed message: msg [cap][128], len [cap],
+ * dig [cap][32]; returns the number kept (or -errno). */
+int64_t orc_balloon_blake3_trace(const uint8_t *pwd, size_t pwd_len, const uint8_t *salt,
+                                 size_t salt_len, const uint8_t *secret,
+                                 size_t secret_len, uint32_t s_cost, uint32_t t_cost,
+                                 uint8_t out32[32], uint64_t stride, uint64_t cap,
+                                 uint8_t *msg, uint32_t *len, uint8_t *dig) {
+  bal_trace tr = {stride ? stride : 1, 0, 0, cap, msg, len, dig};
+  const int rc = balloon_run(&tr, pwd, pwd_len, salt, salt_len, secret, secret_len,
+                             s_cost, t_cost, out32);
+  return rc ? rc : (int64_t)tr.kept;
 }
 
 /* ------------------------------------------------------------------------- */

@@ -4,9 +4,10 @@
 Every value is computed by the C oracle (oracle/sd_oracle.c) AND by the
 independent pure-Python restatement (oracle/blake3_py.py); the script refuses
 to write a fixture on any disagreement.  Both restatements are pinned by the
-reference's own BLAKE3 known-answer test (derive_b3,
-/root/reference/crates/crypto/src/keys/hashing.rs:210-213,324-327), which is
-the first entry of golden.json.  No reference code is executed or copied: the
+reference's own BLAKE3 known-answer tests (derive_b3,
+/root/reference/crates/crypto/src/keys/hashing.rs:210-213,324-327, the first
+entry of golden.json; and the six hash-mode Balloon-BLAKE3 vectors, :180-208,
+269-321, the second).  No reference code is executed or copied: the
 reference is Rust and its toolchain / the blake3 crate are absent.
 """
 from __future__ import annotations
@@ -31,6 +32,31 @@ KAT_MATERIAL = bytes([0x23] * 32 + [0xFF] * 16)
 KAT_EXPECTED = bytes([27, 34, 251, 101, 201, 89, 78, 90, 20, 175, 62, 206, 200, 153, 166, 103,
                       118, 179, 194, 44, 216, 26, 48, 120, 137, 157, 60, 234, 234, 53, 46, 60])
 
+# Balloon-BLAKE3 KATs (hashing.rs:130 password, :138-141 salt, :143-146 secret,
+# :58-63 params, expected :180-208; tests :269-321).  [0] standard, [1] hardened,
+# [2] paranoid -- BLAKE3 in hash mode, the mode of cas.rs / hash.rs.
+BALLOON_PASSWORD = b"password"
+BALLOON_SALT = bytes([0xFF] * 16)
+BALLOON_SECRET = bytes([0x55] * 18)
+BALLOON_S_COST = [131_072, 262_144, 524_288]
+BALLOON_T_COST = 2
+BALLOON_EXPECTED = [
+    bytes([105, 36, 165, 219, 22, 136, 156, 19, 32, 143, 237, 150, 236, 194, 70, 113, 73, 137,
+           243, 106, 80, 31, 43, 73, 207, 210, 29, 251, 88, 6, 132, 77]),
+    bytes([179, 71, 60, 122, 54, 72, 132, 209, 146, 96, 15, 115, 41, 95, 5, 75, 214, 135, 6, 122,
+           82, 42, 158, 9, 117, 19, 19, 40, 48, 233, 207, 237]),
+    bytes([233, 60, 62, 184, 29, 152, 111, 46, 239, 126, 98, 90, 211, 255, 151, 0, 10, 189, 61,
+           84, 229, 11, 245, 228, 47, 114, 87, 74, 227, 67, 24, 141]),
+]
+BALLOON_WITH_SECRET_EXPECTED = [
+    bytes([188, 0, 43, 39, 137, 199, 91, 142, 97, 31, 98, 6, 130, 75, 251, 71, 150, 109, 29, 62,
+           237, 171, 210, 22, 139, 108, 94, 190, 91, 74, 134, 47]),
+    bytes([19, 247, 102, 192, 129, 184, 29, 147, 68, 215, 234, 146, 153, 221, 65, 134, 68, 120,
+           207, 209, 184, 246, 127, 131, 9, 245, 91, 250, 220, 61, 76, 248]),
+    bytes([165, 240, 162, 25, 172, 3, 232, 2, 43, 230, 226, 128, 174, 28, 211, 61, 139, 136, 221,
+           197, 16, 83, 221, 18, 212, 190, 138, 79, 239, 148, 89, 215]),
+]
+
 HASH_LENGTHS = [0, 1, 2, 63, 64, 65, 127, 128, 129, 1023, 1024, 1025, 2047, 2048, 2049, 3072,
                 3073, 4096, 4097, 5120, 5121, 6144, 7168, 8192, 8193, 16384, 31744, 31745, 65536,
                 102400, 102408, 102409]
@@ -52,6 +78,16 @@ def main():
     g = {"derive_key_kat": {"context": KAT_CONTEXT, "material_hex": KAT_MATERIAL.hex(),
                             "expected_hex": KAT_EXPECTED.hex(),
                             "source": "crates/crypto/src/keys/hashing.rs:210-213,324-327"}}
+    bal = []
+    for i, s_cost in enumerate(BALLOON_S_COST):
+        for secret, exp in ((b"", BALLOON_EXPECTED[i]), (BALLOON_SECRET, BALLOON_WITH_SECRET_EXPECTED[i])):
+            got = O.balloon_blake3(BALLOON_PASSWORD, BALLOON_SALT, secret, s_cost, BALLOON_T_COST)
+            assert got == exp, ("C oracle fails a Balloon-BLAKE3 KAT", s_cost, bool(secret))
+            bal.append({"s_cost": s_cost, "t_cost": BALLOON_T_COST, "secret_hex": secret.hex(),
+                        "expected_hex": exp.hex()})
+    g["balloon_blake3_kats"] = {"password_hex": BALLOON_PASSWORD.hex(), "salt_hex": BALLOON_SALT.hex(),
+                                "vectors": bal,
+                                "source": "crates/crypto/src/keys/hashing.rs:58-63,95-114,180-208,269-321"}
     hashes = {}
     for n in HASH_LENGTHS:
         d = pattern(n)

@@ -17,6 +17,59 @@ def test_reference_derive_key_kat(golden):
     assert P.derive_key(KAT_CONTEXT, KAT_MATERIAL) == KAT_EXPECTED
 
 
+def _balloon_cases():
+    from tests.golden import make_golden as G
+    for i, s_cost in enumerate(G.BALLOON_S_COST):
+        yield s_cost, b"", G.BALLOON_EXPECTED[i]
+        yield s_cost, G.BALLOON_SECRET, G.BALLOON_WITH_SECRET_EXPECTED[i]
+
+
+def test_reference_balloon_blake3_kats(golden):
+    """The six HASH_B3BALLOON_* vectors (/root/reference/crates/crypto/src/keys/
+    hashing.rs:180-208, tests :269-321): Balloon (balloon-hash 0.4.0) over BLAKE3
+    in hash mode, the mode cas.rs and hash.rs use.  C oracle, six runs in
+    parallel (the ctypes call releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from tests.golden import make_golden as G
+    cases = list(_balloon_cases())
+    assert [v["expected_hex"] for v in golden["balloon_blake3_kats"]["vectors"]] == \
+        [e.hex() for _, _, e in cases]
+    with ThreadPoolExecutor(6) as ex:
+        got = list(ex.map(lambda c: O.balloon_blake3(G.BALLOON_PASSWORD, G.BALLOON_SALT, c[1],
+                                                      c[0], G.BALLOON_T_COST), cases))
+    for (s_cost, secret, exp), g in zip(cases, got):
+        assert g == exp, (s_cost, bool(secret))
+
+
+@pytest.mark.parametrize("with_secret", [False, True])
+def test_balloon_kat_messages_through_python_hasher(with_secret):
+    """The pure-Python BLAKE3 on the KAT's own messages: every 9973rd message the
+    standard-params Balloon run hashes (40/72/24/74-byte shapes, ~280 of them,
+    recorded by the C run that reproduces the reference vector) hashes to the
+    same digest in blake3_py.  (A full pure-Python Balloon run is ~2.7 M hashes
+    at ~0.35 ms each, too slow for the suite; the Python Balloon driver itself is
+    checked against the C one at small costs below.)"""
+    from tests.golden import make_golden as G
+    secret = G.BALLOON_SECRET if with_secret else b""
+    exp = (G.BALLOON_WITH_SECRET_EXPECTED if with_secret else G.BALLOON_EXPECTED)[0]
+    d, trace = O.balloon_blake3_trace(G.BALLOON_PASSWORD, G.BALLOON_SALT, secret,
+                                      G.BALLOON_S_COST[0], G.BALLOON_T_COST, 9973, 400)
+    assert d == exp
+    assert len(trace) > 250 and {len(m) for m, _ in trace} >= {24, 40, 72}
+    for m, dg in trace:
+        assert P.blake3(m) == dg
+
+
+@pytest.mark.parametrize("s_cost,t_cost,secret", [(1, 1, b""), (3, 2, bytes([0x55] * 18)),
+                                                  (16, 3, b""), (37, 2, b"ab"),
+                                                  (64, 1, bytes([0x55] * 18)), (100, 2, b"")])
+def test_balloon_python_restatement_agrees(s_cost, t_cost, secret):
+    """Independent pure-Python Balloon + BLAKE3 == the C restatement, including
+    s_cost that are not powers of two (the 256-bit `other` reduction)."""
+    assert P.balloon(b"password", bytes([0xFF] * 16), secret, s_cost, t_cost) == \
+        O.balloon_blake3(b"password", bytes([0xFF] * 16), secret, s_cost, t_cost)
+
+
 def test_empty_input_spec_value():
     h = "af1349b9f5f9a1a6a0404dea36dcc9499bcb25c9adc112b7cc9a93cae41f3262"
     assert O.blake3(b"").hex() == h
