@@ -499,6 +499,22 @@ class Runner:
                           f"{dt:.1f} s wall; scalar_value = scalar oracle, same threads"}
 
 
+def self_launch(n: int) -> int:
+    """`bench.py --gpus N` without torch.distributed's environment: start the N
+    ranks ourselves (one process per GPU, 127.0.0.1 rendezvous) as a CHILD
+    process -- before this process touches the GPU -- and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"bench: launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -518,6 +534,11 @@ def main():
                     help="check the sharded grouping against the one-GPU grouping first")
     args = ap.parse_args()
     comps = set(args.components.split(","))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus))
+    if args.gpus != int(os.environ.get("WORLD_SIZE", "1")):
+        log(f"bench: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}: "
+            "reporting the launched world size")
 
     R = Runner(args)
     torch = R.torch

@@ -86,7 +86,12 @@ int sdgpu_memcpy_async(sdgpu_ctx *ctx, void *dst, const void *src, size_t bytes,
  * status may be NULL. */
 int sdgpu_cas_batch(sdgpu_ctx *ctx, const uint8_t *msg_arena, const uint64_t *msg_off,
                     const uint32_t *msg_len, uint32_t n, uint8_t (*out8)[8], int32_t *status);
-/* Device-resident variant; arena_bytes bounds the arena (sizes workspace). */
+/* Device-resident variant.  arena_bytes bounds the arena and sizes the K1
+ * workspace (arena_bytes / 1024 + n chaining-value slots, enough for disjoint
+ * messages inside the arena).  A message ending past arena_bytes gets
+ * status -EINVAL.  Messages may overlap (e.g. duplicates sharing one copy) as
+ * long as their 4-chunk units plus n fit that bound; otherwise EVERY message
+ * gets -ENOBUFS and nothing is hashed (no write past the workspace). */
 int sdgpu_cas_batch_device(sdgpu_ctx *ctx, const uint8_t *d_arena, uint64_t arena_bytes,
                            const uint64_t *d_off, const uint32_t *d_len, uint32_t n,
                            uint8_t *d_out8, int32_t *d_status, void *stream);

@@ -29,20 +29,17 @@ struct KScope {
 // ---- batched short-message BLAKE3 (cas_id, K1) ------------------------------
 // Workspace for one batch of n messages and at most max_chunks chunks.
 struct BatchWork {
-  uint32_t* n_chunks = nullptr;    // [n]
-  uint32_t* chunk_base = nullptr;  // [n + 1]  exclusive prefix of n_chunks
+  uint32_t* n_chunks = nullptr;    // [n]     4-chunk units per message
+  uint32_t* chunk_base = nullptr;  // [n + 1] exclusive prefix of the units
   uint32_t* block_sums = nullptr;  // [scan tiles of n]
-  uint32_t* chunk_msg = nullptr;   // [max_chunks]
-  uint32_t* cvs = nullptr;         // [max_chunks][8]
-  uint32_t* total = nullptr;       // [1]   == chunk_base[n]
-  uint32_t* order = nullptr;       // [2n]  lane orders (v0/v2: [n]; v3: items then folds)
-  uint32_t* bins = nullptr;        // [129] chunk-count bins (counting sort)
-  uint32_t* slot_base = nullptr;   // [n + 1] v2: CV slot prefix (units + 1 per unit-bearing msg)
-  uint32_t* slot_sums = nullptr;   // [scan tiles of n]
-  uint32_t* hist = nullptr;        // [2 * 128 * 256 + 1] v3: per-block sort histograms
+  uint32_t* chunk_msg = nullptr;   // [max_chunks] unit -> message
+  uint32_t* cvs = nullptr;         // [max_chunks][8] CV slots
+  uint32_t* total = nullptr;       // [1]   == chunk_base[n] (units of the batch)
+  uint32_t* order = nullptr;       // [2n]  lane orders: message items, then fold lanes
+  uint32_t* hist = nullptr;        // [2 * 128 * 256 + 1] per-block sort histograms
   uint32_t* hist_sums = nullptr;   // [scan tiles of hist]
-  uint32_t* grab = nullptr;        // [1] v3: work-queue counter
-  uint64_t max_chunks = 0;
+  uint32_t* grab = nullptr;        // [1] work-queue counter
+  uint64_t max_chunks = 0;         // capacity of chunk_msg / cvs (units + n must fit)
 };
 
 // Largest message the batched cas kernel accepts: 8 + 100 KiB (cas.rs:15,27-29).
@@ -50,12 +47,14 @@ constexpr uint32_t CAS_MAX_MSG_LEN = 8u + 100u * 1024u;
 
 // Hash n messages arena[off[i] .. off[i]+len[i]) (off 16-B aligned) and write
 // out_words (2 => cas_id's 8 bytes, 8 => full 32-byte digest) words per message.
-// status[i] = 0, or -EINVAL for len > max_len / misaligned offset.
+// status[i] = 0, -EINVAL for len > max_len / misaligned offset / a message
+// ending past arena_bytes, or -ENOBUFS (every message) when the batch's CV
+// slots (units + n) exceed w.max_chunks (overlapping messages).
 // All pointers are device pointers; fully asynchronous on `s`.
-hipError_t batch_hash_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                             uint32_t n, uint32_t max_len, uint32_t out_words, uint8_t* out,
-                             int32_t* status, const BatchWork& w, hipStream_t s,
-                             KTimer* timer = nullptr);
+hipError_t batch_hash_launch(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* off,
+                             const uint32_t* len, uint32_t n, uint32_t max_len,
+                             uint32_t out_words, uint8_t* out, int32_t* status,
+                             const BatchWork& w, hipStream_t s, KTimer* timer = nullptr);
 
 // Latency path for a few messages of at most 1 MiB each: ONE launch, one
 // workgroup per message (thread per chunk, LDS tree).  max_chunks = largest

@@ -27,192 +27,13 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/sdgpu.h"
+#include "ctx.hpp"
 #include "internal.hpp"
 #include "scan_device.hpp"
 
 using namespace sdgpu;
 
 namespace {
-
-int map_err(hipError_t e) {
-  switch (e) {
-    case hipSuccess: return 0;
-    case hipErrorOutOfMemory: return -ENOMEM;
-    case hipErrorNoDevice:
-    case hipErrorInvalidDevice: return -ENODEV;
-    case hipErrorInvalidValue: return -EINVAL;
-    default: return -EIO;
-  }
-}
-
-#define SD_TRY(expr)                       \
-  do {                                     \
-    const hipError_t e_ = (expr);          \
-    if (e_ != hipSuccess) return map_err(e_); \
-  } while (0)
-
-#define SD_TRY_RC(expr)          \
-  do {                           \
-    const int rc_ = (expr);      \
-    if (rc_ != 0) return rc_;    \
-  } while (0)
-
-inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-};
-
-struct PinBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-};
-
-constexpr uint64_t kChunkLen = 1024;  // BLAKE3 chunk
-constexpr size_t kSlabBytes = size_t(256) << 20;   // pinned staging per slab
-constexpr uint32_t kSlabFiles = 1u << 16;          // files per slab
-constexpr size_t kSliceBytes = size_t(64) << 20;   // file_checksum slice = 2^16 chunks
-constexpr uint32_t kStageMaxMsg = 8u + (64u << 20);  // largest staged cas message
-constexpr size_t kStageSlabBytes = size_t(256) << 20;  // sdgpu_cas_stage_pinned device slab
-constexpr uint64_t kValidateBatchMax = uint64_t(16) << 20;  // larger files are streamed
-constexpr uint32_t kSmallBatch = 64;  // up to this many messages take the latency kernel
-
-// Brackets kernels with HIP events on their own stream; elapsed times are
-// resolved (one sync per event pair) only when read.
-struct EventTimer final : KTimer {
-  struct Pending {
-    std::string name;
-    hipEvent_t a, b;
-  };
-  struct Acc {
-    std::string name;
-    double ms = 0;
-    uint64_t n = 0;
-  };
-  std::vector<Pending> pending;
-  std::vector<hipEvent_t> pool;
-  std::vector<Acc> acc;
-  hipEvent_t get() {
-    if (!pool.empty()) {
-      hipEvent_t e = pool.back();
-      pool.pop_back();
-      return e;
-    }
-    hipEvent_t e = nullptr;
-    (void)hipEventCreate(&e);
-    return e;
-  }
-  void begin(const char* name, hipStream_t s) override {
-    Pending p{name, get(), get()};
-    (void)hipEventRecord(p.a, s);
-    pending.push_back(p);
-  }
-  void end(hipStream_t s) override {
-    if (!pending.empty()) (void)hipEventRecord(pending.back().b, s);
-  }
-  void resolve() {
-    for (auto& p : pending) {
-      float ms = 0;
-      (void)hipEventSynchronize(p.b);
-      (void)hipEventElapsedTime(&ms, p.a, p.b);
-      Acc* a = nullptr;
-      for (auto& x : acc)
-        if (x.name == p.name) a = &x;
-      if (!a) {
-        acc.push_back(Acc{p.name, 0, 0});
-        a = &acc.back();
-      }
-      a->ms += ms;
-      a->n += 1;
-      pool.push_back(p.a);
-      pool.push_back(p.b);
-    }
-    pending.clear();
-  }
-  ~EventTimer() override {
-    resolve();
-    for (auto e : pool) (void)hipEventDestroy(e);
-  }
-};
-
-}  // namespace
-
-struct sdgpu_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t last = nullptr;
-  std::mutex mu;
-  DevBuf batch_ws, tree_ws, dedup_ws, shard_ws, io_a, io_b, link_ws, stage_meta;
-  DevBuf stage_slab[3];
-  // host staging of the path / host-buffer entry points (identify_files,
-  // cas_batch, generate_cas_id, checksum_files, file_checksum): two pinned and
-  // two device slabs kept for the context's lifetime, grown on demand, so a
-  // call pays no pinned allocation (a 256 MiB hipHostMalloc costs ~10^5 us)
-  PinBuf pipe_h[2];
-  DevBuf pipe_d[2];
-  hipEvent_t pipe_evt[2] = {};
-  hipStream_t copy_stream = nullptr;  // H2D of staged slabs (SDMA), created on first use
-  hipEvent_t stage_copied[3] = {}, stage_freed[3] = {};
-  PinBuf plan_pin;
-  hipEvent_t plan_evt = nullptr;
-  bool plan_pending = false;
-  bool timing = false;
-  EventTimer timer;
-  KTimer* kt() { return timing ? &timer : nullptr; }
-};
-
-namespace {
-
-hipStream_t pick(sdgpu_ctx* c, void* stream) {
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-  c->last = s;
-  return s;
-}
-
-// Grow-only device buffer; frees the old one only after the context's work
-// has drained (a kernel may still read it).
-int ensure_dev(sdgpu_ctx* c, DevBuf& b, size_t bytes) {
-  if (bytes <= b.cap) return 0;
-  if (b.p) {
-    (void)hipStreamSynchronize(c->stream);
-    if (c->last && c->last != c->stream) (void)hipStreamSynchronize(c->last);
-    (void)hipFree(b.p);
-    b.p = nullptr;
-    b.cap = 0;
-  }
-  const size_t want = align_up(std::max<size_t>(bytes, 1), size_t(1) << 20);
-  SD_TRY(hipMalloc(&b.p, want));
-  b.cap = want;
-  return 0;
-}
-
-// Grow-only device buffer that keeps its first `keep` bytes.
-int grow_dev_keep(sdgpu_ctx* c, DevBuf& b, size_t bytes, size_t keep) {
-  if (bytes <= b.cap) return 0;
-  void* np = nullptr;
-  const size_t want = align_up(std::max<size_t>(bytes, 2 * b.cap), size_t(1) << 20);
-  SD_TRY(hipMalloc(&np, want));
-  if (b.p) {
-    SD_TRY(hipStreamSynchronize(c->stream));
-    if (keep) SD_TRY(hipMemcpy(np, b.p, std::min(keep, b.cap), hipMemcpyDeviceToDevice));
-    (void)hipFree(b.p);
-  }
-  b.p = np;
-  b.cap = want;
-  return 0;
-}
-
-int ensure_pin(PinBuf& b, size_t bytes) {
-  if (bytes <= b.cap) return 0;
-  if (b.p) (void)hipHostFree(b.p);
-  b.p = nullptr;
-  b.cap = 0;
-  const size_t want = align_up(std::max<size_t>(bytes, 1), size_t(1) << 16);
-  SD_TRY(hipHostMalloc(&b.p, want, hipHostMallocDefault));
-  b.cap = want;
-  return 0;
-}
 
 // Carves the K1 workspace for n messages / max_chunks chunks out of ctx->batch_ws.
 int batch_work(sdgpu_ctx* c, uint32_t n, uint64_t max_chunks, BatchWork& w) {
@@ -221,11 +42,8 @@ int batch_work(sdgpu_ctx* c, uint32_t n, uint64_t max_chunks, BatchWork& w) {
   const size_t o_sums = align_up(o_base + 4ull * (n + 1), 256);
   const size_t o_tot = align_up(o_sums + 4ull * (scan::tiles_for(n) + 1), 256);
   const size_t o_order = align_up(o_tot + 4, 256);
-  const size_t o_bins = align_up(o_order + 8ull * n, 256);
-  const size_t o_slot = align_up(o_bins + 4ull * 129, 256);
-  const size_t o_ssum = align_up(o_slot + 4ull * (n + 1), 256);
   const size_t n_hist = 2ull * 128 * 256;
-  const size_t o_hist = align_up(o_ssum + 4ull * (scan::tiles_for(n) + 1), 256);
+  const size_t o_hist = align_up(o_order + 8ull * n, 256);
   const size_t o_hsum = align_up(o_hist + 4ull * (n_hist + 1), 256);
   const size_t o_grab = align_up(o_hsum + 4ull * (scan::tiles_for(n_hist) + 1), 256);
   const size_t o_map = align_up(o_grab + 4, 256);
@@ -238,9 +56,6 @@ int batch_work(sdgpu_ctx* c, uint32_t n, uint64_t max_chunks, BatchWork& w) {
   w.block_sums = reinterpret_cast<uint32_t*>(b + o_sums);
   w.total = reinterpret_cast<uint32_t*>(b + o_tot);
   w.order = reinterpret_cast<uint32_t*>(b + o_order);
-  w.bins = reinterpret_cast<uint32_t*>(b + o_bins);
-  w.slot_base = reinterpret_cast<uint32_t*>(b + o_slot);
-  w.slot_sums = reinterpret_cast<uint32_t*>(b + o_ssum);
   w.hist = reinterpret_cast<uint32_t*>(b + o_hist);
   w.hist_sums = reinterpret_cast<uint32_t*>(b + o_hsum);
   w.grab = reinterpret_cast<uint32_t*>(b + o_grab);
@@ -416,6 +231,7 @@ int pipe_slot(sdgpu_ctx* c, int k, size_t bytes) {
 // file costs one ~60 KiB slab, not 256 MiB.
 template <typename Est, typename Produce, typename Finish>
 int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&& finish) {
+  (void)pick(c, nullptr);  // runs on the context stream, after earlier work on others
   uint64_t want = 0;
   for (uint32_t i = 0; i < n && want < kSlabBytes; ++i) want += align_up(est(i), 16);
   const SlabLayout L = slab_layout(static_cast<size_t>(std::clamp<uint64_t>(want, 4096, kSlabBytes)),
@@ -495,8 +311,8 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
       ok = (small ? small_hash_launch(db, d_off, d_len, cnt, kStageMaxMsg,
                                       max_msg <= kChunkLen ? 1u : (max_msg + kChunkLen - 1) / kChunkLen,
                                       2, db + L.out, nullptr, s, c->kt())
-                  : batch_hash_launch(db, d_off, d_len, cnt, kStageMaxMsg, 2, db + L.out, nullptr,
-                                      w, s, c->kt())) == hipSuccess;
+                  : batch_hash_launch(db, L.arena_cap, d_off, d_len, cnt, kStageMaxMsg, 2,
+                                      db + L.out, nullptr, w, s, c->kt())) == hipSuccess;
     if (!ok ||
         hipMemcpyAsync(hb + L.out, db + L.out, 8ull * cnt, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipEventRecord(sl.done, s) != hipSuccess) {
@@ -585,6 +401,10 @@ int sdgpu_close(sdgpu_ctx* c) {
   }
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->plan_pin.p) (void)hipHostFree(c->plan_pin.p);
+  for (DevBuf* b : {&c->xs_send, &c->xs_recv, &c->xs_back})
+    if (b->p) (void)hipFree(b->p);
+  if (c->xs_counts.p) (void)hipHostFree(c->xs_counts.p);
+  if (c->handover) (void)hipEventDestroy(c->handover);
   (void)hipEventDestroy(c->plan_evt);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -648,8 +468,8 @@ int sdgpu_cas_batch_device(sdgpu_ctx* c, const uint8_t* d_arena, uint64_t arena_
   hipStream_t s = pick(c, stream);
   BatchWork w;
   SD_TRY_RC(batch_work(c, n, arena_bytes / kChunkLen + n, w));
-  SD_TRY(batch_hash_launch(d_arena, d_off, d_len, n, CAS_MAX_MSG_LEN, 2, d_out8, d_status, w, s,
-                           c->kt()));
+  SD_TRY(batch_hash_launch(d_arena, arena_bytes, d_off, d_len, n, CAS_MAX_MSG_LEN, 2, d_out8,
+                           d_status, w, s, c->kt()));
   return 0;
 }
 
@@ -730,8 +550,8 @@ int sdgpu_cas_stage_pinned(sdgpu_ctx* c, const uint8_t* h_arena, const uint64_t*
     // message i of the piece sits at slab + (off[i] - base): hand K1 an arena
     // origin of slab - base (16-B aligned: slab and off are)
     const uint8_t* origin = slab - pc.base;
-    SD_TRY(batch_hash_launch(origin, d_off + pc.first, d_len + pc.first, pc.count,
-                             CAS_MAX_MSG_LEN, 2, d_out8 + 8ull * pc.first,
+    SD_TRY(batch_hash_launch(origin, pc.base + pc.bytes, d_off + pc.first, d_len + pc.first,
+                             pc.count, CAS_MAX_MSG_LEN, 2, d_out8 + 8ull * pc.first,
                              d_status ? d_status + pc.first : nullptr, w, s, c->kt()));
     SD_TRY(hipEventRecord(c->stage_freed[r], s));
   }
@@ -865,8 +685,7 @@ int sdgpu_checksum(sdgpu_ctx* c, const void* bytes, uint64_t len, uint8_t out32[
   if (!c || (len && !bytes) || !out32) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  c->last = s;
+  hipStream_t s = pick(c, nullptr);
   SD_TRY_RC(ensure_dev(c, c->io_a, align_up(len, 256) + 256));
   uint8_t* d = static_cast<uint8_t*>(c->io_a.p);
   if (len) SD_TRY(hipMemcpyAsync(d, bytes, len, hipMemcpyHostToDevice, s));
@@ -903,8 +722,7 @@ int64_t read_whole_fd(int fd, uint8_t* dst, size_t cap) {
 int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
   const int fd = open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return -errno;
-  hipStream_t s = c->stream;
-  c->last = s;
+  hipStream_t s = pick(c, nullptr);
   // two pinned + two device slices; slice k's subtree CV lands in cvs[k]
   PinBuf* hp = c->pipe_h;  // the context's two staging slots
   int rc = 0;
@@ -1068,8 +886,7 @@ int sdgpu_checksum_files(sdgpu_ctx* c, const char* const* paths, uint32_t n, uin
   if (!c || (n && (!paths || !out32))) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  c->last = s;
+  hipStream_t s = pick(c, nullptr);
   std::vector<int64_t> size(n);
   parallel_for(n, [&](uint32_t i) {
     struct stat st;

@@ -132,25 +132,58 @@ def _tree_edge_lengths():
     return np.array(sorted(ls), np.uint32)
 
 
-@pytest.mark.parametrize("variant", ["0", "2", "3", "4"])
-def test_k1_variants_tree_edges_bit_exact(ctx, variant, monkeypatch):
-    """Every K1 scheduling variant (SDGPU_K1_VARIANT) on every unit/ragged-tail
-    shape: q = 0..25 four-chunk units with 0..4 trailing chunks."""
+def test_k1_tree_edges_bit_exact(ctx):
+    """K1 on every unit/ragged-tail shape: q = 0..25 four-chunk units with 0..4
+    trailing chunks, in both orders in one batch."""
     from spacedrive_amd import cas
-    monkeypatch.setenv("SDGPU_K1_VARIANT", variant)
     lens = _tree_edge_lengths()
-    lens = np.concatenate([lens, lens[::-1]])  # both orders in one batch
+    lens = np.concatenate([lens, lens[::-1]])
     off = np.zeros(lens.size, np.uint64)
     pos = 0
     for i, n in enumerate(lens):
         off[i] = pos
         pos += (int(n) + 127) // 128 * 128
-    rng = np.random.default_rng(int(variant) + 7)
+    rng = np.random.default_rng(7)
     arena = rng.integers(0, 256, pos + 16, dtype=np.uint8)
     out, st = cas.cas_batch(arena, off, lens, ctx)
     assert np.all(st == 0)
     ref = O.cas_batch(arena, off, lens, threads=8)
     np.testing.assert_array_equal(out, ref)
+
+
+def test_device_api_workspace_guards(ctx):
+    """sdgpu_cas_batch_device sizes its workspace from arena_bytes: a message
+    ending past the arena is -EINVAL; overlapping messages whose CV slots fit
+    are hashed normally; overlapping messages that would overflow the workspace
+    are all -ENOBUFS (nothing written past it)."""
+    import torch
+    from spacedrive_amd import cas
+    rng = np.random.default_rng(3)
+    host = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    arena = torch.from_numpy(host).cuda()
+    off = torch.tensor([0, 0, 4096, (1 << 20) - 64, (1 << 20) - 48], dtype=torch.int64,
+                       device="cuda")
+    ln = torch.tensor([102408, 102408, 57352, 64, 64], dtype=torch.int32, device="cuda")
+    out, st = cas.cas_batch_device(arena, off, ln, ctx=ctx)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [0, 0, 0, 0, -22]
+    o = off.cpu().numpy().view(np.uint64)[:4]
+    l_ = ln.cpu().numpy().view(np.uint32)[:4]
+    np.testing.assert_array_equal(out.cpu().numpy()[:4], O.cas_batch(host, o, l_, threads=4))
+    assert not out.cpu().numpy()[4].any()
+    # 2000 copies of one 100 KiB message in a 128 KiB arena: 25 units each,
+    # far beyond arena_bytes / 1024 + n CV slots
+    small = arena[: 128 << 10]
+    off2 = torch.zeros(2000, dtype=torch.int64, device="cuda")
+    ln2 = torch.full((2000,), 102408, dtype=torch.int32, device="cuda")
+    out2, st2 = cas.cas_batch_device(small, off2, ln2, ctx=ctx)
+    torch.cuda.synchronize()
+    assert set(st2.cpu().tolist()) == {-105}  # -ENOBUFS
+    assert not out2.cpu().numpy().any()
+    # the context still works afterwards
+    out3, st3 = cas.cas_batch_device(arena, off[:3], ln[:3], ctx=ctx)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out3.cpu().numpy(), out.cpu().numpy()[:3])
 
 
 @pytest.mark.parametrize("n", [1, 3, 64])
