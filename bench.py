@@ -114,9 +114,36 @@ class Runner:
                 dist.init_process_group("nccl", device_id=self.dev)
             else:
                 dist.init_process_group(backend)
+        from spacedrive_amd import dedup
         from spacedrive_amd._native import default_context
         self.ctx = default_context(self.local)
         self.args = args
+        self.backend = backend if self.world > 1 else None
+        self.ops = dedup.HipOps(self.ctx)
+        self.comm = None
+        if self.world > 1 and backend == "nccl":
+            # the grouping's exchange runs INSIDE libsdgpu over RCCL (what the
+            # Rust host calls): rank 0's communicator id travels over the
+            # torch.distributed group, every rank joins
+            obj = [dedup.Comm.unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            self.comm = dedup.Comm.init_rank(self.ctx, self.world, self.rank, obj[0])
+
+    def exchange_name(self) -> str:
+        if self.world == 1:
+            return "none (one GPU: local grouping)"
+        if self.comm is not None:
+            return "libsdgpu RCCL all-to-all (sdgpu_group_sharded_device)"
+        return f"torch.distributed {self.backend} all-to-all over libsdgpu steps (rehearsal)"
+
+    def group(self, key, has, rank, timings=None):
+        """The cas_id -> Object grouping of this rank's rows against all ranks."""
+        from spacedrive_amd import dedup
+        if self.world == 1:
+            return self.ops.group_rows(key, has, rank, 100, 0)
+        if self.comm is not None:
+            return dedup.group_sharded(key, has, rank, self.comm, None, 100)
+        return dedup.sharded_group_reps(key, has, rank, 100, ops=self.ops, timings=timings)
 
     def barrier(self):
         if self.world > 1:
@@ -156,7 +183,6 @@ class Runner:
         has = torch.from_numpy((sizes != 0).astype(np.uint8)).to(self.dev)
         grank = torch.arange(self.rank * n, (self.rank + 1) * n, dtype=torch.int64,
                              device=self.dev).to(torch.int32)
-        ops = dedup.HipOps(self.ctx)
         torch.cuda.synchronize()
         lens = ln.cpu().numpy().view(np.uint32)
         blk, par = compressions(lens)
@@ -168,7 +194,7 @@ class Runner:
         def job():
             k1()
             key = out.view(torch.int64).view(-1)
-            rep = dedup.sharded_group_reps(key, has, grank, 100, ops=ops)
+            rep = self.group(key, has, grank)
             dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx, trim=False)
 
         # K1 alone, with live per-kernel event timing on its launch stream
@@ -233,13 +259,12 @@ class Runner:
         has = torch.from_numpy((sizes != 0).astype(np.uint8)).to(self.dev)
         grank = torch.arange(self.rank * n, (self.rank + 1) * n, dtype=torch.int64,
                              device=self.dev).to(torch.int32)
-        ops = dedup.HipOps(self.ctx)
         peak = self.h2d_peak()
 
         def step():
             cas.cas_stage_pinned(h_arena, off, ln, out, st, ctx=self.ctx)
             key = out.view(torch.int64).view(-1)
-            rep = dedup.sharded_group_reps(key, has, grank, 100, ops=ops)
+            rep = self.group(key, has, grank)
             dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx, trim=False)
 
         t = self.timed(step, steps, warmup)
@@ -326,28 +351,30 @@ class Runner:
         key, has, rank = corpus.synth_dedup_rows_device(4, total, int(total * 0.8),
                                                         self.rank * per, per,
                                                         device=self.local, ctx=self.ctx)
-        ops = dedup.HipOps(self.ctx)
         if self.args.verify:
-            self.verify_sharded(key, has, rank, ops)
+            self.verify_sharded(key, has, rank)
         self.ctx.set_timing(True)
-        t = self.timed(lambda: dedup.sharded_group_reps(key, has, rank, 100, ops=ops), steps,
-                       warmup)
+        t = self.timed(lambda: self.group(key, has, rank), steps, warmup)
         kt = self.ctx.kernel_times()
         self.ctx.set_timing(False)
-        xinfo = {}
-        dedup.sharded_group_reps(key, has, rank, 100, ops=ops, timings=xinfo)
         xchg = None
         if self.world > 1:
-            # payload of one step on this rank: (key u64, rank u32) out, rep u32 back;
-            # a 1/W share of it stays on the GPU (its own shards)
-            fwd = 12 * (xinfo["sent_rows"] + xinfo["recv_rows"])
-            back = 4 * (xinfo["sent_rows"] + xinfo["recv_rows"])
+            # payload of one step on this rank: (key, rank) 12-B records out to
+            # their owners, 4-B reps back; a 1/W share stays on this GPU
+            keyed = int(has.sum())
+            xinfo = {}
+            if self.comm is None:
+                self.group(key, has, rank, timings=xinfo)
+            sent = xinfo.get("sent_rows", keyed)
+            recv = xinfo.get("recv_rows", keyed)
+            fwd, back = 12 * (sent + recv), 4 * (sent + recv)
             remote = (self.world - 1) / self.world
             xchg = {"payload_bytes_per_gpu": fwd + back,
                     "remote_bytes_per_gpu_est": int((fwd + back) * remote),
                     "remote_GBps_per_gpu_over_step": (fwd + back) * remote / (t / steps) / 1e9,
-                    "note": "bytes sent + received per GPU per step over xGMI (RCCL all-to-all); "
-                            "rate is over the whole step, a lower bound on the link rate"}
+                    "transport": self.exchange_name(),
+                    "note": "bytes sent + received per GPU per step over xGMI; rate is over the "
+                            "whole step, a lower bound on the link rate"}
         kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in kt.items()}
         roof = None
         if self.world == 1:
@@ -355,7 +382,7 @@ class Runner:
             # hist reads key + has_key; the scatter reads key, rank, has_key and writes one
             # 16-B record per keyed row plus every row's initial rep; the group-by reads
             # the records and writes rep for the rows that link to an earlier chunk
-            rep = dedup.sharded_group_reps(key, has, rank, 100, ops=ops)
+            rep = self.group(key, has, rank)
             nk = int(has.sum())
             linked = int((rep != rank).sum())
             alg = {"bucket_hist": 9 * per, "bucket_scatter": 17 * per + 16 * nk,
@@ -366,28 +393,27 @@ class Runner:
                                     "achieved": b / (kernels[k]["avg_ms"] * 1e-3) / 1e9,
                                     "frac": b / (kernels[k]["avg_ms"] * 1e-3) / HBM_PEAK}
                                 for k, b in alg.items() if kernels.get(k, {}).get("avg_ms")},
-                    "note": "algorithmic bytes of this partition + group-by design; the "
-                            "scatter's PMC traffic is ~3x its algorithmic write (16-B records "
-                            "scattered into 4096 buckets, DESIGN.md section 4)"}
+                    "note": "algorithmic bytes of this partition + group-by design "
+                            "(DESIGN.md section 4); PMC traffic in profiles/"}
         return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
                 "exchange": xchg, "roofline": roof,
                 "config": {"workload": "config4: 80% distinct u64 keys + 20% dups, 0.1% keyless",
                            "rows_per_gpu": per, "rows_total": total},
                 "kernels": kernels}
 
-    def verify_sharded(self, key, has, rank, ops):
+    def verify_sharded(self, key, has, rank):
         """--verify: the sharded grouping over all ranks (the exchange path the
         timed steps use) equals the one-GPU grouping of the gathered table."""
         torch, dist = self.torch, self.dist
         from spacedrive_amd import dedup
-        rep = dedup.sharded_group_reps(key, has, rank, 100, ops=ops)
+        rep = self.group(key, has, rank)
         if self.world > 1:
             parts = [[torch.empty_like(t) for _ in range(self.world)] for t in (key, has, rank, rep)]
             for p, t in zip(parts, (key, has, rank, rep)):
                 dist.all_gather(p, t)
             key, has, rank, rep = (torch.cat(p) for p in parts)
         if self.rank == 0:
-            ref = ops.group_rows(key, has, rank, 100, 0)
+            ref = self.ops.group_rows(key, has, rank, 100, 0)
             bad = int((ref != rep).sum())
             log(f"verify: sharded grouping of {key.numel()} rows over {self.world} ranks: "
                 f"{bad} mismatches vs the one-GPU grouping")
@@ -621,9 +647,14 @@ def main():
                                    "sharded cas_id->Object grouping + Object link batch",
                        "files_per_gpu": args.files, "global_files": args.files * R.world,
                        "parallelism": f"dp{R.world} (files) + hash-sharded dedup, RCCL all-to-all"},
-            "components": comp, "kernels": c["kernels"], "roofline": roof, "cpu_baseline": cpu}
+            "components": comp, "kernels": c["kernels"], "roofline": roof, "cpu_baseline": cpu,
+            "world": {"dist_world_size": R.dist.get_world_size() if R.world > 1 else 1,
+                      "devices_visible": torch.cuda.device_count(),
+                      "backend": R.backend, "exchange": R.exchange_name()}}
     if R.rank == 0:
         print(json.dumps(line), flush=True)
+    if R.comm is not None:
+        R.comm.close()
     if R.world > 1:
         R.dist.destroy_process_group()
 

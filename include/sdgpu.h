@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SDGPU_ABI_VERSION 1
+#define SDGPU_ABI_VERSION 2
 
 /* cas.rs:10-15 */
 #define SDGPU_CAS_SAMPLE_COUNT 4u
@@ -154,35 +154,124 @@ int sdgpu_checksum_files(sdgpu_ctx *ctx, const char *const *paths, uint32_t n,
  * Replaces the Object link/create decisions of identifier_job_step
  * (file_identifier/mod.rs:167-333) over the orphan rows in ascending id order
  * processed in chunks of chunk_rows (=100, mod.rs:36; file_identifier_job.rs:286-309).
- * Rows are identified by their rank r (position in id order).  Output rep[r]:
- * the rank of the row whose Object row r is linked to:
+ * Rows are identified by their rank r (position in id order, < 2^31).  Output
+ * rep[r]: the rank of the row whose Object row r is linked to:
  *   - has_key[r] == 0 (empty file, cas_id None): rep[r] = r;
  *   - r in the chunk holding the lowest-rank row f of its key: rep[r] = r
  *     (a new Object per row, mod.rs:233-297);
  *   - otherwise rep[r] = f (linked to an existing Object, mod.rs:189-225).
  * key = the 8 cas bytes read as a little-endian u64 (equality is all the
- * grouping uses, mod.rs:136-141,196-203). */
+ * grouping uses, mod.rs:136-141,196-203).
+ * The calls below group the rows they are given.  Objects that exist BEFORE
+ * the rows (earlier batches of the run, earlier runs, other locations: the
+ * library-wide find_many of mod.rs:168-185) come from an Object index, see
+ * sdgpu_index_* and sdgpu_group_rows_indexed_device. */
 int sdgpu_dedup(sdgpu_ctx *ctx, const uint64_t *key, const uint8_t *has_key, uint32_t n,
                 uint32_t chunk_rows, uint32_t *rep);
 /* Device-resident, one GPU: rows given as (key, rank) pairs (rows without a
  * key are simply not passed); writes rep for each pair at the same index.
- * skip_bits: number of top key bits that are constant on this shard (log2 of
- * the number of GPUs the keys were hash-partitioned over; 0 on one GPU). */
+ * skip_bits: accepted for ABI 1 compatibility and ignored (bucket digits come
+ * from a hash of the key since ABI 2, so shards need no skipped bits). */
 int sdgpu_group_pairs_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint32_t *d_rank,
                              uint64_t n, uint32_t chunk_rows, uint32_t skip_bits, uint32_t *d_rep,
                              void *stream);
 /* Device-resident, one GPU, whole rows: rep[i] for every row i; rows with
  * d_has_key[i] == 0 get rep[i] = rank[i].  d_has_key NULL = every row keyed;
- * d_rank NULL = rank i (rows already in id order). */
+ * d_rank NULL = rank i (rows already in id order).  skip_bits ignored. */
 int sdgpu_group_rows_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t *d_has_key,
                             const uint32_t *d_rank, uint64_t n, uint32_t chunk_rows,
                             uint32_t skip_bits, uint32_t *d_rep, void *stream);
-/* Sharding helpers for the multi-GPU dedup (one process per GPU, RCCL
- * all-to-all between them): shard of a key = its top shard_bits bits.
- * count: h_counts[s] = rows with has_key destined to shard s (host array of
- * 2^shard_bits; synchronises).  partition: packs those rows by shard into
- * d_out_key/d_out_rank (shard s at exclusive prefix of counts) and records each
- * packed row's source index in d_out_pos. */
+
+/* ---- Object index: Objects that exist before a batch ------------------------
+ * Replaces the library-wide lookup of identifier_job_step
+ * (file_identifier/mod.rs:168-185: Objects owning a file_path whose cas_id is
+ * in the step's set) and the link of matching rows to them (:189-225, :233-241).
+ * A device hash table key -> value lives with one context.  Values are either
+ * a row rank (the Object created by that row in an earlier batch of the same
+ * run) or SDGPU_REP_EXISTING | handle for an Object registered by the caller
+ * (handle < 2^31, e.g. the Object's database id).  A key keeps the minimum
+ * value inserted for it (the canonical "first" Object).
+ * Grouping batches in id order through one index yields exactly the grouping
+ * of the whole run (tests/test_gpu_index.py). */
+#define SDGPU_REP_EXISTING 0x80000000u
+typedef struct sdgpu_index sdgpu_index;
+int sdgpu_index_create(sdgpu_ctx *ctx, uint64_t capacity_hint, sdgpu_index **out);
+int sdgpu_index_destroy(sdgpu_index *idx);
+int sdgpu_index_clear(sdgpu_index *idx, void *stream);
+/* Distinct keys stored (synchronises). */
+int sdgpu_index_count(sdgpu_index *idx, uint64_t *count);
+/* Register pre-existing Objects: d_key[i] -> SDGPU_REP_EXISTING | d_handle[i].
+ * Only keys whose shard belongs to `rank` of `world` are kept (world = 1: all),
+ * so every GPU of a sharded grouping can be given the same list.  May
+ * synchronise `stream` when the table grows. */
+int sdgpu_index_add_objects_device(sdgpu_index *idx, const uint64_t *d_key,
+                                   const uint32_t *d_handle, uint64_t n, uint32_t world,
+                                   uint32_t rank, void *stream);
+/* sdgpu_group_rows_device against the index: a keyed row whose key is in the
+ * index gets rep = the index value if it is an existing Object, else (a rank
+ * f of an earlier batch) rep = r when r and f share a chunk and f otherwise;
+ * the other rows are grouped among themselves; afterwards every row that
+ * created an Object (rep == rank) is inserted with its rank.  May synchronise
+ * `stream` when the table grows. */
+int sdgpu_group_rows_indexed_device(sdgpu_ctx *ctx, sdgpu_index *idx, const uint64_t *d_key,
+                                    const uint8_t *d_has_key, const uint32_t *d_rank, uint64_t n,
+                                    uint32_t chunk_rows, uint32_t *d_rep, void *stream);
+/* Host arrays, one batch of n rows with ranks first_rank + i (an identifier
+ * job step over a whole batch); idx may be NULL (group the batch alone). */
+int sdgpu_dedup_batch(sdgpu_ctx *ctx, sdgpu_index *idx, const uint64_t *key,
+                      const uint8_t *has_key, uint32_t first_rank, uint32_t n,
+                      uint32_t chunk_rows, uint32_t *rep);
+
+/* ---- multi-GPU grouping: hash-sharded over a node, RCCL all-to-all over xGMI --
+ * Every key has one owner GPU (shard = top 8 bits of mix64(key), rank d owns
+ * shards s with s * world / 256 == d); each GPU sends its keyed rows to their
+ * owners as packed 12-byte {key, rank} records, the owners group their rows
+ * (and probe their share of the Object index), and the reps return (4 B per
+ * row).  One host synchronisation per call (the count exchange).
+ * Transports: SDGPU_TRANSPORT_RCCL (grouped ncclSend/ncclRecv; one rank per
+ * GPU), SDGPU_TRANSPORT_PEER (device-to-device copies between contexts of one
+ * process; also contexts sharing a GPU), AUTO = RCCL unless devices repeat. */
+#define SDGPU_COMM_ID_BYTES 128
+#define SDGPU_TRANSPORT_AUTO 0
+#define SDGPU_TRANSPORT_RCCL 1
+#define SDGPU_TRANSPORT_PEER 2
+typedef struct sdgpu_comm sdgpu_comm;
+/* One process per GPU: rank 0 creates the id, every rank receives it
+ * out of band and joins (blocks until all nranks have joined). */
+int sdgpu_comm_unique_id(uint8_t id[SDGPU_COMM_ID_BYTES]);
+int sdgpu_comm_init_rank(sdgpu_ctx *ctx, int nranks, int rank,
+                         const uint8_t id[SDGPU_COMM_ID_BYTES], sdgpu_comm **out);
+/* One process driving ngpu contexts: out[r] is rank r's communicator. */
+int sdgpu_comm_init_all(sdgpu_ctx *const *ctx, int ngpu, int transport, sdgpu_comm **out);
+int sdgpu_comm_destroy(sdgpu_comm *comm);
+int sdgpu_comm_info(sdgpu_comm *comm, int *nranks, int *rank, int *transport);
+/* Collective, one process per GPU (RCCL): every rank calls it with its own
+ * rows (global ranks in d_rank, required); rep for each of its rows.  idx
+ * (may be NULL) is this rank's share of the Object index. */
+int sdgpu_group_sharded_device(sdgpu_ctx *ctx, sdgpu_comm *comm, sdgpu_index *idx,
+                               const uint64_t *d_key, const uint8_t *d_has_key,
+                               const uint32_t *d_rank, uint64_t n, uint32_t chunk_rows,
+                               uint32_t *d_rep, void *stream);
+/* The same from one process for all ngpu ranks at once (arrays indexed by
+ * rank; idx, d_has_key and streams may be NULL). */
+int sdgpu_group_sharded_all_device(sdgpu_ctx *const *ctx, sdgpu_comm *const *comm,
+                                   sdgpu_index *const *idx, int ngpu,
+                                   const uint64_t *const *d_key, const uint8_t *const *d_has_key,
+                                   const uint32_t *const *d_rank, const uint64_t *n,
+                                   uint32_t chunk_rows, uint32_t *const *d_rep,
+                                   void *const *streams);
+/* SURVEY §8(b)'s sdgpu_dedup(ctx[], ngpu, ...): host arrays in rank order,
+ * split into ngpu contiguous ranges, grouped across the ngpu contexts
+ * (communicators created and destroyed inside). */
+int sdgpu_dedup_sharded(sdgpu_ctx *const *ctx, int ngpu, const uint64_t *key,
+                        const uint8_t *has_key, uint32_t n, uint32_t chunk_rows, uint32_t *rep);
+
+/* Sharding helpers (single steps of the exchange, for hosts that bring their
+ * own collectives, e.g. torch.distributed): shard of a key = top shard_bits
+ * bits of mix64(key).  count: h_counts[s] = rows with has_key destined to
+ * shard s (host array of 2^shard_bits; synchronises).  partition: packs those
+ * rows by shard into d_out_key/d_out_rank (shard s at exclusive prefix of
+ * counts) and records each packed row's source index in d_out_pos. */
 int sdgpu_shard_count_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t *d_has_key,
                              uint64_t n, uint32_t shard_bits, uint64_t *h_counts, void *stream);
 int sdgpu_shard_partition_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t *d_has_key,

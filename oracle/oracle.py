@@ -245,6 +245,36 @@ def group_reps(key: np.ndarray, has_key: np.ndarray, chunk_rows: int = 100) -> n
     return rep
 
 
+REP_EXISTING = 0x80000000
+
+
+def group_reps_existing(key: np.ndarray, has_key: np.ndarray, chunk_rows: int = 100,
+                        existing_key: np.ndarray | None = None,
+                        existing_handle: np.ndarray | None = None) -> np.ndarray:
+    """The grouping of a whole run of rows (ranks 0..n-1 in id order) when some
+    Objects exist before it (/root/reference/core/src/object/file_identifier/
+    mod.rs:168-185 finds, library-wide, the Objects owning a file_path with the
+    row's cas_id; :189-225 links the row to one of them; only the rest,
+    :233-241, follow the in-run rule of orc_group_reps).  A key owned by several
+    pre-existing Objects links to the lowest handle (the canonical "first").
+    Returns uint32 rep: a rank, or REP_EXISTING | handle."""
+    rep = group_reps(key, has_key, chunk_rows).astype(np.uint32)
+    if existing_key is None or len(existing_key) == 0:
+        return rep
+    ek = np.asarray(existing_key, np.uint64)
+    eh = np.asarray(existing_handle, np.uint32) & np.uint32(0x7FFFFFFF)
+    order = np.lexsort((eh, ek))                # by key, then handle
+    ek, eh = ek[order], eh[order]
+    first = np.concatenate([[True], ek[1:] != ek[:-1]])
+    ek, eh = ek[first], eh[first]               # lowest handle per key
+    key = np.asarray(key, np.uint64)
+    pos = np.searchsorted(ek, key)
+    pos = np.minimum(pos, ek.size - 1)
+    hit = (ek[pos] == key) & (np.asarray(has_key) != 0)
+    rep[hit] = np.uint32(REP_EXISTING) | eh[pos[hit]]
+    return rep
+
+
 def link_batch(rep: np.ndarray, rank: np.ndarray | None = None, valid: np.ndarray | None = None,
                first_rank: int = 0):
     """Object write set of identifier_job_step for a batch of rows

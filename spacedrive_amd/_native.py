@@ -66,6 +66,24 @@ def _proto(L):
         "sdgpu_shard_exchange_device": (i32, [ctx, c_vp, c_vp, c_vp, u64, u32, u32, c_vp, c_vp,
                                               c_vp, c_vp, c_vp]),
         "sdgpu_scatter_rep_device": (i32, [ctx, c_vp, c_vp, u64, c_vp, u64, c_vp, i32, c_vp]),
+        "sdgpu_index_create": (i32, [ctx, u64, P(c_vp)]),
+        "sdgpu_index_destroy": (i32, [c_vp]),
+        "sdgpu_index_clear": (i32, [c_vp, c_vp]),
+        "sdgpu_index_count": (i32, [c_vp, P(ctypes.c_uint64)]),
+        "sdgpu_index_add_objects_device": (i32, [c_vp, c_vp, c_vp, u64, u32, u32, c_vp]),
+        "sdgpu_group_rows_indexed_device": (i32, [ctx, c_vp, c_vp, c_vp, c_vp, u64, u32, c_vp,
+                                                  c_vp]),
+        "sdgpu_dedup_batch": (i32, [ctx, c_vp, c_vp, c_vp, u32, u32, u32, c_vp]),
+        "sdgpu_comm_unique_id": (i32, [c_vp]),
+        "sdgpu_comm_init_rank": (i32, [ctx, i32, i32, c_vp, P(c_vp)]),
+        "sdgpu_comm_init_all": (i32, [c_vp, i32, i32, c_vp]),
+        "sdgpu_comm_destroy": (i32, [c_vp]),
+        "sdgpu_comm_info": (i32, [c_vp, P(i32), P(i32), P(i32)]),
+        "sdgpu_group_sharded_device": (i32, [ctx, c_vp, c_vp, c_vp, c_vp, c_vp, u64, u32, c_vp,
+                                             c_vp]),
+        "sdgpu_group_sharded_all_device": (i32, [c_vp, c_vp, c_vp, i32, c_vp, c_vp, c_vp, c_vp,
+                                                 u32, c_vp, c_vp]),
+        "sdgpu_dedup_sharded": (i32, [c_vp, i32, c_vp, c_vp, u32, u32, c_vp]),
         "sdgpu_synth_cas_arena_device": (i32, [ctx, c_vp, c_vp, c_vp, u32, c_vp, c_vp]),
         "sdgpu_synth_file_device": (i32, [ctx, u64, u64, u64, c_vp, c_vp]),
         "sdgpu_synth_dedup_rows_device": (i32, [ctx, u64, u64, u64, u64, u64, c_vp, c_vp, c_vp,

@@ -2,10 +2,12 @@
 //
 // Replaces the Object link/create decisions of identifier_job_step
 // (/root/reference/core/src/object/file_identifier/mod.rs:136-333): the
-// HashSet of chunk cas_ids (:136-141), the library-wide find_many over
-// file_path.cas_id (:168-175), the per-row `find` of an Object owning the same
-// cas_id (:196-206) and the one-new-Object-per-remaining-row rule (:233-297),
-// evaluated for ALL orphan rows at once instead of 100 per job step.
+// HashSet of chunk cas_ids (:136-141), the per-row `find` of an Object owning
+// the same cas_id (:196-206) and the one-new-Object-per-remaining-row rule
+// (:233-297), evaluated for ALL rows of a batch at once instead of 100 per job
+// step.  The library-wide find_many over file_path.cas_id (:168-175), i.e.
+// Objects that already exist before the batch, is the Object index of
+// index.hip, consulted before this grouping (sdgpu_group_rows_indexed_device).
 //
 // Rows are (key, rank): key = the cas_id's 8 digest bytes as a little-endian
 // u64, rank = position of the file_path in ascending-id order.  The grouping
@@ -14,14 +16,20 @@
 //   rep(r) = r  if r / chunk_rows == f / chunk_rows   (new Object in f's chunk)
 //            f  otherwise                               (linked to f's Object)
 //
+// Digits come from h = mix64(key) (splitmix64 finalizer), not from the raw key
+// bits: the shard of the multi-GPU exchange is h's top 8 bits, a bucket is the
+// `bits` hash bits below them, and the LDS slot uses h's low 32 bits.  Buckets
+// are therefore balanced for any key distribution and any world size (raw key
+// bits left half the buckets empty at 3 ranks), and the three are independent.
+//
 // Pipeline (all asynchronous, no host synchronisation):
-//   K6 partition: digit = `bits` key bits below the top `skip` bits.
+//   K6 partition: digit = `bits` hash bits below the top `skip` bits.
 //      hist:    each of P blocks histograms its contiguous tile in LDS and
 //               writes counts[digit][block] (no global atomics);
 //      scan:    exclusive scan of counts (digit-major) -> (digit, block) offsets;
-//      scatter: each block re-reads its tile and scatters (key, rank, index)
-//               through LDS cursors.
-//      Used twice: by shard (top bits, multi-GPU exchange) and by bucket.
+//      scatter: each block re-reads its tile and scatters its rows through LDS
+//               cursors (16-B bucket records, or the exchange's send layout).
+//      Used twice: by shard (multi-GPU exchange) and by bucket.
 //   K5 group:   one workgroup per bucket builds a linear-probing hash table of
 //               (key -> min rank) in LDS (ds_cmpst_b64 / ds_min_u32), then maps
 //               every row to its rep.  Buckets too large for LDS use a private
@@ -31,6 +39,7 @@
 #include <errno.h>
 
 #include "internal.hpp"
+#include "rows_device.hpp"
 #include "scan_device.hpp"
 
 #include <algorithm>
@@ -50,10 +59,13 @@ constexpr int kGroupThreads = 1024;
 constexpr uint32_t kLdsSlots = 6144;
 constexpr uint32_t kLdsCap = 4608;     // rows per bucket handled in LDS (load <= 75%)
 constexpr uint64_t kBucketRows = 3072; // target mean rows per bucket (bucket_bits_for)
+constexpr uint32_t kMaxBucketBits = 15;  // 32768 LDS cursors = 128 KiB: 100 M rows stay in LDS
+constexpr uint32_t kShardBits = 8;       // multi-GPU shards: h >> 56
 constexpr uint64_t kEmpty = ~0ull;
 
-__device__ __forceinline__ uint32_t digit_of(uint64_t key, uint32_t skip, uint32_t bits) {
-  return bits == 0 ? 0u : static_cast<uint32_t>((key << skip) >> (64u - bits));
+// `bits` hash bits below the top `skip` bits of h.
+__device__ __forceinline__ uint32_t digit_of(uint64_t h, uint32_t skip, uint32_t bits) {
+  return bits == 0 ? 0u : static_cast<uint32_t>((h << skip) >> (64u - bits));
 }
 
 // XCD-aware block numbering: workgroups are dispatched round-robin over the 8
@@ -76,9 +88,8 @@ __device__ __forceinline__ void tile_of(uint64_t n, uint32_t P, uint64_t& t0, ui
 // issued back to back, so one tile costs a few memory latencies, not one per row.
 constexpr int kUnroll = 8;
 
-__global__ __launch_bounds__(kPartThreads) void k_part_hist(const uint64_t* __restrict__ key,
-                                                            const uint8_t* __restrict__ valid,
-                                                            uint64_t n, uint32_t skip,
+template <typename In>
+__global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, uint32_t skip,
                                                             uint32_t bits,
                                                             uint32_t* __restrict__ hist) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
@@ -89,28 +100,32 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(const uint64_t* __re
   tile_of(n, gridDim.x, t0, t1);
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += kUnroll * kPartThreads) {
     uint64_t k[kUnroll];
+    uint32_t r[kUnroll];
     bool v[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      v[u] = i < t1;
-      k[u] = v[u] ? key[i] : 0;
-      if (valid && v[u]) v[u] = valid[i] != 0;
+      v[u] = false;
+      if (i < t1) in.get(i, k[u], r[u], v[u]);
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
-      if (v[u]) atomicAdd(&cnt[digit_of(k[u], skip, bits)], 1u);
+      if (v[u]) atomicAdd(&cnt[digit_of(row_hash(k[u]), skip, bits)], 1u);
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
     hist[static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
 }
 
+// Shard partition of the multi-GPU exchange: keyed rows packed by shard
+// (shard s at the scanned offsets), each row's source index in out_pos.
+// kRec12: one packed 12-byte send record {key lo, key hi, rank} per row (what
+// travels over xGMI); otherwise separate key / rank arrays.
+template <typename In, bool kRec12>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
-    const uint64_t* __restrict__ key, const uint32_t* __restrict__ rank,
-    const uint8_t* __restrict__ valid, uint64_t n, uint32_t skip, uint32_t bits,
-    const uint32_t* __restrict__ offs, uint64_t* __restrict__ out_key,
-    uint32_t* __restrict__ out_rank, uint32_t* __restrict__ out_pos) {
+    In in, uint64_t n, uint32_t skip, uint32_t bits, const uint32_t* __restrict__ offs,
+    uint64_t* __restrict__ out_key, uint32_t* __restrict__ out_rank, uint3* __restrict__ out_rec,
+    uint32_t* __restrict__ out_pos) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
   const uint32_t nbins = 1u << bits;
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
@@ -126,31 +141,34 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      v[u] = i < t1;
-      k[u] = v[u] ? key[i] : 0;
-      r[u] = v[u] ? (rank ? rank[i] : static_cast<uint32_t>(i)) : 0u;
-      if (valid && v[u]) v[u] = valid[i] != 0;
+      v[u] = false;
+      if (i < t1) in.get(i, k[u], r[u], v[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (!v[u]) continue;
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      const uint32_t p = atomicAdd(&cur[digit_of(k[u], skip, bits)], 1u);
-      out_key[p] = k[u];
-      out_rank[p] = r[u];
+      const uint32_t p = atomicAdd(&cur[digit_of(row_hash(k[u]), skip, bits)], 1u);
+      if (kRec12) {
+        out_rec[p] = make_uint3(static_cast<uint32_t>(k[u]), static_cast<uint32_t>(k[u] >> 32), r[u]);
+      } else {
+        out_key[p] = k[u];
+        out_rank[p] = r[u];
+      }
       out_pos[p] = static_cast<uint32_t>(i);
     }
   }
 }
 
 // Bucket partition writing ONE 16-byte record {key lo, key hi, rank, row} per
-// row (a single scattered store instead of three).  Every row's rep is first
-// set to its own rank here (one coalesced store); rows without a key are not
-// partitioned, and K5 rewrites only the rows that link to an earlier chunk.
+// keyed row (a single scattered store instead of three).  kInitRep: every
+// row's rep is first set to its own rank here (one coalesced store); rows
+// without a key are not partitioned, and K5 rewrites only the rows that link
+// to an earlier chunk.  (The indexed grouping initialises rep in its probe.)
+template <typename In, bool kInitRep>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
-    const uint64_t* __restrict__ key, const uint32_t* __restrict__ rank,
-    const uint8_t* __restrict__ valid, uint64_t n, uint32_t skip, uint32_t bits,
-    const uint32_t* __restrict__ offs, uint4* __restrict__ rec, uint32_t* __restrict__ rep) {
+    In in, uint64_t n, uint32_t skip, uint32_t bits, const uint32_t* __restrict__ offs,
+    uint4* __restrict__ rec, uint32_t* __restrict__ rep) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
   const uint32_t nbins = 1u << bits;
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
@@ -162,23 +180,22 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += U * kPartThreads) {
     uint64_t k[U];
     uint32_t r[U];
-    bool in[U], v[U];
+    bool in_[U], v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      in[u] = i < t1;
-      k[u] = in[u] ? key[i] : 0;
-      r[u] = in[u] ? (rank ? rank[i] : static_cast<uint32_t>(i)) : 0u;
-      v[u] = in[u] && (!valid || valid[i] != 0);
+      in_[u] = i < t1;
+      v[u] = false;
+      if (in_[u]) in.get(i, k[u], r[u], v[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
       // every row starts as its own Object (coalesced store): rows without a
       // key stay so (mod.rs:238-239); K5 overwrites only the rows that link
-      if (in[u]) rep[i] = r[u];
+      if (kInitRep && in_[u]) rep[i] = r[u];
       if (!v[u]) continue;
-      const uint32_t p = atomicAdd(&cur[digit_of(k[u], skip, bits)], 1u);
+      const uint32_t p = atomicAdd(&cur[digit_of(row_hash(k[u]), skip, bits)], 1u);
       rec[p] = make_uint4(static_cast<uint32_t>(k[u]), static_cast<uint32_t>(k[u] >> 32), r[u],
                           static_cast<uint32_t>(i));
     }
@@ -191,10 +208,10 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
 // slot are written directly.  Rows are taken 2 per thread per round; each
 // round ends with a flush of the full pairs; the odd rows go out at the end.
 constexpr uint32_t kStageBits = 12;
+template <typename In, bool kInitRep>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
-    const uint64_t* __restrict__ key, const uint32_t* __restrict__ rank,
-    const uint8_t* __restrict__ valid, uint64_t n, uint32_t skip,
-    const uint32_t* __restrict__ offs, uint4* __restrict__ rec, uint32_t* __restrict__ rep) {
+    In in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ offs, uint4* __restrict__ rec,
+    uint32_t* __restrict__ rep) {
   constexpr uint32_t nbins = 1u << kStageBits;
   __shared__ uint4 stage[nbins][2];
   __shared__ uint32_t fill[nbins];
@@ -212,11 +229,13 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads;
       if (i >= t1) continue;
-      const uint64_t k = key[i];
-      const uint32_t r = rank ? rank[i] : static_cast<uint32_t>(i);
-      rep[i] = r;
-      if (valid && valid[i] == 0) continue;
-      const uint32_t b = digit_of(k, skip, kStageBits);
+      uint64_t k;
+      uint32_t r;
+      bool v;
+      in.get(i, k, r, v);
+      if (kInitRep) rep[i] = r;
+      if (!v) continue;
+      const uint32_t b = digit_of(row_hash(k), skip, kStageBits);
       const uint4 q = make_uint4(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32), r,
                                  static_cast<uint32_t>(i));
       const uint32_t sl = atomicAdd(&fill[b], 1u);
@@ -242,14 +261,21 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     if (fill[b] == 1) rec[cur[b]] = stage[b][0];
 }
 
-// First probe slot of key k in a table of tsize slots (any tsize).
-__device__ __forceinline__ uint32_t slot_of(uint64_t k, uint32_t tsize) {
-  const uint32_t h = static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> 32);
-  return static_cast<uint32_t>((static_cast<uint64_t>(h) * tsize) >> 32);
+// First probe slot of key k in the LDS table (kLdsSlots, any size): the low
+// 32 hash bits, scaled.  The digit bits (the top ones) are constant inside a
+// bucket, the low ones are not.
+__device__ __forceinline__ uint32_t lds_slot(uint64_t k) {
+  const uint32_t h = static_cast<uint32_t>(row_hash(k));
+  return static_cast<uint32_t>((static_cast<uint64_t>(h) * kLdsSlots) >> 32);
 }
 
-__device__ __forceinline__ uint32_t next_slot(uint32_t h, uint32_t tsize) {
-  return h + 1 == tsize ? 0u : h + 1;
+__device__ __forceinline__ uint32_t next_slot(uint32_t h) {
+  return h + 1 == kLdsSlots ? 0u : h + 1;
+}
+
+// Global-table slot (tsize a power of two, up to 2^34 for a 2^32-row bucket).
+__device__ __forceinline__ uint64_t global_slot(uint64_t k, uint64_t tsize) {
+  return row_hash(k) & (tsize - 1);
 }
 
 constexpr int kPer = (kLdsCap + kGroupThreads - 1) / kGroupThreads;
@@ -277,16 +303,16 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
   const uint32_t m = end - start;
   if (m == 0) return;
   const bool in_lds = m <= kLdsCap;
-  uint32_t tsize = kLdsSlots;
+  uint64_t tsize = kLdsSlots;
   uint64_t* tk = lkey;
   uint32_t* tm = lmin;
   if (!in_lds) {
-    tsize = 1u;
-    while (tsize * 2u <= 4u * m) tsize *= 2u;  // 2m < tsize <= 4m
+    tsize = 1;
+    while (tsize * 2 <= 4ull * m) tsize *= 2;  // 2m < tsize <= 4m (64-bit: no wrap)
     tk = gkey + 4ull * start;
     tm = gmin + 4ull * start;
   }
-  for (uint32_t s = threadIdx.x; s < tsize; s += kGroupThreads) {
+  for (uint64_t s = threadIdx.x; s < tsize; s += kGroupThreads) {
     tk[s] = kEmpty;
     tm[s] = 0xFFFFFFFFu;
   }
@@ -302,7 +328,7 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
-      h[j] = slot_of(k, tsize);
+      h[j] = lds_slot(k);
       if (start + threadIdx.x + j * kGroupThreads < end) {
         live |= 1u << j;
         if (k == kEmpty)
@@ -331,7 +357,7 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
           atomicMin(&tm[h[j]], q_reg[j].z);
           pend &= ~(1u << j);
         } else {
-          h[j] = next_slot(h[j], tsize);
+          h[j] = next_slot(h[j]);
         }
       }
     }
@@ -355,7 +381,7 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
       atomicMin(&special_min, r);
       continue;
     }
-    uint32_t h = slot_of(k, tsize);
+    uint64_t h = global_slot(k, tsize);
     for (;;) {
       const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tk[h]),
                                       static_cast<unsigned long long>(kEmpty),
@@ -364,7 +390,7 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
         atomicMin(&tm[h], r);
         break;
       }
-      h = next_slot(h, tsize);
+      h = (h + 1) & (tsize - 1);
     }
   }
   __syncthreads();
@@ -376,15 +402,14 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
     if (k == kEmpty) {
       f = special_min;
     } else {
-      uint32_t h = slot_of(k, tsize);
+      uint64_t h = global_slot(k, tsize);
       for (;;) {
-        const uint64_t kk = in_lds ? tk[h]
-                                   : __hip_atomic_load(&tk[h], __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t kk =
+            __hip_atomic_load(&tk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (kk == k) break;
-        h = next_slot(h, tsize);
+        h = (h + 1) & (tsize - 1);
       }
-      f = in_lds ? tm[h] : __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      f = __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (r / chunk_rows != f / chunk_rows) rep[q.w] = f;
   }
@@ -459,9 +484,11 @@ uint32_t bucket_part_blocks() {
   return P;
 }
 
+// ~kBucketRows rows per bucket (LDS table load <= 75 % with slack), up to 2^15
+// buckets: 100 M rows on one GPU still group in LDS.
 uint32_t bucket_bits_for(uint64_t n) {
   uint32_t bits = 1;
-  while (bits < 13 && (n >> bits) > kBucketRows) ++bits;
+  while (bits < kMaxBucketBits && (n >> bits) > kBucketRows) ++bits;
   return bits;
 }
 
@@ -484,21 +511,82 @@ GroupLayout group_layout(uint64_t n) {
   return L;
 }
 
-hipError_t partition(const uint64_t* key, const uint8_t* valid, const uint32_t* rank, uint64_t n,
-                     uint32_t skip, uint32_t bits, uint32_t* hist, uint32_t* tiles,
-                     uint64_t* okey, uint32_t* orank, uint32_t* opos, hipStream_t s,
-                     KTimer* timer, const char* hname, const char* sname) {
-  const uint64_t nh = (static_cast<uint64_t>(1) << bits) * kPartBlocks;
+// Dynamic LDS above the default 64 KiB (cursors of up to 2^15 digits).
+template <typename K>
+void allow_lds(K kernel, size_t bytes) {
+  if (bytes > (size_t(64) << 10))
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+}
+
+template <typename In>
+hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, bool init_rep,
+                        void* ws, hipStream_t s, KTimer* timer) {
+  const GroupLayout L = group_layout(n);
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w + L.hist);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + L.tiles);
+  uint4* rec = reinterpret_cast<uint4*>(w + L.rec);
+  uint64_t* gkey = reinterpret_cast<uint64_t*>(w + L.gkey);
+  uint32_t* gmin = reinterpret_cast<uint32_t*>(w + L.gmin);
+  const uint32_t bits = L.bits;
+  const uint32_t P = bucket_part_blocks();
+  const uint64_t nh = (static_cast<uint64_t>(1) << bits) * P;
   const size_t lds = sizeof(uint32_t) << bits;
   {
-    KScope k(timer, hname, s);
-    k_part_hist<<<kPartBlocks, kPartThreads, lds, s>>>(key, valid, n, skip, bits, hist);
+    KScope k(timer, "bucket_hist", s);
+    allow_lds(k_part_hist<In>, lds);
+    k_part_hist<In><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, hist);
   }
   scan::exclusive(hist, nh, hist, tiles, nullptr, s);
-  if (okey) {
-    KScope k(timer, sname, s);
-    k_part_scatter<<<kPartBlocks, kPartThreads, lds, s>>>(key, rank, valid, n, skip, bits, hist,
-                                                          okey, orank, opos);
+  {
+    KScope k(timer, "bucket_scatter", s);
+    const bool staged = bits == kStageBits && !getenv("SDGPU_SCATTER_UNSTAGED");
+    if (staged && init_rep)
+      k_part_scatter_rec_staged<In, true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, hist, rec,
+                                                                     rep);
+    else if (staged)
+      k_part_scatter_rec_staged<In, false><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, hist,
+                                                                      rec, rep);
+    else if (init_rep) {
+      allow_lds(k_part_scatter_rec<In, true>, lds);
+      k_part_scatter_rec<In, true><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, hist, rec,
+                                                                rep);
+    } else {
+      allow_lds(k_part_scatter_rec<In, false>, lds);
+      k_part_scatter_rec<In, false><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, hist,
+                                                                 rec, rep);
+    }
+  }
+  KScope k(timer, "bucket_group", s);
+  k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, chunk_rows, gkey, gmin, rep);
+  return hipGetLastError();
+}
+
+size_t shard_hist_bytes(uint32_t shard_bits) {
+  const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
+  return align_up(4 * (nh + 1), 256);
+}
+
+// Shard histogram + scan (+ scatter when outputs are given) of the caller's rows.
+hipError_t shard_partition(const RowsIn& in, uint64_t n, uint32_t shard_bits, uint32_t* hist,
+                           uint32_t* tiles, uint64_t* okey, uint32_t* orank, uint3* orec,
+                           uint32_t* opos, hipStream_t s, KTimer* timer) {
+  const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
+  const size_t lds = sizeof(uint32_t) << shard_bits;
+  {
+    KScope k(timer, "shard_hist", s);
+    k_part_hist<RowsIn><<<kPartBlocks, kPartThreads, lds, s>>>(in, n, 0, shard_bits, hist);
+  }
+  scan::exclusive(hist, nh, hist, tiles, nullptr, s);
+  if (opos) {
+    KScope k(timer, "shard_scatter", s);
+    if (orec)
+      k_part_scatter<RowsIn, true><<<kPartBlocks, kPartThreads, lds, s>>>(
+          in, n, 0, shard_bits, hist, nullptr, nullptr, orec, opos);
+    else
+      k_part_scatter<RowsIn, false><<<kPartBlocks, kPartThreads, lds, s>>>(
+          in, n, 0, shard_bits, hist, okey, orank, nullptr, opos);
   }
   return hipGetLastError();
 }
@@ -507,54 +595,29 @@ hipError_t partition(const uint64_t* key, const uint8_t* valid, const uint32_t* 
 
 size_t dedup_workspace_bytes(uint64_t n) { return group_layout(n).total; }
 
-hipError_t dedup_local_launch(const uint64_t* key, const uint8_t* has_key, const uint32_t* rank,
-                              uint64_t n, uint32_t chunk_rows, uint32_t shard_bits, uint32_t* rep,
-                              void* ws, hipStream_t s, KTimer* timer) {
-  if (n == 0) return hipSuccess;
-  const GroupLayout L = group_layout(n);
-  uint8_t* w = static_cast<uint8_t*>(ws);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(w + L.hist);
-  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + L.tiles);
-  uint4* rec = reinterpret_cast<uint4*>(w + L.rec);
-  uint64_t* gkey = reinterpret_cast<uint64_t*>(w + L.gkey);
-  uint32_t* gmin = reinterpret_cast<uint32_t*>(w + L.gmin);
-  const uint32_t bits = std::min<uint32_t>(L.bits, 64u - shard_bits);
-  const uint32_t P = bucket_part_blocks();
-  const uint64_t nh = (static_cast<uint64_t>(1) << bits) * P;
-  const size_t lds = sizeof(uint32_t) << bits;
-  {
-    KScope k(timer, "bucket_hist", s);
-    k_part_hist<<<P, kPartThreads, lds, s>>>(key, has_key, n, shard_bits, bits, hist);
-  }
-  scan::exclusive(hist, nh, hist, tiles, nullptr, s);
-  {
-    KScope k(timer, "bucket_scatter", s);
-    if (bits == kStageBits && !getenv("SDGPU_SCATTER_UNSTAGED"))
-      k_part_scatter_rec_staged<<<P, kPartThreads, 0, s>>>(key, rank, has_key, n, shard_bits, hist,
-                                                           rec, rep);
-    else
-      k_part_scatter_rec<<<P, kPartThreads, lds, s>>>(key, rank, has_key, n, shard_bits, bits,
-                                                      hist, rec, rep);
-  }
-  KScope k(timer, "bucket_group", s);
-  k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, chunk_rows, gkey, gmin, rep);
-  return hipGetLastError();
+hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* rep,
+                              bool init_rep, void* ws, hipStream_t s, KTimer* timer) {
+  if (in.n == 0) return hipSuccess;
+  if (in.rec12)
+    return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
+                        chunk_rows, rep, init_rep, ws, s, timer);
+  return group_launch(RowsIn{in.key, in.valid, in.rank, in.rank_base}, in.n, chunk_rows, rep,
+                      init_rep, ws, s, timer);
 }
 
 size_t shard_workspace_bytes(uint32_t shard_bits) {
   const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
-  return align_up(4 * (nh + 1), 256) + align_up(4 * (scan::tiles_for(nh) + 1), 256) +
+  return shard_hist_bytes(shard_bits) + align_up(4 * (scan::tiles_for(nh) + 1), 256) +
          align_up(8 * (static_cast<uint64_t>(1) << shard_bits), 256);
 }
 
 hipError_t shard_count_launch(const uint64_t* key, const uint8_t* has_key, uint64_t n,
                               uint32_t shard_bits, uint64_t* d_counts, void* ws, hipStream_t s) {
   uint8_t* w = static_cast<uint8_t*>(ws);
-  const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
   uint32_t* hist = reinterpret_cast<uint32_t*>(w);
-  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + align_up(4 * (nh + 1), 256));
-  hipError_t e = partition(key, has_key, nullptr, n, 0, shard_bits, hist, tiles, nullptr, nullptr,
-                           nullptr, s, nullptr, "shard_hist", "shard_scatter");
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + shard_hist_bytes(shard_bits));
+  hipError_t e = shard_partition(RowsIn{key, has_key, nullptr, 0}, n, shard_bits, hist, tiles,
+                                 nullptr, nullptr, nullptr, nullptr, s, nullptr);
   if (e != hipSuccess) return e;
   k_copy_counts<<<1, 256, 0, s>>>(hist, 1u << shard_bits, d_counts);
   return hipGetLastError();
@@ -565,24 +628,23 @@ hipError_t shard_partition_launch(const uint64_t* key, const uint8_t* has_key,
                                   uint64_t* out_key, uint32_t* out_rank, uint32_t* out_pos,
                                   void* ws, hipStream_t s, KTimer* timer) {
   uint8_t* w = static_cast<uint8_t*>(ws);
-  const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
   uint32_t* hist = reinterpret_cast<uint32_t*>(w);
-  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + align_up(4 * (nh + 1), 256));
-  return partition(key, has_key, rank, n, 0, shard_bits, hist, tiles, out_key, out_rank, out_pos,
-                   s, timer, "shard_hist", "shard_scatter");
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + shard_hist_bytes(shard_bits));
+  return shard_partition(RowsIn{key, has_key, rank, 0}, n, shard_bits, hist, tiles, out_key,
+                         out_rank, nullptr, out_pos, s, timer);
 }
 
 hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
                                  const uint32_t* rank, uint64_t n, uint32_t shard_bits,
                                  uint32_t world, uint64_t* out_key, uint32_t* out_rank,
-                                 uint32_t* out_pos, int64_t* d_dest_counts, void* ws,
-                                 hipStream_t s, KTimer* timer) {
+                                 uint32_t* out_rec12, uint32_t* out_pos, int64_t* d_dest_counts,
+                                 void* ws, hipStream_t s, KTimer* timer) {
   uint8_t* w = static_cast<uint8_t*>(ws);
-  const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
   uint32_t* hist = reinterpret_cast<uint32_t*>(w);
-  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + align_up(4 * (nh + 1), 256));
-  hipError_t e = partition(key, has_key, rank, n, 0, shard_bits, hist, tiles, out_key, out_rank,
-                           out_pos, s, timer, "shard_hist", "shard_scatter");
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + shard_hist_bytes(shard_bits));
+  hipError_t e = shard_partition(RowsIn{key, has_key, rank, 0}, n, shard_bits, hist, tiles,
+                                 out_key, out_rank, reinterpret_cast<uint3*>(out_rec12), out_pos,
+                                 s, timer);
   if (e != hipSuccess) return e;
   k_dest_counts<<<1, 64, 0, s>>>(hist, shard_bits, world, d_dest_counts);
   return hipGetLastError();

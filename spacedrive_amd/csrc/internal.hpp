@@ -101,15 +101,24 @@ hipError_t synth_dedup_rows_launch(uint64_t seed, uint64_t total_rows, uint64_t 
                                    uint8_t* has_key, uint32_t* rank, hipStream_t s);
 
 // ---- dedup (K4-K6) ------------------------------------------------------------
+// Rows of one grouping call: either the caller's arrays (key[i], valid[i]
+// (null: all keyed), rank[i] (null: rank_base + i)) or packed 12-byte exchange
+// records {key lo, key hi, rank} (rec12, all keyed unless valid is given).
+struct GroupInput {
+  const uint64_t* key = nullptr;
+  const uint32_t* rec12 = nullptr;
+  const uint8_t* valid = nullptr;
+  const uint32_t* rank = nullptr;
+  uint32_t rank_base = 0;
+  uint64_t n = 0;
+};
 size_t dedup_workspace_bytes(uint64_t n);
-// Group (key, rank) pairs; rep[i] for pair i.  Keys' top shard_bits bits are
-// constant on this shard (skipped by the bucket digit).
-// has_key may be null (all rows keyed); rank may be null (rank = row index).
-// Rows without a key get rep = their own rank.
-hipError_t dedup_local_launch(const uint64_t* key, const uint8_t* has_key, const uint32_t* rank,
-                              uint64_t n, uint32_t chunk_rows, uint32_t shard_bits, uint32_t* rep,
-                              void* ws, hipStream_t s, KTimer* timer = nullptr);
+// rep[i] for row i of `in` (the canonical rule over ranks; rows without a key
+// get rep = their rank when init_rep, and are left untouched otherwise).
+hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* rep,
+                              bool init_rep, void* ws, hipStream_t s, KTimer* timer = nullptr);
 size_t shard_workspace_bytes(uint32_t shard_bits);
+// Shard of a key = top shard_bits bits of mix64(key) (rows_device.hpp row_hash).
 hipError_t shard_count_launch(const uint64_t* key, const uint8_t* has_key, uint64_t n,
                               uint32_t shard_bits, uint64_t* d_counts, void* ws, hipStream_t s);
 hipError_t shard_partition_launch(const uint64_t* key, const uint8_t* has_key,
@@ -117,14 +126,36 @@ hipError_t shard_partition_launch(const uint64_t* key, const uint8_t* has_key,
                                   uint64_t* out_key, uint32_t* out_rank, uint32_t* out_pos,
                                   void* ws, hipStream_t s, KTimer* timer = nullptr);
 // partition by shard (one hist + scan + scatter) and, on device, the rows per
-// destination rank (int64[world]); no host synchronisation.
+// destination rank (int64[world]); no host synchronisation.  Output either
+// separate key / rank arrays or packed 12-byte records (out_rec12 non-null).
 hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
                                  const uint32_t* rank, uint64_t n, uint32_t shard_bits,
                                  uint32_t world, uint64_t* out_key, uint32_t* out_rank,
-                                 uint32_t* out_pos, int64_t* d_dest_counts, void* ws,
-                                 hipStream_t s, KTimer* timer = nullptr);
+                                 uint32_t* out_rec12, uint32_t* out_pos, int64_t* d_dest_counts,
+                                 void* ws, hipStream_t s, KTimer* timer = nullptr);
 hipError_t scatter_rep_launch(const uint32_t* src, const uint32_t* pos, uint64_t n, uint32_t* dst,
                               uint64_t n_dst, const uint32_t* init, bool do_init, hipStream_t s);
+
+// ---- Object index (index.hip) -----------------------------------------------------
+// rep values with this bit name a pre-existing Object handle, not a row rank.
+constexpr uint32_t kRepExisting = 0x80000000u;
+struct IndexRef {
+  uint4* slots = nullptr;              // [cap] {key lo, key hi, value, 0}
+  uint64_t cap = 0;                    // power of two
+  unsigned long long* count = nullptr; // distinct keys stored (device)
+  uint32_t* special = nullptr;         // [2]: key ~0 present, its value
+};
+hipError_t index_clear_launch(const IndexRef& t, hipStream_t s);
+hipError_t index_rehash_launch(const IndexRef& from, const IndexRef& to, hipStream_t s);
+hipError_t index_objects_launch(const IndexRef& t, const uint64_t* key, const uint32_t* handle,
+                                uint64_t n, uint32_t world, uint32_t rank, hipStream_t s);
+// rep[i] / valid_out[i] for every row (see index.hip); valid_out = rows left
+// for the batch's own grouping.
+hipError_t index_probe_launch(const IndexRef& t, const GroupInput& in, uint32_t chunk_rows,
+                              uint32_t* rep, uint8_t* valid_out, hipStream_t s,
+                              KTimer* timer = nullptr);
+hipError_t index_creators_launch(const IndexRef& t, const GroupInput& in, const uint32_t* rep,
+                                 const uint8_t* grouped, hipStream_t s, KTimer* timer = nullptr);
 
 // ---- Object link batch (K7) ----------------------------------------------------
 size_t link_workspace_bytes(uint64_t n);

@@ -1020,8 +1020,11 @@ int sdgpu_group_pairs_device(sdgpu_ctx* c, const uint64_t* d_key, const uint32_t
   hipStream_t s = pick(c, stream);
   if (n == 0) return 0;
   SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(n)));
-  SD_TRY(dedup_local_launch(d_key, nullptr, d_rank, n, chunk_rows, skip_bits, d_rep,
-                            c->dedup_ws.p, s, c->kt()));
+  GroupInput in;
+  in.key = d_key;
+  in.rank = d_rank;
+  in.n = n;
+  SD_TRY(dedup_local_launch(in, chunk_rows, d_rep, true, c->dedup_ws.p, s, c->kt()));
   return 0;
 }
 
@@ -1035,8 +1038,12 @@ int sdgpu_group_rows_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8_t* 
   hipStream_t s = pick(c, stream);
   if (n == 0) return 0;
   SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(n)));
-  SD_TRY(dedup_local_launch(d_key, d_has_key, d_rank, n, chunk_rows, skip_bits, d_rep,
-                            c->dedup_ws.p, s, c->kt()));
+  GroupInput in;
+  in.key = d_key;
+  in.valid = d_has_key;
+  in.rank = d_rank;
+  in.n = n;
+  SD_TRY(dedup_local_launch(in, chunk_rows, d_rep, true, c->dedup_ws.p, s, c->kt()));
   return 0;
 }
 
@@ -1084,7 +1091,8 @@ int sdgpu_shard_exchange_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8
   hipStream_t s = pick(c, stream);
   SD_TRY_RC(ensure_dev(c, c->shard_ws, shard_workspace_bytes(shard_bits)));
   SD_TRY(shard_exchange_launch(d_key, d_has_key, d_rank, n, shard_bits, world, d_out_key,
-                               d_out_rank, d_out_pos, d_dest_counts, c->shard_ws.p, s, c->kt()));
+                               d_out_rank, nullptr, d_out_pos, d_dest_counts, c->shard_ws.p, s,
+                               c->kt()));
   return 0;
 }
 

@@ -1,0 +1,643 @@
+// Multi-GPU cas_id -> Object grouping behind the C ABI, and the Object index.
+//
+// Reference: identifier_job_step's grouping (core/src/object/file_identifier/
+// mod.rs:136-333) -- here one library-wide grouping of all rows, hash-sharded
+// over the GPUs of a node: every key has exactly one owner
+// GPU, so the per-owner grouping is complete and independent; the chunk rule
+// needs only the global rank, which travels with the key.
+//
+// One exchange step per call, on each GPU:
+//   1. shard partition of the GPU's rows into packed 12-byte send records
+//      {key lo, key hi, rank} grouped by owner, + per-owner counts (device);
+//   2. all-to-all of the counts (8 B per pair), then ONE host synchronisation
+//      that reads the send / receive counts (they size the payload);
+//   3. all-to-all of the records -- one message per (source, owner) pair;
+//   4. local grouping of the received rows (Object-index probe first when an
+//      index is given, creators inserted after);
+//   5. all-to-all of the reps back to the sources (4 B per row), scatter to
+//      row order (keyless rows keep their own rank).
+// Transports: RCCL (ncclSend / ncclRecv in one group, over xGMI; one process
+// per GPU via sdgpu_comm_init_rank, or one process driving all GPUs via
+// sdgpu_comm_init_all), and, for contexts that share a device (RCCL refuses
+// two ranks on one GPU: the one-GPU test box), device-to-device peer copies
+// ordered by events.  Both move the same buffers in the same pattern.
+#include <string.h>
+
+#include <memory>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "ctx.hpp"
+
+using namespace sdgpu;
+
+struct sdgpu_comm {
+  int nranks = 1;
+  int rank = 0;
+  int transport = SDGPU_TRANSPORT_RCCL;
+  int device = 0;
+  ncclComm_t nccl = nullptr;
+};
+
+struct sdgpu_index {
+  sdgpu_ctx* ctx = nullptr;
+  DevBuf buf;       // [slots cap*16 | count 8 | special 8]
+  IndexRef ref;
+  uint64_t ub = 0;  // host upper bound of the stored key count
+};
+
+namespace {
+
+constexpr uint32_t kXShardBits = 8;  // 256 shards; rank d owns shards s with s*W>>8 == d
+
+int nccl_err(ncclResult_t r) { return r == ncclSuccess ? 0 : -EIO; }
+
+#define SD_NCCL(expr)                          \
+  do {                                         \
+    const int rc_ = nccl_err(expr);            \
+    if (rc_ != 0) return rc_;                  \
+  } while (0)
+
+// ---- Object index ------------------------------------------------------------
+
+int index_alloc(sdgpu_ctx* c, DevBuf& b, uint64_t cap, IndexRef& r) {
+  const size_t bytes = 16 * cap + 16;
+  void* p = nullptr;
+  SD_TRY(hipMalloc(&p, bytes));
+  b.p = p;
+  b.cap = bytes;
+  r.slots = static_cast<uint4*>(p);
+  r.cap = cap;
+  r.count = reinterpret_cast<unsigned long long*>(static_cast<uint8_t*>(p) + 16 * cap);
+  r.special = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(p) + 16 * cap + 8);
+  (void)c;
+  return 0;
+}
+
+uint64_t pow2_at_least(uint64_t x) {
+  uint64_t p = 1024;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// Make room for `add` more keys at load <= 1/2.  The exact count is read (one
+// synchronisation of s) only when the host-side upper bound says it may not fit.
+int index_reserve(sdgpu_index* x, uint64_t add, hipStream_t s) {
+  if (x->ub + add <= x->ref.cap / 2) {
+    x->ub += add;
+    return 0;
+  }
+  unsigned long long cnt = 0;
+  SD_TRY(hipMemcpyAsync(&cnt, x->ref.count, 8, hipMemcpyDeviceToHost, s));
+  SD_TRY(hipStreamSynchronize(s));
+  if (cnt + add > x->ref.cap / 2) {
+    DevBuf nb;
+    IndexRef nr;
+    SD_TRY_RC(index_alloc(x->ctx, nb, pow2_at_least(4 * (cnt + add)), nr));
+    SD_TRY(index_rehash_launch(x->ref, nr, s));
+    SD_TRY(hipStreamSynchronize(s));
+    (void)hipFree(x->buf.p);
+    x->buf = nb;
+    x->ref = nr;
+  }
+  x->ub = cnt + add;
+  return 0;
+}
+
+// Grouping of one GPU's rows (`in`) with optional Object index: probe, group
+// the rest, insert the creators.  rep[i] for every row.
+int group_with_index(sdgpu_ctx* c, sdgpu_index* idx, GroupInput in, uint32_t chunk_rows,
+                     uint32_t* rep, uint8_t* valid_scratch, hipStream_t s) {
+  if (in.n == 0) return 0;
+  SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(in.n)));
+  if (!idx) {
+    SD_TRY(dedup_local_launch(in, chunk_rows, rep, true, c->dedup_ws.p, s, c->kt()));
+    return 0;
+  }
+  SD_TRY_RC(index_reserve(idx, in.n, s));
+  SD_TRY(index_probe_launch(idx->ref, in, chunk_rows, rep, valid_scratch, s, c->kt()));
+  GroupInput g = in;
+  g.valid = valid_scratch;
+  SD_TRY(dedup_local_launch(g, chunk_rows, rep, false, c->dedup_ws.p, s, c->kt()));
+  SD_TRY(index_creators_launch(idx->ref, in, rep, valid_scratch, s, c->kt()));
+  return 0;
+}
+
+// ---- the sharded grouping engine ------------------------------------------------
+
+struct RankJob {
+  sdgpu_ctx* c = nullptr;
+  sdgpu_comm* comm = nullptr;
+  sdgpu_index* idx = nullptr;
+  hipStream_t s = nullptr;
+  const uint64_t* key = nullptr;
+  const uint8_t* has = nullptr;
+  const uint32_t* rank = nullptr;
+  uint64_t n = 0;
+  uint32_t* rep = nullptr;
+  // device workspace
+  uint32_t* srec = nullptr;   // [n][3]
+  uint32_t* spos = nullptr;   // [n]
+  int64_t* dcnt = nullptr;    // [W] rows to each owner
+  int64_t* rcnt_d = nullptr;  // [W] rows from each source
+  uint32_t* rrec = nullptr;   // [m][3]
+  uint32_t* rrep = nullptr;   // [m]
+  uint8_t* rvalid = nullptr;  // [m]
+  uint32_t* back = nullptr;   // [total] reps of the sent rows, in send order
+  int64_t* h = nullptr;       // pinned [2W]: send counts, receive counts
+  std::vector<uint64_t> scnt, rcnt, soff, roff;
+  uint64_t total = 0, m = 0;
+};
+
+// One all-to-all round: rank j sends bytes(j, p) from sendp(j, p) to every p
+// and receives rbytes(j, p) into recvp(j, p) from every p.
+template <typename SP, typename RP, typename SB, typename RB>
+int alltoallv(std::vector<RankJob>& J, int W, SP sendp, RP recvp, SB sbytes, RB rbytes) {
+  const int transport = J[0].comm->transport;
+  if (transport == SDGPU_TRANSPORT_RCCL) {
+    SD_NCCL(ncclGroupStart());
+    for (auto& j : J) {
+      for (int p = 0; p < W; ++p) {
+        SD_NCCL(ncclSend(sendp(j, p), sbytes(j, p), ncclUint8, p, j.comm->nccl, j.s));
+        SD_NCCL(ncclRecv(recvp(j, p), rbytes(j, p), ncclUint8, p, j.comm->nccl, j.s));
+      }
+    }
+    SD_NCCL(ncclGroupEnd());
+    return 0;
+  }
+  // peer copies: all ranks live in this process (J holds every rank, J[r] is rank r)
+  if (static_cast<int>(J.size()) != W) return -EINVAL;
+  std::vector<hipEvent_t> ready(W), done(W);
+  int rc = 0;
+  for (int r = 0; r < W && rc == 0; ++r) {
+    if (hipEventCreateWithFlags(&ready[r], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&done[r], hipEventDisableTiming) != hipSuccess)
+      rc = -EIO;
+  }
+  for (int r = 0; r < W && rc == 0; ++r)
+    if (hipEventRecord(ready[r], J[r].s) != hipSuccess) rc = -EIO;
+  for (int d = 0; d < W && rc == 0; ++d) {  // receiver d pulls from every source
+    RankJob& jd = J[d];
+    for (int src = 0; src < W && rc == 0; ++src) {
+      const size_t b = rbytes(jd, src);
+      if (b != sbytes(J[src], d)) {
+        rc = -EPROTO;
+        break;
+      }
+      if (hipStreamWaitEvent(jd.s, ready[src], 0) != hipSuccess) rc = -EIO;
+      if (rc == 0 && b &&
+          hipMemcpyPeerAsync(recvp(jd, src), jd.c->device, sendp(J[src], d), J[src].c->device, b,
+                             jd.s) != hipSuccess)
+        rc = -EIO;
+    }
+    if (rc == 0 && hipEventRecord(done[d], jd.s) != hipSuccess) rc = -EIO;
+  }
+  // a source may reuse its send buffer only after every receiver copied it
+  for (int src = 0; src < W && rc == 0; ++src)
+    for (int d = 0; d < W && rc == 0; ++d)
+      if (hipStreamWaitEvent(J[src].s, done[d], 0) != hipSuccess) rc = -EIO;
+  for (int r = 0; r < W; ++r) {
+    if (ready[r]) (void)hipEventDestroy(ready[r]);
+    if (done[r]) (void)hipEventDestroy(done[r]);
+  }
+  return rc;
+}
+
+int run_sharded(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
+  // 1. send side: packed records by owner + per-owner counts, on each GPU
+  for (auto& j : J) {
+    SD_TRY(hipSetDevice(j.c->device));
+    const uint64_t n = j.n;
+    const size_t o_pos = align_up(12 * n, 256);
+    const size_t o_dcnt = align_up(o_pos + 4 * n, 256);
+    const size_t o_rcnt = align_up(o_dcnt + 8ull * W, 256);
+    SD_TRY_RC(ensure_dev(j.c, j.c->xs_send, o_rcnt + 8ull * W));
+    SD_TRY_RC(ensure_dev(j.c, j.c->shard_ws, shard_workspace_bytes(kXShardBits)));
+    SD_TRY_RC(ensure_pin(j.c->xs_counts, 16ull * W));
+    uint8_t* b = static_cast<uint8_t*>(j.c->xs_send.p);
+    j.srec = reinterpret_cast<uint32_t*>(b);
+    j.spos = reinterpret_cast<uint32_t*>(b + o_pos);
+    j.dcnt = reinterpret_cast<int64_t*>(b + o_dcnt);
+    j.rcnt_d = reinterpret_cast<int64_t*>(b + o_rcnt);
+    j.h = static_cast<int64_t*>(j.c->xs_counts.p);
+    SD_TRY(shard_exchange_launch(j.key, j.has, j.rank, n, kXShardBits, W, nullptr, nullptr,
+                                 j.srec, j.spos, j.dcnt, j.c->shard_ws.p, j.s, j.c->kt()));
+  }
+  // 2. counts all-to-all, then the one host synchronisation
+  SD_TRY_RC(alltoallv(
+      J, W, [](RankJob& j, int p) -> void* { return j.dcnt + p; },
+      [](RankJob& j, int p) -> void* { return j.rcnt_d + p; },
+      [](RankJob&, int) -> size_t { return 8; }, [](RankJob&, int) -> size_t { return 8; }));
+  for (auto& j : J) {
+    SD_TRY(hipSetDevice(j.c->device));
+    SD_TRY(hipMemcpyAsync(j.h, j.dcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
+    SD_TRY(hipMemcpyAsync(j.h + W, j.rcnt_d, 8ull * W, hipMemcpyDeviceToHost, j.s));
+  }
+  for (auto& j : J) {
+    SD_TRY(hipSetDevice(j.c->device));
+    SD_TRY(hipStreamSynchronize(j.s));
+    j.scnt.assign(W, 0);
+    j.rcnt.assign(W, 0);
+    j.soff.assign(W + 1, 0);
+    j.roff.assign(W + 1, 0);
+    for (int p = 0; p < W; ++p) {
+      if (j.h[p] < 0 || j.h[W + p] < 0) return -EPROTO;
+      j.scnt[p] = static_cast<uint64_t>(j.h[p]);
+      j.rcnt[p] = static_cast<uint64_t>(j.h[W + p]);
+      j.soff[p + 1] = j.soff[p] + j.scnt[p];
+      j.roff[p + 1] = j.roff[p] + j.rcnt[p];
+    }
+    j.total = j.soff[W];
+    j.m = j.roff[W];
+    if (j.total > j.n || j.m >= (1ull << 32)) return -EPROTO;
+    const size_t o_rep = align_up(12 * j.m, 256);
+    const size_t o_val = align_up(o_rep + 4 * j.m, 256);
+    SD_TRY_RC(ensure_dev(j.c, j.c->xs_recv, o_val + j.m + 256));
+    SD_TRY_RC(ensure_dev(j.c, j.c->xs_back, 4 * j.total + 256));
+    uint8_t* r = static_cast<uint8_t*>(j.c->xs_recv.p);
+    j.rrec = reinterpret_cast<uint32_t*>(r);
+    j.rrep = reinterpret_cast<uint32_t*>(r + o_rep);
+    j.rvalid = r + o_val;
+    j.back = static_cast<uint32_t*>(j.c->xs_back.p);
+  }
+  // 3. the rows, one message per (source, owner) pair
+  SD_TRY_RC(alltoallv(
+      J, W, [](RankJob& j, int p) -> void* { return j.srec + 3 * j.soff[p]; },
+      [](RankJob& j, int p) -> void* { return j.rrec + 3 * j.roff[p]; },
+      [](RankJob& j, int p) -> size_t { return 12 * j.scnt[p]; },
+      [](RankJob& j, int p) -> size_t { return 12 * j.rcnt[p]; }));
+  // 4. local grouping of the received rows (every key's rows are all here)
+  for (auto& j : J) {
+    SD_TRY(hipSetDevice(j.c->device));
+    GroupInput in;
+    in.rec12 = j.rrec;
+    in.n = j.m;
+    SD_TRY_RC(group_with_index(j.c, j.idx, in, chunk_rows, j.rrep, j.rvalid, j.s));
+  }
+  // 5. reps back to their sources, scatter to row order
+  SD_TRY_RC(alltoallv(
+      J, W, [](RankJob& j, int p) -> void* { return j.rrep + j.roff[p]; },
+      [](RankJob& j, int p) -> void* { return j.back + j.soff[p]; },
+      [](RankJob& j, int p) -> size_t { return 4 * j.rcnt[p]; },
+      [](RankJob& j, int p) -> size_t { return 4 * j.scnt[p]; }));
+  for (auto& j : J) {
+    SD_TRY(hipSetDevice(j.c->device));
+    SD_TRY(scatter_rep_launch(j.back, j.spos, j.total, j.rep, j.n, j.rank, true, j.s));
+  }
+  return 0;
+}
+
+bool same_devices(sdgpu_ctx* const* ctx, int ngpu) {
+  for (int a = 0; a < ngpu; ++a)
+    for (int b = a + 1; b < ngpu; ++b)
+      if (ctx[a]->device == ctx[b]->device) return true;
+  return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---- communicators -----------------------------------------------------------------
+
+int sdgpu_comm_unique_id(uint8_t id[SDGPU_COMM_ID_BYTES]) {
+  if (!id) return -EINVAL;
+  static_assert(sizeof(ncclUniqueId) == SDGPU_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId u;
+  SD_NCCL(ncclGetUniqueId(&u));
+  memcpy(id, &u, sizeof u);
+  return 0;
+}
+
+int sdgpu_comm_init_rank(sdgpu_ctx* c, int nranks, int rank, const uint8_t id[SDGPU_COMM_ID_BYTES],
+                         sdgpu_comm** out) {
+  if (!c || !id || !out || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks)
+    return -EINVAL;
+  *out = nullptr;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  ncclComm_t nc = nullptr;
+  SD_NCCL(ncclCommInitRank(&nc, nranks, u, rank));
+  sdgpu_comm* m = new (std::nothrow) sdgpu_comm;
+  if (!m) {
+    (void)ncclCommDestroy(nc);
+    return -ENOMEM;
+  }
+  m->nranks = nranks;
+  m->rank = rank;
+  m->transport = SDGPU_TRANSPORT_RCCL;
+  m->device = c->device;
+  m->nccl = nc;
+  *out = m;
+  return 0;
+}
+
+int sdgpu_comm_init_all(sdgpu_ctx* const* ctx, int ngpu, int transport, sdgpu_comm** out) {
+  if (!ctx || !out || ngpu < 1 || ngpu > 64) return -EINVAL;
+  for (int i = 0; i < ngpu; ++i)
+    if (!ctx[i]) return -EINVAL;
+  const bool dup = same_devices(ctx, ngpu);
+  if (transport == SDGPU_TRANSPORT_AUTO)
+    transport = dup ? SDGPU_TRANSPORT_PEER : SDGPU_TRANSPORT_RCCL;
+  if (transport == SDGPU_TRANSPORT_RCCL && dup) return -EINVAL;  // RCCL: one rank per GPU
+  if (transport != SDGPU_TRANSPORT_RCCL && transport != SDGPU_TRANSPORT_PEER) return -EINVAL;
+  std::vector<ncclComm_t> nc(ngpu, nullptr);
+  if (transport == SDGPU_TRANSPORT_RCCL) {
+    std::vector<int> devs(ngpu);
+    for (int i = 0; i < ngpu; ++i) devs[i] = ctx[i]->device;
+    SD_NCCL(ncclCommInitAll(nc.data(), ngpu, devs.data()));
+  } else {
+    for (int a = 0; a < ngpu; ++a)  // direct xGMI copies where the devices allow it
+      for (int b = 0; b < ngpu; ++b)
+        if (ctx[a]->device != ctx[b]->device) {
+          (void)hipSetDevice(ctx[a]->device);
+          (void)hipDeviceEnablePeerAccess(ctx[b]->device, 0);
+          (void)hipGetLastError();
+        }
+  }
+  for (int i = 0; i < ngpu; ++i) {
+    sdgpu_comm* m = new (std::nothrow) sdgpu_comm;
+    if (!m) return -ENOMEM;
+    m->nranks = ngpu;
+    m->rank = i;
+    m->transport = transport;
+    m->device = ctx[i]->device;
+    m->nccl = nc[i];
+    out[i] = m;
+  }
+  return 0;
+}
+
+int sdgpu_comm_destroy(sdgpu_comm* m) {
+  if (!m) return -EINVAL;
+  if (m->nccl) {
+    (void)hipSetDevice(m->device);
+    (void)ncclCommDestroy(m->nccl);
+  }
+  delete m;
+  return 0;
+}
+
+int sdgpu_comm_info(sdgpu_comm* m, int* nranks, int* rank, int* transport) {
+  if (!m) return -EINVAL;
+  if (nranks) *nranks = m->nranks;
+  if (rank) *rank = m->rank;
+  if (transport) *transport = m->transport;
+  return 0;
+}
+
+// ---- Object index --------------------------------------------------------------------
+
+int sdgpu_index_create(sdgpu_ctx* c, uint64_t capacity_hint, sdgpu_index** out) {
+  if (!c || !out) return -EINVAL;
+  *out = nullptr;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  sdgpu_index* x = new (std::nothrow) sdgpu_index;
+  if (!x) return -ENOMEM;
+  x->ctx = c;
+  int rc = index_alloc(c, x->buf, pow2_at_least(2 * std::max<uint64_t>(capacity_hint, 1)), x->ref);
+  if (rc == 0 && index_clear_launch(x->ref, c->stream) != hipSuccess) rc = -EIO;
+  if (rc == 0 && hipStreamSynchronize(c->stream) != hipSuccess) rc = -EIO;
+  if (rc) {
+    if (x->buf.p) (void)hipFree(x->buf.p);
+    delete x;
+    return rc;
+  }
+  *out = x;
+  return 0;
+}
+
+int sdgpu_index_destroy(sdgpu_index* x) {
+  if (!x) return -EINVAL;
+  {
+    std::lock_guard<std::mutex> g(x->ctx->mu);
+    (void)hipSetDevice(x->ctx->device);
+    (void)hipStreamSynchronize(x->ctx->stream);
+    if (x->ctx->last) (void)hipStreamSynchronize(x->ctx->last);
+    if (x->buf.p) (void)hipFree(x->buf.p);
+  }
+  delete x;
+  return 0;
+}
+
+int sdgpu_index_clear(sdgpu_index* x, void* stream) {
+  if (!x) return -EINVAL;
+  std::lock_guard<std::mutex> g(x->ctx->mu);
+  SD_TRY(hipSetDevice(x->ctx->device));
+  SD_TRY(index_clear_launch(x->ref, pick(x->ctx, stream)));
+  x->ub = 0;
+  return 0;
+}
+
+int sdgpu_index_count(sdgpu_index* x, uint64_t* count) {
+  if (!x || !count) return -EINVAL;
+  std::lock_guard<std::mutex> g(x->ctx->mu);
+  SD_TRY(hipSetDevice(x->ctx->device));
+  hipStream_t s = pick(x->ctx, nullptr);
+  unsigned long long cnt = 0;
+  uint32_t sp[2] = {0, 0};
+  SD_TRY(hipMemcpyAsync(&cnt, x->ref.count, 8, hipMemcpyDeviceToHost, s));
+  SD_TRY(hipMemcpyAsync(sp, x->ref.special, 8, hipMemcpyDeviceToHost, s));
+  SD_TRY(hipStreamSynchronize(s));
+  *count = cnt + (sp[0] ? 1 : 0);
+  return 0;
+}
+
+int sdgpu_index_add_objects_device(sdgpu_index* x, const uint64_t* d_key, const uint32_t* d_handle,
+                                   uint64_t n, uint32_t world, uint32_t rank, void* stream) {
+  if (!x || (n && (!d_key || !d_handle)) || world == 0 || world > 64 || rank >= world)
+    return -EINVAL;
+  std::lock_guard<std::mutex> g(x->ctx->mu);
+  SD_TRY(hipSetDevice(x->ctx->device));
+  hipStream_t s = pick(x->ctx, stream);
+  SD_TRY_RC(index_reserve(x, n, s));
+  SD_TRY(index_objects_launch(x->ref, d_key, d_handle, n, world, rank, s));
+  return 0;
+}
+
+int sdgpu_group_rows_indexed_device(sdgpu_ctx* c, sdgpu_index* x, const uint64_t* d_key,
+                                    const uint8_t* d_has_key, const uint32_t* d_rank, uint64_t n,
+                                    uint32_t chunk_rows, uint32_t* d_rep, void* stream) {
+  if (!c || !x || x->ctx->device != c->device || chunk_rows == 0 ||
+      (n && (!d_key || !d_rep)))
+    return -EINVAL;
+  if (n >= (1ull << 32)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  if (n == 0) return 0;
+  SD_TRY_RC(ensure_dev(c, c->xs_recv, n + 256));  // the probe's valid mask
+  GroupInput in;
+  in.key = d_key;
+  in.valid = d_has_key;
+  in.rank = d_rank;
+  in.n = n;
+  return group_with_index(c, x, in, chunk_rows, d_rep, static_cast<uint8_t*>(c->xs_recv.p), s);
+}
+
+int sdgpu_dedup_batch(sdgpu_ctx* c, sdgpu_index* x, const uint64_t* key, const uint8_t* has_key,
+                      uint32_t first_rank, uint32_t n, uint32_t chunk_rows, uint32_t* rep) {
+  if (!c || chunk_rows == 0 || (n && (!key || !has_key || !rep))) return -EINVAL;
+  if (n == 0) return 0;
+  if (static_cast<uint64_t>(first_rank) + n > kRepExisting) return -EINVAL;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    SD_TRY(hipSetDevice(c->device));
+  }
+  const size_t o_has = align_up(8ull * n, 256), o_rank = align_up(o_has + n, 256),
+               o_rep = align_up(o_rank + 4ull * n, 256), total = align_up(o_rep + 4ull * n, 256);
+  uint8_t* d = nullptr;
+  if (hipMalloc(&d, total) != hipSuccess) return -ENOMEM;
+  std::vector<uint32_t> rank(n);
+  for (uint32_t i = 0; i < n; ++i) rank[i] = first_rank + i;
+  hipStream_t s = c->stream;
+  int rc = 0;
+  do {
+    if (hipMemcpyAsync(d, key, 8ull * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d + o_has, has_key, n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d + o_rank, rank.data(), 4ull * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = -EIO;
+      break;
+    }
+    const uint64_t* dk = reinterpret_cast<const uint64_t*>(d);
+    const uint32_t* dr = reinterpret_cast<const uint32_t*>(d + o_rank);
+    uint32_t* drep = reinterpret_cast<uint32_t*>(d + o_rep);
+    rc = x ? sdgpu_group_rows_indexed_device(c, x, dk, d + o_has, dr, n, chunk_rows, drep, s)
+           : sdgpu_group_rows_device(c, dk, d + o_has, dr, n, chunk_rows, 0, drep, s);
+    if (rc) break;
+    if (hipMemcpyAsync(rep, drep, 4ull * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = -EIO;
+  } while (false);
+  (void)hipStreamSynchronize(s);
+  (void)hipFree(d);
+  return rc;
+}
+
+// ---- sharded grouping ----------------------------------------------------------------
+
+int sdgpu_group_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, sdgpu_index* x,
+                               const uint64_t* d_key, const uint8_t* d_has_key,
+                               const uint32_t* d_rank, uint64_t n, uint32_t chunk_rows,
+                               uint32_t* d_rep, void* stream) {
+  if (!c || !comm || chunk_rows == 0 || (n && (!d_key || !d_rank || !d_rep))) return -EINVAL;
+  if (comm->device != c->device || (x && x->ctx->device != c->device)) return -EINVAL;
+  if (comm->transport != SDGPU_TRANSPORT_RCCL) return -EINVAL;  // peer: sdgpu_group_sharded_all_device
+  if (n >= (1ull << 32)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  std::vector<RankJob> J(1);
+  RankJob& j = J[0];
+  j.c = c;
+  j.comm = comm;
+  j.idx = x;
+  j.s = pick(c, stream);
+  j.key = d_key;
+  j.has = d_has_key;
+  j.rank = d_rank;
+  j.n = n;
+  j.rep = d_rep;
+  return run_sharded(J, comm->nranks, chunk_rows);
+}
+
+int sdgpu_group_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* comm,
+                                   sdgpu_index* const* idx, int ngpu,
+                                   const uint64_t* const* d_key, const uint8_t* const* d_has_key,
+                                   const uint32_t* const* d_rank, const uint64_t* n,
+                                   uint32_t chunk_rows, uint32_t* const* d_rep,
+                                   void* const* streams) {
+  if (!ctx || !comm || ngpu < 1 || ngpu > 64 || !d_key || !d_rank || !n || !d_rep ||
+      chunk_rows == 0)
+    return -EINVAL;
+  std::vector<RankJob> J(ngpu);
+  for (int r = 0; r < ngpu; ++r) {
+    if (!ctx[r] || !comm[r] || comm[r]->nranks != ngpu || comm[r]->rank != r ||
+        comm[r]->device != ctx[r]->device || comm[r]->transport != comm[0]->transport)
+      return -EINVAL;
+    if (n[r] && (!d_key[r] || !d_rank[r] || !d_rep[r])) return -EINVAL;
+    if (n[r] >= (1ull << 32)) return -EINVAL;
+    if (idx && idx[r] && idx[r]->ctx->device != ctx[r]->device) return -EINVAL;
+  }
+  // contexts may repeat a device (peer transport on one GPU); lock each once
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (int r = 0; r < ngpu; ++r) {
+    bool seen = false;
+    for (int q = 0; q < r; ++q) seen |= ctx[q] == ctx[r];
+    if (!seen) locks.emplace_back(ctx[r]->mu);
+  }
+  for (int r = 0; r < ngpu; ++r) {
+    for (int q = 0; q < r; ++q)
+      if (ctx[q] == ctx[r]) return -EINVAL;  // one context per rank: workspaces are per context
+    RankJob& j = J[r];
+    j.c = ctx[r];
+    j.comm = comm[r];
+    j.idx = idx ? idx[r] : nullptr;
+    SD_TRY(hipSetDevice(ctx[r]->device));
+    j.s = pick(ctx[r], streams ? streams[r] : nullptr);
+    j.key = d_key[r];
+    j.has = d_has_key ? d_has_key[r] : nullptr;
+    j.rank = d_rank[r];
+    j.n = n[r];
+    j.rep = d_rep[r];
+  }
+  return run_sharded(J, ngpu, chunk_rows);
+}
+
+int sdgpu_dedup_sharded(sdgpu_ctx* const* ctx, int ngpu, const uint64_t* key,
+                        const uint8_t* has_key, uint32_t n, uint32_t chunk_rows, uint32_t* rep) {
+  if (!ctx || ngpu < 1 || ngpu > 64 || chunk_rows == 0 || (n && (!key || !has_key || !rep)))
+    return -EINVAL;
+  if (n == 0) return 0;
+  if (n >= kRepExisting) return -EINVAL;
+  std::vector<sdgpu_comm*> comm(ngpu, nullptr);
+  SD_TRY_RC(sdgpu_comm_init_all(ctx, ngpu, SDGPU_TRANSPORT_AUTO, comm.data()));
+  // rows split in ngpu contiguous ranges; rank = global row index
+  std::vector<uint64_t> cnt(ngpu), first(ngpu);
+  std::vector<uint8_t*> buf(ngpu, nullptr);
+  std::vector<const uint64_t*> dk(ngpu);
+  std::vector<const uint8_t*> dh(ngpu);
+  std::vector<const uint32_t*> dr(ngpu);
+  std::vector<uint32_t*> drep(ngpu);
+  int rc = 0;
+  for (int r = 0; r < ngpu && rc == 0; ++r) {
+    first[r] = static_cast<uint64_t>(n) * r / ngpu;
+    cnt[r] = static_cast<uint64_t>(n) * (r + 1) / ngpu - first[r];
+    const uint64_t m = std::max<uint64_t>(cnt[r], 1);
+    const size_t o_has = align_up(8 * m, 256), o_rank = align_up(o_has + m, 256),
+                 o_rep = align_up(o_rank + 4 * m, 256), tot = align_up(o_rep + 4 * m, 256);
+    if (hipSetDevice(ctx[r]->device) != hipSuccess || hipMalloc(&buf[r], tot) != hipSuccess) {
+      rc = -ENOMEM;
+      break;
+    }
+    std::vector<uint32_t> rk(cnt[r]);
+    for (uint64_t i = 0; i < cnt[r]; ++i) rk[i] = static_cast<uint32_t>(first[r] + i);
+    dk[r] = reinterpret_cast<const uint64_t*>(buf[r]);
+    dh[r] = buf[r] + o_has;
+    dr[r] = reinterpret_cast<const uint32_t*>(buf[r] + o_rank);
+    drep[r] = reinterpret_cast<uint32_t*>(buf[r] + o_rep);
+    if (hipMemcpy(buf[r], key + first[r], 8 * cnt[r], hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(buf[r] + o_has, has_key + first[r], cnt[r], hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(buf[r] + o_rank, rk.data(), 4 * cnt[r], hipMemcpyHostToDevice) != hipSuccess)
+      rc = -EIO;
+  }
+  if (rc == 0)
+    rc = sdgpu_group_sharded_all_device(ctx, comm.data(), nullptr, ngpu, dk.data(), dh.data(),
+                                        dr.data(), cnt.data(), chunk_rows, drep.data(), nullptr);
+  for (int r = 0; r < ngpu; ++r) {
+    if (!buf[r]) continue;
+    (void)hipSetDevice(ctx[r]->device);
+    (void)hipStreamSynchronize(ctx[r]->stream);
+    if (rc == 0 && hipMemcpy(rep + first[r], drep[r], 4 * cnt[r], hipMemcpyDeviceToHost) != hipSuccess)
+      rc = -EIO;
+    (void)hipFree(buf[r]);
+  }
+  for (auto* m : comm)
+    if (m) (void)sdgpu_comm_destroy(m);
+  return rc;
+}
+
+}  // extern "C"

@@ -6,17 +6,18 @@ canonical rule of SURVEY.md §8 a6 (see include/sdgpu.h, sdgpu_dedup):
 rep[r] = r for rows without a key and for rows in the chunk of their key's
 lowest-rank row f; rep[r] = f otherwise.
 
-Multi-GPU (one process per GPU, torch.distributed over RCCL/xGMI): rows are
-hash-partitioned by the top 8 bits of the cas key (256 shards, shard s owned
-by rank s*W//256), exchanged by all-to-all of (key, rank), grouped locally
-(the chunk rule only needs the global rank carried in the payload) and the
-representatives return with a second all-to-all.  The exchange logic below is
-backend-agnostic (`ops`), so it is tested with gloo on CPU; the product ops are
-the HIP kernels of libsdgpu.
+Multi-GPU: rows are hash-partitioned by the top 8 bits of mix64(key) (256
+shards, shard s owned by rank s*W//256), exchanged by all-to-all of (key,
+rank), grouped locally (the chunk rule only needs the global rank carried in
+the payload) and the representatives return with a second all-to-all.  The
+product path runs the whole exchange inside libsdgpu over RCCL
+(group_sharded / group_sharded_all / dedup_sharded: sdgpu_group_sharded_*),
+callable from the Rust host.  `sharded_group_reps` below is the same
+algorithm over a pluggable exchange (torch.distributed, gloo in the CPU tests)
+built from libsdgpu's single steps.
 """
 from __future__ import annotations
 
-import math
 
 import numpy as np
 
@@ -123,13 +124,14 @@ class HipOps:
 
 
 def shard_plan(world: int):
-    """(shard_bits, owner-of-shard array, skip_bits) for `world` ranks."""
+    """(shard_bits, owner-of-shard array, skip_bits) for `world` ranks.  Shards
+    are the top 8 bits of mix64(key) (shard_of); skip_bits is kept for the ABI
+    and unused (bucket digits are hash bits below the shard byte)."""
     if world <= 1:
         return 0, np.zeros(1, np.int64), 0
     bits = 8
     owner = (np.arange(1 << bits, dtype=np.int64) * world) >> bits
-    skip = int(math.floor(math.log2(world)))
-    return bits, owner, skip
+    return bits, owner, 0
 
 
 class TorchDistExchange:
@@ -188,6 +190,200 @@ def sharded_group_reps(key, has_key, rank, chunk_rows: int = CHUNK_SIZE, group=N
     rep_sent = torch.empty(total, dtype=torch.int32, device=dev)
     exchange.all_to_all(rep_sent, rrep, s_list, r_list)
     return ops.scatter(rep_sent, spos, n, rank)
+
+
+# ---- Object index (objects that exist before a batch) -------------------------
+
+REP_EXISTING = 0x80000000  # include/sdgpu.h SDGPU_REP_EXISTING
+
+
+class ObjectIndex:
+    """Device hash table of cas key -> Object (sdgpu_index_*): the library-wide
+    lookup of identifier_job_step (file_identifier/mod.rs:168-185).  Values are
+    ranks of rows that created an Object in an earlier batch of the run, or
+    REP_EXISTING | handle for Objects registered with add_objects."""
+
+    def __init__(self, ctx=None, capacity: int = 1 << 20):
+        import ctypes
+        self.ctx = ctx or default_context()
+        h = ctypes.c_void_p()
+        check(self.ctx.lib.sdgpu_index_create(self.ctx.h, capacity, ctypes.byref(h)),
+              "sdgpu_index_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.sdgpu_index_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def count(self) -> int:
+        import ctypes
+        c = ctypes.c_uint64()
+        check(self.ctx.lib.sdgpu_index_count(self.h, ctypes.byref(c)), "sdgpu_index_count")
+        return c.value
+
+    def clear(self, stream=None):
+        check(self.ctx.lib.sdgpu_index_clear(self.h, stream), "sdgpu_index_clear")
+
+    def add_objects(self, key, handle, world: int = 1, rank: int = 0):
+        """Pre-existing Objects (device tensors: int64 keys, int32 handles <
+        2^31); with world > 1 only this rank's shards are kept."""
+        import torch
+        s = torch.cuda.current_stream(key.device).cuda_stream
+        check(self.ctx.lib.sdgpu_index_add_objects_device(
+            self.h, key.data_ptr(), handle.data_ptr(), key.numel(), world, rank, s),
+            "sdgpu_index_add_objects_device")
+
+
+def group_rows_indexed(key, has_key, rank, index: ObjectIndex, chunk_rows: int = CHUNK_SIZE):
+    """rep (int32, device) of one batch of rows against `index`, which then
+    also holds the batch's new Objects (sdgpu_group_rows_indexed_device)."""
+    import torch
+    ctx = index.ctx
+    rep = torch.empty(key.numel(), dtype=torch.int32, device=key.device)
+    s = torch.cuda.current_stream(key.device).cuda_stream
+    check(ctx.lib.sdgpu_group_rows_indexed_device(
+        ctx.h, index.h, key.data_ptr(), has_key.data_ptr() if has_key is not None else None,
+        rank.data_ptr() if rank is not None else None, key.numel(), chunk_rows, rep.data_ptr(), s),
+        "sdgpu_group_rows_indexed_device")
+    return rep
+
+
+def dedup_batch(key, has_key, first_rank: int, index: ObjectIndex | None = None,
+                chunk_rows: int = CHUNK_SIZE, ctx=None) -> np.ndarray:
+    """Host arrays: rep of one batch (ranks first_rank + i) via sdgpu_dedup_batch."""
+    ctx = ctx or (index.ctx if index is not None else default_context())
+    key = np.ascontiguousarray(key, np.uint64)
+    has_key = np.ascontiguousarray(has_key, np.uint8)
+    rep = np.zeros(key.size, np.uint32)
+    check(ctx.lib.sdgpu_dedup_batch(ctx.h, index.h if index is not None else None,
+                                    key.ctypes.data, has_key.ctypes.data, first_rank, key.size,
+                                    chunk_rows, rep.ctypes.data), "sdgpu_dedup_batch")
+    return rep
+
+
+# ---- multi-GPU grouping inside libsdgpu (RCCL / peer transport) -----------------
+
+TRANSPORT_AUTO, TRANSPORT_RCCL, TRANSPORT_PEER = 0, 1, 2
+
+
+class Comm:
+    """A libsdgpu communicator (sdgpu_comm_*)."""
+
+    def __init__(self, ctx, handle):
+        self.ctx, self.h = ctx, handle
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+        buf = (ctypes.c_uint8 * 128)()
+        check(default_context().lib.sdgpu_comm_unique_id(buf), "sdgpu_comm_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def init_rank(cls, ctx, nranks: int, rank: int, uid: bytes) -> "Comm":
+        """One process per GPU (RCCL): every rank joins with rank 0's id."""
+        import ctypes
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        check(ctx.lib.sdgpu_comm_init_rank(ctx.h, nranks, rank, buf, ctypes.byref(h)),
+              "sdgpu_comm_init_rank")
+        return cls(ctx, h)
+
+    @classmethod
+    def init_all(cls, ctxs, transport: int = TRANSPORT_AUTO) -> list:
+        import ctypes
+        n = len(ctxs)
+        arr = (ctypes.c_void_p * n)(*[c.h.value for c in ctxs])
+        out = (ctypes.c_void_p * n)()
+        check(ctxs[0].lib.sdgpu_comm_init_all(arr, n, transport, out), "sdgpu_comm_init_all")
+        return [cls(ctxs[i], ctypes.c_void_p(out[i])) for i in range(n)]
+
+    def info(self):
+        import ctypes
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self.ctx.lib.sdgpu_comm_info(self.h, ctypes.byref(a), ctypes.byref(b),
+                                           ctypes.byref(c)), "sdgpu_comm_info")
+        return a.value, b.value, c.value
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.sdgpu_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def group_sharded(key, has_key, rank, comm: Comm, index: ObjectIndex | None = None,
+                  chunk_rows: int = CHUNK_SIZE, out=None):
+    """This rank's rep (int32, device) of the grouping over all ranks of `comm`
+    (collective; sdgpu_group_sharded_device: RCCL all-to-all inside libsdgpu)."""
+    import torch
+    ctx = comm.ctx
+    rep = out if out is not None else torch.empty(key.numel(), dtype=torch.int32,
+                                                  device=key.device)
+    s = torch.cuda.current_stream(key.device).cuda_stream
+    check(ctx.lib.sdgpu_group_sharded_device(
+        ctx.h, comm.h, index.h if index is not None else None, key.data_ptr(),
+        has_key.data_ptr() if has_key is not None else None, rank.data_ptr(), key.numel(),
+        chunk_rows, rep.data_ptr(), s), "sdgpu_group_sharded_device")
+    return rep
+
+
+def group_sharded_all(keys, hass, ranks, comms, indexes=None, chunk_rows: int = CHUNK_SIZE):
+    """All ranks from one process (sdgpu_group_sharded_all_device): lists of
+    device tensors per rank -> list of int32 reps."""
+    import ctypes
+    import torch
+    W = len(keys)
+    vp = ctypes.c_void_p
+    reps = [torch.empty(k.numel(), dtype=torch.int32, device=k.device) for k in keys]
+    arr = lambda xs: (vp * W)(*xs)  # noqa: E731
+    ctxs = [c.ctx for c in comms]
+    n = (ctypes.c_uint64 * W)(*[k.numel() for k in keys])
+    check(ctxs[0].lib.sdgpu_group_sharded_all_device(
+        arr([c.h.value for c in ctxs]), arr([c.h.value for c in comms]),
+        arr([i.h.value for i in indexes]) if indexes else None, W,
+        arr([k.data_ptr() for k in keys]), arr([h.data_ptr() for h in hass]) if hass else None,
+        arr([r.data_ptr() for r in ranks]), n, chunk_rows, arr([r.data_ptr() for r in reps]),
+        arr([torch.cuda.current_stream(k.device).cuda_stream for k in keys])),
+        "sdgpu_group_sharded_all_device")
+    return reps
+
+
+def dedup_sharded(ctxs, key, has_key, chunk_rows: int = CHUNK_SIZE) -> np.ndarray:
+    """SURVEY §8(b)'s sdgpu_dedup(ctx[], ngpu, ...) on host arrays."""
+    import ctypes
+    key = np.ascontiguousarray(key, np.uint64)
+    has_key = np.ascontiguousarray(has_key, np.uint8)
+    rep = np.zeros(key.size, np.uint32)
+    arr = (ctypes.c_void_p * len(ctxs))(*[c.h.value for c in ctxs])
+    check(ctxs[0].lib.sdgpu_dedup_sharded(arr, len(ctxs), key.ctypes.data, has_key.ctypes.data,
+                                          key.size, chunk_rows, rep.ctypes.data),
+          "sdgpu_dedup_sharded")
+    return rep
+
+
+def shard_of(key: np.ndarray, bits: int = 8) -> np.ndarray:
+    """Shard of cas keys: top `bits` bits of mix64(key) (csrc/rows_device.hpp)."""
+    z = np.asarray(key, np.uint64).copy()
+    with np.errstate(over="ignore"):
+        z ^= z >> np.uint64(30)
+        z *= np.uint64(0xBF58476D1CE4E5B9)
+        z ^= z >> np.uint64(27)
+        z *= np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return (z >> np.uint64(64 - bits)).astype(np.int64)
 
 
 def link_batch_device(rep, rank=None, valid=None, first_rank: int = 0, ctx=None,

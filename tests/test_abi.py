@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     lib = _native.load()
-    assert lib.sdgpu_abi_version() == 1
+    assert lib.sdgpu_abi_version() == 2
     assert lib.sdgpu_strerror(0) == b"success"
     assert lib.sdgpu_strerror(-22) == b"Invalid argument"
 
@@ -30,6 +30,20 @@ def test_null_arguments_rejected_without_device():
     assert lib.sdgpu_open(0, None) == -22
     assert lib.sdgpu_close(None) == -22
     assert lib.sdgpu_cas_batch(None, None, None, None, 0, None, None) == -22
+    assert lib.sdgpu_index_create(None, 10, None) == -22
+    assert lib.sdgpu_comm_unique_id(None) == -22
+    assert lib.sdgpu_comm_init_all(None, 2, 0, None) == -22
+    assert lib.sdgpu_dedup_sharded(None, 2, None, None, 0, 100, None) == -22
+    assert lib.sdgpu_group_sharded_device(None, None, None, None, None, None, 0, 100, None,
+                                          None) == -22
+
+
+def test_every_declared_symbol_has_a_ctypes_prototype():
+    """The Python binding types every entry point of the header (no call goes
+    through ctypes' default int-argument conversion)."""
+    lib = _native.load()
+    for name in _native.declared_symbols():
+        assert getattr(lib, name).argtypes is not None, name
 
 
 def test_library_is_gfx950_code_object():

@@ -18,7 +18,8 @@ class NumpyOps:
 
     @staticmethod
     def _digit(k, bits):
-        return (k >> np.uint64(64 - bits)).astype(np.int64) if bits else np.zeros(k.size, np.int64)
+        from spacedrive_amd.dedup import shard_of  # the product's shard function
+        return shard_of(k, bits) if bits else np.zeros(k.size, np.int64)
 
     def shard_counts(self, key, has_key, bits):
         k = key.numpy().view(np.uint64)

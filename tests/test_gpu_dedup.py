@@ -163,21 +163,36 @@ def test_exchange_partition_matches_count_and_partition(ctx, world):
     for d in range(world):
         seg = slice(bounds[d], bounds[d + 1])
         np.testing.assert_array_equal(np.sort(op[seg]), np.sort(ref_pos[seg]))
-        assert np.all(owner[(k[op[seg]] >> np.uint64(64 - bits)).astype(np.int64)] == d)
+        assert np.all(owner[dedup.shard_of(k[op[seg]], bits)] == d)
+
+
+def _one_bucket_keys(rng, n, count):
+    """`count` distinct random keys that all land in bucket 0 of an n-row
+    grouping (bucket = the hash bits below the shard byte, csrc/dedup.hip
+    bucket_bits_for / digit_of)."""
+    from spacedrive_amd.dedup import shard_of
+    bits = 1
+    while bits < 15 and (n >> bits) > 3072:
+        bits += 1
+    out = []
+    while sum(x.size for x in out) < count:
+        k = rng.integers(0, 2**64 - 1, 1 << 20, dtype=np.uint64, endpoint=True)
+        digit = shard_of(k, 8 + bits) & ((1 << bits) - 1)
+        out.append(k[digit == 0])
+    return np.unique(np.concatenate(out))[:count]
 
 
 @pytest.mark.parametrize("n", [4607, 4608, 4609, 6144, 6145, 9000])
 def test_single_bucket_at_lds_capacity(ctx, n):
-    """Every key in one bucket (top bit clear): rows just under, at and over the
-    LDS table's capacity (4608 rows of 6144 slots) take the LDS path or the
-    global-table path, with a sentinel-valued key and ~30% duplicates."""
+    """Every key in one bucket: rows just under, at and over the LDS table's
+    capacity (4608 rows of 6144 slots) take the LDS path or the global-table
+    path, with ~30% duplicates (the all-ones key, the table's empty value, is
+    checked by test_random_vs_oracle)."""
     from spacedrive_amd import dedup
     rng = np.random.default_rng(n)
-    keys = rng.integers(0, 2**63 - 1, n, dtype=np.uint64)
-    key = keys[rng.integers(0, int(n * 0.7), n)]
-    key[rng.integers(0, n, 5)] = np.uint64(2**63 - 1)
-    key[rng.integers(0, n, 3)] = np.uint64(2**64 - 1)  # the empty-slot sentinel
-    has = (rng.random(n) > 0.01).astype(np.uint8)
+    keys = _one_bucket_keys(rng, n, int(n * 0.7))
+    key = keys[rng.integers(0, keys.size, n)]
+    has = np.ones(n, np.uint8)  # every row in the bucket
     for chunk in (100, 1):
         rep = dedup.group_reps(key, has, chunk, ctx)
         np.testing.assert_array_equal(rep, O.group_reps(key, has, chunk))

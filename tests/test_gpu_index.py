@@ -1,0 +1,106 @@
+"""GPU parity: the Object index -- batches grouped one after another through
+one index equal the grouping of the whole run (the reference groups chunk by
+chunk against every Object already in the library, file_identifier/mod.rs:
+168-241), with and without Objects that existed before the run."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _rows(seed, n, distinct, keyless=0.01):
+    rng = np.random.default_rng(seed)
+    pool = rng.integers(0, 2**64 - 1, distinct, dtype=np.uint64, endpoint=True)
+    pool[0] = np.uint64(2**64 - 1)  # the table's empty-slot value is a legal key
+    key = pool[rng.integers(0, pool.size, n)]
+    has = (rng.random(n) > keyless).astype(np.uint8)
+    return key, has
+
+
+def _run_batches(ctx, key, has, bounds, chunk, index):
+    from spacedrive_amd import dedup
+    out = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        out.append(dedup.dedup_batch(key[a:b], has[a:b], a, index, chunk, ctx))
+    return np.concatenate(out)
+
+
+def test_two_batches_second_sees_first(ctx):
+    """Two consecutive 100 k-row batches; the second holds keys of the first:
+    identical to the oracle's grouping of the union (the verdict's bar)."""
+    from spacedrive_amd import dedup
+    key, has = _rows(1, 200_000, 120_000)
+    idx = dedup.ObjectIndex(ctx, 1000)   # small: forces growth + rehash on the way
+    rep = _run_batches(ctx, key, has, [0, 100_000, 200_000], 100, idx)
+    np.testing.assert_array_equal(rep, O.group_reps(key, has, 100))
+    # the second batch linked rows to Objects created by the first
+    r = np.arange(200_000)
+    assert np.count_nonzero((r >= 100_000) & (rep < 100_000)) > 10_000
+    # index holds exactly the distinct keys seen
+    assert idx.count() == np.unique(key[has == 1]).size
+    # grouped alone, the second batch would create those Objects again
+    alone = dedup.dedup_batch(key[100_000:], has[100_000:], 100_000, None, 100, ctx)
+    assert np.any(alone != rep[100_000:])
+
+
+@pytest.mark.parametrize("chunk,bounds", [
+    (100, [0, 150, 1000, 1001, 50_000, 50_037, 120_000]),   # batches split chunks
+    (7, [0, 3, 10, 7000, 80_000, 120_000]),
+    (1, [0, 60_000, 120_000]),
+])
+def test_unaligned_batches(ctx, chunk, bounds):
+    """Batch boundaries inside a chunk: a row of a later batch that shares the
+    chunk of its key's first row still creates its own Object (rule a6)."""
+    from spacedrive_amd import dedup
+    key, has = _rows(chunk + len(bounds), bounds[-1], 30_000)
+    idx = dedup.ObjectIndex(ctx)
+    rep = _run_batches(ctx, key, has, bounds, chunk, idx)
+    np.testing.assert_array_equal(rep, O.group_reps(key, has, chunk))
+
+
+def test_preexisting_objects(ctx):
+    """Objects that existed before the run (other locations / earlier runs):
+    every row with their cas_id links to them (mod.rs:189-225), the lowest
+    handle when several own the key; the rest follow the in-run rule."""
+    import torch
+    from spacedrive_amd import dedup
+    key, has = _rows(5, 150_000, 60_000)
+    rng = np.random.default_rng(9)
+    ek = np.concatenate([rng.choice(key, 5000), rng.integers(0, 2**63, 3000, dtype=np.uint64)])
+    ek = np.concatenate([ek, ek[:700]])           # keys owned by two Objects
+    eh = rng.permutation(ek.size).astype(np.uint32) + 17
+    idx = dedup.ObjectIndex(ctx, 4096)
+    idx.add_objects(torch.from_numpy(ek.view(np.int64)).cuda(),
+                    torch.from_numpy(eh.view(np.int32)).cuda())
+    rep = _run_batches(ctx, key, has, [0, 40_000, 90_000, 150_000], 100, idx)
+    ref = O.group_reps_existing(key, has, 100, ek, eh)
+    np.testing.assert_array_equal(rep, ref)
+    assert np.count_nonzero(rep & np.uint32(dedup.REP_EXISTING)) > 5000
+
+
+def test_device_api_matches_host_api(ctx):
+    import torch
+    from spacedrive_amd import dedup
+    key, has = _rows(11, 300_000, 200_000)
+    rank = np.arange(300_000, dtype=np.uint32)
+    idx = dedup.ObjectIndex(ctx)
+    reps = []
+    for a, b in ((0, 100_000), (100_000, 300_000)):
+        reps.append(dedup.group_rows_indexed(
+            torch.from_numpy(key[a:b].view(np.int64)).cuda(), torch.from_numpy(has[a:b]).cuda(),
+            torch.from_numpy(rank[a:b].view(np.int32)).cuda(), idx, 100).cpu().numpy())
+    np.testing.assert_array_equal(np.concatenate(reps).view(np.uint32),
+                                  O.group_reps(key, has, 100))
+
+
+def test_many_batches_growth(ctx):
+    """40 batches of 25 k rows into an index created for 1 k keys: repeated
+    growth, identical to the whole run."""
+    from spacedrive_amd import dedup
+    n = 1_000_000
+    key, has = _rows(13, n, 700_000)
+    idx = dedup.ObjectIndex(ctx, 1000)
+    rep = _run_batches(ctx, key, has, list(range(0, n + 1, 25_000)), 100, idx)
+    np.testing.assert_array_equal(rep, O.group_reps(key, has, 100))
