@@ -109,7 +109,9 @@ int pread_exact(int fd, uint8_t* buf, size_t n, off_t pos) {
 }
 
 // Writes the cas message of the file at `path` (stat size `size`) into dst
-// (capacity cap).  Returns its length, or -errno.
+// (capacity cap).  Returns its length, or -errno; -EFBIG means a file of at
+// most 100 KiB at stat time outgrew its reservation before the read, and the
+// caller hashes it through cas_grown_locked (no deviation from fs::read).
 int64_t read_cas_message(const char* path, uint64_t size, uint8_t* dst, size_t cap) {
   if (cap < 8) return -ENOBUFS;
   const int fd = open(path, O_RDONLY | O_CLOEXEC);
@@ -161,6 +163,8 @@ int64_t read_cas_message(const char* path, uint64_t size, uint8_t* dst, size_t c
   close(fd);
   return rc ? rc : len;
 }
+
+int cas_grown_locked(sdgpu_ctx* c, const char* path, uint64_t size, uint8_t out8[8]);
 
 template <typename F>
 void parallel_for(uint32_t n, F&& f) {
@@ -605,7 +609,8 @@ int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t*
   if (!c || (n && (!paths || !size || !out8))) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
-  return run_pipeline(
+  std::vector<uint32_t> grown;  // <= 100 KiB at stat, longer than its room at read
+  const int rc = run_pipeline(
       c, n,
       [&](uint32_t i) -> uint64_t {
         if (size[i] == 0) return 16;
@@ -620,12 +625,21 @@ int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t*
         for (uint32_t j = 0; j < cnt; ++j) {
           const int32_t sj = st[j];
           const bool ok = sj == 0;
+          if (sj == -EFBIG) grown.push_back(first + j);
           if (ok) memcpy(out8[first + j], o[j], 8);
           else memset(out8[first + j], 0, 8);
           if (has_key) has_key[first + j] = ok ? 1 : 0;
           if (status) status[first + j] = sj == 1 ? 0 : sj;
         }
       });
+  if (rc) return rc;
+  for (const uint32_t i : grown) {
+    const int r = cas_grown_locked(c, paths[i], size[i], out8[i]);
+    if (r) memset(out8[i], 0, 8);
+    if (has_key) has_key[i] = r == 0 ? 1 : 0;
+    if (status) status[i] = r;
+  }
+  return 0;
 }
 
 int sdgpu_generate_cas_id(sdgpu_ctx* c, const char* path, uint64_t size, char out_hex[17]) {
@@ -649,6 +663,7 @@ int sdgpu_generate_cas_id(sdgpu_ctx* c, const char* path, uint64_t size, char ou
         memcpy(out, o[0], 8);
       });
   if (rc) return rc;
+  if (st == -EFBIG) st = cas_grown_locked(c, path, size, out);  // grew since stat
   if (st) return st;
   to_hex(out, 8, out_hex);
   return 0;
@@ -681,10 +696,10 @@ int sdgpu_subtree_device(sdgpu_ctx* c, const uint8_t* d_bytes, uint64_t len, uin
   return tree_launch(c, &seg, 1, false, d_out32, s);
 }
 
-int sdgpu_checksum(sdgpu_ctx* c, const void* bytes, uint64_t len, uint8_t out32[32]) {
-  if (!c || (len && !bytes) || !out32) return -EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  SD_TRY(hipSetDevice(c->device));
+namespace {
+
+// BLAKE3 of a host buffer through the tree kernels (context lock held).
+int checksum_host_locked(sdgpu_ctx* c, const void* bytes, uint64_t len, uint8_t out32[32]) {
   hipStream_t s = pick(c, nullptr);
   SD_TRY_RC(ensure_dev(c, c->io_a, align_up(len, 256) + 256));
   uint8_t* d = static_cast<uint8_t*>(c->io_a.p);
@@ -695,6 +710,45 @@ int sdgpu_checksum(sdgpu_ctx* c, const void* bytes, uint64_t len, uint8_t out32[
   SD_TRY(hipMemcpyAsync(out32, dout, 32, hipMemcpyDeviceToHost, s));
   SD_TRY(hipStreamSynchronize(s));
   return 0;
+}
+
+// cas_id of a file that was <= 100 KiB at stat time but longer than its slab
+// reservation at read time: fs::read takes whatever the file holds then
+// (cas.rs:27-29), so the message is u64 size LE || the whole current content,
+// of any length; hashed by the tree kernels.  out8 = BLAKE3(M)[0..8).
+int cas_grown_locked(sdgpu_ctx* c, const char* path, uint64_t size, uint8_t out8[8]) {
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  std::vector<uint8_t> msg(8);
+  for (int i = 0; i < 8; ++i) msg[i] = static_cast<uint8_t>(size >> (8 * i));
+  int rc = 0;
+  for (;;) {
+    const size_t at = msg.size();
+    msg.resize(at + (size_t(1) << 20));
+    const ssize_t r = read(fd, msg.data() + at, size_t(1) << 20);
+    if (r < 0 && errno == EINTR) {
+      msg.resize(at);
+      continue;
+    }
+    msg.resize(at + (r > 0 ? static_cast<size_t>(r) : 0));
+    if (r < 0) rc = -errno;
+    if (r <= 0) break;
+  }
+  close(fd);
+  if (rc) return rc;
+  uint8_t d[32];
+  SD_TRY_RC(checksum_host_locked(c, msg.data(), msg.size(), d));
+  memcpy(out8, d, 8);
+  return 0;
+}
+
+}  // namespace
+
+int sdgpu_checksum(sdgpu_ctx* c, const void* bytes, uint64_t len, uint8_t out32[32]) {
+  if (!c || (len && !bytes) || !out32) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  return checksum_host_locked(c, bytes, len, out32);
 }
 
 namespace {
@@ -730,6 +784,7 @@ int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
   uint64_t total = 0;
   hipEvent_t* ev = c->pipe_evt;
   bool inflight[2] = {false, false};
+  bool root_done = false;  // the digest was launched directly (single slice)
   std::vector<uint8_t> out(32);
   do {
     struct stat st;
@@ -803,10 +858,18 @@ int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
       // peek whether more data follows (to know if this slice is the last)
       if (!eof) {
         uint8_t probe;
-        const ssize_t r = pread(fd, &probe, 1, static_cast<off_t>(total + got));
+        ssize_t r;
+        do {
+          r = pread(fd, &probe, 1, static_cast<off_t>(total + got));
+        } while (r < 0 && errno == EINTR);
+        if (r < 0) {
+          rc = -errno;
+          break;
+        }
         if (r == 0) eof = true;
       }
       const bool only = eof && nslices == 0;
+      root_done = only;
       if ((rc = grow_dev_keep(c, c->io_b, 32 * (nslices + 1) + 256, 32 * nslices))) break;
       uint8_t* cvs = static_cast<uint8_t*>(c->io_b.p);
       if (got && hipMemcpyAsync(dslice[k], hb, got, hipMemcpyHostToDevice, s) != hipSuccess) {
@@ -825,6 +888,11 @@ int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
       // fold the slice CVs (equal aligned power-of-two subtrees, last partial)
       const TreeSeg seg{static_cast<uint8_t*>(c->io_b.p), nslices, 0, 1, 0};
       if ((rc = tree_launch(c, &seg, 1, true, droot, s))) break;
+    } else if (!root_done) {
+      // the probe saw more data but the file was truncated before the next
+      // read: the only slice (still in dslice[0]) is the whole message
+      const TreeSeg seg{dslice[0], total, 0, 1, 0};
+      if ((rc = tree_launch(c, &seg, 1, false, droot, s))) break;
     }
     if (hipMemcpyAsync(out.data(), droot, 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)

@@ -10,6 +10,12 @@
 * ``identifier_job(paths)``: the whole job over orphan rows in id order --
   cas ids, then the Object grouping of every row (dedup.group_reps), with the
   reference's per-step (created, linked) accounting.
+* ``FileIdentifierJob`` / ``shallow``: the resumable job
+  (file_identifier_job.rs:32-309) and the light-scan variant (shallow.rs:26-119)
+  over a ``FilePaths`` table: orphan rows fetched in ascending id with the
+  reference's cursor (``id >= cursor``, cursor = last fetched id), grouped
+  against a device Object index so that steps of many chunks give the same
+  Objects as the reference's 100-row steps; pause/resume through a JSON state.
 """
 from __future__ import annotations
 
@@ -101,5 +107,274 @@ def identifier_job(paths, chunk_size: int = CHUNK_SIZE, ctx=None) -> JobResult:
     return JobResult(ident, rep, created, linked)
 
 
+# ---------------------------------------------------------------------------
+# The resumable identifier job and the shallow (light-scan) identifier
+# ---------------------------------------------------------------------------
+
+class FilePaths:
+    """The file_path rows the identifier reads and writes: the columns of
+    file_path_for_file_identifier (core/src/location/file_path_helper/mod.rs:32-40)
+    plus cas_id and object_id (core/prisma/schema.prisma:154-201).  An in-memory
+    stand-in for the library's table -- the prisma/SQLite store is out of scope
+    (SURVEY §2); the job only needs these queries and writes."""
+
+    def __init__(self):
+        self.location_id: list[int] = []
+        self.materialized_path: list[str] = []   # "/a/b/" for a child of /a/b
+        self.name: list[str] = []
+        self.is_dir: list[bool] = []
+        self.cas_id: list[str | None] = []
+        self.object_id: list[int | None] = []
+        self.next_object_id = 1
+
+    def add(self, location_id: int, materialized_path: str, name: str,
+            is_dir: bool = False) -> int:
+        """Appends a row; its file_path.id is its index + 1 (ascending ids)."""
+        self.location_id.append(location_id)
+        self.materialized_path.append(materialized_path)
+        self.name.append(name)
+        self.is_dir.append(is_dir)
+        self.cas_id.append(None)
+        self.object_id.append(None)
+        return len(self.name)
+
+    def __len__(self):
+        return len(self.name)
+
+    def rel_path(self, fid: int) -> str:
+        i = fid - 1
+        return self.materialized_path[i].lstrip("/") + self.name[i]
+
+    def orphans(self, location_id: int, cursor: int | None = None,
+                children_of: str | None = None, under: str | None = None) -> list[int]:
+        """ids of orphan rows in ascending id (orphan_path_filters,
+        file_identifier_job.rs:245-268 / shallow.rs:121-139): object_id NULL,
+        !is_dir, the location, id >= cursor, and either a subtree
+        (materialized_path starts with `under`) or one directory's children."""
+        out = []
+        start = max(1, cursor or 1)
+        for fid in range(start, len(self.name) + 1):
+            i = fid - 1
+            if self.object_id[i] is not None or self.is_dir[i]:
+                continue
+            if self.location_id[i] != location_id:
+                continue
+            mp = self.materialized_path[i]
+            if children_of is not None and mp != children_of:
+                continue
+            if under is not None and not mp.startswith(under):
+                continue
+            out.append(fid)
+        return out
+
+    def existing_objects(self):
+        """(key, object id) of every row linked to an Object and carrying a
+        cas_id, library-wide (what mod.rs:168-175's find_many can return)."""
+        from .cas import keys_of
+        keys, objs = [], []
+        for c, o in zip(self.cas_id, self.object_id):
+            if c is not None and o is not None:
+                keys.append(bytes.fromhex(c))
+                objs.append(o)
+        if not keys:
+            return np.zeros(0, np.uint64), np.zeros(0, np.uint32)
+        k = keys_of(np.frombuffer(b"".join(keys), np.uint8).reshape(-1, 8))
+        return k, np.asarray(objs, np.uint32)
+
+
+@dataclass
+class IdentifierRunMetadata:
+    """FileIdentifierJobRunMetadata (file_identifier_job.rs:53-68)."""
+    cursor: int = 0
+    total_orphan_paths: int = 0
+    total_objects_created: int = 0
+    total_objects_linked: int = 0
+    total_objects_ignored: int = 0
+
+
+class FileIdentifierJob:
+    """FileIdentifierJobInit (file_identifier_job.rs:72-243) over a FilePaths
+    table, run on the GPU.
+
+    init: counts the orphans (early finish if none, :130-136), task_count =
+    ceil(n / 100) steps of CHUNK_SIZE rows, cursor = first orphan id (:140-170).
+    A reference step fetches the next 100 orphans with id >= cursor in id order
+    (:286-309), identifies and groups them (mod.rs:100-336) and sets the cursor
+    to the last fetched id (mod.rs:384-392).  Here one execute_step runs
+    `chunks_per_step` such steps as ONE GPU batch: the chunk boundaries are
+    replayed exactly (a failed last row is fetched again by the next chunk, as
+    the `id >= cursor` query does), every fetched row gets rank = step * 100 +
+    position, and the grouping runs against a device Object index holding the
+    library's existing Objects and this run's creators -- so the Objects are
+    the reference's whatever the step size.  state() / resume() persist the
+    cursor and counters (the JobState of job/mod.rs:701-720); a resumed job
+    re-registers the Objects already in the table."""
+
+    def __init__(self, table: FilePaths, location_id: int, location_path: str,
+                 sub_path: str | None = None, chunks_per_step: int = 64, ctx=None,
+                 _shallow_dir: str | None = None):
+        self.table = table
+        self.location_id = location_id
+        self.location_path = location_path
+        self.sub_path = sub_path
+        self.chunks_per_step = max(1, int(chunks_per_step))
+        self.ctx = ctx or default_context()
+        self._children_of = _shallow_dir
+        self._under = None
+        if sub_path:
+            sp = "/" + sub_path.strip("/") + "/"
+            self._under = sp
+        self.meta = IdentifierRunMetadata()
+        self.step_number = 0      # reference steps (chunks of 100) done
+        self.task_count = 0
+        self._creator_object: dict[int, int] = {}  # rank -> Object id (this run)
+        self.index = None
+
+    # ---- reference: init (file_identifier_job.rs:80-172) -------------------------
+    def init(self) -> "FileIdentifierJob":
+        orphans = self._orphans(None)
+        if not orphans:
+            raise EarlyFinish("Found no orphan file paths to process")
+        self.meta = IdentifierRunMetadata(cursor=orphans[0], total_orphan_paths=len(orphans))
+        self.task_count = -(-len(orphans) // CHUNK_SIZE)
+        self._open_index()
+        return self
+
+    def _orphans(self, cursor):
+        return self.table.orphans(self.location_id, cursor, self._children_of, self._under)
+
+    def _open_index(self):
+        import torch
+        ek, eh = self.table.existing_objects()
+        self.index = _dedup.ObjectIndex(self.ctx, max(1024, 2 * (len(self.table) + ek.size)))
+        if ek.size:
+            dev = torch.device("cuda", self.ctx.device)
+            self.index.add_objects(torch.from_numpy(ek.view(np.int64)).to(dev),
+                                   torch.from_numpy(eh.view(np.int32)).to(dev))
+
+    def done(self) -> bool:
+        return self.step_number >= self.task_count
+
+    # ---- reference: execute_step, chunks_per_step of them at once -----------------
+    def execute_step(self) -> IdentifierRunMetadata:
+        if self.done():
+            return self.meta
+        nchunks = min(self.chunks_per_step, self.task_count - self.step_number)
+        cand = self._orphans(self.meta.cursor)[:nchunks * CHUNK_SIZE + nchunks]
+        if not cand:
+            raise EarlyFinish("Expected orphan Paths not returned from database query for this chunk")
+        paths = [os.path.join(self.location_path, self.table.rel_path(f)) for f in cand]
+        ident = identify(paths, ctx=self.ctx)
+        ok = {f: ident.status[i] == 0 for i, f in enumerate(cand)}
+        pos = {f: i for i, f in enumerate(cand)}
+        # replay the reference's fetches: chunk c = the next 100 orphans with
+        # id >= cursor (a failed last row stays orphan and is fetched again)
+        fetched, cursor = [], self.meta.cursor
+        for _ in range(nchunks):
+            chunk = []
+            for f in cand:
+                if f < cursor or (fetched and f == cursor and ok[f]):
+                    continue  # below the cursor, or identified by the previous chunk
+                chunk.append(f)
+                if len(chunk) == CHUNK_SIZE:
+                    break
+            if not chunk:
+                break
+            fetched.append(chunk)
+            cursor = chunk[-1]
+        rows = [f for ch in fetched for f in ch]
+        first_rank = self.step_number * CHUNK_SIZE
+        key = np.zeros(len(rows), np.uint64)
+        has = np.zeros(len(rows), np.uint8)
+        valid = np.zeros(len(rows), bool)
+        keys8 = _cas.keys_of(ident.cas8)
+        for j, f in enumerate(rows):
+            i = pos[f]
+            valid[j] = ok[f]
+            has[j] = ident.has_key[i] if ok[f] else 0
+            key[j] = keys8[i]
+        rep = _dedup.dedup_batch(key, has, first_rank, self.index, CHUNK_SIZE, self.ctx)
+        created = linked = 0
+        t = self.table
+        for j, f in enumerate(rows):  # the write set, in rank order (mod.rs:144-333)
+            if not valid[j]:
+                continue
+            i = f - 1
+            t.cas_id[i] = bytes(ident.cas8[pos[f]]).hex() if has[j] else None
+            r = first_rank + j
+            if rep[j] == r:
+                obj = t.next_object_id
+                t.next_object_id += 1
+                self._creator_object[r] = obj
+                created += 1
+            elif rep[j] & _dedup.REP_EXISTING:
+                obj = int(rep[j] & 0x7FFFFFFF)
+                linked += 1
+            else:
+                obj = self._creator_object[int(rep[j])]
+                linked += 1
+            t.object_id[i] = obj
+        self.step_number += len(fetched)
+        self.meta.cursor = cursor
+        self.meta.total_objects_created += created
+        self.meta.total_objects_linked += linked
+        self.meta.total_objects_ignored += int((~valid).sum())
+        return self.meta
+
+    def run(self, max_steps: int | None = None) -> IdentifierRunMetadata:
+        k = 0
+        while not self.done() and (max_steps is None or k < max_steps):
+            self.execute_step()
+            k += 1
+        return self.meta
+
+    # ---- pause / resume (job/mod.rs:701-720, cold_resume job/manager.rs:269-320) ---
+    def state(self) -> dict:
+        from dataclasses import asdict
+        return {"location_id": self.location_id, "location_path": self.location_path,
+                "sub_path": self.sub_path, "shallow_dir": self._children_of,
+                "chunks_per_step": self.chunks_per_step, "step_number": self.step_number,
+                "task_count": self.task_count, "run_metadata": asdict(self.meta)}
+
+    @classmethod
+    def resume(cls, table: FilePaths, state: dict, ctx=None) -> "FileIdentifierJob":
+        job = cls(table, state["location_id"], state["location_path"], state["sub_path"],
+                  state["chunks_per_step"], ctx, state.get("shallow_dir"))
+        job.meta = IdentifierRunMetadata(**state["run_metadata"])
+        job.step_number = state["step_number"]
+        job.task_count = state["task_count"]
+        job._open_index()  # this run's earlier Objects are existing Objects now
+        return job
+
+    def close(self):
+        if self.index is not None:
+            self.index.close()
+            self.index = None
+
+
+class EarlyFinish(Exception):
+    """JobError::EarlyFinish (file_identifier_job.rs:131-136, 197-203)."""
+
+
+def shallow(table: FilePaths, location_id: int, location_path: str, sub_path: str = "",
+            chunks_per_step: int = 64, ctx=None) -> IdentifierRunMetadata:
+    """file_identifier::shallow (shallow.rs:26-119): the light scan of one
+    directory -- only its direct children (materialized_path equal to the
+    directory's children path, :121-139), all steps at once, outside the job
+    system; no orphans is not an error (:65-67)."""
+    d = "/" + sub_path.strip("/") + "/" if sub_path.strip("/") else "/"
+    job = FileIdentifierJob(table, location_id, location_path, None, chunks_per_step, ctx,
+                            _shallow_dir=d)
+    try:
+        job.init()
+    except EarlyFinish:
+        return IdentifierRunMetadata()
+    try:
+        return job.run()
+    finally:
+        job.close()
+
+
 __all__ = ["FileMetadata", "file_metadata", "identify", "identifier_job", "IdentifyResult",
-           "JobResult", "SdgpuError"]
+           "JobResult", "SdgpuError", "FilePaths", "FileIdentifierJob", "IdentifierRunMetadata",
+           "EarlyFinish", "shallow"]
