@@ -53,6 +53,21 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def host_cores():
+    """(threads, note): every core this process may run on (its CPU affinity),
+    capped by OMP_NUM_THREADS when the host sets it (the GPU box sets 16: the
+    CPU share of one GPU; nproc shows the whole machine there)."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = total
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    n = min(aff, cap) if cap > 0 else aff
+    return n, (f"{n} threads: sched_getaffinity {aff}, os.cpu_count {total}, "
+               f"OMP_NUM_THREADS {cap or 'unset'}")
+
+
 def compressions(lens: np.ndarray):
     """(chunk-block compressions, parent compressions) of messages of these lengths."""
     L = lens.astype(np.int64)
@@ -236,13 +251,23 @@ class Runner:
         del h, d
         return nbytes * reps / dt
 
-    def run_staged(self, steps, warmup):
-        """Config 5 shape: identifier job whose cas windows sit in PINNED host
-        memory (where the preads land): staged H2D through the slab ring
-        overlapped with K1, then the sharded grouping and the Object link batch."""
+    def run_staged(self):
+        """BASELINE config 5: an identifier RUN over `staged_total_files` files
+        (all GPUs together), in steps of `staged_files` per GPU.  The cas
+        windows sit in PINNED host memory (where the preads land): staged H2D
+        through the slab ring overlapped with K1, then the grouping of the step
+        against the run's Object index (sharded with the rows over the GPUs at
+        N > 1) and the Object link batch.  One pinned pool of config-2 files per
+        GPU serves every step; ~81 % of its files stand for new content in each
+        step (their keys remapped by a bijection after K1, sdgpu_synth_vary_keys
+        _device), the rest are the same files every step -- so later steps link
+        to earlier steps' Objects through the index, and the whole run is ONE
+        grouping (test_gpu_index.py checks that batching is exact)."""
         torch = self.torch
         from spacedrive_amd import cas, corpus, dedup
         n = self.args.staged_files
+        W = self.world
+        nsteps = max(1, -(-self.args.staged_total_files // (W * n)))
         sizes, seeds = corpus.config2_files(n, seed=5 + 1000 * self.rank)
         d_arena, d_off, d_len = corpus.synth_arena_device(sizes, seeds, device=self.local,
                                                           ctx=self.ctx)
@@ -257,28 +282,61 @@ class Runner:
         out = torch.empty((n, 8), dtype=torch.uint8, device=self.dev)
         st = torch.empty(n, dtype=torch.int32, device=self.dev)
         has = torch.from_numpy((sizes != 0).astype(np.uint8)).to(self.dev)
-        grank = torch.arange(self.rank * n, (self.rank + 1) * n, dtype=torch.int64,
-                             device=self.dev).to(torch.int32)
+        vary = torch.from_numpy(corpus.config5_vary_mask(sizes, seeds)).to(self.dev)
+        # global ranks of every step (id order: step, then GPU, then row)
+        base = torch.arange(n, dtype=torch.int64, device=self.dev) + self.rank * n
+        ranks = [(base + s * W * n).to(torch.int32) for s in range(nsteps + 1)]
+        use_index = W == 1 or self.comm is not None
+        index = dedup.ObjectIndex(self.ctx, 2 * nsteps * n // W + (1 << 20)) if use_index else None
         peak = self.h2d_peak()
 
-        def step():
+        def step(s):
             cas.cas_stage_pinned(h_arena, off, ln, out, st, ctx=self.ctx)
             key = out.view(torch.int64).view(-1)
-            rep = self.group(key, has, grank)
-            dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx, trim=False)
+            corpus.vary_keys_device(key, vary, s, ctx=self.ctx)
+            if W == 1:
+                rep = dedup.group_rows_indexed(key, has, ranks[s], index, 100)
+            elif self.comm is not None:
+                rep = dedup.group_sharded(key, has, ranks[s], self.comm, index, 100)
+            else:  # gloo rehearsal: the exchange has no index
+                rep = self.group(key, has, ranks[s])
+            dedup.link_batch_device(rep, ranks[s], None, 0, ctx=self.ctx, trim=False)
+            return rep
 
-        t = self.timed(step, steps, warmup)
+        step(nsteps)  # warm-up on a step outside the run's key space
+        torch.cuda.synchronize()
+        if index is not None:
+            index.clear()
+
+        def run():
+            for s in range(nsteps):
+                rep = step(s)
+            self._staged_last = rep
+
+        t = self.timed(run, 1, 0)
         assert int(st.abs().sum()) == 0
-        per_gpu_Bps = window_bytes * steps / t
-        del h_arena
-        return {"value": self.world * n * steps / t, "unit": "files/s",
-                "ms_per_step": 1e3 * t / steps,
+        last = self._staged_last
+        linked_last = int((last != ranks[nsteps - 1]).sum())
+        distinct = index.count() if index is not None else None
+        files = W * n * nsteps
+        per_gpu_Bps = window_bytes * nsteps / t
+        del h_arena, ranks
+        self._staged_last = None
+        if index is not None:
+            index.close()
+        return {"value": files / t, "unit": "files/s", "ms_per_step": 1e3 * t / nsteps,
+                "files_total": files, "steps": nsteps, "seconds": t,
                 "window_GBps_per_gpu": per_gpu_Bps / 1e9,
                 "h2d_peak_GBps": peak / 1e9, "h2d_frac": per_gpu_Bps / peak,
-                "config": {"workload": "config5 shape: config2 files/GPU, windows in pinned host "
-                                       "memory, staged H2D (3-slab ring) + K1 + sharded grouping "
-                                       "+ Object link batch",
-                           "files_per_gpu": n, "window_bytes_per_gpu": window_bytes}}
+                "index_keys_rank0": distinct, "linked_rows_last_step_rank0": linked_last,
+                "config": {"workload": f"config5: identifier run over {files} files "
+                                       f"({nsteps} steps x {n} files/GPU x {W} GPU), windows in "
+                                       "pinned host memory, staged H2D (3-slab ring) + K1 + "
+                                       "grouping against the run's Object index "
+                                       + ("(sharded, RCCL)" if self.comm is not None else
+                                          "(one GPU)" if W == 1 else "(no index: rehearsal)")
+                                       + " + Object link batch",
+                           "files_per_gpu_per_step": n, "window_bytes_per_gpu_per_step": window_bytes}}
 
     # ---------------------------------------------------------------- config 1
     def run_dir(self, steps):
@@ -298,8 +356,10 @@ class Runner:
             for _ in range(steps):
                 res = fi.identify(paths, sizes=sizes, ctx=self.ctx)
             dt = self.max_over_ranks(time.perf_counter() - t0)
-            assert np.all(res.status == 0)
-            self._dir_sample = (paths, sizes, root)
+            assert np.all(res.status == 0) and np.all(res.has_key == 1)
+            # the GPU's cas ids are compared with the CPU baseline's (same files,
+            # the reference's reads) in the cpu_baseline leg
+            self._dir_sample = (paths, sizes, root, res.cas8.copy())
             return {"value": self.world * len(paths) * steps / dt, "unit": "files/s",
                     "ms_per_step": 1e3 * dt / steps,
                     "config": {"workload": "config1: 10k-file directory, log-uniform 1 KiB-10 MiB, "
@@ -395,11 +455,34 @@ class Runner:
                                 for k, b in alg.items() if kernels.get(k, {}).get("avg_ms")},
                     "note": "algorithmic bytes of this partition + group-by design "
                             "(DESIGN.md section 4); PMC traffic in profiles/"}
+        full = None
+        if self.world == 1 and self.args.dedup_full_rows:
+            full = self.run_dedup_full(steps, warmup)
         return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
-                "exchange": xchg, "roofline": roof,
+                "exchange": xchg, "roofline": roof, "config4_full_one_gpu": full,
                 "config": {"workload": "config4: 80% distinct u64 keys + 20% dups, 0.1% keyless",
                            "rows_per_gpu": per, "rows_total": total},
                 "kernels": kernels}
+
+    def run_dedup_full(self, steps, warmup):
+        """BASELINE config 4 at its full size on ONE GPU (the strong-scaling
+        base of the 1 -> 8 GPU curve): 100 M rows, 2^15 buckets, every bucket
+        grouped in LDS."""
+        torch = self.torch
+        from spacedrive_amd import corpus
+        total = self.args.dedup_full_rows
+        key, has, rank = corpus.synth_dedup_rows_device(4, total, int(total * 0.8), 0, total,
+                                                        device=self.local, ctx=self.ctx)
+        self.ctx.set_timing(True)
+        t = self.timed(lambda: self.ops.group_rows(key, has, rank, 100, 0), steps, warmup)
+        kt = self.ctx.kernel_times()
+        self.ctx.set_timing(False)
+        del key, has, rank
+        torch.cuda.empty_cache()
+        return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
+                "rows": total,
+                "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
+                            for k, v in kt.items()}}
 
     def verify_sharded(self, key, has, rank):
         """--verify: the sharded grouping over all ranks (the exchange path the
@@ -463,7 +546,7 @@ class Runner:
         h_len = ln[:m].cpu().numpy().view(np.uint32)
         end = int(h_off[-1] + h_len[-1])
         host = arena[:end].cpu().numpy()
-        threads = min(16, os.cpu_count() or 1)
+        threads, cores_note = host_cores()
         # the reference crate hashes a message's chunks 8/16 at a time with
         # SIMD: time the AVX2 8-way restatement (oracle/sd_oracle.c
         # orc_cas_batch_simd); the scalar oracle is reported beside it
@@ -490,15 +573,26 @@ class Runner:
         if getattr(self, "_dir_sample", None):
             import shutil
             from concurrent.futures import ThreadPoolExecutor
-            paths, sizes, root = self._dir_sample
+            paths, sizes, root, gpu_cas8 = self._dir_sample
+            O.cas_paths_simd(paths[:200], sizes[:200], threads)  # warm
+            t0 = time.perf_counter()
+            cpu_cas8, dst = O.cas_paths_simd(paths, sizes, threads)
+            ddt = time.perf_counter() - t0
+            assert np.all(dst == 0)
+            mism = int(np.count_nonzero(np.any(cpu_cas8 != gpu_cas8, axis=1)))
+            assert mism == 0, f"config-1 directory: {mism} GPU cas ids differ from the CPU port"
             with ThreadPoolExecutor(threads) as ex:  # the C oracle releases the GIL
-                list(ex.map(O.cas_id_path, paths[:200], sizes[:200].tolist()))
                 t0 = time.perf_counter()
                 list(ex.map(O.cas_id_path, paths, sizes.tolist()))
-                ddt = time.perf_counter() - t0
+                sdt = time.perf_counter() - t0
             dir_res = {"value": len(paths) / ddt, "unit": "files/s", "threads": threads,
-                       "sample": f"config 1: {len(paths)} files, oracle cas_id_path (open, "
-                                 f"header/sample/footer reads, scalar BLAKE3), warm cache"}
+                       "scalar_value": len(paths) / sdt, "gpu_cas_ids_checked": len(paths),
+                       "gpu_cas_id_mismatches": mism,
+                       "sample": f"config 1: {len(paths)} real files, warm cache, the "
+                                 f"reference's reads per file (open, header / 4 samples / "
+                                 f"footer, cas.rs:23-62) + AVX2 8-way BLAKE3 "
+                                 f"(oracle orc_cas_paths_simd), {threads} threads; "
+                                 f"scalar_value = scalar oracle cas_id_path, same threads"}
             shutil.rmtree(root, ignore_errors=True)
             self._dir_sample = None
         single = None
@@ -517,12 +611,15 @@ class Runner:
                         ts.append(time.perf_counter() - t0)
                     single[f"{fn_name}_{name}_us"] = float(np.median(ts) * 1e6)
         return {"value": reps * m / dt, "unit": "files/s", "cores": threads, "kind": "port",
+                "cores_note": cores_note,
                 "value_1thread": one, "scalar_value": scalar,
                 "config1_dir": dir_res, "single_file_1thread": single,
                 "sample": f"first {m} files of config 2 (their {int(h_len.sum())} window bytes "
                           f"in host RAM) hashed {reps}x, AVX2 8-way BLAKE3 port "
                           f"(oracle/sd_oracle.c orc_cas_batch_simd), {threads} threads, "
-                          f"{dt:.1f} s wall; scalar_value = scalar oracle, same threads"}
+                          f"{dt:.1f} s wall; scalar_value = scalar oracle, same threads; "
+                          f"value_1thread = one thread (the reference hashes a 100-file "
+                          f"step on one runtime thread, file_identifier/mod.rs:107-134)"}
 
 
 def self_launch(n: int) -> int:
@@ -548,10 +645,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--files", type=int, default=1_000_000)
     ap.add_argument("--dedup-rows", type=int, default=12_500_000)
+    ap.add_argument("--dedup-full-rows", type=int, default=100_000_000,
+                    help="config 4 at full size on one GPU (N = 1 only; 0 = skip)")
     ap.add_argument("--checksum-files", type=int, default=64)
     ap.add_argument("--checksum-bytes", type=int, default=1 << 32)
     ap.add_argument("--cpu-files", type=int, default=100_000)
     ap.add_argument("--staged-files", type=int, default=250_000)
+    ap.add_argument("--staged-total-files", type=int, default=50_000_000)
     ap.add_argument("--dir-files", type=int, default=10_000)
     ap.add_argument("--components", default="cas,dedup,checksum,staged,dir,single")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -609,7 +709,7 @@ def main():
         comp["dedup"] = d
         torch.cuda.empty_cache()
     if "staged" in comps:
-        g = R.run_staged(max(1, min(args.steps, 5)), 1)
+        g = R.run_staged()
         log("staged:", json.dumps(g))
         comp["staged"] = g
         torch.cuda.empty_cache()

@@ -323,6 +323,13 @@ int sdgpu_synth_dedup_rows_device(sdgpu_ctx *ctx, uint64_t seed, uint64_t total_
                                   uint64_t *d_key, uint8_t *d_has_key, uint32_t *d_rank,
                                   void *stream);
 
+/* Config-5 run (bench): step `step` of a run over one pinned pool of files --
+ * rows with d_vary[i] != 0 stand for files with new content (key' =
+ * mix64(key ^ step * 0x9E3779B97F4A7C15), a bijection); the others are the
+ * same files in every step.  step 0 leaves every key unchanged. */
+int sdgpu_synth_vary_keys_device(sdgpu_ctx *ctx, uint64_t *d_key, const uint8_t *d_vary,
+                                 uint64_t n, uint64_t step, void *stream);
+
 /* ---- instrumentation (bench / profiling) ---------------------------------------
  * With timing enabled every main kernel launched through ctx is bracketed by
  * HIP events on its own stream; sdgpu_timing_read returns, per kernel name

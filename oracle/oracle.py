@@ -71,6 +71,8 @@ def lib():
             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_balloon_blake3_trace.restype = ctypes.c_int64
+        L.orc_cas_paths_simd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         del u8p
         _lib = L
     return _lib
@@ -209,6 +211,20 @@ def cas_batch_simd(arena: np.ndarray, off: np.ndarray, length: np.ndarray,
     out = np.zeros((off.size, 8), np.uint8)
     lib().orc_cas_batch_simd(_ptr(arena), _ptr(off), _ptr(length), off.size, _ptr(out), threads)
     return out
+
+
+def cas_paths_simd(paths, sizes, threads: int = 1):
+    """(cas bytes [n, 8], status [n]) of real files: the reference's reads per
+    file (cas.rs:23-62) + the AVX2 8-way hasher, `threads` C threads (CPU
+    baseline of the config-1 directory)."""
+    n = len(paths)
+    enc = [os.fsencode(os.fspath(p)) for p in paths]
+    arr = (ctypes.c_char_p * n)(*enc)
+    sizes = np.ascontiguousarray(sizes, np.uint64)
+    out = np.zeros((n, 8), np.uint8)
+    st = np.zeros(n, np.int32)
+    lib().orc_cas_paths_simd(arr, _ptr(sizes), n, _ptr(out), _ptr(st), threads)
+    return out, st
 
 
 def synth_file_bytes(seed: int, offset: int, n: int) -> bytes:

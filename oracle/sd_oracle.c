@@ -1215,3 +1215,121 @@ void orc_cas_batch_simd(const uint8_t *arena, const uint64_t *off, const uint32_
   }
   for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
 }
+
+/* ------------------------------------------------------------------------- */
+/* generate_cas_id over real files with the reference's I/O pattern and the  */
+/* AVX2 hasher (CPU BASELINE ONLY: bench.py's config-1 leg).                 */
+/* ------------------------------------------------------------------------- */
+
+/* The bytes orc_cas_id_path feeds its hasher, read the same way (cas.rs:23-62:
+ * fs::read for <= 100 KiB, else open, read_exact header, 4 x {read_exact
+ * sample, seek}, seek End(-8192), read_exact footer) into a growable buffer;
+ * returns its length or -errno. */
+static int64_t cas_read_message(const char *path, uint64_t size, uint8_t **buf,
+                                size_t *cap) {
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  size_t len = 8;
+  int rc = 0;
+  if (*cap < 8 + CAS_MINIMUM_FILE_SIZE + 4096) {
+    free(*buf);
+    *cap = 8 + CAS_MINIMUM_FILE_SIZE + 4096;
+    *buf = (uint8_t *)malloc(*cap);
+    if (!*buf) {
+      close(fd);
+      return -ENOMEM;
+    }
+  }
+  for (int i = 0; i < 8; i++) (*buf)[i] = (uint8_t)(size >> (8 * i));
+  if (size <= CAS_MINIMUM_FILE_SIZE) {
+    for (;;) {
+      if (len == *cap) {
+        uint8_t *nb = (uint8_t *)realloc(*buf, *cap * 2);
+        if (!nb) {
+          rc = -ENOMEM;
+          break;
+        }
+        *buf = nb;
+        *cap *= 2;
+      }
+      ssize_t r = read(fd, *buf + len, *cap - len);
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        rc = -errno;
+        break;
+      }
+      if (r == 0) break;
+      len += (size_t)r;
+    }
+  } else {
+    uint8_t *p = *buf;
+    rc = read_exact_fd(fd, p + len, CAS_HEADER_OR_FOOTER);
+    len += CAS_HEADER_OR_FOOTER;
+    uint64_t current_pos = CAS_HEADER_OR_FOOTER;
+    uint64_t seek_jump = (size - CAS_HEADER_OR_FOOTER * 2) / CAS_SAMPLE_COUNT;
+    while (!rc) {
+      rc = read_exact_fd(fd, p + len, CAS_SAMPLE_SIZE);
+      if (rc) break;
+      len += CAS_SAMPLE_SIZE;
+      if (current_pos >= CAS_HEADER_OR_FOOTER + seek_jump * (CAS_SAMPLE_COUNT - 1)) break;
+      off_t np = lseek(fd, (off_t)(current_pos + seek_jump), SEEK_SET);
+      if (np < 0) rc = -errno;
+      else current_pos = (uint64_t)np;
+    }
+    if (!rc) {
+      if (lseek(fd, -(off_t)CAS_HEADER_OR_FOOTER, SEEK_END) < 0) rc = -errno;
+      if (!rc) rc = read_exact_fd(fd, p + len, CAS_HEADER_OR_FOOTER);
+      len += CAS_HEADER_OR_FOOTER;
+    }
+  }
+  close(fd);
+  return rc ? rc : (int64_t)len;
+}
+
+typedef struct {
+  const char *const *paths;
+  const uint64_t *sizes;
+  uint64_t n;
+  uint8_t *out8;
+  int32_t *status;
+  uint64_t *next; /* shared work counter (atomic) */
+} path_job;
+
+static void *path_worker(void *arg) {
+  path_job *j = (path_job *)arg;
+  uint8_t *buf = NULL;
+  size_t cap = 0;
+  for (;;) {
+    uint64_t i0 = __atomic_fetch_add(j->next, 64, __ATOMIC_RELAXED);
+    if (i0 >= j->n) break;
+    uint64_t i1 = i0 + 64 < j->n ? i0 + 64 : j->n;
+    for (uint64_t i = i0; i < i1; i++) {
+      int64_t len = cas_read_message(j->paths[i], j->sizes[i], &buf, &cap);
+      j->status[i] = len < 0 ? (int32_t)len : 0;
+      if (len < 0) {
+        memset(j->out8 + 8 * i, 0, 8);
+      } else if ((uint64_t)len <= 128u * B3_CHUNK) {
+        simd_hash8(buf, (size_t)len, j->out8 + 8 * i);
+      } else {
+        uint8_t d[32];
+        orc_blake3(buf, (size_t)len, d);
+        memcpy(j->out8 + 8 * i, d, 8);
+      }
+    }
+  }
+  free(buf);
+  return NULL;
+}
+
+/* cas bytes of n files (paths, stat sizes), `threads` threads pulling 64
+ * files at a time: the reference's reads per file + AVX2 hashing. */
+void orc_cas_paths_simd(const char *const *paths, const uint64_t *sizes, uint64_t n,
+                        uint8_t *out8, int32_t *status, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  uint64_t next = 0;
+  pthread_t th[256];
+  path_job job = {paths, sizes, n, out8, status, &next};
+  for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, path_worker, &job);
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}

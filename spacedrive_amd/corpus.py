@@ -153,3 +153,23 @@ def write_config1_dir(root: str, n: int = 10_000, seed: int = 1) -> tuple[list[s
             os.close(fd)
         paths.append(p)
     return paths, sizes
+
+
+def config5_vary_mask(sizes: np.ndarray, seeds: np.ndarray, frac16: int = 13) -> np.ndarray:
+    """Rows of the config-5 pool that stand for NEW files in every step of a
+    run (frac16/16 of the content seeds, ~81 %; duplicates share a seed, so they
+    stay duplicates); the rest are the same files in every step.  Empty files
+    have no key."""
+    sel = ((np.asarray(seeds, np.uint64) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(60)) < frac16
+    return (sel & (np.asarray(sizes) != 0)).astype(np.uint8)
+
+
+def vary_keys_device(key, vary, step: int, ctx=None):
+    """In place: the cas keys of step `step` of a config-5 run
+    (sdgpu_synth_vary_keys_device)."""
+    import torch
+    ctx = ctx or default_context(key.device.index)
+    s = torch.cuda.current_stream(key.device).cuda_stream
+    check(ctx.lib.sdgpu_synth_vary_keys_device(ctx.h, key.data_ptr(), vary.data_ptr(),
+                                               key.numel(), step, s),
+          "sdgpu_synth_vary_keys_device")

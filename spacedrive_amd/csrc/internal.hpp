@@ -96,6 +96,8 @@ hipError_t synth_file_launch(uint64_t seed, uint64_t offset, uint64_t len, uint8
 // kind 0: BLAKE3-G mix; 1 v_xor_b32; 2 v_add3_u32; 3 v_alignbit_b32; 4 v_add_u32.
 hipError_t valu_probe_launch(int kind, uint32_t* sink, uint32_t iters, uint32_t blocks,
                              hipStream_t s);
+hipError_t vary_keys_launch(uint64_t* key, const uint8_t* vary, uint64_t n, uint64_t step,
+                            hipStream_t s);
 hipError_t synth_dedup_rows_launch(uint64_t seed, uint64_t total_rows, uint64_t distinct,
                                    uint64_t first_rank, uint64_t n, uint64_t* key,
                                    uint8_t* has_key, uint32_t* rank, hipStream_t s);

@@ -1229,6 +1229,15 @@ int sdgpu_synth_file_device(sdgpu_ctx* c, uint64_t seed, uint64_t offset, uint64
   return 0;
 }
 
+int sdgpu_synth_vary_keys_device(sdgpu_ctx* c, uint64_t* d_key, const uint8_t* d_vary,
+                                 uint64_t n, uint64_t step, void* stream) {
+  if (!c || (n && (!d_key || !d_vary))) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  SD_TRY(vary_keys_launch(d_key, d_vary, n, step, pick(c, stream)));
+  return 0;
+}
+
 // ---- instrumentation -----------------------------------------------------------
 
 int sdgpu_set_timing(sdgpu_ctx* c, int enable) {

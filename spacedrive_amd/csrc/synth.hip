@@ -208,6 +208,26 @@ __global__ __launch_bounds__(256) void k_compress_probe(uint32_t* __restrict__ s
   if (x == 0x12345u) sink[blockIdx.x] = x;
 }
 
+// Config-5 run: the files of step `step` are the pool's files with new content
+// for the rows marked vary[i] -- a new content gives a new cas key, emulated as
+// key' = mix64(key ^ step * phi) (a bijection, so distinct files stay distinct
+// and duplicates stay duplicates); unmarked rows keep their key (files seen in
+// every step: they link to the Objects of the first).
+__global__ __launch_bounds__(kThreads) void k_vary_keys(uint64_t* __restrict__ key,
+                                                        const uint8_t* __restrict__ vary,
+                                                        uint64_t n, uint64_t step) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (i < n && vary[i]) key[i] = mix64(key[i] ^ (step * 0x9E3779B97F4A7C15ull));
+}
+
+hipError_t vary_keys_launch(uint64_t* key, const uint8_t* vary, uint64_t n, uint64_t step,
+                            hipStream_t s) {
+  if (n && step)
+    k_vary_keys<<<static_cast<uint32_t>((n + kThreads - 1) / kThreads), kThreads, 0, s>>>(
+        key, vary, n, step);
+  return hipGetLastError();
+}
+
 hipError_t valu_probe_launch(int kind, uint32_t* sink, uint32_t iters, uint32_t blocks,
                              hipStream_t s) {
   switch (kind) {
