@@ -4,7 +4,7 @@ ARCH ?= gfx950
 CSRC := spacedrive_amd/csrc
 BUILD := build/obj
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
-HIPSRC := $(CSRC)/b3_batch.hip $(CSRC)/b3_tree.hip $(CSRC)/dedup.hip $(CSRC)/index.hip $(CSRC)/synth.hip $(CSRC)/link.hip
+HIPSRC := $(CSRC)/b3_batch.hip $(CSRC)/b3_tree.hip $(CSRC)/dedup.hip $(CSRC)/index.hip $(CSRC)/consumers.hip $(CSRC)/synth.hip $(CSRC)/link.hip
 HOSTSRC := $(CSRC)/sdgpu.cpp $(CSRC)/shard.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.o,$(HIPSRC)) $(BUILD)/sdgpu.o $(BUILD)/shard.o
 HDRS := $(wildcard $(CSRC)/*.hpp) include/sdgpu.h

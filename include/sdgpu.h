@@ -309,6 +309,23 @@ int sdgpu_link_batch_device(sdgpu_ctx *ctx, const uint32_t *d_rep, const uint32_
                             uint32_t *d_create, uint32_t *d_link_row, uint32_t *d_link_obj,
                             uint32_t *d_counts, void *stream);
 
+/* ---- downstream consumers of the grouping ---------------
+ * Orphan remover (core/src/object/orphan_remover.rs:57-90: Objects with no
+ * file_path, `object::file_paths::none`, deleted 512 at a time): d_orphans
+ * receives the ids of d_object_ids that no entry of d_fp_object_ids (a
+ * file_path's object_id; negative = NULL) references, in list order;
+ * d_count[0] = how many.  Object ids must lie in [0, max_object_id]. */
+int sdgpu_orphan_objects_device(sdgpu_ctx *ctx, const int32_t *d_object_ids, uint64_t n_objects,
+                                const int32_t *d_fp_object_ids, uint64_t n_file_paths,
+                                uint32_t max_object_id, int32_t *d_orphans, uint32_t *d_count,
+                                void *stream);
+/* Thumbnail shards (core/src/object/media/thumbnail/shard.rs:4-8: directory =
+ * cas_id[0..2] = the first digest byte): d_order = the rows (d_valid[i] != 0,
+ * or all when NULL) ordered by shard directory, stable within a directory;
+ * d_counts[256] = rows per directory. */
+int sdgpu_thumbnail_shards_device(sdgpu_ctx *ctx, const uint8_t *d_cas8, const uint8_t *d_valid,
+                                  uint64_t n, uint32_t *d_order, uint32_t *d_counts, void *stream);
+
 /* ---- synthetic corpora (bench / tests; same content function as oracle/) ---- */
 int sdgpu_synth_cas_arena_device(sdgpu_ctx *ctx, const uint64_t *d_sizes, const uint64_t *d_seeds,
                                  const uint64_t *d_off, uint32_t n, uint8_t *d_arena, void *stream);

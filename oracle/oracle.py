@@ -314,3 +314,21 @@ def synth_dedup_rows(seed: int, total: int, distinct: int, first: int, n: int):
     rank = np.zeros(n, np.uint32)
     lib().orc_synth_dedup_rows(seed, total, distinct, first, n, _ptr(key), _ptr(has), _ptr(rank))
     return key, has, rank
+
+
+def orphan_objects(object_ids, fp_object_ids) -> np.ndarray:
+    """Orphan remover's query (/root/reference/core/src/object/orphan_remover.rs:
+    57-90, `object::file_paths::none`): the Objects no file_path references, in
+    list order."""
+    ref = set(int(x) for x in np.asarray(fp_object_ids) if x >= 0)
+    return np.array([o for o in np.asarray(object_ids).tolist() if o not in ref], np.int32)
+
+
+def thumbnail_shards(cas8: np.ndarray, valid=None):
+    """Thumbnail directories (/root/reference/core/src/object/media/thumbnail/
+    shard.rs:4-8: cas_id[0..2] = the first digest byte): rows ordered by
+    directory, stable; rows per directory."""
+    first = np.asarray(cas8)[:, 0].astype(np.int64)
+    rows = np.arange(first.size) if valid is None else np.flatnonzero(np.asarray(valid))
+    order = rows[np.argsort(first[rows], kind="stable")]
+    return order.astype(np.int32), np.bincount(first[rows], minlength=256).astype(np.int32)

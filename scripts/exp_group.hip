@@ -1,0 +1,236 @@
+// Experiment (not shipped): where does K5 bucket_group's time go, and does
+// splitting each bucket over two 512-thread workgroups (4 per CU) help?
+// 12.5 M config-4-shaped rows (80 % distinct keys, 20 % duplicates), the
+// product's partition (hist + scan + staged scatter) done once, then:
+//   G0  the product k_bucket_group (1024 threads, 6144-slot table, 2 per CU)
+//   G1  G0 without the scattered rep writes (a checksum keeps the work live)
+//   G2  two 512-thread workgroups per bucket, each grouping the half of the
+//       bucket's keys selected by hash bit 32 in a 3072-slot table (4 per CU);
+//       both read the whole bucket (the second from L2: same XCD)
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_group.hip -o build/exp_group
+#include "../spacedrive_amd/csrc/dedup.hip"
+
+#include <stdio.h>
+
+#include <vector>
+
+using namespace sdgpu;
+
+namespace {
+
+__global__ void k_rows(uint64_t* key, uint32_t* rank, uint64_t n, uint64_t distinct) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    const uint64_t j = (i * 0x9E3779B1ull) % n;  // a permutation of the rows (n odd multiple ok)
+    key[i] = row_hash((j % distinct) * 0x2545F4914F6CDD1Dull + 7);
+    rank[i] = static_cast<uint32_t>(i);
+  }
+}
+
+template <bool kWrite>
+__global__ __launch_bounds__(kGroupThreads, 8) void g0(const uint4* __restrict__ rec,
+                                                        const uint32_t* __restrict__ offs,
+                                                        uint32_t P, uint32_t chunk_rows,
+                                                        uint32_t* __restrict__ rep,
+                                                        uint32_t* __restrict__ sink) {
+  __shared__ uint64_t lkey[kLdsSlots];
+  __shared__ uint32_t lmin[kLdsSlots];
+  const uint32_t b = blockIdx.x;
+  const uint32_t start = offs[static_cast<uint64_t>(b) * P];
+  const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];
+  if (end - start > kLdsCap) return;  // (no such bucket in this data)
+  uint4 q[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint32_t i = start + threadIdx.x + j * kGroupThreads;
+    q[j] = i < end ? rec[i] : make_uint4(0, 0, 0, 0);
+  }
+  for (uint32_t s = threadIdx.x; s < kLdsSlots; s += kGroupThreads) {
+    lkey[s] = kEmpty;
+    lmin[s] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  uint32_t h[kPer], pend = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+    h[j] = lds_slot(k);
+    if (start + threadIdx.x + j * kGroupThreads < end) pend |= 1u << j;
+  }
+  const uint32_t live = pend;
+  while (pend) {
+    uint64_t prev[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+      prev[j] = (pend >> j & 1u) ? atomicCAS(reinterpret_cast<unsigned long long*>(&lkey[h[j]]),
+                                             static_cast<unsigned long long>(kEmpty),
+                                             static_cast<unsigned long long>(k))
+                                 : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (!(pend >> j & 1u)) continue;
+      const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+      if (prev[j] == kEmpty || prev[j] == k) {
+        atomicMin(&lmin[h[j]], q[j].z);
+        pend &= ~(1u << j);
+      } else {
+        h[j] = next_slot(h[j]);
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if (!(live >> j & 1u)) continue;
+    const uint32_t r = q[j].z, f = lmin[h[j]];
+    if (r / chunk_rows != f / chunk_rows) {
+      if (kWrite) rep[q[j].w] = f;
+      else acc += f ^ q[j].w;
+    }
+  }
+  if (!kWrite && acc == 0x12345678u) sink[0] = acc;
+}
+
+constexpr int kT2 = 512;
+constexpr uint32_t kSlots2 = 3072;
+constexpr int kPer2 = (kLdsCap + kT2 - 1) / kT2;  // 9: the whole bucket per workgroup
+
+__device__ __forceinline__ uint32_t lds_slot2(uint64_t k) {
+  const uint32_t h = static_cast<uint32_t>(row_hash(k));
+  return static_cast<uint32_t>((static_cast<uint64_t>(h) * kSlots2) >> 32);
+}
+
+__global__ __launch_bounds__(kT2, 4) void g2(const uint4* __restrict__ rec,
+                                              const uint32_t* __restrict__ offs, uint32_t P,
+                                              uint32_t chunk_rows, uint32_t* __restrict__ rep) {
+  __shared__ uint64_t lkey[kSlots2];
+  __shared__ uint32_t lmin[kSlots2];
+  // physical block p: XCD p % 8; the two halves of a bucket are consecutive
+  // slots of one XCD (p and p + 8)
+  const uint32_t p = blockIdx.x;
+  const uint32_t b = ((p >> 4) << 3) | (p & 7u);
+  const uint32_t half = (p >> 3) & 1u;
+  const uint32_t start = offs[static_cast<uint64_t>(b) * P];
+  const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];
+  if (end - start > kLdsCap) return;
+  uint4 q[kPer2];
+#pragma unroll
+  for (int j = 0; j < kPer2; ++j) {
+    const uint32_t i = start + threadIdx.x + j * kT2;
+    q[j] = i < end ? rec[i] : make_uint4(0, 0, 0, 0);
+  }
+  for (uint32_t s = threadIdx.x; s < kSlots2; s += kT2) {
+    lkey[s] = kEmpty;
+    lmin[s] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  uint32_t h[kPer2], pend = 0;
+#pragma unroll
+  for (int j = 0; j < kPer2; ++j) {
+    const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+    h[j] = lds_slot2(k);
+    if (start + threadIdx.x + j * kT2 < end && ((row_hash(k) >> 32) & 1u) == half)
+      pend |= 1u << j;
+  }
+  const uint32_t live = pend;
+  while (pend) {
+    uint64_t prev[kPer2];
+#pragma unroll
+    for (int j = 0; j < kPer2; ++j) {
+      const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+      prev[j] = (pend >> j & 1u) ? atomicCAS(reinterpret_cast<unsigned long long*>(&lkey[h[j]]),
+                                             static_cast<unsigned long long>(kEmpty),
+                                             static_cast<unsigned long long>(k))
+                                 : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer2; ++j) {
+      if (!(pend >> j & 1u)) continue;
+      const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+      if (prev[j] == kEmpty || prev[j] == k) {
+        atomicMin(&lmin[h[j]], q[j].z);
+        pend &= ~(1u << j);
+      } else {
+        h[j] = h[j] + 1 == kSlots2 ? 0u : h[j] + 1;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPer2; ++j) {
+    if (!(live >> j & 1u)) continue;
+    const uint32_t r = q[j].z, f = lmin[h[j]];
+    if (r / chunk_rows != f / chunk_rows) rep[q[j].w] = f;
+  }
+}
+
+template <typename F>
+float time_ms(F f, int reps) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  f();
+  std::vector<float> v;
+  for (int r = 0; r < reps; ++r) {
+    (void)hipEventRecord(a, 0);
+    f();
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    v.push_back(ms);
+  }
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 12500000ull;
+  uint64_t* key;
+  uint32_t *rank, *rep, *rep2, *sink;
+  (void)hipMalloc(&key, 8 * n);
+  (void)hipMalloc(&rank, 4 * n);
+  (void)hipMalloc(&rep, 4 * n);
+  (void)hipMalloc(&rep2, 4 * n);
+  (void)hipMalloc(&sink, 64);
+  k_rows<<<4096, 256>>>(key, rank, n, n * 4 / 5);
+  void* ws;
+  const GroupLayout L = group_layout(n);
+  (void)hipMalloc(&ws, L.total);
+  GroupInput in;
+  in.key = key;
+  in.rank = rank;
+  in.n = n;
+  // the product path once (rep = reference answer) -- leaves rec + offsets in ws
+  (void)dedup_local_launch(in, 100, rep, true, ws, 0, nullptr);
+  (void)hipDeviceSynchronize();
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  const uint4* rec = reinterpret_cast<const uint4*>(w + L.rec);
+  const uint32_t* hist = reinterpret_cast<const uint32_t*>(w + L.hist);
+  const uint32_t P = bucket_part_blocks(), nb = 1u << L.bits;
+  printf("n %llu bits %u buckets %u\n", (unsigned long long)n, L.bits, nb);
+  const float full = time_ms([&] { (void)dedup_local_launch(in, 100, rep, true, ws, 0, nullptr); }, 9);
+  const float t0 = time_ms([&] { g0<true><<<nb, kGroupThreads>>>(rec, hist, P, 100, rep2, sink); }, 9);
+  const float t1 = time_ms([&] { g0<false><<<nb, kGroupThreads>>>(rec, hist, P, 100, rep2, sink); }, 9);
+  // G2 correctness: start from the scatter's initial rep (= rank), then G2
+  (void)dedup_local_launch(in, 100, rep2, true, ws, 0, nullptr);
+  (void)hipMemcpy(rep2, rank, 4 * n, hipMemcpyDeviceToDevice);
+  g2<<<2 * nb, kT2>>>(rec, hist, P, 100, rep2);
+  (void)hipDeviceSynchronize();
+  std::vector<uint32_t> a(n), c(n);
+  (void)hipMemcpy(a.data(), rep, 4 * n, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(c.data(), rep2, 4 * n, hipMemcpyDeviceToHost);
+  uint64_t bad = 0;
+  for (uint64_t i = 0; i < n; ++i) bad += a[i] != c[i];
+  const float t2 = time_ms([&] { g2<<<2 * nb, kT2>>>(rec, hist, P, 100, rep2); }, 9);
+  printf("full grouping (hist+scan+scatter+group) %.4f ms\n", full);
+  printf("G0 product group            %.4f ms\n", t0);
+  printf("G1 no rep writes            %.4f ms\n", t1);
+  printf("G2 2x512 halves per bucket  %.4f ms  (mismatches vs product: %llu)\n", t2,
+         (unsigned long long)bad);
+  return bad ? 1 : 0;
+}

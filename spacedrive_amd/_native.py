@@ -88,6 +88,8 @@ def _proto(L):
         "sdgpu_synth_file_device": (i32, [ctx, u64, u64, u64, c_vp, c_vp]),
         "sdgpu_synth_dedup_rows_device": (i32, [ctx, u64, u64, u64, u64, u64, c_vp, c_vp, c_vp,
                                                 c_vp]),
+        "sdgpu_orphan_objects_device": (i32, [ctx, c_vp, u64, c_vp, u64, u32, c_vp, c_vp, c_vp]),
+        "sdgpu_thumbnail_shards_device": (i32, [ctx, c_vp, c_vp, u64, c_vp, c_vp, c_vp]),
         "sdgpu_synth_vary_keys_device": (i32, [ctx, c_vp, c_vp, u64, u64, c_vp]),
         "sdgpu_set_timing": (i32, [ctx, i32]),
         "sdgpu_timing_reset": (i32, [ctx]),

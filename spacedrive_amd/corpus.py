@@ -168,6 +168,7 @@ def vary_keys_device(key, vary, step: int, ctx=None):
     """In place: the cas keys of step `step` of a config-5 run
     (sdgpu_synth_vary_keys_device)."""
     import torch
+    from ._native import check, default_context
     ctx = ctx or default_context(key.device.index)
     s = torch.cuda.current_stream(key.device).cuda_stream
     check(ctx.lib.sdgpu_synth_vary_keys_device(ctx.h, key.data_ptr(), vary.data_ptr(),

@@ -1,0 +1,206 @@
+// Downstream consumers of the grouping, on the device.
+//
+// Orphan remover (/root/reference/core/src/object/orphan_remover.rs:57-90):
+// Objects with no file_path pointing at them (`object::file_paths::none`) are
+// found 512 at a time and deleted.  Here: one pass marks every Object id that
+// some file_path references (a bitmap over ids, atomicOr), a second pass keeps
+// the unreferenced ids of the Object list, in list order (block-local LDS
+// compaction + one scan), ready for the caller's delete batches.
+//
+// Thumbnail shards (/root/reference/core/src/object/media/thumbnail/shard.rs:4-8):
+// a thumbnail lives in directory cas_id[0..2], the first digest byte, i.e. the
+// low byte of the little-endian cas key.  Here: a batch's rows counting-sorted
+// by that byte (256 directories), so a thumbnailer writes each directory's
+// files together; counts per directory alongside.
+#include "internal.hpp"
+#include "scan_device.hpp"
+
+namespace sdgpu {
+
+namespace {
+
+constexpr int kThreads = 256;
+
+uint32_t grid_for(uint64_t n, uint64_t per = kThreads) {
+  const uint64_t g = (n + per - 1) / per;
+  return static_cast<uint32_t>(g == 0 ? 1 : (g < 65535 ? g : 65535));
+}
+
+__global__ __launch_bounds__(kThreads) void k_clear_words(uint32_t* __restrict__ w, uint64_t n) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride)
+    w[i] = 0;
+}
+
+// bitmap bit o = some file_path references Object o (negative = NULL object_id)
+__global__ __launch_bounds__(kThreads) void k_mark(const int32_t* __restrict__ fp_obj, uint64_t n,
+                                                   uint32_t* __restrict__ bits, uint32_t max_id) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n;
+       i += stride) {
+    const int32_t o = fp_obj[i];
+    if (o >= 0 && static_cast<uint32_t>(o) <= max_id) atomicOr(&bits[o >> 5], 1u << (o & 31));
+  }
+}
+
+// Object o is an orphan: no file_path marked it (ids past max_id are never marked)
+__device__ __forceinline__ bool orphan(int32_t o, const uint32_t* bits, uint32_t max_id) {
+  return o >= 0 && (static_cast<uint32_t>(o) > max_id || !(bits[o >> 5] >> (o & 31) & 1u));
+}
+
+// per block of kThreads Objects: how many are orphans
+__global__ __launch_bounds__(kThreads) void k_orphan_count(const int32_t* __restrict__ obj,
+                                                           uint64_t n,
+                                                           const uint32_t* __restrict__ bits,
+                                                           uint32_t max_id,
+                                                           uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t c;
+  if (threadIdx.x == 0) c = 0;
+  __syncthreads();
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (i < n) {
+    if (orphan(obj[i], bits, max_id)) atomicAdd(&c, 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = c;
+}
+
+// stable compaction: block b writes its orphans at the scanned offset, in order
+__global__ __launch_bounds__(kThreads) void k_orphan_write(const int32_t* __restrict__ obj,
+                                                           uint64_t n,
+                                                           const uint32_t* __restrict__ bits,
+                                                           uint32_t max_id,
+                                                           const uint32_t* __restrict__ offs,
+                                                           int32_t* __restrict__ out) {
+  __shared__ uint32_t flag[kThreads];
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  uint32_t f = 0;
+  int32_t o = -1;
+  if (i < n) {
+    o = obj[i];
+    f = orphan(o, bits, max_id) ? 1u : 0u;
+  }
+  flag[threadIdx.x] = f;
+  __syncthreads();
+  for (int d = 1; d < kThreads; d <<= 1) {  // inclusive scan of the block's flags
+    const uint32_t t = threadIdx.x >= d ? flag[threadIdx.x - d] : 0u;
+    __syncthreads();
+    flag[threadIdx.x] += t;
+    __syncthreads();
+  }
+  if (f) out[offs[blockIdx.x] + flag[threadIdx.x] - 1] = o;
+}
+
+// ---- thumbnail shards -----------------------------------------------------------
+constexpr uint32_t kShardBins = 256;
+constexpr uint32_t kShardBlocks = 256;
+
+__device__ __forceinline__ void tile(uint64_t n, uint64_t& t0, uint64_t& t1) {
+  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+  t0 = min<uint64_t>(n, per * blockIdx.x);
+  t1 = min<uint64_t>(n, t0 + per);
+}
+
+__global__ __launch_bounds__(kThreads) void k_thumb_hist(const uint8_t* __restrict__ cas8,
+                                                         const uint8_t* __restrict__ valid,
+                                                         uint64_t n, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kShardBins];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t t0, t1;
+  tile(n, t0, t1);
+  for (uint64_t i = t0 + threadIdx.x; i < t1; i += kThreads)
+    if (!valid || valid[i]) atomicAdd(&h[cas8[8 * i]], 1u);
+  __syncthreads();
+  hist[static_cast<uint64_t>(threadIdx.x) * gridDim.x + blockIdx.x] = h[threadIdx.x];
+}
+
+// stable within a block's tile: one round of kThreads rows at a time; a row's
+// place in its bin = earlier rows of the round with the same byte (LDS scan)
+__global__ __launch_bounds__(kThreads) void k_thumb_scatter(const uint8_t* __restrict__ cas8,
+                                                            const uint8_t* __restrict__ valid,
+                                                            uint64_t n,
+                                                            const uint32_t* __restrict__ offs,
+                                                            uint32_t* __restrict__ order) {
+  __shared__ uint32_t cur[kShardBins];
+  __shared__ uint8_t sb[kThreads];
+  __shared__ uint8_t sv[kThreads];
+  cur[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * gridDim.x + blockIdx.x];
+  uint64_t t0, t1;
+  tile(n, t0, t1);
+  for (uint64_t i0 = t0; i0 < t1; i0 += kThreads) {
+    const uint64_t i = i0 + threadIdx.x;
+    const bool v = i < t1 && (!valid || valid[i]);
+    const uint8_t b = i < t1 ? cas8[8 * i] : 0;
+    __syncthreads();
+    sb[threadIdx.x] = b;
+    sv[threadIdx.x] = v ? 1 : 0;
+    __syncthreads();
+    if (v) {
+      uint32_t before = 0;  // earlier rows of this round in the same bin
+      for (uint32_t t = 0; t < threadIdx.x; ++t) before += (sv[t] && sb[t] == b) ? 1u : 0u;
+      order[cur[b] + before] = static_cast<uint32_t>(i);
+    }
+    __syncthreads();
+    {  // advance the cursors by this round's counts (thread = bin)
+      uint32_t c = 0;
+      for (uint32_t t = 0; t < kThreads; ++t) c += (sv[t] && sb[t] == threadIdx.x) ? 1u : 0u;
+      cur[threadIdx.x] += c;
+    }
+  }
+}
+
+__global__ void k_thumb_counts(const uint32_t* __restrict__ offs, uint32_t* __restrict__ counts) {
+  const uint32_t b = threadIdx.x;
+  counts[b] = offs[static_cast<uint64_t>(b + 1) * kShardBlocks] -
+              offs[static_cast<uint64_t>(b) * kShardBlocks];
+}
+
+}  // namespace
+
+size_t orphan_workspace_bytes(uint64_t n_obj, uint32_t max_id) {
+  const uint64_t words = (static_cast<uint64_t>(max_id) >> 5) + 1;
+  const uint64_t blocks = (n_obj + kThreads - 1) / kThreads;
+  return 4 * words + 4 * (blocks + 1) + 4 * (scan::tiles_for(blocks) + 1) + 1024;
+}
+
+hipError_t orphan_objects_launch(const int32_t* obj, uint64_t n_obj, const int32_t* fp_obj,
+                                 uint64_t n_fp, uint32_t max_id, int32_t* out, uint32_t* d_count,
+                                 void* ws, hipStream_t s) {
+  const uint64_t words = (static_cast<uint64_t>(max_id) >> 5) + 1;
+  const uint64_t blocks = (n_obj + kThreads - 1) / kThreads;
+  uint32_t* bits = static_cast<uint32_t*>(ws);
+  uint32_t* cnt = bits + words;
+  uint32_t* tiles = cnt + blocks + 1;
+  k_clear_words<<<grid_for(words), kThreads, 0, s>>>(bits, words);
+  if (n_fp) k_mark<<<grid_for(n_fp, 4 * kThreads), kThreads, 0, s>>>(fp_obj, n_fp, bits, max_id);
+  if (blocks) {
+    k_orphan_count<<<static_cast<uint32_t>(blocks), kThreads, 0, s>>>(obj, n_obj, bits, max_id,
+                                                                      cnt);
+    scan::exclusive(cnt, blocks, cnt, tiles, d_count, s);
+    k_orphan_write<<<static_cast<uint32_t>(blocks), kThreads, 0, s>>>(obj, n_obj, bits, max_id,
+                                                                      cnt, out);
+  } else {
+    (void)hipMemsetAsync(d_count, 0, 4, s);
+  }
+  return hipGetLastError();
+}
+
+size_t thumb_workspace_bytes() {
+  const uint64_t nh = static_cast<uint64_t>(kShardBins) * kShardBlocks;
+  return 4 * (nh + 1) + 4 * (scan::tiles_for(nh) + 1) + 512;
+}
+
+hipError_t thumbnail_shards_launch(const uint8_t* cas8, const uint8_t* valid, uint64_t n,
+                                   uint32_t* order, uint32_t* counts, void* ws, hipStream_t s) {
+  const uint64_t nh = static_cast<uint64_t>(kShardBins) * kShardBlocks;
+  uint32_t* hist = static_cast<uint32_t*>(ws);
+  uint32_t* tiles = hist + nh + 1;
+  k_thumb_hist<<<kShardBlocks, kThreads, 0, s>>>(cas8, valid, n, hist);
+  scan::exclusive(hist, nh, hist, tiles, nullptr, s);
+  k_thumb_scatter<<<kShardBlocks, kThreads, 0, s>>>(cas8, valid, n, hist, order);
+  k_thumb_counts<<<1, kShardBins, 0, s>>>(hist, counts);
+  return hipGetLastError();
+}
+
+}  // namespace sdgpu

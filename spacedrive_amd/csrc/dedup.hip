@@ -59,7 +59,7 @@ constexpr int kGroupThreads = 1024;
 constexpr uint32_t kLdsSlots = 6144;
 constexpr uint32_t kLdsCap = 4608;     // rows per bucket handled in LDS (load <= 75%)
 constexpr uint64_t kBucketRows = 3072; // target mean rows per bucket (bucket_bits_for)
-constexpr uint32_t kMaxBucketBits = 15;  // 32768 LDS cursors = 128 KiB: 100 M rows stay in LDS
+constexpr uint32_t kMaxBucketBits = 15;  // 2^15 buckets: 100 M rows stay in LDS
 constexpr uint32_t kShardBits = 8;       // multi-GPU shards: h >> 56
 constexpr uint64_t kEmpty = ~0ull;
 
@@ -179,14 +179,14 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
   constexpr int U = kUnroll;
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += U * kPartThreads) {
     uint64_t k[U];
-    uint32_t r[U];
+    uint32_t r[U], row[U];
     bool in_[U], v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
       in_[u] = i < t1;
       v[u] = false;
-      if (in_[u]) in.get(i, k[u], r[u], v[u]);
+      if (in_[u]) in.get_row(i, k[u], r[u], row[u], v[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
       if (!v[u]) continue;
       const uint32_t p = atomicAdd(&cur[digit_of(row_hash(k[u]), skip, bits)], 1u);
       rec[p] = make_uint4(static_cast<uint32_t>(k[u]), static_cast<uint32_t>(k[u] >> 32), r[u],
-                          static_cast<uint32_t>(i));
+                          row[u]);
     }
   }
 }
@@ -207,22 +207,35 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
 // scattered writes are half as many and twice as wide.  Rows arriving at a full
 // slot are written directly.  Rows are taken 2 per thread per round; each
 // round ends with a flush of the full pairs; the odd rows go out at the end.
+// Two-level use (n > 4096 x kBucketRows): blockIdx.y = segment c of a first,
+// coarse pass ([seg[c * P1], seg[(c + 1) * P1]) of its records), the digit is
+// the 12 hash bits below the segment's, and the offsets are laid out
+// [c][digit][block] -- so the group kernel sees 2^(cbits + 12) buckets.
 constexpr uint32_t kStageBits = 12;
 template <typename In, bool kInitRep>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     In in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ offs, uint4* __restrict__ rec,
-    uint32_t* __restrict__ rep) {
+    uint32_t* __restrict__ rep, const uint32_t* __restrict__ seg, uint32_t P1) {
   constexpr uint32_t nbins = 1u << kStageBits;
   __shared__ uint4 stage[nbins][2];
   __shared__ uint32_t fill[nbins];
   __shared__ uint32_t cur[nbins];
+  const uint32_t c = blockIdx.y;
+  const uint64_t obase = static_cast<uint64_t>(c) * nbins * gridDim.x;
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) {
-    cur[b] = offs[static_cast<uint64_t>(b) * gridDim.x + part_block()];
+    cur[b] = offs[obase + static_cast<uint64_t>(b) * gridDim.x + part_block()];
     fill[b] = 0;
   }
   __syncthreads();
   uint64_t t0, t1;
-  tile_of(n, gridDim.x, t0, t1);
+  if (seg) {
+    const uint64_t s0 = seg[static_cast<uint64_t>(c) * P1], s1 = seg[static_cast<uint64_t>(c + 1) * P1];
+    tile_of(s1 - s0, gridDim.x, t0, t1);
+    t0 += s0;
+    t1 += s0;
+  } else {
+    tile_of(n, gridDim.x, t0, t1);
+  }
   constexpr int U = 2;
   for (uint64_t i0 = t0; i0 < t1; i0 += U * kPartThreads) {  // uniform trip count
 #pragma unroll
@@ -230,14 +243,13 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       const uint64_t i = i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads;
       if (i >= t1) continue;
       uint64_t k;
-      uint32_t r;
+      uint32_t r, row;
       bool v;
-      in.get(i, k, r, v);
+      in.get_row(i, k, r, row, v);
       if (kInitRep) rep[i] = r;
       if (!v) continue;
       const uint32_t b = digit_of(row_hash(k), skip, kStageBits);
-      const uint4 q = make_uint4(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32), r,
-                                 static_cast<uint32_t>(i));
+      const uint4 q = make_uint4(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32), r, row);
       const uint32_t sl = atomicAdd(&fill[b], 1u);
       if (sl < 2) {
         stage[b][sl] = q;
@@ -259,6 +271,40 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
   }
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
     if (fill[b] == 1) rec[cur[b]] = stage[b][0];
+}
+
+// Histogram of the second pass: block (j, c) counts tile j of segment c's
+// records on the 12 digit bits below the segment's.
+__global__ __launch_bounds__(kPartThreads) void k_part2_hist(Rec16In in, uint32_t skip,
+                                                             const uint32_t* __restrict__ seg,
+                                                             uint32_t P1,
+                                                             uint32_t* __restrict__ hist) {
+  constexpr uint32_t nbins = 1u << kStageBits;
+  __shared__ uint32_t cnt[nbins];
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) cnt[b] = 0;
+  __syncthreads();
+  const uint32_t c = blockIdx.y;
+  const uint64_t s0 = seg[static_cast<uint64_t>(c) * P1], s1 = seg[static_cast<uint64_t>(c + 1) * P1];
+  uint64_t t0, t1;
+  tile_of(s1 - s0, gridDim.x, t0, t1);
+  for (uint64_t i0 = s0 + t0 + threadIdx.x; i0 < s0 + t1; i0 += kUnroll * kPartThreads) {
+    uint64_t k[kUnroll];
+    bool v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
+      uint32_t r;
+      v[u] = false;
+      if (i < s0 + t1) in.get(i, k[u], r, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+      if (v[u]) atomicAdd(&cnt[digit_of(row_hash(k[u]), skip, kStageBits)], 1u);
+  }
+  __syncthreads();
+  const uint64_t obase = static_cast<uint64_t>(c) * nbins * gridDim.x;
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
+    hist[obase + static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
 }
 
 // First probe slot of key k in the LDS table (kLdsSlots, any size): the low
@@ -492,19 +538,29 @@ uint32_t bucket_bits_for(uint64_t n) {
   return bits;
 }
 
+// Above 2^12 buckets (n > ~12.6 M rows) the partition runs in two passes: a
+// coarse one on the top cbits = bits - 12 digit bits (<= 8 output streams per
+// block: full-line writes) into rec1, then the 12-bit LDS-staged pass per
+// coarse segment into rec.  A single 2^15-way scatter keeps 32 k partially
+// written lines open per block and ran 3.7 ms for 100 M rows
+// (profiles/r2/bench_r2b.json); the two passes move 2 x 32 B per row instead.
 struct GroupLayout {
-  uint32_t bits;
-  size_t hist, tiles, rec, gkey, gmin, total;
+  uint32_t bits, cbits;
+  size_t hist, tiles, rec, hist1, rec1, gkey, gmin, total;
 };
 
 GroupLayout group_layout(uint64_t n) {
   GroupLayout L;
   L.bits = bucket_bits_for(n);
+  L.cbits = L.bits > kStageBits ? L.bits - kStageBits : 0;
   const uint64_t nh = (static_cast<uint64_t>(1) << L.bits) * kMaxPartBlocks;
+  const uint64_t nh1 = (static_cast<uint64_t>(1) << L.cbits) * kMaxPartBlocks;
   size_t o = 0;
   L.hist = o; o = align_up(o + 4 * (nh + 1), 256);
   L.tiles = o; o = align_up(o + 4 * (scan::tiles_for(nh) + 1), 256);
   L.rec = o; o = align_up(o + 16 * n, 256);
+  L.hist1 = o; o = align_up(o + 4 * (nh1 + 1), 256);
+  L.rec1 = o; o = align_up(o + (L.cbits ? 16 * n : 0), 256);
   L.gkey = o; o = align_up(o + 8 * 4 * n, 256);
   L.gmin = o; o = align_up(o + 4 * 4 * n, 256);
   L.total = o;
@@ -533,6 +589,43 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   const uint32_t P = bucket_part_blocks();
   const uint64_t nh = (static_cast<uint64_t>(1) << bits) * P;
   const size_t lds = sizeof(uint32_t) << bits;
+  if (L.cbits) {
+    // pass 1: coarse partition on the top cbits digit bits (rep initialised here)
+    uint32_t* hist1 = reinterpret_cast<uint32_t*>(w + L.hist1);
+    uint4* rec1 = reinterpret_cast<uint4*>(w + L.rec1);
+    const uint32_t nseg = 1u << L.cbits;
+    const size_t lds1 = sizeof(uint32_t) << L.cbits;
+    {
+      KScope k(timer, "bucket_hist", s);
+      k_part_hist<In><<<P, kPartThreads, lds1, s>>>(in, n, kShardBits, L.cbits, hist1);
+    }
+    scan::exclusive(hist1, static_cast<uint64_t>(nseg) * P, hist1, tiles, nullptr, s);
+    {
+      KScope k(timer, "bucket_scatter1", s);
+      if (init_rep)
+        k_part_scatter_rec<In, true><<<P, kPartThreads, lds1, s>>>(in, n, kShardBits, L.cbits,
+                                                                   hist1, rec1, rep);
+      else
+        k_part_scatter_rec<In, false><<<P, kPartThreads, lds1, s>>>(in, n, kShardBits, L.cbits,
+                                                                    hist1, rec1, rep);
+    }
+    // pass 2: 12 bits below, per coarse segment, staged
+    const Rec16In in2{rec1};
+    {
+      KScope k(timer, "bucket_hist2", s);
+      k_part2_hist<<<dim3(P, nseg), kPartThreads, 0, s>>>(in2, kShardBits + L.cbits, hist1, P,
+                                                           hist);
+    }
+    scan::exclusive(hist, nh, hist, tiles, nullptr, s);
+    {
+      KScope k(timer, "bucket_scatter", s);
+      k_part_scatter_rec_staged<Rec16In, false><<<dim3(P, nseg), kPartThreads, 0, s>>>(
+          in2, 0, kShardBits + L.cbits, hist, rec, nullptr, hist1, P);
+    }
+    KScope k(timer, "bucket_group", s);
+    k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, chunk_rows, gkey, gmin, rep);
+    return hipGetLastError();
+  }
   {
     KScope k(timer, "bucket_hist", s);
     allow_lds(k_part_hist<In>, lds);
@@ -544,10 +637,10 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
     const bool staged = bits == kStageBits && !getenv("SDGPU_SCATTER_UNSTAGED");
     if (staged && init_rep)
       k_part_scatter_rec_staged<In, true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, hist, rec,
-                                                                     rep);
+                                                                     rep, nullptr, 0);
     else if (staged)
       k_part_scatter_rec_staged<In, false><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, hist,
-                                                                      rec, rep);
+                                                                      rec, rep, nullptr, 0);
     else if (init_rep) {
       allow_lds(k_part_scatter_rec<In, true>, lds);
       k_part_scatter_rec<In, true><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, hist, rec,

@@ -159,6 +159,15 @@ hipError_t index_probe_launch(const IndexRef& t, const GroupInput& in, uint32_t 
 hipError_t index_creators_launch(const IndexRef& t, const GroupInput& in, const uint32_t* rep,
                                  const uint8_t* grouped, hipStream_t s, KTimer* timer = nullptr);
 
+// ---- downstream consumers (consumers.hip) ---------------------------------------
+size_t orphan_workspace_bytes(uint64_t n_obj, uint32_t max_id);
+hipError_t orphan_objects_launch(const int32_t* obj, uint64_t n_obj, const int32_t* fp_obj,
+                                 uint64_t n_fp, uint32_t max_id, int32_t* out, uint32_t* d_count,
+                                 void* ws, hipStream_t s);
+size_t thumb_workspace_bytes();
+hipError_t thumbnail_shards_launch(const uint8_t* cas8, const uint8_t* valid, uint64_t n,
+                                   uint32_t* order, uint32_t* counts, void* ws, hipStream_t s);
+
 // ---- Object link batch (K7) ----------------------------------------------------
 size_t link_workspace_bytes(uint64_t n);
 // rank may be null (rank = first_rank + i), valid may be null (all rows valid).

@@ -23,6 +23,9 @@ __device__ __forceinline__ uint64_t row_hash(uint64_t z) {
 //           (null: rank_base + i);
 //   RecIn:  packed 12-byte exchange records {key lo, key hi, rank} as received
 //           from the other GPUs, valid[i] optional (the Object-index probe's mask).
+//   Rec16In: 16-byte bucket records {key lo, key hi, rank, row} of a first
+//           partition pass (the row is carried, not the position).
+// get_row also returns the row whose rep the record answers for.
 struct RowsIn {
   const uint64_t* key;
   const uint8_t* valid;
@@ -33,6 +36,11 @@ struct RowsIn {
     r = rank ? rank[i] : rank_base + static_cast<uint32_t>(i);
     v = !valid || valid[i] != 0;
   }
+  __device__ __forceinline__ void get_row(uint64_t i, uint64_t& k, uint32_t& r, uint32_t& row,
+                                          bool& v) const {
+    get(i, k, r, v);
+    row = static_cast<uint32_t>(i);
+  }
 };
 struct RecIn {
   const uint3* rec;
@@ -42,6 +50,28 @@ struct RecIn {
     k = (static_cast<uint64_t>(q.y) << 32) | q.x;
     r = q.z;
     v = !valid || valid[i] != 0;
+  }
+  __device__ __forceinline__ void get_row(uint64_t i, uint64_t& k, uint32_t& r, uint32_t& row,
+                                          bool& v) const {
+    get(i, k, r, v);
+    row = static_cast<uint32_t>(i);
+  }
+};
+struct Rec16In {
+  const uint4* rec;
+  __device__ __forceinline__ void get(uint64_t i, uint64_t& k, uint32_t& r, bool& v) const {
+    const uint4 q = rec[i];
+    k = (static_cast<uint64_t>(q.y) << 32) | q.x;
+    r = q.z;
+    v = true;
+  }
+  __device__ __forceinline__ void get_row(uint64_t i, uint64_t& k, uint32_t& r, uint32_t& row,
+                                          bool& v) const {
+    const uint4 q = rec[i];
+    k = (static_cast<uint64_t>(q.y) << 32) | q.x;
+    r = q.z;
+    row = q.w;
+    v = true;
   }
 };
 

@@ -1229,6 +1229,36 @@ int sdgpu_synth_file_device(sdgpu_ctx* c, uint64_t seed, uint64_t offset, uint64
   return 0;
 }
 
+// ---- downstream consumers --------------------------------------------------------
+
+int sdgpu_orphan_objects_device(sdgpu_ctx* c, const int32_t* d_object_ids, uint64_t n_objects,
+                                const int32_t* d_fp_object_ids, uint64_t n_file_paths,
+                                uint32_t max_object_id, int32_t* d_orphans, uint32_t* d_count,
+                                void* stream) {
+  if (!c || !d_count || (n_objects && (!d_object_ids || !d_orphans)) ||
+      (n_file_paths && !d_fp_object_ids) || max_object_id > 0x7FFFFFFFu)
+    return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  SD_TRY_RC(ensure_dev(c, c->link_ws, orphan_workspace_bytes(n_objects, max_object_id)));
+  SD_TRY(orphan_objects_launch(d_object_ids, n_objects, d_fp_object_ids, n_file_paths,
+                               max_object_id, d_orphans, d_count, c->link_ws.p, s));
+  return 0;
+}
+
+int sdgpu_thumbnail_shards_device(sdgpu_ctx* c, const uint8_t* d_cas8, const uint8_t* d_valid,
+                                  uint64_t n, uint32_t* d_order, uint32_t* d_counts,
+                                  void* stream) {
+  if (!c || !d_counts || (n && (!d_cas8 || !d_order)) || n >= (1ull << 32)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  SD_TRY_RC(ensure_dev(c, c->link_ws, thumb_workspace_bytes()));
+  SD_TRY(thumbnail_shards_launch(d_cas8, d_valid, n, d_order, d_counts, c->link_ws.p, s));
+  return 0;
+}
+
 int sdgpu_synth_vary_keys_device(sdgpu_ctx* c, uint64_t* d_key, const uint8_t* d_vary,
                                  uint64_t n, uint64_t step, void* stream) {
   if (!c || (n && (!d_key || !d_vary))) return -EINVAL;

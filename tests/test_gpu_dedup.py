@@ -245,3 +245,18 @@ def test_config4_full_100m_rows_eight_ranks(ctx):
     # the config's shape: 20 % of the keyed rows link to an earlier row's Object
     linked = np.count_nonzero(rep != rank)
     assert 0.15 * total < linked < 0.21 * total
+
+
+@pytest.mark.parametrize("n,chunk", [(13_000_000, 100), (26_000_000, 7)])
+def test_two_level_partition(ctx, n, chunk):
+    """Past 2^12 buckets the partition runs in two passes (coarse, then 12-bit
+    staged per segment): 13 M rows (2 segments) and 26 M rows (4), with a key
+    repeated 60 k times (a bucket past the LDS table) and keyless rows."""
+    from spacedrive_amd import dedup
+    rng = np.random.default_rng(n)
+    pool = rng.integers(0, 2**64 - 1, int(n * 0.7), dtype=np.uint64, endpoint=True)
+    key = pool[rng.integers(0, pool.size, n)]
+    key[rng.choice(n, 60_000, replace=False)] = pool[5]
+    has = (rng.random(n) > 0.002).astype(np.uint8)
+    rep = dedup.group_reps(key, has, chunk, ctx)
+    np.testing.assert_array_equal(rep, O.group_reps(key, has, chunk))
