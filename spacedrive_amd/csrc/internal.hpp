@@ -6,6 +6,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "tree_plan.hpp"
+
 namespace sdgpu {
 
 // Optional per-kernel timing: the C-ABI layer passes a recorder that brackets
@@ -66,15 +68,7 @@ hipError_t small_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
                              KTimer* timer = nullptr);
 
 // ---- tree BLAKE3 of large segments (file_checksum, K2/K3) -------------------
-struct TreeSeg {
-  const uint8_t* data;    // device pointer, 16-B aligned (bytes, or CVs when cv_input)
-  uint64_t len;           // bytes (or number of CVs when cv_input)
-  uint64_t chunk_offset;  // chunk counter of the first chunk
-  uint32_t root;          // 1: emit the ROOT digest, 0: emit the subtree CV
-  uint32_t pad;
-};
-
-struct TreePlan;  // opaque, built on the host per call
+// TreeSeg: tree_plan.hpp
 // cv_input: every segment's `data` holds `len` 32-byte chaining values of
 // consecutive equal, aligned power-of-two subtrees (the last may be partial);
 // they are folded into the digest / CV of their concatenation.

@@ -28,10 +28,19 @@
 
 #include "../../include/sdgpu.h"
 #include "ctx.hpp"
+#include "host_io.hpp"
 #include "internal.hpp"
 #include "scan_device.hpp"
 
 using namespace sdgpu;
+using sdgpu::hostio::parallel_for;
+using sdgpu::hostio::pread_exact;
+using sdgpu::hostio::read_cas_message;
+using sdgpu::hostio::read_whole;
+using sdgpu::hostio::read_whole_fd;
+using sdgpu::hostio::slab_layout;
+using sdgpu::hostio::SlabLayout;
+using sdgpu::hostio::to_hex;
 
 namespace {
 
@@ -81,113 +90,7 @@ int tree_launch(sdgpu_ctx* c, const TreeSeg* segs, uint32_t nseg, bool cv_input,
   return 0;
 }
 
-const char HEXD[] = "0123456789abcdef";
-void to_hex(const uint8_t* d, int n, char* out) {
-  for (int i = 0; i < n; ++i) {
-    out[2 * i] = HEXD[d[i] >> 4];
-    out[2 * i + 1] = HEXD[d[i] & 15];
-  }
-  out[2 * n] = 0;
-}
-
-// ---------------------------------------------------------------------------
-// File reads with the reference's semantics (cas.rs:23-62)
-// ---------------------------------------------------------------------------
-
-int pread_exact(int fd, uint8_t* buf, size_t n, off_t pos) {
-  size_t got = 0;
-  while (got < n) {
-    const ssize_t r = pread(fd, buf + got, n - got, pos + static_cast<off_t>(got));
-    if (r < 0) {
-      if (errno == EINTR) continue;
-      return -errno;
-    }
-    if (r == 0) return -ENODATA;  // read_exact: io::ErrorKind::UnexpectedEof
-    got += static_cast<size_t>(r);
-  }
-  return 0;
-}
-
-// Writes the cas message of the file at `path` (stat size `size`) into dst
-// (capacity cap).  Returns its length, or -errno; -EFBIG means a file of at
-// most 100 KiB at stat time outgrew its reservation before the read, and the
-// caller hashes it through cas_grown_locked (no deviation from fs::read).
-int64_t read_cas_message(const char* path, uint64_t size, uint8_t* dst, size_t cap) {
-  if (cap < 8) return -ENOBUFS;
-  const int fd = open(path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return -errno;
-  for (int i = 0; i < 8; ++i) dst[i] = static_cast<uint8_t>(size >> (8 * i));
-  int64_t len = 8;
-  int rc = 0;
-  if (size <= SDGPU_CAS_MINIMUM_FILE_SIZE) {
-    // fs::read(path): the whole current content, whatever its length
-    for (;;) {
-      if (static_cast<size_t>(len) == cap) {
-        uint8_t probe;
-        const ssize_t r = read(fd, &probe, 1);
-        rc = r == 0 ? 0 : (r < 0 ? -errno : -EFBIG);
-        break;
-      }
-      const ssize_t r = read(fd, dst + len, cap - static_cast<size_t>(len));
-      if (r < 0) {
-        if (errno == EINTR) continue;
-        rc = -errno;
-        break;
-      }
-      if (r == 0) break;
-      len += r;
-    }
-  } else if (cap < SDGPU_CAS_SAMPLED_MSG_LEN) {
-    rc = -ENOBUFS;
-  } else {
-    const uint64_t hf = SDGPU_CAS_HEADER_OR_FOOTER_SIZE, ss = SDGPU_CAS_SAMPLE_SIZE;
-    rc = pread_exact(fd, dst + len, hf, 0);  // header (cas.rs:35-38)
-    len += hf;
-    const uint64_t jump = (size - 2 * hf) / SDGPU_CAS_SAMPLE_COUNT;  // cas.rs:41
-    for (uint32_t k = 0; k < SDGPU_CAS_SAMPLE_COUNT && rc == 0; ++k) {  // cas.rs:42-51
-      rc = pread_exact(fd, dst + len, ss, static_cast<off_t>(hf + k * jump));
-      len += ss;
-    }
-    if (rc == 0) {  // footer from the ACTUAL end (SeekFrom::End, cas.rs:54-57)
-      struct stat st;
-      if (fstat(fd, &st) != 0) {
-        rc = -errno;
-      } else if (static_cast<uint64_t>(st.st_size) < hf) {
-        rc = -EINVAL;  // seek before byte 0
-      } else {
-        rc = pread_exact(fd, dst + len, hf, static_cast<off_t>(st.st_size - hf));
-        len += hf;
-      }
-    }
-  }
-  close(fd);
-  return rc ? rc : len;
-}
-
 int cas_grown_locked(sdgpu_ctx* c, const char* path, uint64_t size, uint8_t out8[8]);
-
-template <typename F>
-void parallel_for(uint32_t n, F&& f) {
-  const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  const uint32_t nt = std::min<uint32_t>(hw, (n + 63) / 64);
-  if (nt <= 1) {
-    for (uint32_t i = 0; i < n; ++i) f(i);
-    return;
-  }
-  std::atomic<uint32_t> next{0};
-  std::vector<std::thread> th;
-  th.reserve(nt);
-  for (uint32_t t = 0; t < nt; ++t)
-    th.emplace_back([&] {
-      for (;;) {
-        const uint32_t i0 = next.fetch_add(64);
-        if (i0 >= n) break;
-        const uint32_t i1 = std::min(n, i0 + 64);
-        for (uint32_t i = i0; i < i1; ++i) f(i);
-      }
-    });
-  for (auto& t : th) t.join();
-}
 
 // ---------------------------------------------------------------------------
 // K1 staging pipeline: slabs of messages packed into pinned memory by a
@@ -202,23 +105,6 @@ struct Slab {
   bool busy = false;
   uint32_t first = 0, count = 0;
 };
-
-struct SlabLayout {
-  size_t arena_cap, off, len, out, status, total;
-  uint32_t files_cap;
-};
-
-SlabLayout slab_layout(size_t arena_cap, uint32_t files_cap) {
-  SlabLayout L;
-  L.arena_cap = arena_cap;
-  L.files_cap = files_cap;
-  L.off = align_up(arena_cap, 256);
-  L.len = align_up(L.off + 8ull * files_cap, 256);
-  L.out = align_up(L.len + 4ull * files_cap, 256);
-  L.status = align_up(L.out + 8ull * files_cap, 256);
-  L.total = align_up(L.status + 4ull * files_cap, 256);
-  return L;
-}
 
 // Pinned + device staging slot k of the context (grown on demand, kept).  Only
 // called when no work of the context is in flight.
@@ -753,25 +639,6 @@ int sdgpu_checksum(sdgpu_ctx* c, const void* bytes, uint64_t len, uint8_t out32[
 
 namespace {
 
-// Reads all of fd (from its current offset) into dst; -EFBIG past cap bytes.
-int64_t read_whole_fd(int fd, uint8_t* dst, size_t cap) {
-  size_t len = 0;
-  for (;;) {
-    if (len == cap) {
-      uint8_t probe;
-      const ssize_t r = read(fd, &probe, 1);
-      return r == 0 ? static_cast<int64_t>(len) : (r < 0 ? -errno : -EFBIG);
-    }
-    const ssize_t r = read(fd, dst + len, cap - len);
-    if (r < 0) {
-      if (errno == EINTR) continue;
-      return -errno;
-    }
-    if (r == 0) return static_cast<int64_t>(len);
-    len += static_cast<size_t>(r);
-  }
-}
-
 // file_checksum of one file, streamed in slices (context lock held).
 int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
   const int fd = open(path, O_RDONLY | O_CLOEXEC);
@@ -903,33 +770,6 @@ int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
   if (rc) return rc;
   memcpy(digest, out.data(), 32);
   return 0;
-}
-
-// Reads the whole file into dst (capacity cap).  Returns its length, -errno,
-// or -EFBIG when it holds more than cap bytes (grown since stat).
-int64_t read_whole(const char* path, uint8_t* dst, size_t cap) {
-  const int fd = open(path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return -errno;
-  size_t len = 0;
-  int64_t rc = 0;
-  for (;;) {
-    if (len == cap) {
-      uint8_t probe;
-      const ssize_t r = read(fd, &probe, 1);
-      rc = r == 0 ? 0 : (r < 0 ? -errno : -EFBIG);
-      break;
-    }
-    const ssize_t r = read(fd, dst + len, cap - len);
-    if (r < 0) {
-      if (errno == EINTR) continue;
-      rc = -errno;
-      break;
-    }
-    if (r == 0) break;
-    len += static_cast<size_t>(r);
-  }
-  close(fd);
-  return rc ? rc : static_cast<int64_t>(len);
 }
 
 }  // namespace
