@@ -136,6 +136,12 @@ class Runner:
         self.backend = backend if self.world > 1 else None
         self.ops = dedup.HipOps(self.ctx)
         self.comm = None
+        # SD_BENCH_FORCE_COMM=1: also at N = 1 through a one-rank RCCL
+        # communicator (rehearses the N > 1 code path on a one-GPU box)
+        force = os.environ.get("SD_BENCH_FORCE_COMM") == "1" and self.world == 1
+        if force:
+            self.backend = "nccl (one-rank rehearsal)"
+            self.comm = dedup.Comm.init_rank(self.ctx, 1, 0, dedup.Comm.unique_id())
         if self.world > 1 and backend == "nccl":
             # the grouping's exchange runs INSIDE libsdgpu over RCCL (what the
             # Rust host calls): rank 0's communicator id travels over the
@@ -145,19 +151,19 @@ class Runner:
             self.comm = dedup.Comm.init_rank(self.ctx, self.world, self.rank, obj[0])
 
     def exchange_name(self) -> str:
-        if self.world == 1:
-            return "none (one GPU: local grouping)"
         if self.comm is not None:
             return "libsdgpu RCCL all-to-all (sdgpu_group_sharded_device)"
+        if self.world == 1:
+            return "none (one GPU: local grouping)"
         return f"torch.distributed {self.backend} all-to-all over libsdgpu steps (rehearsal)"
 
     def group(self, key, has, rank, timings=None):
         """The cas_id -> Object grouping of this rank's rows against all ranks."""
         from spacedrive_amd import dedup
-        if self.world == 1:
-            return self.ops.group_rows(key, has, rank, 100, 0)
         if self.comm is not None:
             return dedup.group_sharded(key, has, rank, self.comm, None, 100)
+        if self.world == 1:
+            return self.ops.group_rows(key, has, rank, 100, 0)
         return dedup.sharded_group_reps(key, has, rank, 100, ops=self.ops, timings=timings)
 
     def barrier(self):
@@ -294,10 +300,10 @@ class Runner:
             cas.cas_stage_pinned(h_arena, off, ln, out, st, ctx=self.ctx)
             key = out.view(torch.int64).view(-1)
             corpus.vary_keys_device(key, vary, s, ctx=self.ctx)
-            if W == 1:
-                rep = dedup.group_rows_indexed(key, has, ranks[s], index, 100)
-            elif self.comm is not None:
+            if self.comm is not None:
                 rep = dedup.group_sharded(key, has, ranks[s], self.comm, index, 100)
+            elif W == 1:
+                rep = dedup.group_rows_indexed(key, has, ranks[s], index, 100)
             else:  # gloo rehearsal: the exchange has no index
                 rep = self.group(key, has, ranks[s])
             dedup.link_batch_device(rep, ranks[s], None, 0, ctx=self.ctx, trim=False)
@@ -662,6 +668,12 @@ def main():
     comps = set(args.components.split(","))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args.gpus))
+    # stdout carries exactly one JSON line: everything else the process (or a
+    # library it loads -- RCCL prints a version banner on communicator init)
+    # writes to fd 1 goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     if args.gpus != int(os.environ.get("WORLD_SIZE", "1")):
         log(f"bench: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}: "
             "reporting the launched world size")
@@ -752,7 +764,7 @@ def main():
                       "devices_visible": torch.cuda.device_count(),
                       "backend": R.backend, "exchange": R.exchange_name()}}
     if R.rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     if R.comm is not None:
         R.comm.close()
     if R.world > 1:

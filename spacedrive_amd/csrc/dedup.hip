@@ -88,12 +88,43 @@ __device__ __forceinline__ void tile_of(uint64_t n, uint32_t P, uint64_t& t0, ui
 // issued back to back, so one tile costs a few memory latencies, not one per row.
 constexpr int kUnroll = 8;
 
+// Partition digit of a row hash: the destination rank of the multi-GPU
+// exchange when world != 0 (shard s = top `bits` hash bits belongs to rank
+// s * world >> bits), else `bits` hash bits below the top `skip` bits.
+__device__ __forceinline__ uint32_t part_digit(uint64_t h, uint32_t skip, uint32_t bits,
+                                               uint32_t world) {
+  return world ? static_cast<uint32_t>(((h >> (64 - bits)) * world) >> bits)
+               : digit_of(h, skip, bits);
+}
+
+// Wave-aggregated LDS counter add for few, heavily shared bins (the exchange's
+// W destination ranks): one atomic per distinct digit in the wave instead of
+// one per row.  Every active lane of the wave must call it (v = row counts);
+// returns the row's slot (base of its bin + its rank among the wave's lanes
+// with the same digit).
+__device__ __forceinline__ uint32_t wave_add(uint32_t* cnt, uint32_t d, bool v) {
+  const uint32_t lane = __lane_id();
+  uint64_t pending = __ballot(v);
+  uint32_t slot = 0;
+  while (pending) {
+    const int leader = __ffsll(static_cast<unsigned long long>(pending)) - 1;
+    const uint32_t dl = __shfl(d, leader);
+    const uint64_t m = __ballot(v && d == dl);
+    uint32_t base = 0;
+    if (lane == static_cast<uint32_t>(leader)) base = atomicAdd(&cnt[dl], __popcll(m));
+    base = __shfl(base, leader);
+    if ((m >> lane) & 1ull) slot = base + __popcll(m & ((1ull << lane) - 1ull));
+    pending &= ~m;
+  }
+  return slot;
+}
+
 template <typename In>
 __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, uint32_t skip,
-                                                            uint32_t bits,
+                                                            uint32_t bits, uint32_t world,
                                                             uint32_t* __restrict__ hist) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
-  const uint32_t nbins = 1u << bits;
+  const uint32_t nbins = world ? world : 1u << bits;
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) cnt[b] = 0;
   __syncthreads();
   uint64_t t0, t1;
@@ -109,25 +140,34 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
       if (i < t1) in.get(i, k[u], r[u], v[u]);
     }
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u)
-      if (v[u]) atomicAdd(&cnt[digit_of(row_hash(k[u]), skip, bits)], 1u);
+    for (int u = 0; u < kUnroll; ++u) {
+      if (world) {
+        (void)wave_add(cnt, v[u] ? part_digit(row_hash(k[u]), skip, bits, world) : 0u, v[u]);
+      } else if (v[u]) {
+        atomicAdd(&cnt[part_digit(row_hash(k[u]), skip, bits, world)], 1u);
+      }
+    }
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
     hist[static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
 }
 
-// Shard partition of the multi-GPU exchange: keyed rows packed by shard
-// (shard s at the scanned offsets), each row's source index in out_pos.
-// kRec12: one packed 12-byte send record {key lo, key hi, rank} per row (what
-// travels over xGMI); otherwise separate key / rank arrays.
+// Shard partition of the multi-GPU exchange: keyed rows packed by digit (the
+// destination rank, or a shard) at the scanned offsets.
+//   kRec12: one packed 12-byte send record {key lo, key hi, rank} per row
+//           (what travels over xGMI) and, per SOURCE row i, out_pos[i] = its
+//           send position (~0 for keyless rows): a coalesced write, and the
+//           reps come back through a gather (k_gather_rep);
+//   else:   separate key / rank arrays and out_pos[p] = source row of packed
+//           row p (the single-step ABI for hosts with their own collectives).
 template <typename In, bool kRec12>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
-    In in, uint64_t n, uint32_t skip, uint32_t bits, const uint32_t* __restrict__ offs,
-    uint64_t* __restrict__ out_key, uint32_t* __restrict__ out_rank, uint3* __restrict__ out_rec,
-    uint32_t* __restrict__ out_pos) {
+    In in, uint64_t n, uint32_t skip, uint32_t bits, uint32_t world,
+    const uint32_t* __restrict__ offs, uint64_t* __restrict__ out_key,
+    uint32_t* __restrict__ out_rank, uint3* __restrict__ out_rec, uint32_t* __restrict__ out_pos) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cur[];
-  const uint32_t nbins = 1u << bits;
+  const uint32_t nbins = world ? world : 1u << bits;
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
     cur[b] = offs[static_cast<uint64_t>(b) * gridDim.x + part_block()];
   __syncthreads();
@@ -137,25 +177,31 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += U * kPartThreads) {
     uint64_t k[U];
     uint32_t r[U];
-    bool v[U];
+    bool in_[U], v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
+      in_[u] = i < t1;
       v[u] = false;
-      if (i < t1) in.get(i, k[u], r[u], v[u]);
+      if (in_[u]) in.get(i, k[u], r[u], v[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (!v[u]) continue;
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      const uint32_t p = atomicAdd(&cur[digit_of(row_hash(k[u]), skip, bits)], 1u);
+      const uint32_t d = v[u] ? part_digit(row_hash(k[u]), skip, bits, world) : 0u;
+      const uint32_t p = world ? wave_add(cur, d, v[u]) : (v[u] ? atomicAdd(&cur[d], 1u) : 0u);
+      if (!v[u]) {
+        if (kRec12 && in_[u]) out_pos[i] = 0xFFFFFFFFu;
+        continue;
+      }
       if (kRec12) {
         out_rec[p] = make_uint3(static_cast<uint32_t>(k[u]), static_cast<uint32_t>(k[u] >> 32), r[u]);
+        out_pos[i] = p;
       } else {
         out_key[p] = k[u];
         out_rank[p] = r[u];
+        out_pos[p] = static_cast<uint32_t>(i);
       }
-      out_pos[p] = static_cast<uint32_t>(i);
     }
   }
 }
@@ -501,18 +547,27 @@ __global__ void k_copy_counts(const uint32_t* __restrict__ offs, uint32_t nbins,
                 offs[static_cast<uint64_t>(b) * kPartBlocks];
 }
 
-// Rows per destination rank of the exchange, from the scanned shard offsets
-// (owner of shard s = s * world >> bits, shard_plan in spacedrive_amd/dedup.py).
-__global__ void k_dest_counts(const uint32_t* __restrict__ offs, uint32_t bits, uint32_t world,
+// Rows per destination rank of the exchange, from the scanned offsets of the
+// destination-digit partition.
+__global__ void k_dest_counts(const uint32_t* __restrict__ offs, uint32_t world,
                               int64_t* __restrict__ counts) {
   const uint32_t d = threadIdx.x;
-  if (d >= world) return;
-  int64_t c = 0;
-  for (uint32_t b = 0; b < (1u << bits); ++b)
-    if (((static_cast<uint64_t>(b) * world) >> bits) == d)
-      c += offs[static_cast<uint64_t>(b + 1) * kPartBlocks] -
-           offs[static_cast<uint64_t>(b) * kPartBlocks];
-  counts[d] = c;
+  if (d < world)
+    counts[d] = static_cast<int64_t>(offs[static_cast<uint64_t>(d + 1) * kPartBlocks]) -
+                offs[static_cast<uint64_t>(d) * kPartBlocks];
+}
+
+// rep[i] of the sender's rows from the reps returned in send order: row i was
+// sent at position pos[i] (~0: no key, it keeps its own rank).
+__global__ __launch_bounds__(256) void k_gather_rep(const uint32_t* __restrict__ back,
+                                                    const uint32_t* __restrict__ pos,
+                                                    const uint32_t* __restrict__ rank, uint64_t n,
+                                                    uint32_t* __restrict__ rep) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) {
+    const uint32_t p = pos[i];
+    rep[i] = p == 0xFFFFFFFFu ? rank[i] : back[p];
+  }
 }
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -597,7 +652,7 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
     const size_t lds1 = sizeof(uint32_t) << L.cbits;
     {
       KScope k(timer, "bucket_hist", s);
-      k_part_hist<In><<<P, kPartThreads, lds1, s>>>(in, n, kShardBits, L.cbits, hist1);
+      k_part_hist<In><<<P, kPartThreads, lds1, s>>>(in, n, kShardBits, L.cbits, 0, hist1);
     }
     scan::exclusive(hist1, static_cast<uint64_t>(nseg) * P, hist1, tiles, nullptr, s);
     {
@@ -629,7 +684,7 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   {
     KScope k(timer, "bucket_hist", s);
     allow_lds(k_part_hist<In>, lds);
-    k_part_hist<In><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, hist);
+    k_part_hist<In><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, 0, hist);
   }
   scan::exclusive(hist, nh, hist, tiles, nullptr, s);
   {
@@ -661,25 +716,27 @@ size_t shard_hist_bytes(uint32_t shard_bits) {
   return align_up(4 * (nh + 1), 256);
 }
 
-// Shard histogram + scan (+ scatter when outputs are given) of the caller's rows.
-hipError_t shard_partition(const RowsIn& in, uint64_t n, uint32_t shard_bits, uint32_t* hist,
-                           uint32_t* tiles, uint64_t* okey, uint32_t* orank, uint3* orec,
-                           uint32_t* opos, hipStream_t s, KTimer* timer) {
-  const uint64_t nh = (static_cast<uint64_t>(1) << shard_bits) * kPartBlocks;
-  const size_t lds = sizeof(uint32_t) << shard_bits;
+// Shard histogram + scan (+ scatter when outputs are given) of the caller's
+// rows; digit = destination rank when world != 0, else the top shard_bits.
+hipError_t shard_partition(const RowsIn& in, uint64_t n, uint32_t shard_bits, uint32_t world,
+                           uint32_t* hist, uint32_t* tiles, uint64_t* okey, uint32_t* orank,
+                           uint3* orec, uint32_t* opos, hipStream_t s, KTimer* timer) {
+  const uint32_t nbins = world ? world : 1u << shard_bits;
+  const uint64_t nh = static_cast<uint64_t>(nbins) * kPartBlocks;
+  const size_t lds = sizeof(uint32_t) * nbins;
   {
     KScope k(timer, "shard_hist", s);
-    k_part_hist<RowsIn><<<kPartBlocks, kPartThreads, lds, s>>>(in, n, 0, shard_bits, hist);
+    k_part_hist<RowsIn><<<kPartBlocks, kPartThreads, lds, s>>>(in, n, 0, shard_bits, world, hist);
   }
   scan::exclusive(hist, nh, hist, tiles, nullptr, s);
   if (opos) {
     KScope k(timer, "shard_scatter", s);
     if (orec)
       k_part_scatter<RowsIn, true><<<kPartBlocks, kPartThreads, lds, s>>>(
-          in, n, 0, shard_bits, hist, nullptr, nullptr, orec, opos);
+          in, n, 0, shard_bits, world, hist, nullptr, nullptr, orec, opos);
     else
       k_part_scatter<RowsIn, false><<<kPartBlocks, kPartThreads, lds, s>>>(
-          in, n, 0, shard_bits, hist, okey, orank, nullptr, opos);
+          in, n, 0, shard_bits, world, hist, okey, orank, nullptr, opos);
   }
   return hipGetLastError();
 }
@@ -709,7 +766,7 @@ hipError_t shard_count_launch(const uint64_t* key, const uint8_t* has_key, uint6
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(w);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(w + shard_hist_bytes(shard_bits));
-  hipError_t e = shard_partition(RowsIn{key, has_key, nullptr, 0}, n, shard_bits, hist, tiles,
+  hipError_t e = shard_partition(RowsIn{key, has_key, nullptr, 0}, n, shard_bits, 0, hist, tiles,
                                  nullptr, nullptr, nullptr, nullptr, s, nullptr);
   if (e != hipSuccess) return e;
   k_copy_counts<<<1, 256, 0, s>>>(hist, 1u << shard_bits, d_counts);
@@ -723,7 +780,7 @@ hipError_t shard_partition_launch(const uint64_t* key, const uint8_t* has_key,
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(w);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(w + shard_hist_bytes(shard_bits));
-  return shard_partition(RowsIn{key, has_key, rank, 0}, n, shard_bits, hist, tiles, out_key,
+  return shard_partition(RowsIn{key, has_key, rank, 0}, n, shard_bits, 0, hist, tiles, out_key,
                          out_rank, nullptr, out_pos, s, timer);
 }
 
@@ -735,11 +792,20 @@ hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(w);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(w + shard_hist_bytes(shard_bits));
-  hipError_t e = shard_partition(RowsIn{key, has_key, rank, 0}, n, shard_bits, hist, tiles,
+  hipError_t e = shard_partition(RowsIn{key, has_key, rank, 0}, n, shard_bits, world, hist, tiles,
                                  out_key, out_rank, reinterpret_cast<uint3*>(out_rec12), out_pos,
                                  s, timer);
   if (e != hipSuccess) return e;
-  k_dest_counts<<<1, 64, 0, s>>>(hist, shard_bits, world, d_dest_counts);
+  k_dest_counts<<<1, 64, 0, s>>>(hist, world, d_dest_counts);
+  return hipGetLastError();
+}
+
+hipError_t gather_rep_launch(const uint32_t* back, const uint32_t* pos, const uint32_t* rank,
+                             uint64_t n, uint32_t* rep, hipStream_t s) {
+  if (n) {
+    const uint64_t g = std::min<uint64_t>((n + 255) / 256, 16384);
+    k_gather_rep<<<static_cast<uint32_t>(g), 256, 0, s>>>(back, pos, rank, n, rep);
+  }
   return hipGetLastError();
 }
 

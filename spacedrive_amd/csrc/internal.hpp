@@ -121,14 +121,20 @@ hipError_t shard_partition_launch(const uint64_t* key, const uint8_t* has_key,
                                   const uint32_t* rank, uint64_t n, uint32_t shard_bits,
                                   uint64_t* out_key, uint32_t* out_rank, uint32_t* out_pos,
                                   void* ws, hipStream_t s, KTimer* timer = nullptr);
-// partition by shard (one hist + scan + scatter) and, on device, the rows per
+// partition by destination rank (one hist + scan + scatter; shard s = top 8
+// hash bits belongs to rank s * world >> 8) and, on device, the rows per
 // destination rank (int64[world]); no host synchronisation.  Output either
-// separate key / rank arrays or packed 12-byte records (out_rec12 non-null).
+// separate key / rank arrays + out_pos[p] = source row of packed row p, or
+// packed 12-byte records (out_rec12 non-null) + out_pos[i] = send position of
+// source row i (~0 = keyless).
 hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
                                  const uint32_t* rank, uint64_t n, uint32_t shard_bits,
                                  uint32_t world, uint64_t* out_key, uint32_t* out_rank,
                                  uint32_t* out_rec12, uint32_t* out_pos, int64_t* d_dest_counts,
                                  void* ws, hipStream_t s, KTimer* timer = nullptr);
+// rep[i] = pos[i] == ~0 ? rank[i] : back[pos[i]] (the exchange's return path)
+hipError_t gather_rep_launch(const uint32_t* back, const uint32_t* pos, const uint32_t* rank,
+                             uint64_t n, uint32_t* rep, hipStream_t s);
 hipError_t scatter_rep_launch(const uint32_t* src, const uint32_t* pos, uint64_t n, uint32_t* dst,
                               uint64_t n_dst, const uint32_t* init, bool do_init, hipStream_t s);
 

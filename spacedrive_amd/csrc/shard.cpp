@@ -7,14 +7,15 @@
 // needs only the global rank, which travels with the key.
 //
 // One exchange step per call, on each GPU:
-//   1. shard partition of the GPU's rows into packed 12-byte send records
-//      {key lo, key hi, rank} grouped by owner, + per-owner counts (device);
+//   1. partition of the GPU's rows by owner GPU (a W-way scatter) into packed
+//      12-byte send records {key lo, key hi, rank}, each row's send position
+//      (coalesced) and the per-owner counts (device);
 //   2. all-to-all of the counts (8 B per pair), then ONE host synchronisation
 //      that reads the send / receive counts (they size the payload);
 //   3. all-to-all of the records -- one message per (source, owner) pair;
 //   4. local grouping of the received rows (Object-index probe first when an
 //      index is given, creators inserted after);
-//   5. all-to-all of the reps back to the sources (4 B per row), scatter to
+//   5. all-to-all of the reps back to the sources (4 B per row), gathered to
 //      row order (keyless rows keep their own rank).
 // Transports: RCCL (ncclSend / ncclRecv in one group, over xGMI; one process
 // per GPU via sdgpu_comm_init_rank, or one process driving all GPUs via
@@ -138,7 +139,7 @@ struct RankJob {
   uint32_t* rep = nullptr;
   // device workspace
   uint32_t* srec = nullptr;   // [n][3]
-  uint32_t* spos = nullptr;   // [n]
+  uint32_t* spos = nullptr;   // [n] send position of row i (~0: keyless)
   int64_t* dcnt = nullptr;    // [W] rows to each owner
   int64_t* rcnt_d = nullptr;  // [W] rows from each source
   uint32_t* rrec = nullptr;   // [m][3]
@@ -283,7 +284,7 @@ int run_sharded(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
       [](RankJob& j, int p) -> size_t { return 4 * j.scnt[p]; }));
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
-    SD_TRY(scatter_rep_launch(j.back, j.spos, j.total, j.rep, j.n, j.rank, true, j.s));
+    SD_TRY(gather_rep_launch(j.back, j.spos, j.rank, j.n, j.rep, j.s));
   }
   return 0;
 }
