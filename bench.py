@@ -93,20 +93,20 @@ def k1_split(lens: np.ndarray):
     return leaves, blk + par - leaves
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, section: str = "kernels"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/<round>/pmc_traffic.json, written by scripts/pmc_summary.py from
-    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench's workload)."""
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench's workload; section
+    "kernels" = the K1 pass over config 2, "dedup" = the 12.5 M-row grouping)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")),
-                   key=os.path.getmtime)
-    for f in reversed(files):
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    for f in reversed(files):  # newest round first (profiles/r1, r2, ...)
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if kernel in d.get("kernels", {}):
-            k = d["kernels"][kernel]
+        if kernel in d.get(section, {}):
+            k = d[section][kernel]
             return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
     return None, None
 
@@ -363,11 +363,20 @@ class Runner:
                 res = fi.identify(paths, sizes=sizes, ctx=self.ctx)
             dt = self.max_over_ranks(time.perf_counter() - t0)
             assert np.all(res.status == 0) and np.all(res.has_key == 1)
+            # one more call with the library's phase timers on: file reads into
+            # the pinned slabs (pool threads), waits for the device, K1 kernels
+            self.ctx.set_timing(True)
+            t1 = time.perf_counter()
+            fi.identify(paths, sizes=sizes, ctx=self.ctx)
+            one = 1e3 * (time.perf_counter() - t1)
+            phases = {k: {"ms": v[0], "n": v[1]} for k, v in self.ctx.kernel_times().items()}
+            self.ctx.set_timing(False)
+            phases["call_ms"] = one
             # the GPU's cas ids are compared with the CPU baseline's (same files,
             # the reference's reads) in the cpu_baseline leg
             self._dir_sample = (paths, sizes, root, res.cas8.copy())
             return {"value": self.world * len(paths) * steps / dt, "unit": "files/s",
-                    "ms_per_step": 1e3 * dt / steps,
+                    "ms_per_step": 1e3 * dt / steps, "phases_one_call": phases,
                     "config": {"workload": "config1: 10k-file directory, log-uniform 1 KiB-10 MiB, "
                                            "sparse files, warm page cache, real pread I/O",
                                "files_per_gpu": len(paths)}}
@@ -461,6 +470,26 @@ class Runner:
                                 for k, b in alg.items() if kernels.get(k, {}).get("avg_ms")},
                     "note": "algorithmic bytes of this partition + group-by design "
                             "(DESIGN.md section 4); PMC traffic in profiles/"}
+            # PMC HBM bytes per launch (committed FETCH_SIZE / WRITE_SIZE passes of
+            # this 12.5 M-row grouping) beside the algorithmic bytes, and the whole
+            # step against SURVEY 8(d)'s 16 B per row
+            pmc_names = {"bucket_hist": "k_part_hist", "bucket_scatter": "k_part_scatter_rec_staged",
+                         "bucket_group": "k_bucket_group"}
+            src = None
+            for k, kn in pmc_names.items():
+                b_, src_ = pmc_traffic(kn, "dedup")
+                if k in roof["kernels"]:
+                    roof["kernels"][k]["pmc_traffic"] = b_
+                src = src or src_
+            step_s = t / steps
+            pmc_sum = [roof["kernels"].get(k, {}).get("pmc_traffic") for k in pmc_names]
+            roof["step"] = {"survey_8d_bytes": 16 * per,
+                            "achieved": 16 * per / step_s / 1e9,
+                            "frac": 16 * per / step_s / HBM_PEAK,
+                            "design_bytes": sum(alg.values()),
+                            "pmc_traffic": (sum(pmc_sum) if all(x is not None for x in pmc_sum)
+                                            else None),
+                            "pmc_source": src}
         full = None
         if self.world == 1 and self.args.dedup_full_rows:
             full = self.run_dedup_full(steps, warmup)
@@ -686,8 +715,10 @@ def main():
                [(1, "v_xor_b32"), (2, "v_add3_u32"), (3, "v_alignbit_b32"), (4, "v_add_u32")]}
     log(f"measured int32 VALU peak: {valu_peak / 1e12:.1f} T lane-ops/s "
         f"(spec {VALU_PEAK_SPEC / 1e12:.1f}); per class {json.dumps(classes)}")
-    c = R.run_cas(args.steps, args.warmup)
-    log("cas:", json.dumps(c["cas"]), json.dumps(c["kernels"]))
+    c = None
+    if "cas" in comps:  # the headline step; only profiling passes leave it out
+        c = R.run_cas(args.steps, args.warmup)
+        log("cas:", json.dumps(c["cas"]), json.dumps(c["kernels"]))
     single = None
     if "single" in comps:
         single = R.run_single()
@@ -710,7 +741,7 @@ def main():
         shutil.rmtree(R._dir_sample[2], ignore_errors=True)
         R._dir_sample = None
     torch.cuda.empty_cache()
-    comp = {"cas": c["cas"], "identifier_job": c["job"]}
+    comp = {"cas": c["cas"], "identifier_job": c["job"]} if c else {}
     if dir_comp:
         comp["dir"] = dir_comp
     if single:
@@ -731,6 +762,16 @@ def main():
         comp["checksum"] = k
         torch.cuda.empty_cache()
 
+    if c is None:  # profiling pass over some components: no headline value
+        if R.rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "components": comp,
+                              "note": "--components without cas: profiling pass, no headline"}),
+                  file=json_out, flush=True)
+        if R.comm is not None:
+            R.comm.close()
+        if R.world > 1:
+            R.dist.destroy_process_group()
+        return
     ri = c["roofline_inputs"]
     ops = ri["leaf_compressions"] * ISA_PER_COMPRESSION
     t_leaf = ri["avg_leaves_s"]

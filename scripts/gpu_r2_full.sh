@@ -1,0 +1,11 @@
+# Round-2 checkpoint on one GPU box: the whole -m gpu suite, smoke(), the
+# default N=1 bench line.  Usage: TAG=r2x bash scripts/gpu_r2_full.sh
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  > gpurun_out/${TAG}_pytest.log 2>&1 || exit 1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit 1
+timeout -k 10 900 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit 1
+echo "exit 0"

@@ -53,7 +53,8 @@ struct PinBuf {
 };
 
 constexpr uint64_t kChunkLen = 1024;  // BLAKE3 chunk
-constexpr size_t kSlabBytes = size_t(256) << 20;   // pinned staging per slab
+constexpr size_t kSlabBytes = size_t(256) << 20;   // pinned staging per slab (max)
+constexpr uint64_t kSlabMinBytes = uint64_t(16) << 20;  // smallest slab of a large call
 constexpr uint32_t kSlabFiles = 1u << 16;          // files per slab
 constexpr size_t kSliceBytes = size_t(64) << 20;   // file_checksum slice = 2^16 chunks
 constexpr uint32_t kStageMaxMsg = 8u + (64u << 20);  // largest staged cas message
@@ -113,6 +114,16 @@ struct EventTimer final : KTimer {
     }
     pending.clear();
   }
+  // a host-side phase (ms of wall time), reported beside the kernels
+  void host(const char* name, double ms) {
+    for (auto& x : acc)
+      if (x.name == name) {
+        x.ms += ms;
+        x.n += 1;
+        return;
+      }
+    acc.push_back(Acc{name, ms, 1});
+  }
   ~EventTimer() override {
     resolve();
     for (auto e : pool) (void)hipEventDestroy(e);
@@ -134,12 +145,13 @@ struct sdgpu_ctx {
   DevBuf batch_ws, tree_ws, dedup_ws, shard_ws, io_a, io_b, link_ws, stage_meta;
   DevBuf stage_slab[3];
   // host staging of the path / host-buffer entry points (identify_files,
-  // cas_batch, generate_cas_id, checksum_files, file_checksum): two pinned and
-  // two device slabs kept for the context's lifetime, grown on demand, so a
-  // call pays no pinned allocation (a 256 MiB hipHostMalloc costs ~10^5 us)
-  PinBuf pipe_h[2];
-  DevBuf pipe_d[2];
-  hipEvent_t pipe_evt[2] = {};
+  // cas_batch, generate_cas_id, checksum_files, file_checksum): pinned and
+  // device slabs kept for the context's lifetime, grown on demand, so a call
+  // pays no pinned allocation (a 256 MiB hipHostMalloc costs ~10^5 us)
+  static constexpr int kPipeSlabs = 3;
+  PinBuf pipe_h[kPipeSlabs];
+  DevBuf pipe_d[kPipeSlabs];
+  hipEvent_t pipe_evt[kPipeSlabs] = {};
   hipStream_t copy_stream = nullptr;  // H2D of staged slabs (SDMA), created on first use
   hipEvent_t stage_copied[3] = {}, stage_freed[3] = {};
   PinBuf plan_pin;

@@ -13,6 +13,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -107,12 +110,96 @@ inline int64_t read_cas_message(const char* path, uint64_t size, uint8_t* dst, s
 }
 
 
+inline uint32_t io_threads() {
+  return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+// Persistent workers for the per-slab file reads: a staging call fills many
+// slabs, and starting 16 threads per slab cost more than reading a small one.
+// run(n, f) hands out f(i) in blocks of 64 indices to the workers and the
+// calling thread, and returns when all n are done.  One run at a time.
+class Pool {
+ public:
+  explicit Pool(uint32_t workers) {
+    for (uint32_t t = 0; t < workers; ++t) th_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void run(uint32_t n, const std::function<void(uint32_t)>& f) {
+    std::unique_lock<std::mutex> lk(m_);
+    job_ = &f;
+    n_ = n;
+    next_.store(0);
+    pending_ = static_cast<uint32_t>(th_.size());
+    ++gen_;
+    cv_.notify_all();
+    lk.unlock();
+    work(&f, n);
+    lk.lock();
+    done_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+  std::mutex busy;  // held by the thread using the pool
+
+ private:
+  void work(const std::function<void(uint32_t)>* f, uint32_t n) {
+    for (;;) {
+      const uint32_t i0 = next_.fetch_add(64);
+      if (i0 >= n) break;
+      const uint32_t i1 = std::min(n, i0 + 64);
+      for (uint32_t i = i0; i < i1; ++i) (*f)(i);
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(m_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      const auto* f = job_;
+      const uint32_t n = n_;
+      lk.unlock();
+      work(f, n);
+      lk.lock();
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(uint32_t)>* job_ = nullptr;
+  uint32_t n_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  std::atomic<uint32_t> next_{0};
+};
+
+inline Pool& pool() {
+  static Pool p(io_threads() - 1);
+  return p;
+}
+
+// f(i) for i < n on up to io_threads() threads (the persistent pool; fresh
+// threads when another thread is using the pool).
 template <typename F>
 inline void parallel_for(uint32_t n, F&& f) {
-  const uint32_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  const uint32_t nt = std::min<uint32_t>(hw, (n + 63) / 64);
+  const uint32_t nt = std::min<uint32_t>(io_threads(), (n + 63) / 64);
   if (nt <= 1) {
     for (uint32_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  Pool& p = pool();
+  if (p.busy.try_lock()) {
+    const std::function<void(uint32_t)> fn = [&](uint32_t i) { f(i); };
+    p.run(n, fn);
+    p.busy.unlock();
     return;
   }
   std::atomic<uint32_t> next{0};

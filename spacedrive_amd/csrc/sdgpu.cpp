@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <mutex>
 #include <new>
@@ -94,8 +95,11 @@ int cas_grown_locked(sdgpu_ctx* c, const char* path, uint64_t size, uint8_t out8
 
 // ---------------------------------------------------------------------------
 // K1 staging pipeline: slabs of messages packed into pinned memory by a
-// producer, H2D + K1 + D2H on the context stream, two slabs in flight so the
-// host fills slab k+1 while the GPU works on slab k.
+// producer (the file reads, on the pool threads), H2D + K1 + D2H on the
+// context stream, three slabs in rotation so the host fills slab k+1 while the
+// GPU works on slab k.  The reads are the bound, so slabs are sized to about a
+// sixth of the call's bytes (16-256 MiB): the device work left after the last
+// read is one small slab, not half the input.
 // ---------------------------------------------------------------------------
 
 struct Slab {
@@ -122,13 +126,20 @@ int pipe_slot(sdgpu_ctx* c, int k, size_t bytes) {
 template <typename Est, typename Produce, typename Finish>
 int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&& finish) {
   (void)pick(c, nullptr);  // runs on the context stream, after earlier work on others
-  uint64_t want = 0;
-  for (uint32_t i = 0; i < n && want < kSlabBytes; ++i) want += align_up(est(i), 16);
-  const SlabLayout L = slab_layout(static_cast<size_t>(std::clamp<uint64_t>(want, 4096, kSlabBytes)),
-                                   std::clamp<uint32_t>(n, 1, kSlabFiles));
-  Slab slabs[2];
+  constexpr int S = sdgpu_ctx::kPipeSlabs;
+  uint64_t want = 0, biggest = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t e = align_up(est(i), 16);
+    want += e;
+    biggest = std::max(biggest, e);
+  }
+  const uint64_t target = want <= (kSlabMinBytes << 1) ? want : std::max(want / 6, kSlabMinBytes);
+  const SlabLayout L = slab_layout(
+      static_cast<size_t>(std::clamp<uint64_t>(std::max(target, biggest), 4096, kSlabBytes)),
+      std::clamp<uint32_t>(n, 1, kSlabFiles));
+  Slab slabs[S];
   int rc = 0;
-  for (int k = 0; k < 2 && rc == 0; ++k) {
+  for (int k = 0; k < S && rc == 0; ++k) {
     if ((rc = pipe_slot(c, k, L.total)) != 0) break;
     slabs[k].h = static_cast<uint8_t*>(c->pipe_h[k].p);
     slabs[k].d = static_cast<uint8_t*>(c->pipe_d[k].p);
@@ -136,9 +147,16 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
   }
   BatchWork w;
   if (rc == 0) rc = batch_work(c, L.files_cap, L.arena_cap / kChunkLen + L.files_cap, w);
+  EventTimer* ht = c->timing ? &c->timer : nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms_since = [&](std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(now() - t0).count();
+  };
   auto drain = [&](Slab& sl) -> int {
     if (!sl.busy) return 0;
+    const auto t0 = now();
     if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
+    if (ht) ht->host("stage_wait", ms_since(t0));
     sl.busy = false;
     finish(sl.first, sl.count, reinterpret_cast<const uint8_t(*)[8]>(sl.h + L.out),
            reinterpret_cast<const int32_t*>(sl.h + L.status));
@@ -146,7 +164,7 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
   };
   uint32_t i = 0, k = 0;
   while (rc == 0 && i < n) {
-    Slab& sl = slabs[k & 1];
+    Slab& sl = slabs[k % S];
     if ((rc = drain(sl)) != 0) break;
     // assign files to this slab
     uint8_t* hb = sl.h;
@@ -164,7 +182,8 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
       ++cnt;
     }
     sl.count = cnt;
-    // fill (threads): message bytes + per-file pre-status
+    // fill (pool threads): message bytes + per-file pre-status
+    const auto t_fill = now();
     parallel_for(cnt, [&](uint32_t j) {
       const uint64_t cap =
           (j + 1 < cnt ? off[j + 1] : std::min<uint64_t>(pos, L.arena_cap)) - off[j];
@@ -177,6 +196,7 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
         pst[j] = r == 0x7fffffff ? 1 : static_cast<int32_t>(r);
       }
     });
+    if (ht) ht->host("stage_fill", ms_since(t_fill));
     // device: copy, hash, copy back.  A few messages of <= 1 MiB take the
     // one-launch latency kernel and one H2D copy of the whole slab prefix.
     hipStream_t s = c->stream;
@@ -279,9 +299,10 @@ int sdgpu_close(sdgpu_ctx* c) {
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   for (DevBuf* b : {&c->batch_ws, &c->tree_ws, &c->dedup_ws, &c->shard_ws, &c->io_a, &c->io_b,
                     &c->link_ws, &c->stage_meta, &c->stage_slab[0], &c->stage_slab[1],
-                    &c->stage_slab[2], &c->pipe_d[0], &c->pipe_d[1]})
+                    &c->stage_slab[2]})
     if (b->p) (void)hipFree(b->p);
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < sdgpu_ctx::kPipeSlabs; ++k) {
+    if (c->pipe_d[k].p) (void)hipFree(c->pipe_d[k].p);
     if (c->pipe_h[k].p) (void)hipHostFree(c->pipe_h[k].p);
     if (c->pipe_evt[k]) (void)hipEventDestroy(c->pipe_evt[k]);
   }
