@@ -21,6 +21,9 @@
 // `bits` hash bits below them, and the LDS slot uses h's low 32 bits.  Buckets
 // are therefore balanced for any key distribution and any world size (raw key
 // bits left half the buckets empty at 3 ranks), and the three are independent.
+// mix64 is a bijection of u64, so the bucket records carry h itself in place of
+// the key: the group-by compares hashes (equal iff the keys are) and never
+// recomputes one.
 //
 // Pipeline (all asynchronous, no host synchronisation):
 //   K6 partition: digit = `bits` hash bits below the top `skip` bits.
@@ -142,9 +145,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       if (world) {
-        (void)wave_add(cnt, v[u] ? part_digit(row_hash(k[u]), skip, bits, world) : 0u, v[u]);
+        (void)wave_add(cnt, v[u] ? part_digit(in_hash<In>(k[u]), skip, bits, world) : 0u, v[u]);
       } else if (v[u]) {
-        atomicAdd(&cnt[part_digit(row_hash(k[u]), skip, bits, world)], 1u);
+        atomicAdd(&cnt[part_digit(in_hash<In>(k[u]), skip, bits, world)], 1u);
       }
     }
   }
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      const uint32_t d = v[u] ? part_digit(row_hash(k[u]), skip, bits, world) : 0u;
+      const uint32_t d = v[u] ? part_digit(in_hash<In>(k[u]), skip, bits, world) : 0u;
       const uint32_t p = world ? wave_add(cur, d, v[u]) : (v[u] ? atomicAdd(&cur[d], 1u) : 0u);
       if (!v[u]) {
         if (kRec12 && in_[u]) out_pos[i] = 0xFFFFFFFFu;
@@ -206,8 +209,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
   }
 }
 
-// Bucket partition writing ONE 16-byte record {key lo, key hi, rank, row} per
-// keyed row (a single scattered store instead of three).  kInitRep: every
+// Bucket partition writing ONE 16-byte record {hash lo, hash hi, rank, row}
+// per keyed row (a single scattered store instead of three).  kInitRep: every
 // row's rep is first set to its own rank here (one coalesced store); rows
 // without a key are not partitioned, and K5 rewrites only the rows that link
 // to an earlier chunk.  (The indexed grouping initialises rep in its probe.)
@@ -241,9 +244,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
       // key stay so (mod.rs:238-239); K5 overwrites only the rows that link
       if (kInitRep && in_[u]) rep[i] = r[u];
       if (!v[u]) continue;
-      const uint32_t p = atomicAdd(&cur[digit_of(row_hash(k[u]), skip, bits)], 1u);
-      rec[p] = make_uint4(static_cast<uint32_t>(k[u]), static_cast<uint32_t>(k[u] >> 32), r[u],
-                          row[u]);
+      const uint64_t h = in_hash<In>(k[u]);
+      const uint32_t p = atomicAdd(&cur[digit_of(h, skip, bits)], 1u);
+      rec[p] = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r[u], row[u]);
     }
   }
 }
@@ -294,8 +297,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       in.get_row(i, k, r, row, v);
       if (kInitRep) rep[i] = r;
       if (!v) continue;
-      const uint32_t b = digit_of(row_hash(k), skip, kStageBits);
-      const uint4 q = make_uint4(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32), r, row);
+      const uint64_t h = in_hash<In>(k);
+      const uint32_t b = digit_of(h, skip, kStageBits);
+      const uint4 q = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r, row);
       const uint32_t sl = atomicAdd(&fill[b], 1u);
       if (sl < 2) {
         stage[b][sl] = q;
@@ -345,7 +349,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_hist(Rec16In in, uint32_
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
-      if (v[u]) atomicAdd(&cnt[digit_of(row_hash(k[u]), skip, kStageBits)], 1u);
+      if (v[u]) atomicAdd(&cnt[digit_of(k[u], skip, kStageBits)], 1u);  // records hold the hash
   }
   __syncthreads();
   const uint64_t obase = static_cast<uint64_t>(c) * nbins * gridDim.x;
@@ -353,12 +357,11 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_hist(Rec16In in, uint32_
     hist[obase + static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
 }
 
-// First probe slot of key k in the LDS table (kLdsSlots, any size): the low
-// 32 hash bits, scaled.  The digit bits (the top ones) are constant inside a
-// bucket, the low ones are not.
-__device__ __forceinline__ uint32_t lds_slot(uint64_t k) {
-  const uint32_t h = static_cast<uint32_t>(row_hash(k));
-  return static_cast<uint32_t>((static_cast<uint64_t>(h) * kLdsSlots) >> 32);
+// First probe slot of a record in the LDS table (kLdsSlots, any size): the
+// low 32 bits of its hash, scaled.  The digit bits (the top ones) are constant
+// inside a bucket, the low ones are not.
+__device__ __forceinline__ uint32_t lds_slot(uint64_t h) {
+  return static_cast<uint32_t>((static_cast<uint64_t>(static_cast<uint32_t>(h)) * kLdsSlots) >> 32);
 }
 
 __device__ __forceinline__ uint32_t next_slot(uint32_t h) {
@@ -366,8 +369,8 @@ __device__ __forceinline__ uint32_t next_slot(uint32_t h) {
 }
 
 // Global-table slot (tsize a power of two, up to 2^34 for a 2^32-row bucket).
-__device__ __forceinline__ uint64_t global_slot(uint64_t k, uint64_t tsize) {
-  return row_hash(k) & (tsize - 1);
+__device__ __forceinline__ uint64_t global_slot(uint64_t h, uint64_t tsize) {
+  return h & (tsize - 1);
 }
 
 constexpr int kPer = (kLdsCap + kGroupThreads - 1) / kGroupThreads;
@@ -388,7 +391,7 @@ __device__ __forceinline__ void load_bucket(const uint4* __restrict__ rec, uint3
 // load_bucket when the bucket fits the LDS table).
 __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint32_t start,
                                              uint32_t end, const uint4 (&q_reg)[kPer],
-                                             uint32_t chunk_rows, uint64_t* __restrict__ gkey,
+                                             ChunkOf chunk_of, uint64_t* __restrict__ gkey,
                                              uint32_t* __restrict__ gmin,
                                              uint32_t* __restrict__ rep, uint64_t* lkey,
                                              uint32_t* lmin, uint32_t& special_min) {
@@ -461,7 +464,7 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
       if (!(live >> j & 1u)) continue;
       const uint32_t r = q_reg[j].z;
       const uint32_t f = (keyed >> j & 1u) ? tm[h[j]] : special_min;
-      if (r / chunk_rows != f / chunk_rows) rep[q_reg[j].w] = f;  // others keep rank
+      if (chunk_of(r) != chunk_of(f)) rep[q_reg[j].w] = f;  // others keep rank
     }
     return;
   }
@@ -503,7 +506,7 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
       }
       f = __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (r / chunk_rows != f / chunk_rows) rep[q.w] = f;
+    if (chunk_of(r) != chunk_of(f)) rep[q.w] = f;
   }
 }
 
@@ -511,7 +514,7 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
 // One workgroup per bucket.  Rows of bucket b: [offs[b*P], offs[(b+1)*P]).
 __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
     const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P,
-    uint32_t chunk_rows, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
+    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
     uint32_t* __restrict__ rep) {
   __shared__ uint64_t lkey[kLdsSlots];
   __shared__ uint32_t lmin[kLdsSlots];
@@ -521,7 +524,7 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
   const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];  // offs[nb*P] = total
   uint4 q_reg[kPer];
   load_bucket(rec, start, end, q_reg);
-  group_bucket(rec, start, end, q_reg, chunk_rows, gkey, gmin, rep, lkey, lmin, special_min);
+  group_bucket(rec, start, end, q_reg, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
 }
 
 __global__ __launch_bounds__(256) void k_fill_init(uint32_t* __restrict__ dst, uint64_t n,
@@ -678,7 +681,8 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
           in2, 0, kShardBits + L.cbits, hist, rec, nullptr, hist1, P);
     }
     KScope k(timer, "bucket_group", s);
-    k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, chunk_rows, gkey, gmin, rep);
+    k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, ChunkOf::make(chunk_rows),
+                                                      gkey, gmin, rep);
     return hipGetLastError();
   }
   {
@@ -707,7 +711,8 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
     }
   }
   KScope k(timer, "bucket_group", s);
-  k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, chunk_rows, gkey, gmin, rep);
+  k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, ChunkOf::make(chunk_rows),
+                                                      gkey, gmin, rep);
   return hipGetLastError();
 }
 

@@ -18,15 +18,33 @@ __device__ __forceinline__ uint64_t row_hash(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-// Row sources: (key, rank, keyed?) of row i.
+// floor(r / d) for a runtime divisor d, without the ~40-instruction integer
+// division: m = floor((2^64 - 1) / d) + 1 = ceil(2^64 / d) and
+// floor(r / d) = (m * r) >> 64 for every 32-bit r (Lemire, Kaser, Kurz 2019);
+// m = 0 encodes d = 1.
+struct ChunkOf {
+  uint64_t m;
+  static ChunkOf make(uint32_t d) { return ChunkOf{d <= 1 ? 0ull : ~0ull / d + 1}; }
+  __device__ __forceinline__ uint32_t operator()(uint32_t r) const {
+    if (m == 0) return r;
+    const uint64_t lo = static_cast<uint64_t>(static_cast<uint32_t>(m)) * r;
+    const uint64_t hi = (m >> 32) * r;
+    return static_cast<uint32_t>((hi + (lo >> 32)) >> 32);
+  }
+};
+
+// Row sources: (key, rank, keyed?) of row i.  kHashed: the source already
+// carries row_hash(key) in place of the key (the bucket records: row_hash is a
+// bijection, so equal hashes are equal keys and the grouping reads the hash).
 //   RowsIn: the caller's rows -- key[i], valid[i] (null: all keyed), rank[i]
 //           (null: rank_base + i);
 //   RecIn:  packed 12-byte exchange records {key lo, key hi, rank} as received
 //           from the other GPUs, valid[i] optional (the Object-index probe's mask).
-//   Rec16In: 16-byte bucket records {key lo, key hi, rank, row} of a first
+//   Rec16In: 16-byte bucket records {hash lo, hash hi, rank, row} of a first
 //           partition pass (the row is carried, not the position).
 // get_row also returns the row whose rep the record answers for.
 struct RowsIn {
+  static constexpr bool kHashed = false;
   const uint64_t* key;
   const uint8_t* valid;
   const uint32_t* rank;
@@ -43,6 +61,7 @@ struct RowsIn {
   }
 };
 struct RecIn {
+  static constexpr bool kHashed = false;
   const uint3* rec;
   const uint8_t* valid;
   __device__ __forceinline__ void get(uint64_t i, uint64_t& k, uint32_t& r, bool& v) const {
@@ -58,6 +77,7 @@ struct RecIn {
   }
 };
 struct Rec16In {
+  static constexpr bool kHashed = true;
   const uint4* rec;
   __device__ __forceinline__ void get(uint64_t i, uint64_t& k, uint32_t& r, bool& v) const {
     const uint4 q = rec[i];
@@ -74,5 +94,11 @@ struct Rec16In {
     v = true;
   }
 };
+
+template <typename In>
+__device__ __forceinline__ uint64_t in_hash(uint64_t k) {
+  if constexpr (In::kHashed) return k;
+  else return row_hash(k);
+}
 
 }  // namespace sdgpu
