@@ -148,7 +148,19 @@ class Runner:
             # torch.distributed group, every rank joins
             obj = [dedup.Comm.unique_id() if self.rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
-            self.comm = dedup.Comm.init_rank(self.ctx, self.world, self.rank, obj[0])
+            err = None
+            try:
+                self.comm = dedup.Comm.init_rank(self.ctx, self.world, self.rank, obj[0])
+            except Exception as e:  # reported, and every rank takes the same path
+                err = e
+            ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=self.dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0:
+                log(f"bench: libsdgpu RCCL communicator unavailable on some rank ({err!r}); "
+                    "the exchange runs over torch.distributed instead")
+                if self.comm is not None:
+                    self.comm.close()
+                    self.comm = None
 
     def exchange_name(self) -> str:
         if self.comm is not None:
@@ -428,6 +440,7 @@ class Runner:
                                                         device=self.local, ctx=self.ctx)
         if self.args.verify:
             self.verify_sharded(key, has, rank)
+        self.group(key, has, rank)  # first launches (lazy code-object loads) untimed
         self.ctx.set_timing(True)
         t = self.timed(lambda: self.group(key, has, rank), steps, warmup)
         kt = self.ctx.kernel_times()
@@ -508,6 +521,8 @@ class Runner:
         total = self.args.dedup_full_rows
         key, has, rank = corpus.synth_dedup_rows_device(4, total, int(total * 0.8), 0, total,
                                                         device=self.local, ctx=self.ctx)
+        self.ops.group_rows(key, has, rank, 100, 0)  # two-level kernels' first launches
+        torch.cuda.synchronize()
         self.ctx.set_timing(True)
         t = self.timed(lambda: self.ops.group_rows(key, has, rank, 100, 0), steps, warmup)
         kt = self.ctx.kernel_times()
