@@ -15,9 +15,11 @@ Components reported on the same line (each timed the same way, K steps after W
 warm-up, barrier + synchronize on both sides, max over ranks):
   cas      K1 alone over config 2                              files/s
   dedup    config 4: 12.5 M rows per GPU (100 M at 8 GPUs)     rows/s
+           (+ at N = 1 the whole 100 M-row table on one GPU)
   checksum config 3: 64 x 4 GiB files per GPU, device-resident GB/s
-  staged   config 5 shape: 250 k config-2 files per GPU whose windows sit in
-           pinned host memory, streamed H2D + K1 + grouping + link batch files/s
+  staged   config 5: a 50 M-file identifier run, steps of 250 k config-2
+           files per GPU whose windows sit in pinned host memory, streamed
+           H2D + K1 + grouping against the run's Object index + link batch files/s
   dir      config 1: a real 10 k-file directory (sparse files, warm cache)
            through sdgpu_identify_files (pread -> pinned -> K1)         files/s
 `roofline` is for the dominant kernel (K1 "cas_leaves"), timed live with HIP
@@ -38,10 +40,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# int32 VALU peak: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz.  The 32-bit integer
-# ops BLAKE3 uses (v_add3_u32, v_alignbit_b32, v_xor_b32, v_add_u32) issue a
-# wave64 in 4 cycles on gfx950 (measured: sdgpu_valu_probe ~ 33 T/s under load,
-# DESIGN.md §4); the 157 TFLOP/s FP32 figure counts packed-FMA lanes instead.
+# int32 VALU peak: 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz.  BLAKE3's mix of
+# 32-bit ops (v_add3_u32, v_alignbit_b32, v_xor_b32, v_add_u32) issues at that
+# rate: a register-only compression loop measures ~38.7 T lane-ops/s whatever
+# the VOP2/VOP3 split (profiles/r2/exp_g_mix_r2f.log); the
+# 157 TFLOP/s FP32 figure counts packed-FMA lanes instead.
 VALU_PEAK_SPEC = 256 * 4 * 16 * 2.4e9
 HBM_PEAK = 8.0e12                       # B/s (MI355X spec)
 ISA_PER_COMPRESSION = 680               # fused VALU instructions per BLAKE3 compression
@@ -645,6 +648,23 @@ class Runner:
                                  f"scalar_value = scalar oracle cas_id_path, same threads"}
             shutil.rmtree(root, ignore_errors=True)
             self._dir_sample = None
+        # config 3's hashing (file_checksum, hash.rs:10-24): the AVX2 subtree
+        # hasher, one 256 MiB buffer per thread (one file per thread, as that
+        # many validator jobs would run), and on one thread (the reference
+        # hashes a file on one blocking-pool thread)
+        buf = np.random.default_rng(3).integers(0, 256, 256 << 20, dtype=np.uint8)
+        t0 = time.perf_counter()
+        O.blake3_simd(buf)
+        ck1 = buf.size / (time.perf_counter() - t0)
+        ck_reps = int(max(1, min(20, np.ceil(3.0 * ck1 / buf.size))))
+        t0 = time.perf_counter()
+        O.checksum_simd_mt(buf, threads, ck_reps)
+        ckt = time.perf_counter() - t0
+        ck = {"value": threads * ck_reps * buf.size / ckt / 1e9, "unit": "GB/s",
+              "threads": threads, "value_1thread": ck1 / 1e9,
+              "sample": f"{threads} threads x {ck_reps} x 256 MiB in host RAM, AVX2 8-way "
+                        f"BLAKE3 over 1024-chunk subtrees (oracle orc_checksum_simd_mt)"}
+        del buf
         single = None
         if getattr(self, "_single_sample", None):
             single = {}
@@ -663,7 +683,8 @@ class Runner:
         return {"value": reps * m / dt, "unit": "files/s", "cores": threads, "kind": "port",
                 "cores_note": cores_note,
                 "value_1thread": one, "scalar_value": scalar,
-                "config1_dir": dir_res, "single_file_1thread": single,
+                "config1_dir": dir_res, "config3_checksum": ck,
+                "single_file_1thread": single,
                 "sample": f"first {m} files of config 2 (their {int(h_len.sum())} window bytes "
                           f"in host RAM) hashed {reps}x, AVX2 8-way BLAKE3 port "
                           f"(oracle/sd_oracle.c orc_cas_batch_simd), {threads} threads, "

@@ -73,6 +73,9 @@ def lib():
         L.orc_balloon_blake3_trace.restype = ctypes.c_int64
         L.orc_cas_paths_simd.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.orc_blake3_simd.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.orc_checksum_simd_mt.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_void_p]
         del u8p
         _lib = L
     return _lib
@@ -211,6 +214,24 @@ def cas_batch_simd(arena: np.ndarray, off: np.ndarray, length: np.ndarray,
     out = np.zeros((off.size, 8), np.uint8)
     lib().orc_cas_batch_simd(_ptr(arena), _ptr(off), _ptr(length), off.size, _ptr(out), threads)
     return out
+
+
+def blake3_simd(data: np.ndarray) -> bytes:
+    """BLAKE3 of a buffer with the AVX2 subtree hasher (CPU baseline of
+    file_checksum, hash.rs:10-24)."""
+    data = np.ascontiguousarray(data, np.uint8)
+    out = np.zeros(32, np.uint8)
+    lib().orc_blake3_simd(_ptr(data), data.size, _ptr(out))
+    return out.tobytes()
+
+
+def checksum_simd_mt(data: np.ndarray, threads: int, reps: int) -> bytes:
+    """`threads` threads each hash `data` `reps` times with the AVX2 hasher
+    (one file per thread); returns thread 0's digest."""
+    data = np.ascontiguousarray(data, np.uint8)
+    out = np.zeros(32, np.uint8)
+    lib().orc_checksum_simd_mt(_ptr(data), data.size, threads, reps, _ptr(out))
+    return out.tobytes()
 
 
 def cas_paths_simd(paths, sizes, threads: int = 1):

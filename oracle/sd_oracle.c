@@ -1217,6 +1217,96 @@ void orc_cas_batch_simd(const uint8_t *arena, const uint64_t *off, const uint32_
 }
 
 /* ------------------------------------------------------------------------- */
+/* file_checksum's hashing with AVX2 (CPU BASELINE ONLY: bench.py's config-3 */
+/* leg): the crate hashes a file's chunks 8/16 at a time (hash_many); here   */
+/* aligned 1024-chunk subtrees go through v_chunks8 / v_parents8 and are     */
+/* pushed on the incremental hasher's CV stack; the tail (>= 1 byte, so the  */
+/* last chunk stays in the chunk state for ROOT) through h_update.           */
+/* ------------------------------------------------------------------------- */
+
+/* CV (non-root) of the aligned subtree of 1024 full chunks at chunk ctr0. */
+static void simd_subtree1024(const uint8_t *p, uint64_t ctr0, uint32_t cv[8]) {
+  uint32_t cvs[1024][8] __attribute__((aligned(32)));
+  for (size_t c = 0; c < 1024; c += 8) {
+    const uint8_t *pp[8];
+    uint32_t *o[8];
+    for (int j = 0; j < 8; ++j) {
+      pp[j] = p + (c + j) * B3_CHUNK;
+      o[j] = cvs[c + j];
+    }
+    v_chunks8(pp, ctr0 + c, o);
+  }
+  for (size_t cnt = 1024; cnt > 2; cnt /= 2) {
+    const size_t half = cnt / 2;
+    size_t k = 0;
+    for (; k + 8 <= half; k += 8) {
+      const uint32_t *pr[8];
+      uint32_t *o[8];
+      uint32_t tmp[8][8] __attribute__((aligned(32)));
+      for (int j = 0; j < 8; ++j) {
+        pr[j] = cvs[2 * (k + j)];
+        o[j] = tmp[j];
+      }
+      v_parents8(pr, o);
+      for (int j = 0; j < 8; ++j) memcpy(cvs[k + j], tmp[j], 32);
+    }
+    for (; k < half; ++k) {
+      uint32_t t[8];
+      s_parent_cv(cvs[2 * k], cvs[2 * k + 1], 0, t);
+      memcpy(cvs[k], t, 32);
+    }
+  }
+  s_parent_cv(cvs[0], cvs[1], 0, cv);
+}
+
+void orc_blake3_simd(const uint8_t *in, size_t len, uint8_t out32[32]) {
+  orc_hasher h;
+  h_init(&h);
+  const size_t S = (size_t)1024 * B3_CHUNK;
+  size_t off = 0;
+  while (len - off > S) {
+    uint32_t cv[8];
+    simd_subtree1024(in + off, off / B3_CHUNK, cv);
+    off += S;
+    h_push_cv(&h, cv, (off / B3_CHUNK) >> 10); /* totals in units of subtrees */
+  }
+  h.chunk_counter = off / B3_CHUNK;
+  h_update(&h, in + off, len - off);
+  h_finalize(&h, out32);
+}
+
+typedef struct {
+  const uint8_t *in;
+  size_t len;
+  int reps;
+  uint8_t out32[32];
+} ck_job;
+
+static void *ck_worker(void *arg) {
+  ck_job *j = (ck_job *)arg;
+  for (int r = 0; r < j->reps; ++r) orc_blake3_simd(j->in, j->len, j->out32);
+  return NULL;
+}
+
+/* `threads` threads, each hashing the buffer `reps` times (one file per
+ * thread, as N validator jobs would); out32 = the digest of thread 0. */
+void orc_checksum_simd_mt(const uint8_t *in, size_t len, int threads, int reps,
+                          uint8_t out32[32]) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  ck_job jobs[256];
+  for (int t = 0; t < threads; t++) {
+    jobs[t].in = in;
+    jobs[t].len = len;
+    jobs[t].reps = reps;
+    pthread_create(&th[t], NULL, ck_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  memcpy(out32, jobs[0].out32, 32);
+}
+
+/* ------------------------------------------------------------------------- */
 /* generate_cas_id over real files with the reference's I/O pattern and the  */
 /* AVX2 hasher (CPU BASELINE ONLY: bench.py's config-1 leg).                 */
 /* ------------------------------------------------------------------------- */

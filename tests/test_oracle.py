@@ -261,3 +261,16 @@ def test_simd_paths_baseline_matches_path_oracle(tmp_path):
     assert st[-1] == -2 and np.all(st[:-1] == 0)
     for p, s, o in zip(paths[:-1], sizes[:-1].tolist(), out[:-1]):
         assert bytes(o).hex() == O.cas_id_path(p, s)
+
+
+def test_simd_file_hasher_matches_oracle():
+    """The config-3 CPU baseline's AVX2 subtree hasher (1024-chunk subtrees on
+    the CV stack, tail through the incremental hasher) is bit-exact with the
+    recursive oracle around every subtree boundary it has."""
+    S = 1024 * 1024
+    rng = np.random.default_rng(11)
+    data = rng.integers(0, 256, 5 * S + 3000, dtype=np.uint8)
+    for n in (0, 1, 1024, 1025, S - 1, S, S + 1, 2 * S, 2 * S + 1, 3 * S + 777, 4 * S,
+              4 * S + 1024, 5 * S + 3000):
+        assert O.blake3_simd(data[:n]) == O.blake3(data[:n].tobytes()), n
+    assert O.checksum_simd_mt(data[:3 * S + 5], 3, 2) == O.blake3(data[:3 * S + 5].tobytes())
