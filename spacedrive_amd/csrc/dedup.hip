@@ -91,6 +91,14 @@ __device__ __forceinline__ void tile_of(uint64_t n, uint32_t P, uint64_t& t0, ui
 // issued back to back, so one tile costs a few memory latencies, not one per row.
 constexpr int kUnroll = 8;
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not for its global loads and stores (__syncthreads' release
+// fence waits for all of them: vmcnt(0) before every round barrier).  The
+// "memory" clobber keeps the compiler from moving memory accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Partition digit of a row hash: the destination rank of the multi-GPU
 // exchange when world != 0 (shard s = top `bits` hash bits belongs to rank
 // s * world >> bits), else `bits` hash bits below the top `skip` bits.
@@ -133,21 +141,16 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += kUnroll * kPartThreads) {
-    uint64_t k[kUnroll];
-    uint32_t r[kUnroll];
-    bool v[kUnroll];
+    RowBatch<kUnroll> q;
+    in.template load_many<kUnroll>(i0, kPartThreads, t1, i0, q);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      v[u] = false;
-      if (i < t1) in.get(i, k[u], r[u], v[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+      const bool v = in.valid_of(q, u);
+      const uint64_t k = in.key_of(q, u);
       if (world) {
-        (void)wave_add(cnt, v[u] ? part_digit(in_hash<In>(k[u]), skip, bits, world) : 0u, v[u]);
-      } else if (v[u]) {
-        atomicAdd(&cnt[part_digit(in_hash<In>(k[u]), skip, bits, world)], 1u);
+        (void)wave_add(cnt, v ? part_digit(in_hash<In>(k), skip, bits, world) : 0u, v);
+      } else if (v) {
+        atomicAdd(&cnt[part_digit(in_hash<In>(k), skip, bits, world)], 1u);
       }
     }
   }
@@ -178,31 +181,26 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
   tile_of(n, gridDim.x, t0, t1);
   constexpr int U = kUnroll / 2;
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += U * kPartThreads) {
-    uint64_t k[U];
-    uint32_t r[U];
-    bool in_[U], v[U];
+    RowBatch<U> q;
+    in.template load_many<U>(i0, kPartThreads, t1, i0, q);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      in_[u] = i < t1;
-      v[u] = false;
-      if (in_[u]) in.get(i, k[u], r[u], v[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      const uint32_t d = v[u] ? part_digit(in_hash<In>(k[u]), skip, bits, world) : 0u;
-      const uint32_t p = world ? wave_add(cur, d, v[u]) : (v[u] ? atomicAdd(&cur[d], 1u) : 0u);
-      if (!v[u]) {
-        if (kRec12 && in_[u]) out_pos[i] = 0xFFFFFFFFu;
+      const bool v = in.valid_of(q, u);
+      const uint64_t k = in.key_of(q, u);
+      const uint32_t d = v ? part_digit(in_hash<In>(k), skip, bits, world) : 0u;
+      const uint32_t p = world ? wave_add(cur, d, v) : (v ? atomicAdd(&cur[d], 1u) : 0u);
+      if (!v) {
+        if (kRec12 && q.in[u]) out_pos[i] = 0xFFFFFFFFu;
         continue;
       }
+      const uint32_t r = in.rank_of(q, u);
       if (kRec12) {
-        out_rec[p] = make_uint3(static_cast<uint32_t>(k[u]), static_cast<uint32_t>(k[u] >> 32), r[u]);
+        out_rec[p] = make_uint3(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32), r);
         out_pos[i] = p;
       } else {
-        out_key[p] = k[u];
-        out_rank[p] = r[u];
+        out_key[p] = k;
+        out_rank[p] = r;
         out_pos[p] = static_cast<uint32_t>(i);
       }
     }
@@ -227,26 +225,20 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
   tile_of(n, gridDim.x, t0, t1);
   constexpr int U = kUnroll;
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += U * kPartThreads) {
-    uint64_t k[U];
-    uint32_t r[U], row[U];
-    bool in_[U], v[U];
+    RowBatch<U> q;
+    in.template load_many<U>(i0, kPartThreads, t1, i0, q);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      in_[u] = i < t1;
-      v[u] = false;
-      if (in_[u]) in.get_row(i, k[u], r[u], row[u], v[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
+      const uint32_t r = in.rank_of(q, u);
       // every row starts as its own Object (coalesced store): rows without a
       // key stay so (mod.rs:238-239); K5 overwrites only the rows that link
-      if (kInitRep && in_[u]) rep[i] = r[u];
-      if (!v[u]) continue;
-      const uint64_t h = in_hash<In>(k[u]);
+      if (kInitRep && q.in[u]) rep[i] = r;
+      if (!in.valid_of(q, u)) continue;
+      const uint64_t h = in_hash<In>(in.key_of(q, u));
       const uint32_t p = atomicAdd(&cur[digit_of(h, skip, bits)], 1u);
-      rec[p] = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r[u], row[u]);
+      rec[p] = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r,
+                          in.row_of(q, u));
     }
   }
 }
@@ -286,29 +278,37 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     tile_of(n, gridDim.x, t0, t1);
   }
   constexpr int U = 2;
-  for (uint64_t i0 = t0; i0 < t1; i0 += U * kPartThreads) {  // uniform trip count
+  constexpr uint64_t kStep = static_cast<uint64_t>(U) * kPartThreads;
+  // software pipeline: round r + 1's rows are loaded while round r is staged
+  // and flushed; the round barriers wait for LDS only (lds_barrier), so the
+  // loads and the record stores stay in flight across them
+  // one round: stage (or write) the batch's rows, then flush the full pairs
+  auto round = [&](const RowBatch<U>& q, uint64_t i0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads;
-      if (i >= t1) continue;
-      uint64_t k;
-      uint32_t r, row;
-      bool v;
-      in.get_row(i, k, r, row, v);
+      if (!q.in[u]) continue;
+      const uint32_t r = in.rank_of(q, u);
       if (kInitRep) rep[i] = r;
-      if (!v) continue;
-      const uint64_t h = in_hash<In>(k);
+      if (!in.valid_of(q, u)) continue;
+      const uint64_t h = in_hash<In>(in.key_of(q, u));
       const uint32_t b = digit_of(h, skip, kStageBits);
-      const uint4 q = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r, row);
+      const uint4 rq = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r,
+                                  in.row_of(q, u));
       const uint32_t sl = atomicAdd(&fill[b], 1u);
       if (sl < 2) {
-        stage[b][sl] = q;
+        stage[b][sl] = rq;
       } else {
-        rec[atomicAdd(&cur[b], 1u)] = q;
+        rec[atomicAdd(&cur[b], 1u)] = rq;
       }
     }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) {
+    lds_barrier();
+    // unrolled, not a loop: the compiler drains every load in flight before a
+    // store-only loop that reads registers loaded outside it (vmcnt(0))
+    static_assert(nbins % kPartThreads == 0, "flush slots per thread");
+#pragma unroll
+    for (uint32_t j = 0; j < nbins / kPartThreads; ++j) {
+      const uint32_t b = threadIdx.x + j * kPartThreads;
       if (fill[b] >= 2) {
         const uint32_t p = cur[b];
         cur[b] = p + 2;
@@ -317,7 +317,23 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
         fill[b] = 0;
       }
     }
-    __syncthreads();
+    lds_barrier();
+  };
+  // two batches in ping-pong (no register copy between rounds, which would
+  // wait for the loads just issued)
+  // and the prefetches unconditional (past the tile they re-read row t0), so
+  // the compiler's wait counts need not cover a path without them
+  if (t0 < t1) {
+    RowBatch<U> qa, qb;
+    in.template load_many<U>(t0 + threadIdx.x, kPartThreads, t1, t0, qa);
+    for (uint64_t i0 = t0;; i0 += 2 * kStep) {  // uniform trip count
+      in.template load_many<U>(i0 + kStep + threadIdx.x, kPartThreads, t1, t0, qb);
+      round(qa, i0);
+      if (i0 + kStep >= t1) break;
+      in.template load_many<U>(i0 + 2 * kStep + threadIdx.x, kPartThreads, t1, t0, qa);
+      round(qb, i0 + kStep);
+      if (i0 + 2 * kStep >= t1) break;
+    }
   }
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
     if (fill[b] == 1) rec[cur[b]] = stage[b][0];
@@ -338,18 +354,12 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_hist(Rec16In in, uint32_
   uint64_t t0, t1;
   tile_of(s1 - s0, gridDim.x, t0, t1);
   for (uint64_t i0 = s0 + t0 + threadIdx.x; i0 < s0 + t1; i0 += kUnroll * kPartThreads) {
-    uint64_t k[kUnroll];
-    bool v[kUnroll];
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const uint64_t i = i0 + static_cast<uint64_t>(u) * kPartThreads;
-      uint32_t r;
-      v[u] = false;
-      if (i < s0 + t1) in.get(i, k[u], r, v[u]);
-    }
+    RowBatch<kUnroll> q;
+    in.template load_many<kUnroll>(i0, kPartThreads, s0 + t1, i0, q);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
-      if (v[u]) atomicAdd(&cnt[digit_of(k[u], skip, kStageBits)], 1u);  // records hold the hash
+      if (in.valid_of(q, u))  // records hold the hash
+        atomicAdd(&cnt[digit_of(in.key_of(q, u), skip, kStageBits)], 1u);
   }
   __syncthreads();
   const uint64_t obase = static_cast<uint64_t>(c) * nbins * gridDim.x;

@@ -42,7 +42,33 @@ struct ChunkOf {
 //           from the other GPUs, valid[i] optional (the Object-index probe's mask).
 //   Rec16In: 16-byte bucket records {hash lo, hash hi, rank, row} of a first
 //           partition pass (the row is carried, not the position).
-// get_row also returns the row whose rep the record answers for.
+// get / get_row read one row (get_row also returns the row whose rep the
+// record answers for).  The partition kernels read U rows per thread with
+// load_many into a RowBatch: every load is issued, and nothing derived from a
+// loaded value is computed, before the batch is used (key_of / rank_of /
+// valid_of resolve a row at its use) -- guarded one-row reads, or a validity
+// test right after the byte load, made the compiler wait out each row's
+// memory latency in turn.  Rows at or past `end` read row `safe` (in = false).
+template <int U>
+struct RowBatch {
+  uint64_t k[U];
+  uint32_t a[U];    // rank as loaded (RowsIn with rank / records)
+  uint32_t b[U];    // valid byte as loaded (RowsIn / RecIn), or the record's row
+  uint32_t row[U];  // the row index read
+  bool in[U];
+};
+
+template <int U>
+__device__ __forceinline__ void batch_index(uint64_t i0, uint64_t stride, uint64_t end,
+                                            uint64_t safe, RowBatch<U>& q) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint64_t i = i0 + static_cast<uint64_t>(u) * stride;
+    q.in[u] = i < end;
+    q.row[u] = static_cast<uint32_t>(q.in[u] ? i : safe);
+  }
+}
+
 struct RowsIn {
   static constexpr bool kHashed = false;
   const uint64_t* key;
@@ -59,6 +85,35 @@ struct RowsIn {
     get(i, k, r, v);
     row = static_cast<uint32_t>(i);
   }
+  // null rank / valid: the loads read the key array instead (same lines) and
+  // the value is replaced at use, so the batch has no branch
+  template <int U>
+  __device__ __forceinline__ void load_many(uint64_t i0, uint64_t stride, uint64_t end,
+                                            uint64_t safe, RowBatch<U>& q) const {
+    batch_index(i0, stride, end, safe, q);
+    const uint32_t* rs = rank ? rank : reinterpret_cast<const uint32_t*>(key);
+    const uint8_t* vs = valid ? valid : reinterpret_cast<const uint8_t*>(key);
+#pragma unroll
+    for (int u = 0; u < U; ++u) q.k[u] = key[q.row[u]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) q.a[u] = rs[q.row[u]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) q.b[u] = vs[q.row[u]];
+  }
+  template <int U>
+  __device__ __forceinline__ uint64_t key_of(const RowBatch<U>& q, int u) const { return q.k[u]; }
+  template <int U>
+  __device__ __forceinline__ uint32_t rank_of(const RowBatch<U>& q, int u) const {
+    return rank ? q.a[u] : rank_base + q.row[u];
+  }
+  template <int U>
+  __device__ __forceinline__ bool valid_of(const RowBatch<U>& q, int u) const {
+    return q.in[u] && (!valid || (q.b[u] & 0xFFu) != 0);
+  }
+  template <int U>
+  __device__ __forceinline__ uint32_t row_of(const RowBatch<U>& q, int u) const {
+    return q.row[u];
+  }
 };
 struct RecIn {
   static constexpr bool kHashed = false;
@@ -74,6 +129,34 @@ struct RecIn {
                                           bool& v) const {
     get(i, k, r, v);
     row = static_cast<uint32_t>(i);
+  }
+  template <int U>
+  __device__ __forceinline__ void load_many(uint64_t i0, uint64_t stride, uint64_t end,
+                                            uint64_t safe, RowBatch<U>& q) const {
+    batch_index(i0, stride, end, safe, q);
+    const uint8_t* vs = valid ? valid : reinterpret_cast<const uint8_t*>(rec);
+    uint3 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = rec[q.row[u]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) q.b[u] = vs[q.row[u]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      q.k[u] = (static_cast<uint64_t>(t[u].y) << 32) | t[u].x;
+      q.a[u] = t[u].z;
+    }
+  }
+  template <int U>
+  __device__ __forceinline__ uint64_t key_of(const RowBatch<U>& q, int u) const { return q.k[u]; }
+  template <int U>
+  __device__ __forceinline__ uint32_t rank_of(const RowBatch<U>& q, int u) const { return q.a[u]; }
+  template <int U>
+  __device__ __forceinline__ bool valid_of(const RowBatch<U>& q, int u) const {
+    return q.in[u] && (!valid || (q.b[u] & 0xFFu) != 0);
+  }
+  template <int U>
+  __device__ __forceinline__ uint32_t row_of(const RowBatch<U>& q, int u) const {
+    return q.row[u];
   }
 };
 struct Rec16In {
@@ -93,6 +176,28 @@ struct Rec16In {
     row = q.w;
     v = true;
   }
+  template <int U>
+  __device__ __forceinline__ void load_many(uint64_t i0, uint64_t stride, uint64_t end,
+                                            uint64_t safe, RowBatch<U>& q) const {
+    batch_index(i0, stride, end, safe, q);
+    uint4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = rec[q.row[u]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      q.k[u] = (static_cast<uint64_t>(t[u].y) << 32) | t[u].x;
+      q.a[u] = t[u].z;
+      q.b[u] = t[u].w;
+    }
+  }
+  template <int U>
+  __device__ __forceinline__ uint64_t key_of(const RowBatch<U>& q, int u) const { return q.k[u]; }
+  template <int U>
+  __device__ __forceinline__ uint32_t rank_of(const RowBatch<U>& q, int u) const { return q.a[u]; }
+  template <int U>
+  __device__ __forceinline__ bool valid_of(const RowBatch<U>& q, int u) const { return q.in[u]; }
+  template <int U>
+  __device__ __forceinline__ uint32_t row_of(const RowBatch<U>& q, int u) const { return q.b[u]; }
 };
 
 template <typename In>
