@@ -9,5 +9,4 @@ done
 for P in ${PLIST:-256 128 512}; do
   SDGPU_BUCKET_PART_BLOCKS=$P timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --components dedup --no-cpu --files 100000 > gpurun_out/${T}_bench_P$P.json 2> gpurun_out/${T}_bench_P$P.err || { echo "bench P=$P failed"; exit 1; }
 done
-SDGPU_SCATTER_UNSTAGED=1 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --components dedup --no-cpu --files 100000 > gpurun_out/${T}_bench_unstaged.json 2> gpurun_out/${T}_bench_unstaged.err || { echo "bench unstaged failed"; exit 1; }
 echo "exit 0"

@@ -712,7 +712,7 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   scan::exclusive(hist, nh, hist, tiles, nullptr, s);
   {
     KScope k(timer, "bucket_scatter", s);
-    const bool staged = bits == kStageBits && !getenv("SDGPU_SCATTER_UNSTAGED");
+    const bool staged = bits == kStageBits;
     if (staged && init_rep)
       k_part_scatter_rec_staged<In, true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, hist, rec,
                                                                      rep, nullptr, 0);
