@@ -243,22 +243,23 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
   }
 }
 
-// Bucket partition with LDS pair staging (12-bit digits only): a keyed row is
-// parked in its bucket's 2-record LDS slot and leaves as a 32-B pair, so the
-// scattered writes are half as many and twice as wide.  Rows arriving at a full
-// slot are written directly.  Rows are taken 2 per thread per round; each
-// round ends with a flush of the full pairs; the odd rows go out at the end.
+// Bucket partition with LDS staging (12-bit digits, 2 slots in the product): a
+// keyed row is parked in its bucket's kSlots-record LDS slot and leaves with
+// the slot's other rows as one kSlots x 16-B run, so the scattered writes are
+// kSlots times fewer and wider.  Rows arriving at a full slot are written
+// directly.  Rows are taken kRows per thread per round; each round ends with a
+// flush of the full slots; partly filled slots go out at the end.
 // Two-level use (n > 4096 x kBucketRows): blockIdx.y = segment c of a first,
 // coarse pass ([seg[c * P1], seg[(c + 1) * P1]) of its records), the digit is
 // the 12 hash bits below the segment's, and the offsets are laid out
 // [c][digit][block] -- so the group kernel sees 2^(cbits + 12) buckets.
 constexpr uint32_t kStageBits = 12;
-template <typename In, bool kInitRep>
+template <typename In, bool kInitRep, uint32_t kBits = kStageBits, uint32_t kSlots = 2, int kRows = 2>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     In in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ offs, uint4* __restrict__ rec,
     uint32_t* __restrict__ rep, const uint32_t* __restrict__ seg, uint32_t P1) {
-  constexpr uint32_t nbins = 1u << kStageBits;
-  __shared__ uint4 stage[nbins][2];
+  constexpr uint32_t nbins = 1u << kBits;
+  __shared__ uint4 stage[nbins][kSlots];
   __shared__ uint32_t fill[nbins];
   __shared__ uint32_t cur[nbins];
   const uint32_t c = blockIdx.y;
@@ -277,12 +278,11 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
   } else {
     tile_of(n, gridDim.x, t0, t1);
   }
-  constexpr int U = 2;
+  constexpr int U = kRows;
   constexpr uint64_t kStep = static_cast<uint64_t>(U) * kPartThreads;
-  // software pipeline: round r + 1's rows are loaded while round r is staged
-  // and flushed; the round barriers wait for LDS only (lds_barrier), so the
-  // loads and the record stores stay in flight across them
-  // one round: stage (or write) the batch's rows, then flush the full pairs
+  // one round: stage (or write) the batch's rows, then flush the full slots.
+  // The round barriers wait for LDS only (lds_barrier), so the next round's
+  // loads and this round's record stores stay in flight across them.
   auto round = [&](const RowBatch<U>& q, uint64_t i0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -292,11 +292,11 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       if (kInitRep) rep[i] = r;
       if (!in.valid_of(q, u)) continue;
       const uint64_t h = in_hash<In>(in.key_of(q, u));
-      const uint32_t b = digit_of(h, skip, kStageBits);
+      const uint32_t b = digit_of(h, skip, kBits);
       const uint4 rq = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r,
                                   in.row_of(q, u));
       const uint32_t sl = atomicAdd(&fill[b], 1u);
-      if (sl < 2) {
+      if (sl < kSlots) {
         stage[b][sl] = rq;
       } else {
         rec[atomicAdd(&cur[b], 1u)] = rq;
@@ -309,20 +309,21 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
 #pragma unroll
     for (uint32_t j = 0; j < nbins / kPartThreads; ++j) {
       const uint32_t b = threadIdx.x + j * kPartThreads;
-      if (fill[b] >= 2) {
+      if (fill[b] >= kSlots) {
         const uint32_t p = cur[b];
-        cur[b] = p + 2;
-        rec[p] = stage[b][0];
-        rec[p + 1] = stage[b][1];
+        cur[b] = p + kSlots;
+#pragma unroll
+        for (uint32_t k = 0; k < kSlots; ++k) rec[p + k] = stage[b][k];
         fill[b] = 0;
       }
     }
     lds_barrier();
   };
-  // two batches in ping-pong (no register copy between rounds, which would
-  // wait for the loads just issued)
-  // and the prefetches unconditional (past the tile they re-read row t0), so
-  // the compiler's wait counts need not cover a path without them
+  // Software pipeline: round r + 1's rows are loaded while round r is staged
+  // and flushed.  Two batches in ping-pong (a register copy between rounds
+  // would wait for the loads just issued), and the prefetches unconditional
+  // (past the tile they re-read row t0) so that the compiler's wait counts need
+  // not cover a path without them.
   if (t0 < t1) {
     RowBatch<U> qa, qb;
     in.template load_many<U>(t0 + threadIdx.x, kPartThreads, t1, t0, qa);
@@ -336,7 +337,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     }
   }
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
-    if (fill[b] == 1) rec[cur[b]] = stage[b][0];
+    for (uint32_t k = 0; k < fill[b]; ++k) rec[cur[b] + k] = stage[b][k];
 }
 
 // Histogram of the second pass: block (j, c) counts tile j of segment c's

@@ -276,7 +276,7 @@ int run_sharded(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
     in.n = j.m;
     SD_TRY_RC(group_with_index(j.c, j.idx, in, chunk_rows, j.rrep, j.rvalid, j.s));
   }
-  // 5. reps back to their sources, scatter to row order
+  // 5. reps back to their sources, gathered to row order
   SD_TRY_RC(alltoallv(
       J, W, [](RankJob& j, int p) -> void* { return j.rrep + j.roff[p]; },
       [](RankJob& j, int p) -> void* { return j.back + j.soff[p]; },
