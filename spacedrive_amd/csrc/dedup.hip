@@ -243,6 +243,83 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
   }
 }
 
+// Partition into few digits (<= 64: the coarse pass of the two-level
+// partition) in sorted runs: each round the block's kPartThreads x 4 rows are
+// counting-sorted by digit in LDS (64 KiB) and leave as one contiguous run per
+// digit (~4096 / nbins records, consecutive lanes on consecutive addresses)
+// instead of one scattered 16-B store per row.  The next round's rows are
+// loaded during the current one (ping-pong batches, LDS-only barriers).
+constexpr uint32_t kRunMaxBins = 64;
+template <typename In, bool kInitRep>
+__global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
+    In in, uint64_t n, uint32_t skip, uint32_t bits, const uint32_t* __restrict__ offs,
+    uint4* __restrict__ rec, uint32_t* __restrict__ rep) {
+  constexpr int U = 4;
+  constexpr uint32_t R = U * kPartThreads;
+  __shared__ uint4 buf[R];
+  __shared__ uint32_t cnt[kRunMaxBins], base[kRunMaxBins + 1], cur[kRunMaxBins];
+  const uint32_t nbins = 1u << bits;
+  if (threadIdx.x < nbins)
+    cur[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * gridDim.x + part_block()];
+  uint64_t t0, t1;
+  tile_of(n, gridDim.x, t0, t1);
+  auto round = [&](const RowBatch<U>& q, uint64_t i0) {
+    if (threadIdx.x < nbins) cnt[threadIdx.x] = 0;
+    lds_barrier();
+    uint32_t dg[U], lr[U];
+    uint4 rq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads;
+      dg[u] = ~0u;
+      if (!q.in[u]) continue;
+      const uint32_t r = in.rank_of(q, u);
+      if (kInitRep) rep[i] = r;
+      if (!in.valid_of(q, u)) continue;
+      const uint64_t h = in_hash<In>(in.key_of(q, u));
+      dg[u] = digit_of(h, skip, bits);
+      lr[u] = atomicAdd(&cnt[dg[u]], 1u);
+      rq[u] = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r,
+                         in.row_of(q, u));
+    }
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      uint32_t run = 0;
+      for (uint32_t b = 0; b < nbins; ++b) {
+        base[b] = run;
+        run += cnt[b];
+      }
+      base[nbins] = run;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (dg[u] != ~0u) buf[base[dg[u]] + lr[u]] = rq[u];
+    lds_barrier();
+    const uint32_t total = base[nbins];
+    for (uint32_t k = threadIdx.x; k < total; k += kPartThreads) {
+      const uint4 v = buf[k];
+      const uint32_t b = digit_of((static_cast<uint64_t>(v.y) << 32) | v.x, skip, bits);
+      rec[cur[b] + (k - base[b])] = v;
+    }
+    lds_barrier();
+    if (threadIdx.x < nbins) cur[threadIdx.x] += cnt[threadIdx.x];
+  };
+  constexpr uint64_t kStep = R;
+  if (t0 < t1) {
+    RowBatch<U> qa, qb;
+    in.template load_many<U>(t0 + threadIdx.x, kPartThreads, t1, t0, qa);
+    for (uint64_t i0 = t0;; i0 += 2 * kStep) {  // uniform trip count
+      in.template load_many<U>(i0 + kStep + threadIdx.x, kPartThreads, t1, t0, qb);
+      round(qa, i0);
+      if (i0 + kStep >= t1) break;
+      in.template load_many<U>(i0 + 2 * kStep + threadIdx.x, kPartThreads, t1, t0, qa);
+      round(qb, i0 + kStep);
+      if (i0 + 2 * kStep >= t1) break;
+    }
+  }
+}
+
 // Bucket partition with LDS staging (12-bit digits, 2 slots in the product): a
 // keyed row is parked in its bucket's kSlots-record LDS slot and leaves with
 // the slot's other rows as one kSlots x 16-B run, so the scattered writes are
@@ -251,9 +328,17 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
 // flush of the full slots; partly filled slots go out at the end.
 // Two-level use (n > 4096 x kBucketRows): blockIdx.y = segment c of a first,
 // coarse pass ([seg[c * P1], seg[(c + 1) * P1]) of its records), the digit is
-// the 12 hash bits below the segment's, and the offsets are laid out
-// [c][digit][block] -- so the group kernel sees 2^(cbits + 12) buckets.
+// the kBits hash bits below the segment's, and the offsets are laid out
+// [c][digit][block] -- so the group kernel sees 2^(cbits + kBits) buckets.
 constexpr uint32_t kStageBits = 12;
+// Second pass of the two-level partition: 10 digit bits, 8-record runs, 4 rows
+// per thread per round, 64 blocks per coarse segment (~48 rows per bucket per
+// block: whole 128-B runs).  Measured on the staged scatter alone
+// (profiles/r2/exp_scatter_slots_r2t.log): 12/2 0.163 ms, 10/8 0.123 ms.
+constexpr uint32_t kStage2Bits = 10;
+constexpr uint32_t kStage2Slots = 8;
+constexpr int kStage2Rows = 4;
+constexpr uint32_t kStage2Blocks = 64;
 template <typename In, bool kInitRep, uint32_t kBits = kStageBits, uint32_t kSlots = 2, int kRows = 2>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     In in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ offs, uint4* __restrict__ rec,
@@ -342,11 +427,12 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
 
 // Histogram of the second pass: block (j, c) counts tile j of segment c's
 // records on the 12 digit bits below the segment's.
+template <uint32_t kBits>
 __global__ __launch_bounds__(kPartThreads) void k_part2_hist(Rec16In in, uint32_t skip,
                                                              const uint32_t* __restrict__ seg,
                                                              uint32_t P1,
                                                              uint32_t* __restrict__ hist) {
-  constexpr uint32_t nbins = 1u << kStageBits;
+  constexpr uint32_t nbins = 1u << kBits;
   __shared__ uint32_t cnt[nbins];
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) cnt[b] = 0;
   __syncthreads();
@@ -360,7 +446,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_hist(Rec16In in, uint32_
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
       if (in.valid_of(q, u))  // records hold the hash
-        atomicAdd(&cnt[digit_of(in.key_of(q, u), skip, kStageBits)], 1u);
+        atomicAdd(&cnt[digit_of(in.key_of(q, u), skip, kBits)], 1u);
   }
   __syncthreads();
   const uint64_t obase = static_cast<uint64_t>(c) * nbins * gridDim.x;
@@ -617,10 +703,10 @@ uint32_t bucket_bits_for(uint64_t n) {
 }
 
 // Above 2^12 buckets (n > ~12.6 M rows) the partition runs in two passes: a
-// coarse one on the top cbits = bits - 12 digit bits (<= 8 output streams per
-// block: full-line writes) into rec1, then the 12-bit LDS-staged pass per
-// coarse segment into rec.  A single 2^15-way scatter keeps 32 k partially
-// written lines open per block and ran 3.7 ms for 100 M rows
+// coarse one on the top cbits = bits - 10 digit bits (<= 32 output streams per
+// block) into rec1, then a 10-bit LDS-staged pass per coarse segment into rec
+// (8-record runs, 64 blocks per segment).  A single 2^15-way scatter keeps 32 k
+// partially written lines open per block and ran 3.7 ms for 100 M rows
 // (profiles/r2/bench_r2b.json); the two passes move 2 x 32 B per row instead.
 struct GroupLayout {
   uint32_t bits, cbits;
@@ -630,7 +716,7 @@ struct GroupLayout {
 GroupLayout group_layout(uint64_t n) {
   GroupLayout L;
   L.bits = bucket_bits_for(n);
-  L.cbits = L.bits > kStageBits ? L.bits - kStageBits : 0;
+  L.cbits = L.bits > kStageBits ? L.bits - kStage2Bits : 0;
   const uint64_t nh = (static_cast<uint64_t>(1) << L.bits) * kMaxPartBlocks;
   const uint64_t nh1 = (static_cast<uint64_t>(1) << L.cbits) * kMaxPartBlocks;
   size_t o = 0;
@@ -680,28 +766,33 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
     scan::exclusive(hist1, static_cast<uint64_t>(nseg) * P, hist1, tiles, nullptr, s);
     {
       KScope k(timer, "bucket_scatter1", s);
+      static_assert(kMaxBucketBits - kStage2Bits <= 6, "coarse digits fit k_part_scatter_runs");
       if (init_rep)
-        k_part_scatter_rec<In, true><<<P, kPartThreads, lds1, s>>>(in, n, kShardBits, L.cbits,
-                                                                   hist1, rec1, rep);
+        k_part_scatter_runs<In, true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, L.cbits,
+                                                                 hist1, rec1, rep);
       else
-        k_part_scatter_rec<In, false><<<P, kPartThreads, lds1, s>>>(in, n, kShardBits, L.cbits,
-                                                                    hist1, rec1, rep);
+        k_part_scatter_runs<In, false><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, L.cbits,
+                                                                  hist1, rec1, rep);
     }
-    // pass 2: 12 bits below, per coarse segment, staged
+    // pass 2: kStage2Bits below, per coarse segment, staged in 8-record runs
+    // (offsets [c][digit][block] = bucket-major with P2 blocks per bucket)
     const Rec16In in2{rec1};
+    const uint32_t P2 = kStage2Blocks;
+    static_assert(kStage2Blocks <= kMaxPartBlocks, "hist sized for kMaxPartBlocks");
     {
       KScope k(timer, "bucket_hist2", s);
-      k_part2_hist<<<dim3(P, nseg), kPartThreads, 0, s>>>(in2, kShardBits + L.cbits, hist1, P,
-                                                           hist);
+      k_part2_hist<kStage2Bits><<<dim3(P2, nseg), kPartThreads, 0, s>>>(
+          in2, kShardBits + L.cbits, hist1, P, hist);
     }
-    scan::exclusive(hist, nh, hist, tiles, nullptr, s);
+    scan::exclusive(hist, (static_cast<uint64_t>(1) << bits) * P2, hist, tiles, nullptr, s);
     {
       KScope k(timer, "bucket_scatter", s);
-      k_part_scatter_rec_staged<Rec16In, false><<<dim3(P, nseg), kPartThreads, 0, s>>>(
-          in2, 0, kShardBits + L.cbits, hist, rec, nullptr, hist1, P);
+      k_part_scatter_rec_staged<Rec16In, false, kStage2Bits, kStage2Slots, kStage2Rows>
+          <<<dim3(P2, nseg), kPartThreads, 0, s>>>(in2, 0, kShardBits + L.cbits, hist, rec,
+                                                    nullptr, hist1, P);
     }
     KScope k(timer, "bucket_group", s);
-    k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, ChunkOf::make(chunk_rows),
+    k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P2, ChunkOf::make(chunk_rows),
                                                       gkey, gmin, rep);
     return hipGetLastError();
   }
