@@ -249,6 +249,27 @@ class Runner:
         # identifier job step: K1 + sharded grouping (RCCL all-to-all at N > 1)
         t_job = self.timed(job, steps, warmup)
         res["job"] = {"value": self.world * n * steps / t_job, "ms_per_step": 1e3 * t_job / steps}
+        if self.world == 1 and self.comm is None:
+            # the same step captured once into a HIP graph and replayed (fixed
+            # buffers and shapes: what a host re-running same-size device
+            # batches can do); every replay recomputes everything
+            try:
+                s = torch.cuda.Stream(device=self.dev)
+                s.wait_stream(torch.cuda.current_stream(self.dev))
+                with torch.cuda.stream(s):
+                    job()
+                    job()
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    job()
+                t_g = self.timed(g.replay, steps, warmup)
+                res["job"]["graph_replay"] = {"value": n * steps / t_g,
+                                              "ms_per_step": 1e3 * t_g / steps}
+                del g
+            except Exception as e:  # reported, the eager figure stands
+                log(f"bench: graph capture of the job step failed: {e!r}")
+                res["job"]["graph_replay"] = {"error": repr(e)[:200]}
         leaves, fold = k1_split(lens)
         res["roofline_inputs"] = {"chunk_blocks": blk, "parents": par, "leaf_compressions": leaves,
                                   "fold_compressions": fold, "avg_leaves_s": avg_leaves,
