@@ -978,7 +978,7 @@ int sdgpu_group_rows_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8_t* 
 
 int sdgpu_shard_count_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8_t* d_has_key,
                              uint64_t n, uint32_t shard_bits, uint64_t* h_counts, void* stream) {
-  if (!c || !h_counts || shard_bits > 8 || (n && !d_key)) return -EINVAL;
+  if (!c || !h_counts || shard_bits > 8 || (n && !d_key) || n >= (1ull << 32)) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);
@@ -996,7 +996,8 @@ int sdgpu_shard_partition_device(sdgpu_ctx* c, const uint64_t* d_key, const uint
                                  const uint32_t* d_rank, uint64_t n, uint32_t shard_bits,
                                  uint64_t* d_out_key, uint32_t* d_out_rank, uint32_t* d_out_pos,
                                  void* stream) {
-  if (!c || shard_bits > 8 || (n && (!d_key || !d_out_key || !d_out_rank || !d_out_pos)))
+  if (!c || shard_bits > 8 || (n && (!d_key || !d_out_key || !d_out_rank || !d_out_pos)) ||
+      n >= (1ull << 32))
     return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
@@ -1012,7 +1013,7 @@ int sdgpu_shard_exchange_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8
                                 uint32_t world, uint64_t* d_out_key, uint32_t* d_out_rank,
                                 uint32_t* d_out_pos, int64_t* d_dest_counts, void* stream) {
   if (!c || shard_bits == 0 || shard_bits > 8 || world == 0 || world > 64 ||
-      world > (1u << shard_bits) || !d_dest_counts ||
+      world > (1u << shard_bits) || !d_dest_counts || n >= (1ull << 32) ||
       (n && (!d_key || !d_out_key || !d_out_rank || !d_out_pos)))
     return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
