@@ -1,8 +1,8 @@
-"""GPU parity of the single-file latency kernel (k_small): batches of <= 64
-cas messages (<= 102 408 B) and files of <= 1 MiB for file_checksum, where
-chunks are hashed by a quad of lanes (b3_compress_quad) when the batch's
-largest message has <= 256 chunks and by one lane each otherwise (file
-checksums of 256 KiB - 1 MiB); checked bit-exact against the oracle."""
+"""GPU parity of the single-file latency kernel (k_small: one workgroup per
+message, a lane per chunk, the tree level by level in LDS): batches of <= 64
+cas messages (<= 102 408 B), single files through generate_cas_id and
+file_checksum up to 1 MiB (1024 chunks, the kernel's limit); checked
+bit-exact against the oracle."""
 import os
 
 import numpy as np
@@ -57,7 +57,7 @@ def test_small_batch_edge_lengths(ctx):
 def test_file_checksum_small_files(ctx, tmp_path):
     from spacedrive_amd import validation
     rng = np.random.default_rng(5)
-    for n in FILE_EDGE:  # > 256 chunks: one lane per chunk; below: quads
+    for n in FILE_EDGE:
         p = os.path.join(tmp_path, f"f{n}")
         rng.integers(0, 256, n, dtype=np.uint8).tofile(p)
         assert validation.file_checksum(p, ctx) == O.file_checksum_path(p), n
