@@ -392,6 +392,9 @@ class Runner:
         root = tempfile.mkdtemp(prefix=f"sd_cfg1_r{self.rank}_")
         try:
             paths, sizes = corpus.write_config1_dir(root, self.args.dir_files, seed=1)
+            # the listing encoded once for the C ABI (as a host holds its
+            # CStrings); the CPU port below gets the same pre-encoded array
+            paths = fi.PathList(paths)
             fi.identify(paths, sizes=sizes, ctx=self.ctx)  # warm page cache
             self.barrier()
             t0 = time.perf_counter()

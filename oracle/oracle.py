@@ -239,8 +239,10 @@ def cas_paths_simd(paths, sizes, threads: int = 1):
     file (cas.rs:23-62) + the AVX2 8-way hasher, `threads` C threads (CPU
     baseline of the config-1 directory)."""
     n = len(paths)
-    enc = [os.fsencode(os.fspath(p)) for p in paths]
-    arr = (ctypes.c_char_p * n)(*enc)
+    arr = getattr(paths, "c_paths", None)  # pre-encoded (file_identifier.PathList)
+    if arr is None:
+        enc = [os.fsencode(os.fspath(p)) for p in paths]
+        arr = (ctypes.c_char_p * n)(*enc)
     sizes = np.ascontiguousarray(sizes, np.uint64)
     out = np.zeros((n, 8), np.uint8)
     st = np.zeros(n, np.int32)

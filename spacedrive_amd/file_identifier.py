@@ -61,8 +61,29 @@ class IdentifyResult:
                 for i in range(self.has_key.size)]
 
 
+class PathList:
+    """A list of paths encoded once as the C ABI's `const char *const *` (a
+    host that identifies the same listing repeatedly -- the bench, a rescan --
+    pays the encoding once; a Rust host passes its CString pointers directly)."""
+
+    def __init__(self, paths):
+        self.paths = list(paths)
+        self._enc = [os.fsencode(os.fspath(p)) for p in self.paths]
+        self.c_paths = (ctypes.c_char_p * len(self._enc))(*self._enc)
+
+    def __len__(self):
+        return len(self.paths)
+
+    def __iter__(self):
+        return iter(self.paths)
+
+    def __getitem__(self, i):
+        return self.paths[i]
+
+
 def identify(paths, sizes=None, ctx=None) -> IdentifyResult:
-    """cas ids of many files in one pipelined call."""
+    """cas ids of many files in one pipelined call (paths: a sequence of
+    paths, or a PathList)."""
     ctx = ctx or default_context()
     n = len(paths)
     st = np.zeros(n, np.int32)
@@ -74,8 +95,7 @@ def identify(paths, sizes=None, ctx=None) -> IdentifyResult:
             except OSError as e:
                 st[i] = -e.errno
     sizes = np.ascontiguousarray(sizes, np.uint64)
-    enc = [os.fsencode(os.fspath(p)) for p in paths]
-    arr = (ctypes.c_char_p * n)(*enc)
+    arr = paths.c_paths if isinstance(paths, PathList) else PathList(paths).c_paths
     out = np.zeros((n, 8), np.uint8)
     has = np.zeros(n, np.uint8)
     status = np.zeros(n, np.int32)
