@@ -104,3 +104,21 @@ def test_many_batches_growth(ctx):
     idx = dedup.ObjectIndex(ctx, 1000)
     rep = _run_batches(ctx, key, has, list(range(0, n + 1, 25_000)), 100, idx)
     np.testing.assert_array_equal(rep, O.group_reps(key, has, 100))
+
+
+def test_two_level_batch_through_index(ctx):
+    """A batch past 2^12 buckets (13 M rows: the two-level partition, fed by
+    the index probe's mask instead of initialising rep) after a first batch,
+    with Objects that existed before the run."""
+    import torch
+    from spacedrive_amd import dedup
+    n = 13_500_000
+    key, has = _rows(21, n, 9_000_000, keyless=0.002)
+    rng = np.random.default_rng(22)
+    ek = np.concatenate([rng.choice(key[:1_000_000], 20_000), rng.choice(key[-1_000_000:], 20_000)])
+    eh = rng.permutation(ek.size).astype(np.uint32) + 5
+    idx = dedup.ObjectIndex(ctx, 1 << 20)
+    idx.add_objects(torch.from_numpy(ek.view(np.int64)).cuda(),
+                    torch.from_numpy(eh.view(np.int32)).cuda())
+    rep = _run_batches(ctx, key, has, [0, 500_000, n], 100, idx)
+    np.testing.assert_array_equal(rep, O.group_reps_existing(key, has, 100, ek, eh))

@@ -33,6 +33,17 @@ def test_dedup_sharded_host_api(ctxs, ngpu):
         np.testing.assert_array_equal(rep, O.group_reps(k, h, chunk))
 
 
+def test_dedup_sharded_two_level_per_rank(ctxs):
+    """2 ranks x 13.5 M rows: every rank receives ~13.5 M exchanged 12-B
+    records, so its local grouping takes the two-level partition with packed
+    records as input."""
+    from spacedrive_amd import dedup
+    n = 27_000_000
+    k, h, _ = O.synth_dedup_rows(31, n, int(n * 0.8), 0, n)
+    rep = dedup.dedup_sharded(ctxs[:2], k, h, 100)
+    np.testing.assert_array_equal(rep, O.group_reps(k, h, 100))
+
+
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_all_device_with_index_batches(ctxs, world):
     """Device API over `world` ranks, two batches through per-rank Object
