@@ -56,18 +56,35 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time this process's cgroup may use (cgroup v2 cpu.max),
+    or None when unlimited / unknown."""
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(period)
+    except (OSError, ValueError):
+        return None
+
+
 def host_cores():
     """(threads, note): every core this process may run on (its CPU affinity),
-    capped by OMP_NUM_THREADS when the host sets it (the GPU box sets 16: the
-    CPU share of one GPU; nproc shows the whole machine there)."""
+    capped by its cgroup CPU quota and by OMP_NUM_THREADS when the host sets
+    it (the GPU box: 16, the CPU share of one GPU; nproc and os.cpu_count show
+    the whole machine there)."""
     total = os.cpu_count() or 1
     try:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = total
+    quota = cgroup_cpu_quota()
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    n = min(aff, cap) if cap > 0 else aff
-    return n, (f"{n} threads: sched_getaffinity {aff}, os.cpu_count {total}, "
+    n = aff
+    if quota:
+        n = min(n, max(1, int(quota)))
+    if cap > 0:
+        n = min(n, cap)
+    return n, (f"{n} threads: sched_getaffinity {aff}, os.cpu_count {total}, cgroup cpu.max "
+               f"{'unlimited' if quota is None else f'{quota:g} CPUs'}, "
                f"OMP_NUM_THREADS {cap or 'unset'}")
 
 
