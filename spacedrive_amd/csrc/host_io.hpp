@@ -148,6 +148,7 @@ class Pool {
     job_ = nullptr;
   }
   std::mutex busy;  // held by the thread using the pool
+  const pid_t pid = getpid();  // a fork()ed child has the object but not the threads
 
  private:
   void work(const std::function<void(uint32_t)>* f, uint32_t n, uint32_t grain) {
@@ -202,7 +203,7 @@ inline void parallel_for(uint32_t n, F&& f) {
   }
   const uint32_t grain = std::max(1u, std::min(64u, n / (8 * nt)));
   Pool& p = pool();
-  if (p.busy.try_lock()) {
+  if (p.pid == getpid() && p.busy.try_lock()) {
     const std::function<void(uint32_t)> fn = [&](uint32_t i) { f(i); };
     p.run(n, grain, fn);
     p.busy.unlock();

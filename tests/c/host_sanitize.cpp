@@ -8,6 +8,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <random>
 #include <string>
 
@@ -107,6 +110,29 @@ static void test_parallel_for() {
   }
 }
 
+// A fork()ed child inherits the pool object but not its threads: its
+// parallel_for must fall back to fresh threads instead of waiting forever.
+static void test_parallel_for_after_fork() {
+#if defined(__SANITIZE_THREAD__)
+  return;  // ThreadSanitizer cannot start threads after a multi-threaded fork
+#endif
+  hostio::parallel_for(4096, [](uint32_t) {});  // the pool exists in the parent
+  const pid_t pid = fork();
+  if (pid == 0) {
+    alarm(20);  // a hang ends the child (nonzero status)
+    std::vector<std::atomic<int>> hit(5000);
+    for (auto& h : hit) h = 0;
+    hostio::parallel_for(5000, [&](uint32_t i) { hit[i].fetch_add(1); });
+    int bad = 0;
+    for (auto& h : hit) bad += h != 1;
+    _exit(bad == 0 ? 0 : 3);
+  }
+  int status = 0;
+  waitpid(pid, &status, 0);
+  CHECK(WIFEXITED(status) && WEXITSTATUS(status) == 0, "parallel_for in a forked child: status %d",
+        status);
+}
+
 static void test_slab_layout() {
   const size_t caps[] = {4096, 65536 + 17, size_t(256) << 20};
   const uint32_t files[] = {1, 7, 65536};
@@ -176,6 +202,7 @@ int main(int argc, char** argv) {
   dir = argc > 1 ? argv[1] : mkdtemp(tmpl);
   test_cas_reads();
   test_parallel_for();
+  test_parallel_for_after_fork();
   test_slab_layout();
   test_tree_plan();
   if (fails) {
