@@ -597,6 +597,33 @@ class Runner:
             assert bad == 0, "sharded grouping differs from the one-GPU grouping"
         self.barrier()
 
+    # ------------------------------------------- downstream consumers (§8 f4)
+    def run_consumers(self, steps, warmup):
+        """The orphan remover's query over 10 M Objects / 12.5 M file_paths
+        (orphan_remover.rs:57-90) and the thumbnail-shard grouping of 1 M cas
+        ids (media/thumbnail/shard.rs:4-8), each one API call including its
+        count read-back, on this GPU's own synthetic tables."""
+        torch = self.torch
+        from spacedrive_amd import consumers
+        n_obj, n_fp, n_th = 10_000_000, 12_500_000, 1_000_000
+        g = torch.Generator(device=self.dev)
+        g.manual_seed(5 + self.rank)
+        obj = torch.arange(n_obj, dtype=torch.int32, device=self.dev)
+        fp = torch.randint(0, n_obj, (n_fp,), dtype=torch.int32, device=self.dev, generator=g)
+        fp[::1000] = -1                       # file_paths with object_id NULL
+        cas8 = torch.randint(0, 256, (n_th, 8), dtype=torch.uint8, device=self.dev, generator=g)
+        orphans = int(consumers.orphan_objects(obj, fp, n_obj - 1, ctx=self.ctx).numel())
+        t_o = self.timed(lambda: consumers.orphan_objects(obj, fp, n_obj - 1, ctx=self.ctx),
+                         steps, warmup)
+        t_t = self.timed(lambda: consumers.thumbnail_shards(cas8, ctx=self.ctx), steps, warmup)
+        del obj, fp, cas8
+        return {"orphan_remover": {"value": self.world * (n_obj + n_fp) * steps / t_o,
+                                   "unit": "rows/s", "ms_per_step": 1e3 * t_o / steps,
+                                   "objects_per_gpu": n_obj, "file_paths_per_gpu": n_fp,
+                                   "orphans_rank0": orphans},
+                "thumbnail_shards": {"value": self.world * n_th * steps / t_t, "unit": "rows/s",
+                                     "ms_per_step": 1e3 * t_t / steps, "rows_per_gpu": n_th}}
+
     # ---------------------------------------------------------------- config 3
     def run_checksum(self, steps, warmup):
         torch = self.torch
@@ -765,7 +792,7 @@ def main():
     ap.add_argument("--staged-files", type=int, default=250_000)
     ap.add_argument("--staged-total-files", type=int, default=50_000_000)
     ap.add_argument("--dir-files", type=int, default=10_000)
-    ap.add_argument("--components", default="cas,dedup,checksum,staged,dir,single")
+    ap.add_argument("--components", default="cas,dedup,consumers,checksum,staged,dir,single")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verify", action="store_true",
@@ -827,6 +854,11 @@ def main():
         d = R.run_dedup(args.steps, args.warmup)
         log("dedup:", json.dumps(d))
         comp["dedup"] = d
+        torch.cuda.empty_cache()
+    if "consumers" in comps:
+        k = R.run_consumers(args.steps, args.warmup)
+        log("consumers:", json.dumps(k))
+        comp["consumers"] = k
         torch.cuda.empty_cache()
     if "staged" in comps:
         g = R.run_staged()

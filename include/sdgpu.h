@@ -314,7 +314,8 @@ int sdgpu_link_batch_device(sdgpu_ctx *ctx, const uint32_t *d_rep, const uint32_
  * file_path, `object::file_paths::none`, deleted 512 at a time): d_orphans
  * receives the ids of d_object_ids that no entry of d_fp_object_ids (a
  * file_path's object_id; negative = NULL) references, in list order;
- * d_count[0] = how many.  Object ids must lie in [0, max_object_id]. */
+ * d_count[0] = how many.  Object ids must lie in [0, max_object_id]; the
+ * context keeps a workspace of max_object_id + 1 bytes (a mark per id). */
 int sdgpu_orphan_objects_device(sdgpu_ctx *ctx, const int32_t *d_object_ids, uint64_t n_objects,
                                 const int32_t *d_fp_object_ids, uint64_t n_file_paths,
                                 uint32_t max_object_id, int32_t *d_orphans, uint32_t *d_count,

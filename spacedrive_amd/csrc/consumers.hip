@@ -3,7 +3,8 @@
 // Orphan remover (/root/reference/core/src/object/orphan_remover.rs:57-90):
 // Objects with no file_path pointing at them (`object::file_paths::none`) are
 // found 512 at a time and deleted.  Here: one pass marks every Object id that
-// some file_path references (a bitmap over ids, atomicOr), a second pass keeps
+// some file_path references (a byte per id, plain stores: marking is
+// idempotent, so no atomics are needed), a second pass keeps
 // the unreferenced ids of the Object list, in list order (block-local LDS
 // compaction + one scan), ready for the caller's delete batches.
 //
@@ -26,32 +27,26 @@ uint32_t grid_for(uint64_t n, uint64_t per = kThreads) {
   return static_cast<uint32_t>(g == 0 ? 1 : (g < 65535 ? g : 65535));
 }
 
-__global__ __launch_bounds__(kThreads) void k_clear_words(uint32_t* __restrict__ w, uint64_t n) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride)
-    w[i] = 0;
-}
-
-// bitmap bit o = some file_path references Object o (negative = NULL object_id)
+// mark[o] = 1: some file_path references Object o (negative = NULL object_id)
 __global__ __launch_bounds__(kThreads) void k_mark(const int32_t* __restrict__ fp_obj, uint64_t n,
-                                                   uint32_t* __restrict__ bits, uint32_t max_id) {
+                                                   uint8_t* __restrict__ mark, uint32_t max_id) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n;
        i += stride) {
     const int32_t o = fp_obj[i];
-    if (o >= 0 && static_cast<uint32_t>(o) <= max_id) atomicOr(&bits[o >> 5], 1u << (o & 31));
+    if (o >= 0 && static_cast<uint32_t>(o) <= max_id) mark[o] = 1;
   }
 }
 
 // Object o is an orphan: no file_path marked it (ids past max_id are never marked)
-__device__ __forceinline__ bool orphan(int32_t o, const uint32_t* bits, uint32_t max_id) {
-  return o >= 0 && (static_cast<uint32_t>(o) > max_id || !(bits[o >> 5] >> (o & 31) & 1u));
+__device__ __forceinline__ bool orphan(int32_t o, const uint8_t* mark, uint32_t max_id) {
+  return o >= 0 && (static_cast<uint32_t>(o) > max_id || mark[o] == 0);
 }
 
 // per block of kThreads Objects: how many are orphans
 __global__ __launch_bounds__(kThreads) void k_orphan_count(const int32_t* __restrict__ obj,
                                                            uint64_t n,
-                                                           const uint32_t* __restrict__ bits,
+                                                           const uint8_t* __restrict__ bits,
                                                            uint32_t max_id,
                                                            uint32_t* __restrict__ cnt) {
   __shared__ uint32_t c;
@@ -68,7 +63,7 @@ __global__ __launch_bounds__(kThreads) void k_orphan_count(const int32_t* __rest
 // stable compaction: block b writes its orphans at the scanned offset, in order
 __global__ __launch_bounds__(kThreads) void k_orphan_write(const int32_t* __restrict__ obj,
                                                            uint64_t n,
-                                                           const uint32_t* __restrict__ bits,
+                                                           const uint8_t* __restrict__ bits,
                                                            uint32_t max_id,
                                                            const uint32_t* __restrict__ offs,
                                                            int32_t* __restrict__ out) {
@@ -115,38 +110,52 @@ __global__ __launch_bounds__(kThreads) void k_thumb_hist(const uint8_t* __restri
   hist[static_cast<uint64_t>(threadIdx.x) * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
 
-// stable within a block's tile: one round of kThreads rows at a time; a row's
-// place in its bin = earlier rows of the round with the same byte (LDS scan)
+// Stable within a block's tile: one round of kThreads rows at a time.  A row's
+// place in its bin = cursor + rows with the same byte in earlier waves of the
+// round + earlier lanes of its own wave with the same byte (a ballot per
+// distinct byte in the wave: ~57 for random bytes, instead of a scan of the
+// whole round per row).
 __global__ __launch_bounds__(kThreads) void k_thumb_scatter(const uint8_t* __restrict__ cas8,
                                                             const uint8_t* __restrict__ valid,
                                                             uint64_t n,
                                                             const uint32_t* __restrict__ offs,
                                                             uint32_t* __restrict__ order) {
+  constexpr uint32_t kWaves = kThreads / 64;
   __shared__ uint32_t cur[kShardBins];
-  __shared__ uint8_t sb[kThreads];
-  __shared__ uint8_t sv[kThreads];
+  __shared__ uint32_t wcnt[kWaves][kShardBins];
+  static_assert(kShardBins == kThreads, "one cursor per thread");
   cur[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * gridDim.x + blockIdx.x];
+  const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
   uint64_t t0, t1;
   tile(n, t0, t1);
-  for (uint64_t i0 = t0; i0 < t1; i0 += kThreads) {
+  for (uint64_t i0 = t0; i0 < t1; i0 += kThreads) {  // uniform trip count
     const uint64_t i = i0 + threadIdx.x;
     const bool v = i < t1 && (!valid || valid[i]);
-    const uint8_t b = i < t1 ? cas8[8 * i] : 0;
+    const uint32_t b = i < t1 ? cas8[8 * i] : 0u;
+    for (uint32_t k = threadIdx.x; k < kWaves * kShardBins; k += kThreads) (&wcnt[0][0])[k] = 0;
     __syncthreads();
-    sb[threadIdx.x] = b;
-    sv[threadIdx.x] = v ? 1 : 0;
+    uint64_t rem = __ballot(v);
+    uint32_t rank = 0;
+    while (rem) {  // wave-uniform
+      const int leader = __ffsll(static_cast<unsigned long long>(rem)) - 1;
+      const uint32_t bl = __shfl(b, leader);
+      const uint64_t m = __ballot(v && b == bl);
+      if (v && b == bl) rank = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == static_cast<uint32_t>(leader)) wcnt[wave][bl] = __popcll(m);
+      rem &= ~m;
+    }
     __syncthreads();
     if (v) {
-      uint32_t before = 0;  // earlier rows of this round in the same bin
-      for (uint32_t t = 0; t < threadIdx.x; ++t) before += (sv[t] && sb[t] == b) ? 1u : 0u;
-      order[cur[b] + before] = static_cast<uint32_t>(i);
+      uint32_t p = cur[b] + rank;
+      for (uint32_t w = 0; w < wave; ++w) p += wcnt[w][b];
+      order[p] = static_cast<uint32_t>(i);
     }
     __syncthreads();
-    {  // advance the cursors by this round's counts (thread = bin)
-      uint32_t c = 0;
-      for (uint32_t t = 0; t < kThreads; ++t) c += (sv[t] && sb[t] == threadIdx.x) ? 1u : 0u;
-      cur[threadIdx.x] += c;
-    }
+    uint32_t add = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kWaves; ++w) add += wcnt[w][threadIdx.x];
+    cur[threadIdx.x] += add;
+    __syncthreads();
   }
 }
 
@@ -159,20 +168,20 @@ __global__ void k_thumb_counts(const uint32_t* __restrict__ offs, uint32_t* __re
 }  // namespace
 
 size_t orphan_workspace_bytes(uint64_t n_obj, uint32_t max_id) {
-  const uint64_t words = (static_cast<uint64_t>(max_id) >> 5) + 1;
+  const uint64_t map = (static_cast<uint64_t>(max_id) + 1 + 255) / 256 * 256;
   const uint64_t blocks = (n_obj + kThreads - 1) / kThreads;
-  return 4 * words + 4 * (blocks + 1) + 4 * (scan::tiles_for(blocks) + 1) + 1024;
+  return map + 4 * (blocks + 1) + 4 * (scan::tiles_for(blocks) + 1) + 1024;
 }
 
 hipError_t orphan_objects_launch(const int32_t* obj, uint64_t n_obj, const int32_t* fp_obj,
                                  uint64_t n_fp, uint32_t max_id, int32_t* out, uint32_t* d_count,
                                  void* ws, hipStream_t s) {
-  const uint64_t words = (static_cast<uint64_t>(max_id) >> 5) + 1;
+  const uint64_t map = (static_cast<uint64_t>(max_id) + 1 + 255) / 256 * 256;
   const uint64_t blocks = (n_obj + kThreads - 1) / kThreads;
-  uint32_t* bits = static_cast<uint32_t*>(ws);
-  uint32_t* cnt = bits + words;
+  uint8_t* bits = static_cast<uint8_t*>(ws);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(bits + map);
   uint32_t* tiles = cnt + blocks + 1;
-  k_clear_words<<<grid_for(words), kThreads, 0, s>>>(bits, words);
+  (void)hipMemsetAsync(bits, 0, map, s);
   if (n_fp) k_mark<<<grid_for(n_fp, 4 * kThreads), kThreads, 0, s>>>(fp_obj, n_fp, bits, max_id);
   if (blocks) {
     k_orphan_count<<<static_cast<uint32_t>(blocks), kThreads, 0, s>>>(obj, n_obj, bits, max_id,
