@@ -106,3 +106,41 @@ def test_fuzz_checksum_batches(ctx, seed):
     out = validation.checksum_batch_device(files, ctx=ctx).cpu().numpy()
     for i, d in enumerate(data):
         assert bytes(out[i]) == O.blake3(d.tobytes(), 8), (seed, i, lens[i])
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    from spacedrive_amd._native import Context
+    cs = [Context(0) for _ in range(8)]
+    yield cs
+    for c in cs:
+        c.close()
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzz_sharded_and_indexed(ctxs, seed):
+    """The multi-GPU grouping (peer transport between contexts on the one
+    GPU) at a random world size, and the same rows grouped in random batches
+    through an Object index with some pre-existing Objects."""
+    import torch
+    from spacedrive_amd import dedup
+    rng = np.random.default_rng(4000 + seed)
+    n = int(rng.choice([3, 1000, 50_000, 400_000]))
+    world = int(rng.integers(1, 9))
+    distinct = max(1, int(n * rng.choice([0.05, 0.7])))
+    pool = rng.integers(0, 2**64 - 1, distinct, dtype=np.uint64, endpoint=True)
+    key = pool[rng.integers(0, distinct, n)]
+    has = (rng.random(n) > 0.02).astype(np.uint8)
+    chunk = int(rng.choice([1, 100, 333]))
+    rep = dedup.dedup_sharded(ctxs[:world], key, has, chunk)
+    np.testing.assert_array_equal(rep, O.group_reps(key, has, chunk))
+    # batches through one index, with pre-existing Objects
+    ek = rng.choice(key, max(1, n // 50))
+    eh = rng.permutation(ek.size).astype(np.uint32) + 1
+    idx = dedup.ObjectIndex(ctxs[0], 1024)
+    idx.add_objects(torch.from_numpy(ek.view(np.int64)).cuda(),
+                    torch.from_numpy(eh.view(np.int32)).cuda())
+    cuts = np.unique(np.concatenate([[0, n], rng.integers(0, n + 1, int(rng.integers(0, 6)))]))
+    out = [dedup.dedup_batch(key[a:b], has[a:b], int(a), idx, chunk, ctxs[0])
+           for a, b in zip(cuts[:-1], cuts[1:])]
+    np.testing.assert_array_equal(np.concatenate(out), O.group_reps_existing(key, has, chunk, ek, eh))
