@@ -209,6 +209,20 @@ class Runner:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def timed_kernels(self, fn, steps, warmup):
+        """(seconds for `steps` steps, per-kernel event times): the steps are
+        timed un-instrumented, then run once more with libsdgpu's per-kernel
+        HIP events (on each kernel's launch stream) for the breakdown -- the
+        events' own gaps stay out of the reported rate."""
+        t = self.timed(fn, steps, warmup)
+        self.ctx.set_timing(True)
+        for _ in range(steps):
+            fn()
+        self.torch.cuda.synchronize()
+        kt = self.ctx.kernel_times()
+        self.ctx.set_timing(False)
+        return t, kt
+
     def timed(self, fn, steps, warmup) -> float:
         torch = self.torch
         for _ in range(warmup):
@@ -251,10 +265,7 @@ class Runner:
             dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx, trim=False)
 
         # K1 alone, with live per-kernel event timing on its launch stream
-        self.ctx.set_timing(True)
-        t_cas = self.timed(k1, steps, warmup)
-        kt = self.ctx.kernel_times()
-        self.ctx.set_timing(False)
+        t_cas, kt = self.timed_kernels(k1, steps, warmup)
         assert int(st.abs().sum()) == 0
         res["cas"] = {"value": self.world * n * steps / t_cas, "unit": "files/s",
                       "ms_per_step": 1e3 * t_cas / steps,
@@ -485,10 +496,7 @@ class Runner:
         if self.args.verify:
             self.verify_sharded(key, has, rank)
         self.group(key, has, rank)  # first launches (lazy code-object loads) untimed
-        self.ctx.set_timing(True)
-        t = self.timed(lambda: self.group(key, has, rank), steps, warmup)
-        kt = self.ctx.kernel_times()
-        self.ctx.set_timing(False)
+        t, kt = self.timed_kernels(lambda: self.group(key, has, rank), steps, warmup)
         xchg = None
         if self.world > 1:
             # payload of one step on this rank: (key, rank) 12-B records out to
@@ -567,10 +575,8 @@ class Runner:
                                                         device=self.local, ctx=self.ctx)
         self.ops.group_rows(key, has, rank, 100, 0)  # two-level kernels' first launches
         torch.cuda.synchronize()
-        self.ctx.set_timing(True)
-        t = self.timed(lambda: self.ops.group_rows(key, has, rank, 100, 0), steps, warmup)
-        kt = self.ctx.kernel_times()
-        self.ctx.set_timing(False)
+        t, kt = self.timed_kernels(lambda: self.ops.group_rows(key, has, rank, 100, 0), steps,
+                                   warmup)
         del key, has, rank
         torch.cuda.empty_cache()
         return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
@@ -638,11 +644,8 @@ class Runner:
             log(f"checksum: only {len(files)} of {nf} files fit: {e}")
         torch.cuda.synchronize()
         out = torch.empty((len(files), 32), dtype=torch.uint8, device=self.dev)
-        self.ctx.set_timing(True)
-        t = self.timed(lambda: validation.checksum_batch_device(files, out=out, ctx=self.ctx),
-                       steps, warmup)
-        kt = self.ctx.kernel_times()
-        self.ctx.set_timing(False)
+        t, kt = self.timed_kernels(
+            lambda: validation.checksum_batch_device(files, out=out, ctx=self.ctx), steps, warmup)
         nbytes = len(files) * flen
         res = {"value": self.world * nbytes * steps / t / 1e9, "unit": "GB/s",
                "ms_per_step": 1e3 * t / steps,

@@ -133,9 +133,11 @@ __device__ __forceinline__ uint32_t wave_add(uint32_t* cnt, uint32_t d, bool v) 
 template <typename In>
 __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, uint32_t skip,
                                                             uint32_t bits, uint32_t world,
-                                                            uint32_t* __restrict__ hist) {
+                                                            uint32_t* __restrict__ hist,
+                                                            uint32_t* __restrict__ zero = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
   const uint32_t nbins = world ? world : 1u << bits;
+  if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;  // a flag of the next kernels
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) cnt[b] = 0;
   __syncthreads();
   uint64_t t0, t1;
@@ -249,18 +251,28 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
 // digit (~4096 / nbins records, consecutive lanes on consecutive addresses)
 // instead of one scattered 16-B store per row.  The next round's rows are
 // loaded during the current one (ping-pong batches, LDS-only barriers).
+// The block also counts its rows per FINAL bucket (the fbits hash bits below
+// `skip`: coarse digit + second-pass digit) in 16-bit LDS counters and writes
+// them to fine[block][bucket] -- the second pass's histogram, which therefore
+// needs no pass over the records of its own.  A counter that would pass 65535
+// (one key filling more than 64 Ki rows of a block's tile) sets *ovf, and
+// k_fine_recount rebuilds the counts from the records instead.
 constexpr uint32_t kRunMaxBins = 64;
 template <typename In, bool kInitRep>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
     In in, uint64_t n, uint32_t skip, uint32_t bits, const uint32_t* __restrict__ offs,
-    uint4* __restrict__ rec, uint32_t* __restrict__ rep) {
+    uint4* __restrict__ rec, uint32_t* __restrict__ rep, uint32_t fbits,
+    uint32_t* __restrict__ fine, uint32_t* __restrict__ ovf) {
   constexpr int U = 4;
   constexpr uint32_t R = U * kPartThreads;
   __shared__ uint4 buf[R];
   __shared__ uint32_t cnt[kRunMaxBins], base[kRunMaxBins + 1], cur[kRunMaxBins];
-  const uint32_t nbins = 1u << bits;
+  __shared__ uint32_t fc[1u << (kMaxBucketBits - 1)];  // 2 x 16-bit counters per word
+  const uint32_t nbins = 1u << bits, nfine = 1u << fbits;
   if (threadIdx.x < nbins)
     cur[threadIdx.x] = offs[static_cast<uint64_t>(threadIdx.x) * gridDim.x + part_block()];
+  for (uint32_t b = threadIdx.x; b < nfine / 2; b += kPartThreads) fc[b] = 0;
+  bool over = false;
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
   auto round = [&](const RowBatch<U>& q, uint64_t i0) {
@@ -279,6 +291,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
       const uint64_t h = in_hash<In>(in.key_of(q, u));
       dg[u] = digit_of(h, skip, bits);
       lr[u] = atomicAdd(&cnt[dg[u]], 1u);
+      const uint32_t fb = digit_of(h, skip, fbits), sh = (fb & 1u) << 4;
+      over |= ((atomicAdd(&fc[fb >> 1], 1u << sh) >> sh) & 0xFFFFu) == 0xFFFFu;
       rq[u] = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r,
                          in.row_of(q, u));
     }
@@ -318,6 +332,89 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
       if (i0 + 2 * kStep >= t1) break;
     }
   }
+  if (over) *ovf = 1u;
+  __syncthreads();
+  uint32_t* f = fine + static_cast<uint64_t>(part_block()) * nfine;
+  for (uint32_t b = threadIdx.x; b < nfine; b += kPartThreads)
+    f[b] = (fc[b >> 1] >> ((b & 1u) << 4)) & 0xFFFFu;
+}
+
+// Only after a 16-bit counter overflow in k_part_scatter_runs (*ovf): for
+// every (coarse block j, segment c) -- a grid-stride loop, so the usual call
+// costs one small launch -- recount the records j wrote to segment c
+// ([seg[c * P + j], seg[c * P + j + 1])) on the kB2 second-pass digit bits.
+template <uint32_t kB2>
+__global__ __launch_bounds__(kPartThreads) void k_fine_recount(const uint4* __restrict__ rec,
+                                                                uint32_t skip,
+                                                                const uint32_t* __restrict__ seg,
+                                                                uint32_t P, uint32_t nseg,
+                                                                uint32_t fbits,
+                                                                uint32_t* __restrict__ fine,
+                                                                const uint32_t* __restrict__ ovf) {
+  if (*ovf == 0) return;
+  constexpr uint32_t nb = 1u << kB2;
+  __shared__ uint32_t cnt[nb];
+  for (uint32_t jc = blockIdx.x; jc < P * nseg; jc += gridDim.x) {
+    const uint32_t j = jc % P, c = jc / P;
+    for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads) cnt[b] = 0;
+    __syncthreads();
+    const uint32_t s0 = seg[static_cast<uint64_t>(c) * P + j];
+    const uint32_t s1 = seg[static_cast<uint64_t>(c) * P + j + 1];
+    for (uint32_t i = s0 + threadIdx.x; i < s1; i += kPartThreads) {
+      const uint4 v = rec[i];
+      atomicAdd(&cnt[digit_of((static_cast<uint64_t>(v.y) << 32) | v.x, skip, kB2)], 1u);
+    }
+    __syncthreads();
+    uint32_t* f = fine + static_cast<uint64_t>(j) * (1u << fbits) + (static_cast<uint64_t>(c) << kB2);
+    for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads) f[b] = cnt[b];
+    __syncthreads();
+  }
+}
+
+// Per final bucket b: E[j][b] = rows of b that coarse blocks [0, kR j) wrote
+// (the start of second-pass block j inside bucket b; block j takes coarse
+// blocks [kR j, kR (j + 1))) and tot[b] = the bucket's size.  A block covers 64
+// buckets x kP2 blocks: thread (bi, jg) sums the fine counts of its kP2 / 16
+// second-pass blocks (each wave reads 256 contiguous bytes per load), then the
+// 16 partial sums of a bucket are scanned in LDS.  Resets *ovf for the next call.
+template <uint32_t kP2, uint32_t kR>
+__global__ __launch_bounds__(1024) void k_fine_scan(const uint32_t* __restrict__ fine,
+                                                    uint32_t nfine, uint32_t* __restrict__ E,
+                                                    uint32_t* __restrict__ tot,
+                                                    uint32_t* __restrict__ ovf) {
+  static_assert(kP2 % 16 == 0, "second-pass blocks per thread");
+  constexpr uint32_t kJ = kP2 / 16;
+  __shared__ uint32_t part[16][64];
+  const uint32_t bi = threadIdx.x & 63u, jg = threadIdx.x >> 6;
+  const uint32_t b = blockIdx.x * 64 + bi;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ovf = 0;
+  uint32_t sj[kJ], local = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kJ; ++k) {
+    const uint64_t j = jg * kJ + k;
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kR; ++r)
+      v += b < nfine ? fine[(j * kR + r) * nfine + b] : 0u;
+    sj[k] = v;
+    local += v;
+  }
+  part[jg][bi] = local;
+  __syncthreads();
+  uint32_t pre = 0, all = 0;
+#pragma unroll
+  for (uint32_t g = 0; g < 16; ++g) {
+    const uint32_t v = part[g][bi];
+    pre += g < jg ? v : 0u;
+    all += v;
+  }
+  if (b >= nfine) return;
+#pragma unroll
+  for (uint32_t k = 0; k < kJ; ++k) {
+    E[static_cast<uint64_t>(jg * kJ + k) * nfine + b] = pre;
+    pre += sj[k];
+  }
+  if (jg == 0) tot[b] = all;
 }
 
 // Bucket partition with LDS staging (12-bit digits, 2 slots in the product): a
@@ -331,31 +428,69 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
 // the kBits hash bits below the segment's, and the offsets are laid out
 // [c][digit][block] -- so the group kernel sees 2^(cbits + kBits) buckets.
 constexpr uint32_t kStageBits = 12;
-// Second pass of the two-level partition: 10 digit bits, 8-record runs, 4 rows
-// per thread per round, 64 blocks per coarse segment (~48 rows per bucket per
-// block: whole 128-B runs).  Measured on the staged scatter alone
-// (profiles/r2/exp_scatter_slots_r2t.log): 12/2 0.163 ms, 10/8 0.123 ms.
-constexpr uint32_t kStage2Bits = 10;
-constexpr uint32_t kStage2Slots = 8;
+// Second pass of the two-level partition: 9 digit bits, 16-record runs, 4 rows
+// per thread per round, 64 blocks per coarse segment (each takes what 4
+// coarse blocks wrote to its segment).  Wider runs write fewer partial lines:
+// on the staged scatter alone 12/2 0.163 ms, 10/8 0.123 ms
+// (profiles/r2/exp_scatter_slots_r2t.log); at 100 M rows the 6 + 9-bit split
+// with 16-record runs beat 5 + 10 with 8 (profiles/r2/exp_twolevel_r2E.log).
+constexpr uint32_t kStage2Bits = 9;
+constexpr uint32_t kStage2Slots = 16;
 constexpr int kStage2Rows = 4;
 constexpr uint32_t kStage2Blocks = 64;
 template <typename In, bool kInitRep, uint32_t kBits = kStageBits, uint32_t kSlots = 2, int kRows = 2>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     In in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ offs, uint4* __restrict__ rec,
-    uint32_t* __restrict__ rep, const uint32_t* __restrict__ seg, uint32_t P1) {
+    uint32_t* __restrict__ rep, const uint32_t* __restrict__ seg, uint32_t P1,
+    const uint32_t* __restrict__ ftot = nullptr, uint32_t* __restrict__ fbase = nullptr,
+    uint32_t R = 1) {
   constexpr uint32_t nbins = 1u << kBits;
   __shared__ uint4 stage[nbins][kSlots];
   __shared__ uint32_t fill[nbins];
   __shared__ uint32_t cur[nbins];
   const uint32_t c = blockIdx.y;
-  const uint64_t obase = static_cast<uint64_t>(c) * nbins * gridDim.x;
-  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) {
-    cur[b] = offs[obase + static_cast<uint64_t>(b) * gridDim.x + part_block()];
-    fill[b] = 0;
+  uint64_t t0 = 0, t1 = 0;
+  if (ftot) {
+    // second pass fed by the coarse pass's fine counts: block j takes what
+    // coarse blocks [R j, R (j + 1)) wrote to segment c, offs = E (k_fine_scan).
+    // Bucket starts: segment c's first record (the coarse offsets) + the
+    // exclusive scan of its buckets' sizes, scanned here; block 0 of each
+    // segment publishes them (fbase, + the total) for the group kernel.
+    if constexpr (nbins <= kPartThreads) {  // the two-level second pass only
+      __shared__ uint32_t wsum[kPartThreads / 64];
+      const uint32_t j = part_block(), t = threadIdx.x, lane = __lane_id();
+      const uint64_t nfine = static_cast<uint64_t>(gridDim.y) << kBits, b0 = static_cast<uint64_t>(c) << kBits;
+      const uint32_t v = t < nbins ? ftot[b0 + t] : 0u;
+      uint32_t inc = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d);
+        if (lane >= static_cast<uint32_t>(d)) inc += o;
+      }
+      if (lane == 63) wsum[t >> 6] = inc;
+      __syncthreads();
+      uint32_t base = seg[static_cast<uint64_t>(c) * P1] + inc - v;
+      for (uint32_t w = 0; w < (t >> 6); ++w) base += wsum[w];
+      if (t < nbins) {
+        cur[t] = base + offs[j * nfine + b0 + t];
+        fill[t] = 0;
+        if (j == 0) fbase[b0 + t] = base;
+      }
+      if (j == 0 && c == gridDim.y - 1 && t == 0) fbase[nfine] = seg[static_cast<uint64_t>(gridDim.y) * P1];
+      t0 = seg[static_cast<uint64_t>(c) * P1 + min(P1, R * j)];
+      t1 = seg[static_cast<uint64_t>(c) * P1 + min(P1, R * (j + 1))];
+    }
+  } else {
+    const uint64_t obase = static_cast<uint64_t>(c) * nbins * gridDim.x;
+    for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) {
+      cur[b] = offs[obase + static_cast<uint64_t>(b) * gridDim.x + part_block()];
+      fill[b] = 0;
+    }
   }
   __syncthreads();
-  uint64_t t0, t1;
-  if (seg) {
+  if (ftot) {
+    // tile set above
+  } else if (seg) {
     const uint64_t s0 = seg[static_cast<uint64_t>(c) * P1], s1 = seg[static_cast<uint64_t>(c + 1) * P1];
     tile_of(s1 - s0, gridDim.x, t0, t1);
     t0 += s0;
@@ -390,16 +525,33 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     lds_barrier();
     // unrolled, not a loop: the compiler drains every load in flight before a
     // store-only loop that reads registers loaded outside it (vmcnt(0))
-    static_assert(nbins % kPartThreads == 0, "flush slots per thread");
+    if constexpr (nbins >= kPartThreads) {
+      static_assert(nbins % kPartThreads == 0, "flush slots per thread");
 #pragma unroll
-    for (uint32_t j = 0; j < nbins / kPartThreads; ++j) {
-      const uint32_t b = threadIdx.x + j * kPartThreads;
-      if (fill[b] >= kSlots) {
-        const uint32_t p = cur[b];
-        cur[b] = p + kSlots;
+      for (uint32_t j = 0; j < nbins / kPartThreads; ++j) {
+        const uint32_t b = threadIdx.x + j * kPartThreads;
+        if (fill[b] >= kSlots) {
+          const uint32_t p = cur[b];
+          cur[b] = p + kSlots;
 #pragma unroll
-        for (uint32_t k = 0; k < kSlots; ++k) rec[p + k] = stage[b][k];
-        fill[b] = 0;
+          for (uint32_t k = 0; k < kSlots; ++k) rec[p + k] = stage[b][k];
+          fill[b] = 0;
+        }
+      }
+    } else {
+      // T adjacent lanes of one wave per bin, each writing every T-th record;
+      // the wave reads fill / cur before its first lane updates them
+      constexpr uint32_t T = kPartThreads / nbins;
+      static_assert(kPartThreads % nbins == 0 && T <= 64 && kSlots % T == 0, "flush lanes per bin");
+      const uint32_t b = threadIdx.x / T, part = threadIdx.x % T;
+      const uint32_t f = fill[b], p = cur[b];
+      if (f >= kSlots) {
+#pragma unroll
+        for (uint32_t k = part; k < kSlots; k += T) rec[p + k] = stage[b][k];
+        if (part == 0) {
+          cur[b] = p + kSlots;
+          fill[b] = 0;
+        }
       }
     }
     lds_barrier();
@@ -423,35 +575,6 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
   }
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
     for (uint32_t k = 0; k < fill[b]; ++k) rec[cur[b] + k] = stage[b][k];
-}
-
-// Histogram of the second pass: block (j, c) counts tile j of segment c's
-// records on the 12 digit bits below the segment's.
-template <uint32_t kBits>
-__global__ __launch_bounds__(kPartThreads) void k_part2_hist(Rec16In in, uint32_t skip,
-                                                             const uint32_t* __restrict__ seg,
-                                                             uint32_t P1,
-                                                             uint32_t* __restrict__ hist) {
-  constexpr uint32_t nbins = 1u << kBits;
-  __shared__ uint32_t cnt[nbins];
-  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) cnt[b] = 0;
-  __syncthreads();
-  const uint32_t c = blockIdx.y;
-  const uint64_t s0 = seg[static_cast<uint64_t>(c) * P1], s1 = seg[static_cast<uint64_t>(c + 1) * P1];
-  uint64_t t0, t1;
-  tile_of(s1 - s0, gridDim.x, t0, t1);
-  for (uint64_t i0 = s0 + t0 + threadIdx.x; i0 < s0 + t1; i0 += kUnroll * kPartThreads) {
-    RowBatch<kUnroll> q;
-    in.template load_many<kUnroll>(i0, kPartThreads, s0 + t1, i0, q);
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u)
-      if (in.valid_of(q, u))  // records hold the hash
-        atomicAdd(&cnt[digit_of(in.key_of(q, u), skip, kBits)], 1u);
-  }
-  __syncthreads();
-  const uint64_t obase = static_cast<uint64_t>(c) * nbins * gridDim.x;
-  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
-    hist[obase + static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
 }
 
 // First probe slot of a record in the LDS table (kLdsSlots, any size): the
@@ -681,18 +804,10 @@ __global__ __launch_bounds__(256) void k_gather_rep(const uint32_t* __restrict__
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Blocks of the bucket partition (<= kMaxPartBlocks, which sizes the workspace).
-// Each block keeps one open output line per bucket, so the blocks resident on
-// one XCD hold blocks/8 x buckets x 128 B of partially written lines in its
-// 4 MB L2; fewer blocks trade parallelism for fewer evicted partial lines.
-uint32_t bucket_part_blocks() {
-  static const uint32_t P = [] {
-    const char* e = getenv("SDGPU_BUCKET_PART_BLOCKS");
-    const long v = e ? strtol(e, nullptr, 10) : 0;
-    return (v >= 8 && v <= static_cast<long>(kMaxPartBlocks)) ? static_cast<uint32_t>(v) : kPartBlocks;
-  }();
-  return P;
-}
+// Blocks of the bucket partition: one per CU.  Each block keeps one open
+// output line per bucket, so the blocks resident on one XCD hold blocks/8 x
+// buckets x 128 B of partially written lines in its 4 MB L2.
+uint32_t bucket_part_blocks() { return kPartBlocks; }
 
 // ~kBucketRows rows per bucket (LDS table load <= 75 % with slack), up to 2^15
 // buckets: 100 M rows on one GPU still group in LDS.
@@ -703,20 +818,23 @@ uint32_t bucket_bits_for(uint64_t n) {
 }
 
 // Above 2^12 buckets (n > ~12.6 M rows) the partition runs in two passes: a
-// coarse one on the top cbits = bits - 10 digit bits (<= 32 output streams per
-// block) into rec1, then a 10-bit LDS-staged pass per coarse segment into rec
-// (8-record runs, 64 blocks per segment).  A single 2^15-way scatter keeps 32 k
-// partially written lines open per block and ran 3.7 ms for 100 M rows
+// coarse one on the top cbits = bits - 9 digit bits (<= 64 output streams per
+// block) into rec1, which also counts every row's final bucket (fine counts),
+// then a 9-bit LDS-staged pass per coarse segment into rec (16-record runs, 64
+// blocks per segment).  A single 2^15-way scatter keeps 32 k partially written
+// lines open per block and ran 3.7 ms for 100 M rows
 // (profiles/r2/bench_r2b.json); the two passes move 2 x 32 B per row instead.
 struct GroupLayout {
   uint32_t bits, cbits;
-  size_t hist, tiles, rec, hist1, rec1, gkey, gmin, total;
+  size_t hist, tiles, rec, hist1, rec1, gkey, gmin;
+  size_t fine, fE, ftot, fbase, ovf;  // two-level only: the coarse pass's fine counts
+  size_t total;
 };
 
-GroupLayout group_layout(uint64_t n) {
+GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
   GroupLayout L;
   L.bits = bucket_bits_for(n);
-  L.cbits = L.bits > kStageBits ? L.bits - kStage2Bits : 0;
+  L.cbits = L.bits > kStageBits ? L.bits - b2 : 0;
   const uint64_t nh = (static_cast<uint64_t>(1) << L.bits) * kMaxPartBlocks;
   const uint64_t nh1 = (static_cast<uint64_t>(1) << L.cbits) * kMaxPartBlocks;
   size_t o = 0;
@@ -727,6 +845,12 @@ GroupLayout group_layout(uint64_t n) {
   L.rec1 = o; o = align_up(o + (L.cbits ? 16 * n : 0), 256);
   L.gkey = o; o = align_up(o + 8 * 4 * n, 256);
   L.gmin = o; o = align_up(o + 4 * 4 * n, 256);
+  const uint64_t nf = L.cbits ? static_cast<uint64_t>(1) << L.bits : 0;
+  L.fine = o; o = align_up(o + 4 * nf * kPartBlocks, 256);
+  L.fE = o; o = align_up(o + 4 * nf * kPartBlocks, 256);
+  L.ftot = o; o = align_up(o + 4 * nf, 256);
+  L.fbase = o; o = align_up(o + 4 * (nf + 1), 256);
+  L.ovf = o; o = align_up(o + 4, 256);
   L.total = o;
   return L;
 }
@@ -737,6 +861,71 @@ void allow_lds(K kernel, size_t bytes) {
   if (bytes > (size_t(64) << 10))
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+}
+
+// Two-level partition (n > 4096 x kBucketRows) + group: see group_layout.
+// kB2 digit bits per segment in the second pass, kS2-record staging runs, kR2
+// rows per thread per round, kP2 blocks per segment.  The second pass's offsets
+// come from the coarse pass's fine counts (k_fine_scan; bucket starts scanned
+// in the second pass's prologue): no histogram pass over the coarse records.
+template <typename In, uint32_t kB2, uint32_t kS2, int kR2, uint32_t kP2>
+hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t chunk_rows,
+                            uint32_t* rep, bool init_rep, void* ws, hipStream_t s, KTimer* timer) {
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(w + L.tiles);
+  uint4* rec = reinterpret_cast<uint4*>(w + L.rec);
+  uint64_t* gkey = reinterpret_cast<uint64_t*>(w + L.gkey);
+  uint32_t* gmin = reinterpret_cast<uint32_t*>(w + L.gmin);
+  uint32_t* fine = reinterpret_cast<uint32_t*>(w + L.fine);
+  uint32_t* fE = reinterpret_cast<uint32_t*>(w + L.fE);
+  uint32_t* ftot = reinterpret_cast<uint32_t*>(w + L.ftot);
+  uint32_t* fbase = reinterpret_cast<uint32_t*>(w + L.fbase);
+  uint32_t* ovf = reinterpret_cast<uint32_t*>(w + L.ovf);
+  const uint32_t bits = L.bits, nfine = 1u << bits;
+  const uint32_t P = bucket_part_blocks();
+  const uint32_t skip2 = kShardBits + L.cbits;
+  static_assert(kMaxBucketBits - kB2 <= 6, "coarse digits fit k_part_scatter_runs");
+  static_assert(kP2 <= kPartBlocks && kPartBlocks % kP2 == 0, "second-pass blocks per segment");
+  static_assert((1u << kB2) <= kPartThreads, "second-pass bucket starts: one bucket per thread");
+  // pass 1: coarse partition on the top cbits digit bits (rep initialised
+  // here), counting every row's final bucket on the way
+  uint32_t* hist1 = reinterpret_cast<uint32_t*>(w + L.hist1);
+  uint4* rec1 = reinterpret_cast<uint4*>(w + L.rec1);
+  const uint32_t nseg = 1u << L.cbits;
+  const size_t lds1 = sizeof(uint32_t) << L.cbits;
+  {
+    KScope k(timer, "bucket_hist", s);
+    k_part_hist<In><<<P, kPartThreads, lds1, s>>>(in, n, kShardBits, L.cbits, 0, hist1, ovf);
+  }
+  scan::exclusive(hist1, static_cast<uint64_t>(nseg) * P, hist1, tiles, nullptr, s);
+  {
+    KScope k(timer, "bucket_scatter1", s);
+    if (init_rep)
+      k_part_scatter_runs<In, true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, L.cbits, hist1,
+                                                               rec1, rep, bits, fine, ovf);
+    else
+      k_part_scatter_runs<In, false><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, L.cbits, hist1,
+                                                                rec1, rep, bits, fine, ovf);
+  }
+  // pass 2: kB2 bits below, per coarse segment, staged in kS2-record runs
+  const Rec16In in2{rec1};
+  constexpr uint32_t P2 = kP2;
+  {
+    KScope k(timer, "bucket_fine_scan", s);
+    k_fine_recount<kB2><<<kPartBlocks, kPartThreads, 0, s>>>(rec1, skip2, hist1, P, nseg, bits,
+                                                             fine, ovf);
+    k_fine_scan<P2, kPartBlocks / kP2><<<(nfine + 63) / 64, 1024, 0, s>>>(fine, nfine, fE, ftot,
+                                                                          ovf);
+  }
+  {
+    KScope k(timer, "bucket_scatter", s);
+    k_part_scatter_rec_staged<Rec16In, false, kB2, kS2, kR2><<<dim3(P2, nseg), kPartThreads, 0, s>>>(
+        in2, 0, skip2, fE, rec, nullptr, hist1, P, ftot, fbase, kPartBlocks / kP2);
+  }
+  KScope k(timer, "bucket_group", s);
+  k_bucket_group<<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, ChunkOf::make(chunk_rows), gkey,
+                                                 gmin, rep);
+  return hipGetLastError();
 }
 
 template <typename In>
@@ -753,49 +942,9 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   const uint32_t P = bucket_part_blocks();
   const uint64_t nh = (static_cast<uint64_t>(1) << bits) * P;
   const size_t lds = sizeof(uint32_t) << bits;
-  if (L.cbits) {
-    // pass 1: coarse partition on the top cbits digit bits (rep initialised here)
-    uint32_t* hist1 = reinterpret_cast<uint32_t*>(w + L.hist1);
-    uint4* rec1 = reinterpret_cast<uint4*>(w + L.rec1);
-    const uint32_t nseg = 1u << L.cbits;
-    const size_t lds1 = sizeof(uint32_t) << L.cbits;
-    {
-      KScope k(timer, "bucket_hist", s);
-      k_part_hist<In><<<P, kPartThreads, lds1, s>>>(in, n, kShardBits, L.cbits, 0, hist1);
-    }
-    scan::exclusive(hist1, static_cast<uint64_t>(nseg) * P, hist1, tiles, nullptr, s);
-    {
-      KScope k(timer, "bucket_scatter1", s);
-      static_assert(kMaxBucketBits - kStage2Bits <= 6, "coarse digits fit k_part_scatter_runs");
-      if (init_rep)
-        k_part_scatter_runs<In, true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, L.cbits,
-                                                                 hist1, rec1, rep);
-      else
-        k_part_scatter_runs<In, false><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, L.cbits,
-                                                                  hist1, rec1, rep);
-    }
-    // pass 2: kStage2Bits below, per coarse segment, staged in 8-record runs
-    // (offsets [c][digit][block] = bucket-major with P2 blocks per bucket)
-    const Rec16In in2{rec1};
-    const uint32_t P2 = kStage2Blocks;
-    static_assert(kStage2Blocks <= kMaxPartBlocks, "hist sized for kMaxPartBlocks");
-    {
-      KScope k(timer, "bucket_hist2", s);
-      k_part2_hist<kStage2Bits><<<dim3(P2, nseg), kPartThreads, 0, s>>>(
-          in2, kShardBits + L.cbits, hist1, P, hist);
-    }
-    scan::exclusive(hist, (static_cast<uint64_t>(1) << bits) * P2, hist, tiles, nullptr, s);
-    {
-      KScope k(timer, "bucket_scatter", s);
-      k_part_scatter_rec_staged<Rec16In, false, kStage2Bits, kStage2Slots, kStage2Rows>
-          <<<dim3(P2, nseg), kPartThreads, 0, s>>>(in2, 0, kShardBits + L.cbits, hist, rec,
-                                                    nullptr, hist1, P);
-    }
-    KScope k(timer, "bucket_group", s);
-    k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P2, ChunkOf::make(chunk_rows),
-                                                      gkey, gmin, rep);
-    return hipGetLastError();
-  }
+  if (L.cbits)
+    return two_level_launch<In, kStage2Bits, kStage2Slots, kStage2Rows, kStage2Blocks>(
+        in, n, L, chunk_rows, rep, init_rep, ws, s, timer);
   {
     KScope k(timer, "bucket_hist", s);
     allow_lds(k_part_hist<In>, lds);

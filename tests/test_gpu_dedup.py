@@ -249,9 +249,10 @@ def test_config4_full_100m_rows_eight_ranks(ctx):
 
 @pytest.mark.parametrize("n,chunk", [(13_000_000, 100), (26_000_000, 7)])
 def test_two_level_partition(ctx, n, chunk):
-    """Past 2^12 buckets the partition runs in two passes (coarse, then 12-bit
-    staged per segment): 13 M rows (2 segments) and 26 M rows (4), with a key
-    repeated 60 k times (a bucket past the LDS table) and keyless rows."""
+    """Past 2^12 buckets the partition runs in two passes (coarse, then 9-bit
+    staged per segment, offsets from the coarse pass's fine counts): 13 M rows
+    (16 segments) and 26 M rows (32), with a key repeated 60 k times (a bucket
+    past the LDS table) and keyless rows."""
     from spacedrive_amd import dedup
     rng = np.random.default_rng(n)
     pool = rng.integers(0, 2**64 - 1, int(n * 0.7), dtype=np.uint64, endpoint=True)
@@ -260,3 +261,23 @@ def test_two_level_partition(ctx, n, chunk):
     has = (rng.random(n) > 0.002).astype(np.uint8)
     rep = dedup.group_reps(key, has, chunk, ctx)
     np.testing.assert_array_equal(rep, O.group_reps(key, has, chunk))
+
+
+def test_two_level_fine_count_overflow(ctx):
+    """One key on the first 150 k rows of a 20 M-row table: the first coarse
+    block's tile (~78 k rows) holds more than 65 535 rows of one final bucket,
+    so its 16-bit fine counter overflows and the second pass's offsets are
+    recounted from the records (k_fine_recount).  Bit-exact with the oracle,
+    and a second call (flag reset) too."""
+    from spacedrive_amd import dedup
+    n = 20_000_000
+    rng = np.random.default_rng(20)
+    key = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    key[: n // 4] = key[rng.integers(0, n, n // 4)]  # duplicates elsewhere too
+    key[:150_000] = np.uint64(0x5EED)
+    has = (rng.random(n) > 0.001).astype(np.uint8)
+    ref = O.group_reps(key, has, 100)
+    np.testing.assert_array_equal(dedup.group_reps(key, has, 100, ctx), ref)
+    np.testing.assert_array_equal(dedup.group_reps(key, has, 100, ctx), ref)
+    key2 = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)  # no overflow now
+    np.testing.assert_array_equal(dedup.group_reps(key2, has, 100, ctx), O.group_reps(key2, has, 100))
