@@ -117,7 +117,8 @@ def pmc_traffic(kernel: str, section: str = "kernels"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/<round>/pmc_traffic.json, written by scripts/pmc_summary.py from
     rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench's workload; section
-    "kernels" = the K1 pass over config 2, "dedup" = the 12.5 M-row grouping)."""
+    "kernels" = the K1 pass over config 2, "dedup" = the 12.5 M-row grouping,
+    "dedup_full" = the 100 M-row two-level grouping)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
     for f in reversed(files):  # newest round first (profiles/r1, r2, ...)
@@ -577,12 +578,45 @@ class Runner:
         torch.cuda.synchronize()
         t, kt = self.timed_kernels(lambda: self.ops.group_rows(key, has, rank, 100, 0), steps,
                                    warmup)
-        del key, has, rank
+        rep = self.ops.group_rows(key, has, rank, 100, 0)
+        nk = int(has.sum())
+        linked = int((rep != rank).sum())
+        del key, has, rank, rep
         torch.cuda.empty_cache()
-        return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
-                "rows": total,
-                "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
-                            for k, v in kt.items()}}
+        kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in kt.items()}
+        # algorithmic HBM bytes per launch of the two-level path:
+        # coarse pass reads key + rank + has_key, writes rep, one record per keyed row
+        # and the fine counts (2^15 buckets x 256 blocks x 4 B); the fine scan reads
+        # those and writes the 64 block starts per bucket; the second pass moves every
+        # record once more; the group-by as in the one-level path
+        nfine = 1 << 15
+        alg = {"bucket_hist": 9 * total,
+               "bucket_scatter1": 17 * total + 16 * nk + 4 * nfine * 256,
+               "bucket_fine_scan": 4 * nfine * 256 + 4 * nfine * 64 + 4 * nfine,
+               "bucket_scatter": 32 * nk,
+               "bucket_group": 16 * nk + 4 * linked}
+        pmc_names = {"bucket_hist": "k_part_hist", "bucket_scatter1": "k_part_scatter_runs",
+                     "bucket_scatter": "k_part_scatter_rec_staged", "bucket_group": "k_bucket_group"}
+        step_s = t / steps
+        roof = {"bound": "hbm", "peak": HBM_PEAK / 1e9, "unit": "GB/s", "linked_rows": linked,
+                "kernels": {}, "note": "algorithmic bytes of the two-level partition + group-by "
+                                       "(DESIGN.md section 4); PMC traffic in profiles/"}
+        src = None
+        for k, b in alg.items():
+            ms = kernels.get(k, {}).get("avg_ms")
+            if not ms:
+                continue
+            e = {"algorithmic_bytes": b, "achieved": b / (ms * 1e-3) / 1e9,
+                 "frac": b / (ms * 1e-3) / HBM_PEAK}
+            if k in pmc_names:
+                e["pmc_traffic"], src_ = pmc_traffic(pmc_names[k], "dedup_full")
+                src = src or src_
+            roof["kernels"][k] = e
+        roof["step"] = {"survey_8d_bytes": 16 * total, "achieved": 16 * total / step_s / 1e9,
+                        "frac": 16 * total / step_s / HBM_PEAK, "design_bytes": sum(alg.values()),
+                        "pmc_source": src}
+        return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * step_s,
+                "rows": total, "roofline": roof, "kernels": kernels}
 
     def verify_sharded(self, key, has, rank):
         """--verify: the sharded grouping over all ranks (the exchange path the

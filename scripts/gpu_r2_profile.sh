@@ -1,7 +1,8 @@
 # Round-2 rocprofv3 captures: kernel trace + stats of a short bench run, then
 # separate PMC passes (never combined with tracing): FETCH_SIZE / WRITE_SIZE /
 # SQ VALU / GRBM over the config-2 K1 step, FETCH_SIZE / WRITE_SIZE over the
-# 12.5 M-row grouping; then the 2-rank gloo rehearsal through bench --gpus 2.
+# 12.5 M-row grouping and over the 100 M-row (two-level) grouping; then the
+# 2-rank gloo rehearsal through bench --gpus 2.
 # Usage: TAG=r2x bash scripts/gpu_r2_profile.sh
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -21,8 +22,15 @@ for C in FETCH_SIZE WRITE_SIZE; do
     -- python3 bench.py --steps 2 --warmup 1 --no-cpu --components dedup --dedup-full-rows 0 \
     > "$OUT/dedup_pmc_$C.log" 2>&1 || exit 1
 done
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 240 rocprofv3 --pmc $C -d "$OUT/dedup_full/pmc_$C" -o pmc --output-format csv \
+    -- python3 bench.py --steps 2 --warmup 1 --no-cpu --components dedup --dedup-rows 100000000 \
+    --dedup-full-rows 0 > "$OUT/dedup_full_pmc_$C.log" 2>&1 || exit 1
+done
 python3 scripts/pmc_summary.py "$OUT/cas" "$OUT/pmc_cas.json" > "$OUT/pmc_cas.txt" || exit 1
 python3 scripts/pmc_summary.py "$OUT/dedup" "$OUT/pmc_dedup.json" > "$OUT/pmc_dedup.txt" || exit 1
+python3 scripts/pmc_summary.py "$OUT/dedup_full" "$OUT/pmc_dedup_full.json" > "$OUT/pmc_dedup_full.txt" || exit 1
+python3 scripts/pmc_merge.py "$OUT" "$OUT/pmc_traffic.json" "$TAG" || exit 1
 SD_BENCH_BACKEND=gloo timeout -k 10 600 python -u bench.py --gpus 2 --steps 3 --warmup 1 \
   --files 100000 --dedup-rows 2000000 --staged-files 50000 --staged-total-files 1000000 \
   --checksum-files 2 --checksum-bytes 268435456 --dir-files 1000 --no-cpu --verify \
