@@ -134,7 +134,8 @@ template <typename In>
 __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, uint32_t skip,
                                                             uint32_t bits, uint32_t world,
                                                             uint32_t* __restrict__ hist,
-                                                            uint32_t* __restrict__ zero = nullptr) {
+                                                            uint32_t* __restrict__ zero = nullptr,
+                                                            bool blk_major = false) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
   const uint32_t nbins = world ? world : 1u << bits;
   if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;  // a flag of the next kernels
@@ -157,8 +158,11 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
     }
   }
   __syncthreads();
+  // digit-major [digit][block] for scan::exclusive, or block-major (one
+  // coalesced row per block) for k_fine_scan
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
-    hist[static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
+    hist[blk_major ? static_cast<uint64_t>(part_block()) * nbins + b
+                   : static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
 }
 
 // Shard partition of the multi-GPU exchange: keyed rows packed by digit (the
@@ -451,34 +455,57 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
   const uint32_t c = blockIdx.y;
   uint64_t t0 = 0, t1 = 0;
   if (ftot) {
-    // second pass fed by the coarse pass's fine counts: block j takes what
-    // coarse blocks [R j, R (j + 1)) wrote to segment c, offs = E (k_fine_scan).
-    // Bucket starts: segment c's first record (the coarse offsets) + the
-    // exclusive scan of its buckets' sizes, scanned here; block 0 of each
-    // segment publishes them (fbase, + the total) for the group kernel.
-    if constexpr (nbins <= kPartThreads) {  // the two-level second pass only
-      __shared__ uint32_t wsum[kPartThreads / 64];
-      const uint32_t j = part_block(), t = threadIdx.x, lane = __lane_id();
-      const uint64_t nfine = static_cast<uint64_t>(gridDim.y) << kBits, b0 = static_cast<uint64_t>(c) << kBits;
-      const uint32_t v = t < nbins ? ftot[b0 + t] : 0u;
-      uint32_t inc = v;
+    // offsets from block-major counts (k_fine_scan): offs = E[j][bucket], the
+    // rows of each bucket that blocks before j hold; ftot = bucket sizes.
+    // Two-level second pass (seg): block j takes what coarse blocks
+    // [R j, R (j + 1)) wrote to segment c, whose first record is seg[c P1].
+    // One level (no seg): block j takes tile j of the rows.  Bucket starts:
+    // segment start + exclusive scan of the segment's bucket sizes, scanned
+    // here (kPerT per thread); block 0 of each segment publishes them (fbase,
+    // + the total) for the group kernel.
+    constexpr uint32_t kPerT = nbins > kPartThreads ? nbins / kPartThreads : 1u;
+    static_assert(nbins <= kPartThreads || nbins % kPartThreads == 0, "buckets per thread");
+    uint32_t* wsum = fill;  // scratch for the 16 wave sums (LDS is full)
+    const uint32_t j = part_block(), t = threadIdx.x, lane = __lane_id();
+    const uint64_t nfine = static_cast<uint64_t>(gridDim.y) << kBits, b0 = static_cast<uint64_t>(c) << kBits;
+    uint32_t v[kPerT], sum = 0;
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(inc, d);
-        if (lane >= static_cast<uint32_t>(d)) inc += o;
+    for (uint32_t k = 0; k < kPerT; ++k) {
+      const uint32_t b = t * kPerT + k;
+      v[k] = b < nbins ? ftot[b0 + b] : 0u;
+      sum += v[k];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
+    }
+    if (lane == 63) wsum[t >> 6] = inc;
+    __syncthreads();
+    uint32_t base = (seg ? seg[static_cast<uint64_t>(c) * P1] : 0u) + inc - sum, total = 0;
+    for (uint32_t w = 0; w < kPartThreads / 64; ++w) {
+      if (w < (t >> 6)) base += wsum[w];
+      total += wsum[w];
+    }
+    __syncthreads();  // wsum (= fill) is cleared below
+#pragma unroll
+    for (uint32_t k = 0; k < kPerT; ++k) {
+      const uint32_t b = t * kPerT + k;
+      if (b < nbins) {
+        cur[b] = base + offs[j * nfine + b0 + b];
+        fill[b] = 0;
+        if (j == 0) fbase[b0 + b] = base;
       }
-      if (lane == 63) wsum[t >> 6] = inc;
-      __syncthreads();
-      uint32_t base = seg[static_cast<uint64_t>(c) * P1] + inc - v;
-      for (uint32_t w = 0; w < (t >> 6); ++w) base += wsum[w];
-      if (t < nbins) {
-        cur[t] = base + offs[j * nfine + b0 + t];
-        fill[t] = 0;
-        if (j == 0) fbase[b0 + t] = base;
-      }
-      if (j == 0 && c == gridDim.y - 1 && t == 0) fbase[nfine] = seg[static_cast<uint64_t>(gridDim.y) * P1];
+      base += v[k];
+    }
+    if (j == 0 && c == gridDim.y - 1 && t == 0)
+      fbase[nfine] = seg ? seg[static_cast<uint64_t>(gridDim.y) * P1] : total;
+    if (seg) {
       t0 = seg[static_cast<uint64_t>(c) * P1 + min(P1, R * j)];
       t1 = seg[static_cast<uint64_t>(c) * P1 + min(P1, R * (j + 1))];
+    } else {
+      tile_of(n, gridDim.x, t0, t1);
     }
   } else {
     const uint64_t obase = static_cast<uint64_t>(c) * nbins * gridDim.x;
@@ -845,7 +872,7 @@ GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
   L.rec1 = o; o = align_up(o + (L.cbits ? 16 * n : 0), 256);
   L.gkey = o; o = align_up(o + 8 * 4 * n, 256);
   L.gmin = o; o = align_up(o + 4 * 4 * n, 256);
-  const uint64_t nf = L.cbits ? static_cast<uint64_t>(1) << L.bits : 0;
+  const uint64_t nf = static_cast<uint64_t>(1) << L.bits;  // block-major counts (12-bit and two-level)
   L.fine = o; o = align_up(o + 4 * nf * kPartBlocks, 256);
   L.fE = o; o = align_up(o + 4 * nf * kPartBlocks, 256);
   L.ftot = o; o = align_up(o + 4 * nf, 256);
@@ -945,6 +972,36 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   if (L.cbits)
     return two_level_launch<In, kStage2Bits, kStage2Slots, kStage2Rows, kStage2Blocks>(
         in, n, L, chunk_rows, rep, init_rep, ws, s, timer);
+  if (bits == kStageBits) {
+    // 12-bit digits: block-major counts, k_fine_scan for every block's start
+    // inside every bucket (one launch instead of the 3-launch scan), bucket
+    // starts scanned in the staged scatter's prologue
+    uint32_t* fine = reinterpret_cast<uint32_t*>(w + L.fine);
+    uint32_t* fE = reinterpret_cast<uint32_t*>(w + L.fE);
+    uint32_t* ftot = reinterpret_cast<uint32_t*>(w + L.ftot);
+    uint32_t* fbase = reinterpret_cast<uint32_t*>(w + L.fbase);
+    uint32_t* ovf = reinterpret_cast<uint32_t*>(w + L.ovf);
+    const uint32_t nb = 1u << kStageBits;
+    static_assert(kPartBlocks % 16 == 0, "k_fine_scan: blocks per thread");
+    {
+      KScope k(timer, "bucket_hist", s);
+      k_part_hist<In><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, 0, fine, nullptr, true);
+      k_fine_scan<kPartBlocks, 1><<<nb / 64, 1024, 0, s>>>(fine, nb, fE, ftot, ovf);
+    }
+    {
+      KScope k(timer, "bucket_scatter", s);
+      if (init_rep)
+        k_part_scatter_rec_staged<In, true><<<P, kPartThreads, 0, s>>>(
+            in, n, kShardBits, fE, rec, rep, nullptr, 0, ftot, fbase);
+      else
+        k_part_scatter_rec_staged<In, false><<<P, kPartThreads, 0, s>>>(
+            in, n, kShardBits, fE, rec, rep, nullptr, 0, ftot, fbase);
+    }
+    KScope k(timer, "bucket_group", s);
+    k_bucket_group<<<nb, kGroupThreads, 0, s>>>(rec, fbase, 1, ChunkOf::make(chunk_rows), gkey,
+                                                gmin, rep);
+    return hipGetLastError();
+  }
   {
     KScope k(timer, "bucket_hist", s);
     allow_lds(k_part_hist<In>, lds);
@@ -953,14 +1010,7 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   scan::exclusive(hist, nh, hist, tiles, nullptr, s);
   {
     KScope k(timer, "bucket_scatter", s);
-    const bool staged = bits == kStageBits;
-    if (staged && init_rep)
-      k_part_scatter_rec_staged<In, true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, hist, rec,
-                                                                     rep, nullptr, 0);
-    else if (staged)
-      k_part_scatter_rec_staged<In, false><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, hist,
-                                                                      rec, rep, nullptr, 0);
-    else if (init_rep) {
+    if (init_rep) {
       allow_lds(k_part_scatter_rec<In, true>, lds);
       k_part_scatter_rec<In, true><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, hist, rec,
                                                                 rep);
