@@ -556,11 +556,31 @@ class Runner:
                             "pmc_traffic": (sum(pmc_sum) if all(x is not None for x in pmc_sum)
                                             else None),
                             "pmc_source": src}
+        # K7 Object link batch over the same 12.5 M rows: the
+        # create list and the (row, creator) connect pairs as dense arrays
+        repv = self.group(key, has, rank)
+        link_t, link_kt = self.timed_kernels(
+            lambda: dedup.link_batch_device(repv, rank, has, 0, ctx=self.ctx, trim=False),
+            steps, warmup)
+        c_, l_ = (int(x) for x in dedup.link_batch_device(repv, rank, has, 0, ctx=self.ctx,
+                                                          trim=False)[3].cpu().tolist())
+        link_bytes = 9 * per + 4 * c_ + 8 * l_
+        link = {"value": self.world * per * steps / link_t, "unit": "rows/s",
+                "ms_per_step": 1e3 * link_t / steps, "created": c_, "linked": l_,
+                "roofline": {"bound": "hbm", "algorithmic_bytes": link_bytes,
+                             "achieved": link_bytes / (link_t / steps) / 1e9,
+                             "frac": link_bytes / (link_t / steps) / HBM_PEAK, "unit": "GB/s",
+                             "note": "reads rep + rank + has_key, writes the create list and "
+                                     "the connect pairs; the flag scans' own traffic on top"},
+                "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
+                            for k, v in link_kt.items()}}
+        del repv
         full = None
         if self.world == 1 and self.args.dedup_full_rows:
             full = self.run_dedup_full(steps, warmup)
         return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
                 "exchange": xchg, "roofline": roof, "config4_full_one_gpu": full,
+                "link_batch": link,
                 "config": {"workload": "config4: 80% distinct u64 keys + 20% dups, 0.1% keyless",
                            "rows_per_gpu": per, "rows_total": total},
                 "kernels": kernels}
@@ -657,10 +677,19 @@ class Runner:
                          steps, warmup)
         t_t = self.timed(lambda: consumers.thumbnail_shards(cas8, ctx=self.ctx), steps, warmup)
         del obj, fp, cas8
+        # algorithmic bytes: object_id of every file_path (4 B) + a mark byte per
+        # Object id, the Object ids (4 B) and the orphan list written (4 B each)
+        ob = 4 * n_fp + n_obj + 4 * n_obj + 4 * orphans
         return {"orphan_remover": {"value": self.world * (n_obj + n_fp) * steps / t_o,
                                    "unit": "rows/s", "ms_per_step": 1e3 * t_o / steps,
                                    "objects_per_gpu": n_obj, "file_paths_per_gpu": n_fp,
-                                   "orphans_rank0": orphans},
+                                   "orphans_rank0": orphans,
+                                   "roofline": {"bound": "hbm", "algorithmic_bytes": ob,
+                                                "achieved": ob / (t_o / steps) / 1e9,
+                                                "frac": ob / (t_o / steps) / HBM_PEAK,
+                                                "unit": "GB/s",
+                                                "note": "per call, incl. the count read-back "
+                                                        "(one host synchronisation)"}},
                 "thumbnail_shards": {"value": self.world * n_th * steps / t_t, "unit": "rows/s",
                                      "ms_per_step": 1e3 * t_t / steps, "rows_per_gpu": n_th}}
 
