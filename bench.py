@@ -556,6 +556,8 @@ class Runner:
                             "pmc_traffic": (sum(pmc_sum) if all(x is not None for x in pmc_sum)
                                             else None),
                             "pmc_source": src}
+        if self.world == 1 and not self.args.no_cpu:
+            self._cpu_dedup = self.cpu_grouping(key, has, rank)
         # K7 Object link batch over the same 12.5 M rows: the
         # create list and the (row, creator) connect pairs as dense arrays
         repv = self.group(key, has, rank)
@@ -584,6 +586,25 @@ class Runner:
                 "config": {"workload": "config4: 80% distinct u64 keys + 20% dups, 0.1% keyless",
                            "rows_per_gpu": per, "rows_total": total},
                 "kernels": kernels}
+
+    def cpu_grouping(self, key, has, rank):
+        """CPU leg of config 4: the oracle's C grouping (orc_group_reps, one
+        thread: a restatement of the chunk rule over rows in rank order) on the
+        same 12.5 M rows, timed; its reps must equal the GPU's (a parity check
+        at full size)."""
+        from oracle import oracle as O
+        order = np.argsort(rank.cpu().numpy().view(np.uint32), kind="stable")
+        k = key.cpu().numpy().view(np.uint64)[order]
+        h = has.cpu().numpy()[order]
+        gpu = self.group(key, has, rank).cpu().numpy().view(np.uint32)[order]
+        t0 = time.perf_counter()
+        ref = O.group_reps(k, h, 100)
+        dt = time.perf_counter() - t0
+        return {"value": k.size / dt, "unit": "rows/s", "threads": 1, "kind": "port",
+                "gpu_rep_mismatches": int(np.count_nonzero(ref != gpu)),
+                "sample": f"config 4: the same {k.size} rows (rank order), oracle orc_group_reps "
+                          f"(C, one thread; the reference groups with SQLite queries per "
+                          f"100-row chunk), {dt:.1f} s"}
 
     def run_dedup_full(self, steps, warmup):
         """BASELINE config 4 at its full size on ONE GPU (the strong-scaling
@@ -911,6 +932,7 @@ def main():
         shutil.rmtree(R._dir_sample[2], ignore_errors=True)
         R._dir_sample = None
     torch.cuda.empty_cache()
+    R._cpu_dedup = None
     comp = {"cas": c["cas"], "identifier_job": c["job"]} if c else {}
     if dir_comp:
         comp["dir"] = dir_comp
@@ -920,6 +942,8 @@ def main():
         d = R.run_dedup(args.steps, args.warmup)
         log("dedup:", json.dumps(d))
         comp["dedup"] = d
+        if cpu is not None and R._cpu_dedup:
+            cpu["config4_grouping"] = R._cpu_dedup
         torch.cuda.empty_cache()
     if "consumers" in comps:
         k = R.run_consumers(args.steps, args.warmup)
