@@ -12,7 +12,8 @@
 // so the host issues one create_many + one batched connect per large batch
 // instead of 4-5 queries per 100 rows.  Rows with valid == 0 (metadata or
 // hash failed, mod.rs:113,127) are in neither list: they stay orphans.
-// HBM-bound: reads 4-9 B/row, writes 4 B per created row and 8 B per linked row.
+// HBM-bound: reads 9 B/row twice, writes 4 B per created row and 8 B per
+// linked row; three launches + a scan of two counters per 4096-row tile.
 #include "internal.hpp"
 #include "scan_device.hpp"
 
@@ -20,73 +21,148 @@ namespace sdgpu {
 
 namespace {
 
+// A block takes a tile of kTile rows: row tile + k * kThreads + t for k in
+// [0, kRows) -- coalesced loads, and (k, t) order is row order, so in-block
+// ranks from per-(k, wave) ballots keep both lists in row order.
 constexpr int kThreads = 256;
+constexpr int kRows = 16;
+constexpr uint32_t kTile = kThreads * kRows;
+constexpr int kWaves = kThreads / 64;
 
-__global__ __launch_bounds__(kThreads) void k_link_flags(const uint32_t* __restrict__ rep,
+struct LinkRow {
+  uint32_t r, p;
+  bool c, l;  // creates an Object / connects to one
+};
+
+__device__ __forceinline__ LinkRow link_row(const uint32_t* __restrict__ rep,
+                                            const uint32_t* __restrict__ rank,
+                                            const uint8_t* __restrict__ valid, uint32_t first_rank,
+                                            uint64_t n, uint64_t i) {
+  LinkRow x{0, 0, false, false};
+  if (i >= n) return x;
+  x.r = rank ? rank[i] : first_rank + static_cast<uint32_t>(i);
+  x.p = rep[i];
+  const bool v = valid ? valid[i] != 0 : true;
+  x.c = v && x.p == x.r;
+  x.l = v && x.p != x.r;
+  return x;
+}
+
+// Creators and connectors per tile: cnt[blk] and cnt[nb + blk].
+__global__ __launch_bounds__(kThreads) void k_link_count(const uint32_t* __restrict__ rep,
                                                          const uint32_t* __restrict__ rank,
                                                          const uint8_t* __restrict__ valid,
                                                          uint32_t first_rank, uint64_t n,
-                                                         uint32_t* __restrict__ fc,
-                                                         uint32_t* __restrict__ fl) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t r = rank ? rank[i] : first_rank + static_cast<uint32_t>(i);
-  const bool v = valid ? valid[i] != 0 : true;
-  const bool self = rep[i] == r;
-  fc[i] = (v && self) ? 1u : 0u;
-  fl[i] = (v && !self) ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(kThreads) void k_link_scatter(const uint32_t* __restrict__ rep,
-                                                           const uint32_t* __restrict__ rank,
-                                                           const uint8_t* __restrict__ valid,
-                                                           uint32_t first_rank, uint64_t n,
-                                                           const uint32_t* __restrict__ pc,
-                                                           const uint32_t* __restrict__ pl,
-                                                           uint32_t* __restrict__ create,
-                                                           uint32_t* __restrict__ link_row,
-                                                           uint32_t* __restrict__ link_obj) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (i >= n) return;
-  if (valid && valid[i] == 0) return;
-  const uint32_t r = rank ? rank[i] : first_rank + static_cast<uint32_t>(i);
-  const uint32_t p = rep[i];
-  if (p == r) {
-    create[pc[i]] = r;
-  } else {
-    const uint32_t k = pl[i];
-    link_row[k] = r;
-    link_obj[k] = p;
+                                                         uint32_t nb, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t sc[kWaves], sl[kWaves];
+  const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * kTile;
+  uint32_t c = 0, l = 0;
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const LinkRow x = link_row(rep, rank, valid, first_rank, n, tile + k * kThreads + threadIdx.x);
+    c += x.c;
+    l += x.l;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    c += __shfl_xor(c, d);
+    l += __shfl_xor(l, d);
+  }
+  if (__lane_id() == 0) {
+    sc[threadIdx.x >> 6] = c;
+    sl[threadIdx.x >> 6] = l;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tc = 0, tl = 0;
+    for (int w = 0; w < kWaves; ++w) {
+      tc += sc[w];
+      tl += sl[w];
+    }
+    cnt[blockIdx.x] = tc;
+    cnt[nb + blockIdx.x] = tl;
   }
 }
+
+// cnt = exclusive scan over [C counts | L counts] (cnt[2 nb] = total): tile
+// blk writes its creators from cnt[blk], its connectors from cnt[nb + blk] - C.
+__global__ __launch_bounds__(kThreads) void k_link_write(
+    const uint32_t* __restrict__ rep, const uint32_t* __restrict__ rank,
+    const uint8_t* __restrict__ valid, uint32_t first_rank, uint64_t n, uint32_t nb,
+    const uint32_t* __restrict__ cnt, uint32_t* __restrict__ create, uint32_t* __restrict__ link_row_out,
+    uint32_t* __restrict__ link_obj, uint32_t* __restrict__ d_counts) {
+  __shared__ uint32_t oc[kRows][kWaves], ol[kRows][kWaves];
+  const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * kTile;
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t total_c = cnt[nb];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    d_counts[0] = total_c;
+    d_counts[1] = cnt[2 * static_cast<uint64_t>(nb)] - total_c;
+  }
+  LinkRow x[kRows];
+  uint32_t pc[kRows], pl[kRows];
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    x[k] = link_row(rep, rank, valid, first_rank, n, tile + k * kThreads + threadIdx.x);
+    const uint64_t bc = __ballot(x[k].c), bl = __ballot(x[k].l);
+    pc[k] = __popcll(bc & lt);
+    pl[k] = __popcll(bl & lt);
+    if (lane == 0) {
+      oc[k][w] = __popcll(bc);
+      ol[k][w] = __popcll(bl);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // (k, wave) order is row order
+    uint32_t rc = cnt[blockIdx.x], rl = cnt[nb + blockIdx.x] - total_c;
+    for (int k = 0; k < kRows; ++k)
+      for (int v = 0; v < kWaves; ++v) {
+        const uint32_t a = oc[k][v], b = ol[k][v];
+        oc[k][v] = rc;
+        ol[k][v] = rl;
+        rc += a;
+        rl += b;
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    if (x[k].c) create[oc[k][w] + pc[k]] = x[k].r;
+    if (x[k].l) {
+      const uint32_t q = ol[k][w] + pl[k];
+      link_row_out[q] = x[k].r;
+      link_obj[q] = x[k].p;
+    }
+  }
+}
+
+inline uint32_t link_tiles(uint64_t n) { return static_cast<uint32_t>((n + kTile - 1) / kTile); }
 
 }  // namespace
 
 size_t link_workspace_bytes(uint64_t n) {
-  const size_t a = ((n + 1) * 4 + 255) / 256 * 256;
-  const size_t t = ((scan::tiles_for(n) + 1) * 4 + 255) / 256 * 256;
-  return 2 * a + 2 * t;
+  const uint64_t m = 2ull * link_tiles(n);
+  return ((m + 1) * 4 + 255) / 256 * 256 + ((scan::tiles_for(m) + 1) * 4 + 255) / 256 * 256;
 }
 
+// Two passes over the rows (count per tile, then rank and write), one scan of
+// the 2 x tiles counts in between: ~18 B read per row plus the lists written.
 hipError_t link_batch_launch(const uint32_t* rep, const uint32_t* rank, const uint8_t* valid,
                              uint32_t first_rank, uint64_t n, uint32_t* create, uint32_t* link_row,
                              uint32_t* link_obj, uint32_t* d_counts, void* ws, hipStream_t s,
                              KTimer* timer) {
   if (n == 0) return hipMemsetAsync(d_counts, 0, 2 * sizeof(uint32_t), s);
-  const size_t a = ((n + 1) * 4 + 255) / 256 * 256;
-  const size_t t = ((scan::tiles_for(n) + 1) * 4 + 255) / 256 * 256;
+  const uint32_t nb = link_tiles(n);
+  const uint64_t m = 2ull * nb;
   uint8_t* b = static_cast<uint8_t*>(ws);
-  uint32_t* fc = reinterpret_cast<uint32_t*>(b);
-  uint32_t* fl = reinterpret_cast<uint32_t*>(b + a);
-  uint32_t* tc = reinterpret_cast<uint32_t*>(b + 2 * a);
-  uint32_t* tl = reinterpret_cast<uint32_t*>(b + 2 * a + t);
-  const uint32_t blocks = static_cast<uint32_t>((n + kThreads - 1) / kThreads);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(b);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(b + ((m + 1) * 4 + 255) / 256 * 256);
   KScope k(timer, "link_batch", s);
-  k_link_flags<<<blocks, kThreads, 0, s>>>(rep, rank, valid, first_rank, n, fc, fl);
-  scan::exclusive(fc, n, fc, tc, d_counts, s);
-  scan::exclusive(fl, n, fl, tl, d_counts + 1, s);
-  k_link_scatter<<<blocks, kThreads, 0, s>>>(rep, rank, valid, first_rank, n, fc, fl, create,
-                                             link_row, link_obj);
+  k_link_count<<<nb, kThreads, 0, s>>>(rep, rank, valid, first_rank, n, nb, cnt);
+  scan::exclusive(cnt, m, cnt, tiles, nullptr, s);
+  k_link_write<<<nb, kThreads, 0, s>>>(rep, rank, valid, first_rank, n, nb, cnt, create, link_row,
+                                       link_obj, d_counts);
   return hipGetLastError();
 }
 
