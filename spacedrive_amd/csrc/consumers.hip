@@ -5,8 +5,9 @@
 // found 512 at a time and deleted.  Here: one pass marks every Object id that
 // some file_path references (a byte per id, plain stores: marking is
 // idempotent, so no atomics are needed), a second pass keeps
-// the unreferenced ids of the Object list, in list order (block-local LDS
-// compaction + one scan), ready for the caller's delete batches.
+// the unreferenced ids of the Object list, in list order (4096-id tiles:
+// count, one scan of the tile counts, in-tile ballot ranks), ready for the
+// caller's delete batches.
 //
 // Thumbnail shards (/root/reference/core/src/object/media/thumbnail/shard.rs:4-8):
 // a thumbnail lives in directory cas_id[0..2], the first digest byte, i.e. the
@@ -43,47 +44,80 @@ __device__ __forceinline__ bool orphan(int32_t o, const uint8_t* mark, uint32_t 
   return o >= 0 && (static_cast<uint32_t>(o) > max_id || mark[o] == 0);
 }
 
-// per block of kThreads Objects: how many are orphans
+// The Object list in tiles of kORows x kThreads ids: id tile + k * kThreads + t
+// (coalesced), and (k, t) order is list order, so in-tile ranks from
+// per-(k, wave) ballots keep the orphans in list order.
+constexpr int kORows = 16;
+constexpr uint64_t kOTile = static_cast<uint64_t>(kORows) * kThreads;
+constexpr int kOWaves = kThreads / 64;
+
+__device__ __forceinline__ int32_t obj_at(const int32_t* __restrict__ obj, uint64_t n,
+                                          uint64_t i) {
+  return i < n ? obj[i] : -1;
+}
+
+// orphans per tile
 __global__ __launch_bounds__(kThreads) void k_orphan_count(const int32_t* __restrict__ obj,
                                                            uint64_t n,
                                                            const uint8_t* __restrict__ bits,
                                                            uint32_t max_id,
                                                            uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t c;
-  if (threadIdx.x == 0) c = 0;
+  __shared__ uint32_t sw[kOWaves];
+  const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * kOTile;
+  int32_t o[kORows];
+#pragma unroll
+  for (int k = 0; k < kORows; ++k) o[k] = obj_at(obj, n, tile + k * kThreads + threadIdx.x);
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kORows; ++k) c += orphan(o[k], bits, max_id) ? 1u : 0u;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+  if (__lane_id() == 0) sw[threadIdx.x >> 6] = c;
   __syncthreads();
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (i < n) {
-    if (orphan(obj[i], bits, max_id)) atomicAdd(&c, 1u);
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kOWaves; ++w) t += sw[w];
+    cnt[blockIdx.x] = t;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) cnt[blockIdx.x] = c;
 }
 
-// stable compaction: block b writes its orphans at the scanned offset, in order
+// stable compaction: tile b writes its orphans from the scanned offset, in order
 __global__ __launch_bounds__(kThreads) void k_orphan_write(const int32_t* __restrict__ obj,
                                                            uint64_t n,
                                                            const uint8_t* __restrict__ bits,
                                                            uint32_t max_id,
                                                            const uint32_t* __restrict__ offs,
                                                            int32_t* __restrict__ out) {
-  __shared__ uint32_t flag[kThreads];
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  uint32_t f = 0;
-  int32_t o = -1;
-  if (i < n) {
-    o = obj[i];
-    f = orphan(o, bits, max_id) ? 1u : 0u;
+  __shared__ uint32_t off[kORows][kOWaves];
+  const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * kOTile;
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int32_t o[kORows];
+  uint32_t pre[kORows], f = 0;
+#pragma unroll
+  for (int k = 0; k < kORows; ++k) o[k] = obj_at(obj, n, tile + k * kThreads + threadIdx.x);
+#pragma unroll
+  for (int k = 0; k < kORows; ++k) {
+    const bool is = orphan(o[k], bits, max_id);
+    f |= (is ? 1u : 0u) << k;
+    const uint64_t b = __ballot(is);
+    pre[k] = __popcll(b & lt);
+    if (lane == 0) off[k][w] = __popcll(b);
   }
-  flag[threadIdx.x] = f;
   __syncthreads();
-  for (int d = 1; d < kThreads; d <<= 1) {  // inclusive scan of the block's flags
-    const uint32_t t = threadIdx.x >= d ? flag[threadIdx.x - d] : 0u;
-    __syncthreads();
-    flag[threadIdx.x] += t;
-    __syncthreads();
+  if (threadIdx.x == 0) {  // (k, wave) order is list order
+    uint32_t run = offs[blockIdx.x];
+    for (int k = 0; k < kORows; ++k)
+      for (int v = 0; v < kOWaves; ++v) {
+        const uint32_t a = off[k][v];
+        off[k][v] = run;
+        run += a;
+      }
   }
-  if (f) out[offs[blockIdx.x] + flag[threadIdx.x] - 1] = o;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kORows; ++k)
+    if (f >> k & 1u) out[off[k][w] + pre[k]] = o[k];
 }
 
 // ---- thumbnail shards -----------------------------------------------------------
@@ -169,7 +203,7 @@ __global__ void k_thumb_counts(const uint32_t* __restrict__ offs, uint32_t* __re
 
 size_t orphan_workspace_bytes(uint64_t n_obj, uint32_t max_id) {
   const uint64_t map = (static_cast<uint64_t>(max_id) + 1 + 255) / 256 * 256;
-  const uint64_t blocks = (n_obj + kThreads - 1) / kThreads;
+  const uint64_t blocks = (n_obj + kOTile - 1) / kOTile;
   return map + 4 * (blocks + 1) + 4 * (scan::tiles_for(blocks) + 1) + 1024;
 }
 
@@ -177,7 +211,7 @@ hipError_t orphan_objects_launch(const int32_t* obj, uint64_t n_obj, const int32
                                  uint64_t n_fp, uint32_t max_id, int32_t* out, uint32_t* d_count,
                                  void* ws, hipStream_t s) {
   const uint64_t map = (static_cast<uint64_t>(max_id) + 1 + 255) / 256 * 256;
-  const uint64_t blocks = (n_obj + kThreads - 1) / kThreads;
+  const uint64_t blocks = (n_obj + kOTile - 1) / kOTile;
   uint8_t* bits = static_cast<uint8_t*>(ws);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(bits + map);
   uint32_t* tiles = cnt + blocks + 1;
