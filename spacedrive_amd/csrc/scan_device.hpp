@@ -43,29 +43,37 @@ __global__ __launch_bounds__(kThreads) static void k_tiles(const uint32_t* __res
   if (threadIdx.x == kThreads - 1) tile_sums[blockIdx.x] = sh[threadIdx.x];
 }
 
-// Single block: exclusive scan of tile sums; writes the grand total to
-// out[n] (if out_total_slot) and *total (if non-null).
-__global__ __launch_bounds__(kThreads) static void k_sums(uint32_t* __restrict__ tile_sums,
-                                                          uint32_t ntiles,
-                                                          uint32_t* __restrict__ out_total_slot,
-                                                          uint32_t* __restrict__ total) {
-  __shared__ uint32_t sh[kThreads];
+// Single block of kSumThreads: exclusive scan of the tile sums (wave shuffles,
+// then the 16 wave totals); writes the grand total to out[n] (if
+// out_total_slot) and *total (if non-null).
+constexpr int kSumThreads = 1024;
+__global__ __launch_bounds__(kSumThreads) static void k_sums(uint32_t* __restrict__ tile_sums,
+                                                             uint32_t ntiles,
+                                                             uint32_t* __restrict__ out_total_slot,
+                                                             uint32_t* __restrict__ total) {
+  __shared__ uint32_t wsum[kSumThreads / 64];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   uint32_t carry = 0;
-  for (uint32_t b0 = 0; b0 < ntiles; b0 += kThreads) {
+  for (uint32_t b0 = 0; b0 < ntiles; b0 += kSumThreads) {
     const uint32_t i = b0 + threadIdx.x;
     const uint32_t v = i < ntiles ? tile_sums[i] : 0u;
-    sh[threadIdx.x] = v;
-    __syncthreads();
-    for (int d = 1; d < kThreads; d <<= 1) {
-      const uint32_t t = threadIdx.x >= d ? sh[threadIdx.x - d] : 0u;
-      __syncthreads();
-      sh[threadIdx.x] += t;
-      __syncthreads();
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
     }
-    if (i < ntiles) tile_sums[i] = carry + sh[threadIdx.x] - v;
-    const uint32_t blk = sh[kThreads - 1];
+    if (lane == 63) wsum[w] = inc;
     __syncthreads();
+    uint32_t pre = 0, blk = 0;
+    for (uint32_t k = 0; k < kSumThreads / 64; ++k) {
+      const uint32_t x = wsum[k];
+      pre += k < w ? x : 0u;
+      blk += x;
+    }
+    if (i < ntiles) tile_sums[i] = carry + pre + inc - v;
     carry += blk;
+    __syncthreads();  // wsum is rewritten by the next chunk
   }
   if (threadIdx.x == 0) {
     if (out_total_slot) *out_total_slot = carry;
@@ -90,7 +98,7 @@ inline void exclusive(const uint32_t* in, uint64_t n, uint32_t* out, uint32_t* t
     return;
   }
   k_tiles<<<tiles, kThreads, 0, s>>>(in, n, out, tile_sums);
-  k_sums<<<1, kThreads, 0, s>>>(tile_sums, tiles, out + n, total);
+  k_sums<<<1, kSumThreads, 0, s>>>(tile_sums, tiles, out + n, total);
   k_add<<<static_cast<uint32_t>((n + kThreads - 1) / kThreads), kThreads, 0, s>>>(out, n,
                                                                                    tile_sums);
 }
