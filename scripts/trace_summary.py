@@ -14,8 +14,8 @@ import csv
 import sys
 
 KERNELS = ["k_leaves3", "k_fold3", "k_tree_level<true>", "k_tree_level<false>",
-           "k_part_hist", "k_part_scatter_rec", "k_bucket_group", "k_link_flags",
-           "k_link_scatter", "k_small"]
+           "k_part_hist", "k_part_scatter_runs", "k_part_scatter_rec_staged", "k_part_scatter_rec",
+           "k_fine_scan", "k_bucket_group", "k_link_count", "k_link_write", "k_small"]
 LONG_MS = 5.0  # K1 launches over a whole 1 M-file step take ~13 ms; every other K1 launch < 2 ms
 
 
@@ -32,9 +32,12 @@ def main(path, out=None):
             key = (short, "1M-file step" if ms >= LONG_MS or short == "k_fold3" and ms > 0.1
                    else "other")
         groups[key].append(ms)
-    lines = [f"{'kernel':24s} {'group':>14s} {'launches':>8s} {'avg_ms':>10s} {'min_ms':>9s} {'max_ms':>9s}"]
+    lines = [f"{'kernel':26s} {'group':>14s} {'launches':>8s} {'avg_ms':>10s} {'median_ms':>10s} "
+             f"{'min_ms':>9s} {'max_ms':>9s}"]
     for (k, g), v in sorted(groups.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
-        lines.append(f"{k:24s} {str(g):>14s} {len(v):8d} {sum(v) / len(v):10.4f} {min(v):9.4f} {max(v):9.4f}")
+        med = sorted(v)[len(v) // 2]
+        lines.append(f"{k:26s} {str(g):>14s} {len(v):8d} {sum(v) / len(v):10.4f} {med:10.4f} "
+                     f"{min(v):9.4f} {max(v):9.4f}")
     text = "\n".join(lines)
     print(text)
     if out:
