@@ -8,7 +8,8 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n_obj,n_fp", [(0, 10), (1, 0), (1000, 800), (300_000, 1_000_000)])
+@pytest.mark.parametrize("n_obj,n_fp", [(0, 10), (1, 0), (1000, 800), (4095, 5000), (4096, 100),
+                                         (4097, 9000), (300_000, 1_000_000)])
 def test_orphan_objects(ctx, n_obj, n_fp):
     import torch
     from spacedrive_amd import consumers

@@ -69,6 +69,9 @@ def test_stage_pinned_rejects_unordered_arena(ctx):
 
 
 @pytest.mark.parametrize("n,first_rank,with_valid", [(0, 0, False), (1, 0, False),
+                                                     (255, 3, True), (4095, 0, True),
+                                                     (4096, 0, False), (4097, 11, True),
+                                                     (65_537, 0, True),
                                                      (100_000, 0, True), (2_000_000, 7_000, True)])
 def test_link_batch_vs_oracle(ctx, n, first_rank, with_valid):
     import torch
