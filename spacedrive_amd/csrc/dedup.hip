@@ -28,11 +28,16 @@
 // Pipeline (all asynchronous, no host synchronisation):
 //   K6 partition: digit = `bits` hash bits below the top `skip` bits.
 //      hist:    each of P blocks histograms its contiguous tile in LDS and
-//               writes counts[digit][block] (no global atomics);
-//      scan:    exclusive scan of counts (digit-major) -> (digit, block) offsets;
+//               writes its counts (no global atomics): block-major rows for
+//               the 12-bit bucket partition, digit-major elsewhere;
+//      offsets: k_fine_scan (block-major: every block's start inside every
+//               bucket, one launch; bucket starts scanned in the scatter's
+//               prologue) or scan::exclusive (digit-major);
 //      scatter: each block re-reads its tile and scatters its rows through LDS
 //               cursors (16-B bucket records, or the exchange's send layout).
-//      Used twice: by shard (multi-GPU exchange) and by bucket.
+//      Used by shard (multi-GPU exchange) and by bucket; past 2^12 buckets the
+//      bucket partition takes two passes, the coarse one counting every row's
+//      final bucket for the second (group_layout).
 //   K5 group:   one workgroup per bucket builds a linear-probing hash table of
 //               (key -> min rank) in LDS (ds_cmpst_b64 / ds_min_u32), then maps
 //               every row to its rep.  Buckets too large for LDS use a private
