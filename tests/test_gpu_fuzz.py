@@ -80,6 +80,42 @@ def test_fuzz_grouping_device(ctx, seed):
     np.testing.assert_array_equal(rep, ref[rank])
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_grouping_large(ctx, seed):
+    """The 12-bit path (block-major counts, one-launch offsets) and the
+    two-level path (fine counts from the coarse pass) over random large shapes:
+    6.5-20 M rows, the same key families as above (random, small integers,
+    high bits only, the empty value), random rank permutations, keyless rows."""
+    import torch
+    from spacedrive_amd import dedup
+    rng = np.random.default_rng(3000 + seed)
+    n = int(rng.choice([6_500_000, 12_500_000, 12_600_000, 13_000_000, 20_000_000]))
+    distinct = max(1, int(n * rng.choice([0.001, 0.5, 0.9, 1.0])))
+    mode = seed % 4
+    if mode == 0:
+        pool = rng.integers(0, 2**64 - 1, distinct, dtype=np.uint64, endpoint=True)
+    elif mode == 1:
+        pool = np.arange(distinct, dtype=np.uint64)
+    elif mode == 2:
+        pool = (np.arange(distinct, dtype=np.uint64) << np.uint64(40))
+    else:
+        pool = np.full(min(distinct, 3), np.uint64(2**64 - 1))
+    key = pool[rng.integers(0, pool.size, n)]
+    has = (rng.random(n) >= rng.choice([0.0, 0.01])).astype(np.uint8)
+    chunk = int(rng.choice([7, 100]))
+    rank = rng.permutation(n).astype(np.uint32)
+    t = lambda a, dt: torch.from_numpy(a.view(dt)).cuda()
+    ops = dedup.HipOps(ctx)
+    rep = ops.group_rows(t(key, np.int64), t(has, np.uint8), t(rank, np.int32), chunk, 0)
+    rep = rep.cpu().numpy().view(np.uint32)
+    key_r = np.empty_like(key)
+    has_r = np.empty_like(has)
+    key_r[rank] = key
+    has_r[rank] = has
+    ref = O.group_reps(key_r, has_r, chunk).astype(np.uint32)
+    np.testing.assert_array_equal(rep, ref[rank])
+
+
 @pytest.mark.parametrize("seed", range(20))
 def test_fuzz_checksum_batches(ctx, seed):
     """Tree hashing of random device-resident file batches (1..40 files,
