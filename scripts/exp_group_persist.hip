@@ -9,6 +9,8 @@
 //   GP5  persistent, <= 5 records per thread (the product's 4608-row LDS cap)
 //   GW   one workgroup per bucket; the inserting row stores its rank plainly,
 //        only duplicate rows take a ds_min (after a barrier)
+//   GR2/GR4  read-ahead probing: read 2 / 4 slots per round, CAS only the
+//        first empty-or-equal one (fewer probe rounds, more registers)
 // On the product's own records: 12.5 M rows (one-level) and 100 M rows (two-level).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_group_persist.hip -o build/exp_group_persist
 #include "../spacedrive_amd/csrc/dedup.hip"
@@ -226,6 +228,115 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_winner(
   }
 }
 
+
+// GR: the product kernel with read-ahead probing: each round a pending record
+// first READS kLook consecutive slots from its probe position (plain ds_read,
+// independent, issued together), picks the first that is empty or holds its
+// key, and only then issues the CAS there; a lost race continues from that
+// slot.  Linear probing's invariant is unchanged (a CAS only fills an empty
+// slot), but one round now covers kLook slots instead of one.
+template <int kLook>
+__global__ __launch_bounds__(kGroupThreads, 8) void k_group_lookahead(
+    const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P, ChunkOf chunk_of,
+    uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin, uint32_t* __restrict__ rep) {
+  __shared__ uint64_t lkey[kLdsSlots];
+  __shared__ uint32_t lmin[kLdsSlots];
+  __shared__ uint32_t special_min;
+  const uint32_t b = blockIdx.x;
+  const uint32_t start = offs[static_cast<uint64_t>(b) * P];
+  const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];
+  uint4 q[kPer];
+  load_bucket(rec, start, end, q);
+  if (end - start > kLdsCap) {
+    group_bucket(rec, start, end, q, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
+    return;
+  }
+  if (end == start) return;
+  for (uint32_t s = threadIdx.x; s < kLdsSlots; s += kGroupThreads) {
+    lkey[s] = kEmpty;
+    lmin[s] = 0xFFFFFFFFu;
+  }
+  if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
+  __syncthreads();
+  uint32_t h[kPer];
+  uint32_t live = 0, pend = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+    h[j] = lds_slot(k);
+    if (start + threadIdx.x + j * kGroupThreads < end) {
+      live |= 1u << j;
+      if (k == kEmpty)
+        atomicMin(&special_min, q[j].z);
+      else
+        pend |= 1u << j;
+    }
+  }
+  const uint32_t keyed = pend;
+  while (pend) {
+    // read-ahead: kLook slots per pending record
+    uint64_t look[kPer][kLook];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (!(pend >> j & 1u)) continue;
+      uint32_t s = h[j];
+#pragma unroll
+      for (int t = 0; t < kLook; ++t) {
+        look[j][t] = lkey[s];
+        s = next_slot(s);
+      }
+    }
+    uint64_t prev[kPer];
+    uint32_t skip = 0;  // records whose kLook slots all hold other keys
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      prev[j] = 0;
+      if (!(pend >> j & 1u)) continue;
+      const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+      // first slot (of the kLook read) that is empty or holds k; else the last
+      int t0 = kLook;
+#pragma unroll
+      for (int t = kLook - 1; t >= 0; --t)
+        if (look[j][t] == kEmpty || look[j][t] == k) t0 = t;
+      if (t0 == kLook) {  // all kLook slots hold other keys: skip past them
+#pragma unroll
+        for (int t = 0; t < kLook; ++t) h[j] = next_slot(h[j]);
+        skip |= 1u << j;
+        continue;
+      }
+#pragma unroll
+      for (int t = 0; t < kLook; ++t)
+        if (t < t0) h[j] = next_slot(h[j]);
+      if (look[j][t0] == k) {
+        prev[j] = k;  // already there: no CAS needed
+      } else {
+        prev[j] = atomicCAS(reinterpret_cast<unsigned long long*>(&lkey[h[j]]),
+                            static_cast<unsigned long long>(kEmpty),
+                            static_cast<unsigned long long>(k));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (!(pend >> j & 1u) || (skip >> j & 1u)) continue;
+      const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+      if (prev[j] == kEmpty || prev[j] == k) {
+        atomicMin(&lmin[h[j]], q[j].z);
+        pend &= ~(1u << j);
+      } else {
+        h[j] = next_slot(h[j]);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if (!(live >> j & 1u)) continue;
+    const uint32_t r = q[j].z;
+    const uint32_t f = (keyed >> j & 1u) ? lmin[h[j]] : special_min;
+    if (chunk_of(r) != chunk_of(f)) rep[q[j].w] = f;
+  }
+}
+
 template <typename F>
 float time_ms(F f, int reps) {
   hipEvent_t a, b;
@@ -277,8 +388,11 @@ void run(uint64_t n) {
   (void)hipDeviceSynchronize();
   uint8_t* w = static_cast<uint8_t*>(ws);
   const uint4* rec = reinterpret_cast<const uint4*>(w + L.rec);
-  const uint32_t* offs = reinterpret_cast<const uint32_t*>(w + (L.cbits ? L.fbase : L.hist));
-  const uint32_t P = L.cbits ? 1u : kPartBlocks, nb = 1u << L.bits;
+  // bucket starts: the fine-count paths (12-bit one-level, two-level) publish
+  // them with stride 1; narrower one-level partitions use the digit-major scan
+  const bool fine = L.cbits || L.bits == kStageBits;
+  const uint32_t* offs = reinterpret_cast<const uint32_t*>(w + (fine ? L.fbase : L.hist));
+  const uint32_t P = fine ? 1u : kPartBlocks, nb = 1u << L.bits;
   uint64_t* gkey = reinterpret_cast<uint64_t*>(w + L.gkey);
   uint32_t* gmin = reinterpret_cast<uint32_t*>(w + L.gmin);
   const ChunkOf c = ChunkOf::make(100);
@@ -288,15 +402,19 @@ void run(uint64_t n) {
   auto gp4 = [&] { k_group_persist<4><<<std::min(G, nb), kGroupThreads>>>(rec, offs, P, nb, c, gkey, gmin, rep2); };
   auto gp5 = [&] { k_group_persist<5><<<std::min(G, nb), kGroupThreads>>>(rec, offs, P, nb, c, gkey, gmin, rep2); };
   auto gw = [&] { k_group_winner<<<nb, kGroupThreads>>>(rec, offs, P, c, gkey, gmin, rep2); };
-  for (int v = 0; v < 4; ++v) {
+  auto gr2 = [&] { k_group_lookahead<2><<<nb, kGroupThreads>>>(rec, offs, P, c, gkey, gmin, rep2); };
+  auto gr4 = [&] { k_group_lookahead<4><<<nb, kGroupThreads>>>(rec, offs, P, c, gkey, gmin, rep2); };
+  for (int v = 0; v < 6; ++v) {
     (void)hipMemcpy(rep2, rank, 4 * n, hipMemcpyDeviceToDevice);  // rows keep their rank
     // (keyless rows: rank; the product's init_rep wrote rank for every row)
     if (v == 0) g0();
     else if (v == 1) gp4();
     else if (v == 2) gp5();
-    else gw();
+    else if (v == 3) gw();
+    else if (v == 4) gr2();
+    else gr4();
     (void)hipDeviceSynchronize();
-    printf("%s mismatches vs product grouping: %llu\n", v == 0 ? "G0 " : v == 1 ? "GP4" : v == 2 ? "GP5" : "GW ",
+    printf("%s mismatches vs product grouping: %llu\n", v == 0 ? "G0 " : v == 1 ? "GP4" : v == 2 ? "GP5" : v == 3 ? "GW " : v == 4 ? "GR2" : "GR4",
            (unsigned long long)mismatches(rep, rep2, n));
   }
   for (int r = 0; r < 2; ++r) {
@@ -304,6 +422,8 @@ void run(uint64_t n) {
     printf("GP4 persistent 4/thread  %.4f ms\n", time_ms(gp4, 9));
     printf("GP5 persistent 5/thread  %.4f ms\n", time_ms(gp5, 9));
     printf("GW  winner-store         %.4f ms\n", time_ms(gw, 9));
+    printf("GR2 read-ahead 2 slots   %.4f ms\n", time_ms(gr2, 9));
+    printf("GR4 read-ahead 4 slots   %.4f ms\n", time_ms(gr4, 9));
   }
   (void)hipFree(ws);
   (void)hipFree(key);
