@@ -491,6 +491,94 @@ __global__ __launch_bounds__(1024) void k_small(const uint8_t* __restrict__ aren
   }
 }
 
+// Host-staged latency path: ONE message of at most kHostStageMax bytes in
+// pinned host memory (the caller's staging slab), copied into LDS by the
+// workgroup (16 B per lane, eight loads in flight per lane: a couple of PCIe
+// round trips), hashed there exactly as k_small does, and the out_words
+// written straight into pinned host memory -- no H2D / D2H copy commands
+// around the launch (they are ~2/3 of a 4 KiB single-file call's fixed cost,
+// profiles/r2/latency/).
+constexpr uint32_t kHostStageChunks = kHostStageMax / B3_CHUNK_LEN;
+
+__global__ __launch_bounds__(1024) void k_small_host(const uint8_t* __restrict__ msg, uint32_t l,
+                                                     uint32_t out_words,
+                                                     uint32_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
+  __shared__ uint32_t cv[8][kHostStageChunks];
+  const uint32_t t = threadIdx.x;
+  {
+    const uint32_t nvec = (l + 15) / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(msg);
+    uint4* dst = reinterpret_cast<uint4*>(stage);
+    constexpr int kU = 8;
+    for (uint32_t i0 = t; i0 < nvec; i0 += kU * blockDim.x) {
+      uint4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        v[u] = i < nvec ? src[i] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        if (i < nvec) dst[i] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  const uint8_t* p = stage;
+  const uint32_t nch = n_chunks_of(l);
+  uint32_t c[8];
+  if (nch == 1) {
+    if (t == 0) {
+      b3_chunk(p, l, 0, B3_ROOT, c);
+      for (uint32_t w = 0; w < out_words; ++w) out[w] = c[w];
+    }
+    return;
+  }
+  if (t < nch) {
+    chunk_any(p, l, t, 0u, c);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
+  }
+  __syncthreads();
+  uint32_t cnt = nch;
+  while (cnt > 2) {
+    const uint32_t half = cnt >> 1;
+    uint32_t a[8], b[8];
+    const bool merge = t < half;
+    const bool carry = (cnt & 1u) && t == half;
+    if (merge) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        a[w] = cv[w][2 * t];
+        b[w] = cv[w][2 * t + 1];
+      }
+      b3_parent(c, a, b, 0u);
+    } else if (carry) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) c[w] = cv[w][cnt - 1];
+    }
+    __syncthreads();
+    if (merge || carry) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
+    }
+    __syncthreads();
+    cnt = half + (cnt & 1u);
+  }
+  if (t == 0) {
+    uint32_t a[8], b[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      a[w] = cv[w][0];
+      b[w] = cv[w][1];
+    }
+    b3_parent(c, a, b, B3_ROOT);
+    for (uint32_t w = 0; w < out_words; ++w) out[w] = c[w];
+  }
+}
+
 }  // namespace
 
 hipError_t batch_hash_launch(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* off,
@@ -541,6 +629,25 @@ hipError_t small_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
   KScope k(timer, "cas_small", s);
   k_small<<<n, threads, 0, s>>>(arena, off, len, max_len, out_words,
                                 reinterpret_cast<uint32_t*>(out), status);
+  return hipGetLastError();
+}
+
+// One message in pinned host memory (16-B aligned, readable past `len` up to
+// the next 16 bytes), digest words written to pinned host memory `h_out`.
+hipError_t small_host_launch(const uint8_t* h_msg, uint32_t len, uint32_t out_words,
+                             uint8_t* h_out, hipStream_t s, KTimer* timer) {
+  if (len > kHostStageMax || (reinterpret_cast<uintptr_t>(h_msg) & 15u)) return hipErrorInvalidValue;
+  const uint32_t nch = len <= B3_CHUNK_LEN ? 1u : (len + B3_CHUNK_LEN - 1) / B3_CHUNK_LEN;
+  const uint32_t threads = std::max<uint32_t>(256, (nch + 63) / 64 * 64);
+  const size_t lds = (static_cast<size_t>(len) + 15) / 16 * 16 + 16;
+  static const bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(k_small_host),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               static_cast<int>(kHostStageMax + 16)) == hipSuccess;
+  }();
+  if (!attr) return hipErrorInvalidValue;
+  KScope k(timer, "cas_small_host", s);
+  k_small_host<<<1, threads, lds, s>>>(h_msg, len, out_words, reinterpret_cast<uint32_t*>(h_out));
   return hipGetLastError();
 }
 

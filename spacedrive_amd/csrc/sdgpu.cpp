@@ -205,8 +205,13 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     for (uint32_t j = 0; j < cnt; ++j) max_msg = std::max(max_msg, len[j]);
     const bool small = cnt <= kSmallBatch && max_msg <= SMALL_MAX_BYTES;
     const size_t prefix = L.len + 4ull * cnt;
+    // one message (the single-file callers): read from the pinned slab and
+    // written back into it by the kernel itself, no copy commands
+    const bool host1 = small && cnt == 1 && len[0] <= kHostStageMax;
     bool ok;
-    if (small && prefix <= (size_t(8) << 20)) {
+    if (host1) {
+      ok = small_host_launch(hb + off[0], len[0], 2, hb + L.out, s, c->kt()) == hipSuccess;
+    } else if (small && prefix <= (size_t(8) << 20)) {
       ok = hipMemcpyAsync(db, hb, prefix, hipMemcpyHostToDevice, s) == hipSuccess;
     } else {
       ok = hipMemcpyAsync(db, hb, pos, hipMemcpyHostToDevice, s) == hipSuccess &&
@@ -217,14 +222,15 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     }
     const uint64_t* d_off = reinterpret_cast<const uint64_t*>(db + L.off);
     const uint32_t* d_len = reinterpret_cast<const uint32_t*>(db + L.len);
-    if (ok)
+    if (ok && !host1)
       ok = (small ? small_hash_launch(db, d_off, d_len, cnt, kStageMaxMsg,
                                       max_msg <= kChunkLen ? 1u : (max_msg + kChunkLen - 1) / kChunkLen,
                                       2, db + L.out, nullptr, s, c->kt())
                   : batch_hash_launch(db, L.arena_cap, d_off, d_len, cnt, kStageMaxMsg, 2,
                                       db + L.out, nullptr, w, s, c->kt())) == hipSuccess;
     if (!ok ||
-        hipMemcpyAsync(hb + L.out, db + L.out, 8ull * cnt, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (!host1 &&
+         hipMemcpyAsync(hb + L.out, db + L.out, 8ull * cnt, hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipEventRecord(sl.done, s) != hipSuccess) {
       rc = -EIO;
       break;
@@ -689,6 +695,17 @@ int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
         meta[0] = 0;
         meta[1] = static_cast<uint64_t>(got);
         const uint32_t nch = got <= 1024 ? 1u : static_cast<uint32_t>((got + 1023) / 1024);
+        if (static_cast<uint64_t>(got) <= kHostStageMax) {
+          // the whole file hashed from the pinned buffer, digest written back
+          // into it by the kernel: no copy commands
+          uint8_t* hout = hb + cap + 64;
+          if (small_host_launch(hb, static_cast<uint32_t>(got), 8, hout, s, c->kt()) != hipSuccess ||
+              hipStreamSynchronize(s) != hipSuccess)
+            rc = -EIO;
+          else
+            memcpy(out.data(), hout, 32);
+          break;
+        }
         if (hipMemcpyAsync(db, hb, static_cast<size_t>(got), hipMemcpyHostToDevice, s) != hipSuccess ||
             hipMemcpyAsync(db + cap, hb + cap, 16, hipMemcpyHostToDevice, s) != hipSuccess ||
             small_hash_launch(db, reinterpret_cast<const uint64_t*>(db + cap),
