@@ -491,21 +491,26 @@ __global__ __launch_bounds__(1024) void k_small(const uint8_t* __restrict__ aren
   }
 }
 
-// Host-staged latency path: ONE message of at most kHostStageMax bytes in
-// pinned host memory (the caller's staging slab), copied into LDS by the
-// workgroup (16 B per lane, eight loads in flight per lane: a couple of PCIe
+// Host-staged latency path: a few messages of at most kHostStageMax bytes in
+// pinned host memory (the caller's staging slab), one workgroup each, copied
+// into LDS by the workgroup (16 B per lane, eight loads in flight per lane: a couple of PCIe
 // round trips), hashed there exactly as k_small does, and the out_words
 // written straight into pinned host memory -- no H2D / D2H copy commands
 // around the launch (they are ~2/3 of a 4 KiB single-file call's fixed cost,
 // profiles/r2/latency/).
 constexpr uint32_t kHostStageChunks = kHostStageMax / B3_CHUNK_LEN;
 
-__global__ __launch_bounds__(1024) void k_small_host(const uint8_t* __restrict__ msg, uint32_t l,
+__global__ __launch_bounds__(1024) void k_small_host(const uint8_t* __restrict__ arena,
+                                                     const uint64_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ len,
                                                      uint32_t out_words,
-                                                     uint32_t* __restrict__ out) {
+                                                     uint32_t* __restrict__ out_all) {
   extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
   __shared__ uint32_t cv[8][kHostStageChunks];
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, m = blockIdx.x;
+  const uint8_t* __restrict__ msg = arena + off[m];
+  const uint32_t l = len[m];
+  uint32_t* __restrict__ out = out_all + static_cast<uint64_t>(m) * out_words;
   {
     const uint32_t nvec = (l + 15) / 16;
     const uint4* src = reinterpret_cast<const uint4*>(msg);
@@ -632,14 +637,18 @@ hipError_t small_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
   return hipGetLastError();
 }
 
-// One message in pinned host memory (16-B aligned, readable past `len` up to
-// the next 16 bytes), digest words written to pinned host memory `h_out`.
-hipError_t small_host_launch(const uint8_t* h_msg, uint32_t len, uint32_t out_words,
-                             uint8_t* h_out, hipStream_t s, KTimer* timer) {
-  if (len > kHostStageMax || (reinterpret_cast<uintptr_t>(h_msg) & 15u)) return hipErrorInvalidValue;
-  const uint32_t nch = len <= B3_CHUNK_LEN ? 1u : (len + B3_CHUNK_LEN - 1) / B3_CHUNK_LEN;
+// Messages in pinned host memory (16-B aligned offsets, readable past `len`
+// up to the next 16 bytes; off / len host-visible too), digest words written
+// to pinned host memory `h_out` (out_words per message).
+hipError_t small_host_launch(const uint8_t* h_arena, const uint64_t* h_off, const uint32_t* h_len,
+                             uint32_t n, uint32_t max_len, uint32_t out_words, uint8_t* h_out,
+                             hipStream_t s, KTimer* timer) {
+  if (n == 0) return hipSuccess;
+  if (max_len > kHostStageMax || (reinterpret_cast<uintptr_t>(h_arena) & 15u))
+    return hipErrorInvalidValue;
+  const uint32_t nch = max_len <= B3_CHUNK_LEN ? 1u : (max_len + B3_CHUNK_LEN - 1) / B3_CHUNK_LEN;
   const uint32_t threads = std::max<uint32_t>(256, (nch + 63) / 64 * 64);
-  const size_t lds = (static_cast<size_t>(len) + 15) / 16 * 16 + 16;
+  const size_t lds = (static_cast<size_t>(max_len) + 15) / 16 * 16 + 16;
   static const bool attr = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(k_small_host),
                                hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -647,7 +656,8 @@ hipError_t small_host_launch(const uint8_t* h_msg, uint32_t len, uint32_t out_wo
   }();
   if (!attr) return hipErrorInvalidValue;
   KScope k(timer, "cas_small_host", s);
-  k_small_host<<<1, threads, lds, s>>>(h_msg, len, out_words, reinterpret_cast<uint32_t*>(h_out));
+  k_small_host<<<n, threads, lds, s>>>(h_arena, h_off, h_len, out_words,
+                                       reinterpret_cast<uint32_t*>(h_out));
   return hipGetLastError();
 }
 

@@ -66,12 +66,14 @@ hipError_t small_hash_launch(const uint8_t* arena, const uint64_t* off, const ui
                              uint32_t n, uint32_t max_len, uint32_t max_chunks,
                              uint32_t out_words, uint8_t* out, int32_t* status, hipStream_t s,
                              KTimer* timer = nullptr);
-// One message of at most kHostStageMax bytes read straight from pinned host
-// memory (16-B aligned) and its digest words written straight to pinned host
-// memory: the single-file callers' path without copy commands.
+// A few messages of at most kHostStageMax bytes read straight from pinned
+// host memory (16-B aligned offsets; off / len in pinned memory too), one
+// workgroup each, digest words written straight to pinned host memory: the
+// single-file and small-batch callers' path without copy commands.
 constexpr uint32_t kHostStageMax = 112u * 1024u;
-hipError_t small_host_launch(const uint8_t* h_msg, uint32_t len, uint32_t out_words,
-                             uint8_t* h_out, hipStream_t s, KTimer* timer = nullptr);
+hipError_t small_host_launch(const uint8_t* h_arena, const uint64_t* h_off, const uint32_t* h_len,
+                             uint32_t n, uint32_t max_len, uint32_t out_words, uint8_t* h_out,
+                             hipStream_t s, KTimer* timer = nullptr);
 
 // ---- tree BLAKE3 of large segments (file_checksum, K2/K3) -------------------
 // TreeSeg: tree_plan.hpp

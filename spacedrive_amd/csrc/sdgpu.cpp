@@ -205,12 +205,13 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     for (uint32_t j = 0; j < cnt; ++j) max_msg = std::max(max_msg, len[j]);
     const bool small = cnt <= kSmallBatch && max_msg <= SMALL_MAX_BYTES;
     const size_t prefix = L.len + 4ull * cnt;
-    // one message (the single-file callers): read from the pinned slab and
-    // written back into it by the kernel itself, no copy commands
-    const bool host1 = small && cnt == 1 && len[0] <= kHostStageMax;
+    // a few cas messages (the single-file and small-batch callers): read from
+    // the pinned slab and the ids written back into it by the kernel itself,
+    // no copy commands
+    const bool host1 = small && max_msg <= kHostStageMax;
     bool ok;
     if (host1) {
-      ok = small_host_launch(hb + off[0], len[0], 2, hb + L.out, s, c->kt()) == hipSuccess;
+      ok = small_host_launch(hb, off, len, cnt, max_msg, 2, hb + L.out, s, c->kt()) == hipSuccess;
     } else if (small && prefix <= (size_t(8) << 20)) {
       ok = hipMemcpyAsync(db, hb, prefix, hipMemcpyHostToDevice, s) == hipSuccess;
     } else {
@@ -699,7 +700,11 @@ int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
           // the whole file hashed from the pinned buffer, digest written back
           // into it by the kernel: no copy commands
           uint8_t* hout = hb + cap + 64;
-          if (small_host_launch(hb, static_cast<uint32_t>(got), 8, hout, s, c->kt()) != hipSuccess ||
+          uint64_t* hoff = reinterpret_cast<uint64_t*>(hb + cap + 128);  // {0}, then the length
+          hoff[0] = 0;
+          hoff[1] = static_cast<uint64_t>(got);
+          if (small_host_launch(hb, hoff, reinterpret_cast<const uint32_t*>(hoff + 1), 1,
+                                static_cast<uint32_t>(got), 8, hout, s, c->kt()) != hipSuccess ||
               hipStreamSynchronize(s) != hipSuccess)
             rc = -EIO;
           else
