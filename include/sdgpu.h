@@ -136,6 +136,13 @@ int sdgpu_checksum_batch_device(sdgpu_ctx *ctx, const uint8_t *const *d_files,
  * of a whole message (chunk_offset 0). */
 int sdgpu_subtree_device(sdgpu_ctx *ctx, const uint8_t *d_bytes, uint64_t len,
                          uint64_t chunk_offset, int root, uint8_t *d_out32, void *stream);
+/* Digest of a message from the chaining values of its consecutive aligned
+ * subtree slices (sdgpu_subtree_device with root=0): d_cvs is device [n][32]
+ * (16-B aligned), n >= 2, every slice of the same power-of-two chunk count
+ * except a shorter last one.  One large file split over several GPUs: each
+ * GPU computes its slices' CVs, one GPU combines them. */
+int sdgpu_combine_subtrees_device(sdgpu_ctx *ctx, const uint8_t *d_cvs, uint64_t n,
+                                  uint8_t *d_out32, void *stream);
 /* Path-based drop-in for file_checksum(path): streams the file in 64 MiB
  * power-of-two slices through double-buffered pinned memory; out_hex = 64
  * lowercase hex chars + NUL. */

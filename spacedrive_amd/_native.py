@@ -55,6 +55,7 @@ def _proto(L):
         "sdgpu_checksum": (i32, [ctx, c_vp, u64, c_vp]),
         "sdgpu_checksum_batch_device": (i32, [ctx, c_vp, c_vp, u32, c_vp, c_vp]),
         "sdgpu_subtree_device": (i32, [ctx, c_vp, u64, u64, i32, c_vp, c_vp]),
+        "sdgpu_combine_subtrees_device": (i32, [ctx, c_vp, u64, c_vp, c_vp]),
         "sdgpu_checksum_files": (i32, [ctx, c_vp, u32, c_vp, c_vp]),
         "sdgpu_file_checksum": (i32, [ctx, ctypes.c_char_p, ctypes.c_char_p]),
         "sdgpu_dedup": (i32, [ctx, c_vp, c_vp, u32, u32, c_vp]),

@@ -610,6 +610,18 @@ int sdgpu_subtree_device(sdgpu_ctx* c, const uint8_t* d_bytes, uint64_t len, uin
   return tree_launch(c, &seg, 1, false, d_out32, s);
 }
 
+int sdgpu_combine_subtrees_device(sdgpu_ctx* c, const uint8_t* d_cvs, uint64_t n, uint8_t* d_out32,
+                                  void* stream) {
+  if (!c || !d_cvs || !d_out32 || n < 2 || reinterpret_cast<uintptr_t>(d_cvs) % 16) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  // the slices' CVs are the leaves of the tree's top levels (file_checksum's
+  // slice fold, hash.rs:10-24 as one message)
+  const TreeSeg seg{d_cvs, n, 0, 1u, 0};
+  return tree_launch(c, &seg, 1, true, d_out32, s);
+}
+
 namespace {
 
 // BLAKE3 of a host buffer through the tree kernels (context lock held).

@@ -98,3 +98,19 @@ def subtree_device(data, chunk_offset: int, root: bool, out=None, ctx=None, stre
                                        1 if root else 0, out.data_ptr(), s),
           "sdgpu_subtree_device")
     return out
+
+
+def combine_subtrees_device(cvs, out=None, ctx=None, stream=None):
+    """Digest of a message from the [n, 32] chaining values of its consecutive
+    aligned subtree slices (sdgpu_combine_subtrees_device): the last step of a
+    file checksummed slice by slice on several GPUs."""
+    import torch
+    ctx = ctx or default_context(cvs.device.index)
+    cvs = cvs.contiguous()
+    if out is None:
+        out = torch.empty(32, dtype=torch.uint8, device=cvs.device)
+    s = stream if stream is not None else torch.cuda.current_stream(cvs.device).cuda_stream
+    check(ctx.lib.sdgpu_combine_subtrees_device(ctx.h, cvs.data_ptr(), cvs.shape[0],
+                                                out.data_ptr(), s),
+          "sdgpu_combine_subtrees_device")
+    return out

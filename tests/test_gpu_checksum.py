@@ -54,6 +54,37 @@ def test_subtree_slices_compose(ctx):
     assert bytes(d.cpu().numpy()) == O.blake3(whole.cpu().numpy(), threads=16)
 
 
+@pytest.mark.parametrize("slice_chunks,n_slices,tail", [(1 << 16, 4, 12345), (1 << 10, 7, 0),
+                                                       (1 << 12, 2, 1), (16, 3, 1000)])
+def test_file_split_over_contexts(ctx, slice_chunks, n_slices, tail):
+    """One file checksummed as SURVEY 8(e) splits it over GPUs: aligned
+    power-of-two slices hashed to chaining values on different contexts
+    (separate workspaces and streams, as separate GPUs would), the CVs gathered
+    and combined on one: equal to the whole file's digest and the oracle's."""
+    import torch
+    from spacedrive_amd import corpus, validation
+    from spacedrive_amd._native import Context
+    others = [Context(0) for _ in range(3)]
+    try:
+        n = n_slices * slice_chunks * 1024 + tail
+        whole = corpus.synth_file_device(91 + n_slices, n, ctx=ctx)
+        step = slice_chunks * 1024
+        cvs = torch.empty((n_slices + (1 if tail else 0), 32), dtype=torch.uint8, device="cuda")
+        for i in range(cvs.shape[0]):
+            c = others[i % len(others)]
+            part = whole[i * step:min(n, (i + 1) * step)]
+            validation.subtree_device(part, i * slice_chunks, False, out=cvs[i], ctx=c)
+        torch.cuda.synchronize()
+        d = validation.combine_subtrees_device(cvs, ctx=ctx)
+        full = validation.subtree_device(whole, 0, True, ctx=ctx)
+        torch.cuda.synchronize()
+        assert torch.equal(d, full)
+        assert bytes(d.cpu().numpy()) == O.blake3(whole.cpu().numpy(), threads=16)
+    finally:
+        for c in others:
+            c.close()
+
+
 @pytest.mark.parametrize("n", [0, 1, 1 << 20, 64 << 20, (64 << 20) + 1, (128 << 20),
                                (130 << 20) + 5, 3 * (64 << 20) - 1])
 def test_file_checksum_path(ctx, tmp_path, n):
