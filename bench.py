@@ -379,12 +379,33 @@ class Runner:
         if index is not None:
             index.clear()
 
+        # N = 1: every step's keys and reps are kept (a device copy of 12 B per
+        # row, next to the step's ~42 KB of windows per file) so
+        # the run can be checked after timing against ONE grouping of all its
+        # rows: batching through the Object index must equal the whole-run rule
+        verify = W == 1 and index is not None
+        if verify:
+            keys_all = torch.empty(nsteps * n, dtype=torch.int64, device=self.dev)
+            reps_all = torch.empty(nsteps * n, dtype=torch.int32, device=self.dev)
+
         def run():
             for s in range(nsteps):
                 rep = step(s)
+                if verify:
+                    keys_all[s * n:(s + 1) * n].copy_(out.view(torch.int64).view(-1))
+                    reps_all[s * n:(s + 1) * n].copy_(rep)
             self._staged_last = rep
 
         t = self.timed(run, 1, 0)
+        whole = None
+        if verify:
+            has_all = has.repeat(nsteps)
+            rank_all = torch.arange(nsteps * n, dtype=torch.int64, device=self.dev).to(torch.int32)
+            ref = self.ops.group_rows(keys_all, has_all, rank_all, 100, 0)
+            whole = {"rows": nsteps * n, "mismatches": int((ref != reps_all).sum()),
+                     "note": "reps of the batched run (Object index) vs one grouping of all "
+                             "its rows on the GPU (the canonical rule over global ranks)"}
+            del keys_all, reps_all, has_all, rank_all, ref
         assert int(st.abs().sum()) == 0
         last = self._staged_last
         linked_last = int((last != ranks[nsteps - 1]).sum())
@@ -400,6 +421,7 @@ class Runner:
                 "window_GBps_per_gpu": per_gpu_Bps / 1e9,
                 "h2d_peak_GBps": peak / 1e9, "h2d_frac": per_gpu_Bps / peak,
                 "index_keys_rank0": distinct, "linked_rows_last_step_rank0": linked_last,
+                "verify_whole_run": whole,
                 "config": {"workload": f"config5: identifier run over {files} files "
                                        f"({nsteps} steps x {n} files/GPU x {W} GPU), windows in "
                                        "pinned host memory, staged H2D (3-slab ring) + K1 + "
