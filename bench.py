@@ -303,7 +303,8 @@ class Runner:
         res["roofline_inputs"] = {"chunk_blocks": blk, "parents": par, "leaf_compressions": leaves,
                                   "fold_compressions": fold, "avg_leaves_s": avg_leaves,
                                   "bytes": int(lens.sum())}
-        self._cpu_sample = (arena, off, ln, min(n, self.args.cpu_files))
+        self._cpu_sample = (arena, off, ln, min(n, self.args.cpu_files),
+                            out[:min(n, self.args.cpu_files)].cpu().numpy())
         return res
 
     # ---------------------------------------------------------------- config 5
@@ -771,7 +772,7 @@ class Runner:
 
     def cpu_baseline(self):
         from oracle import oracle as O
-        arena, off, ln, m = self._cpu_sample
+        arena, off, ln, m, gpu_cas8 = self._cpu_sample
         h_off = off[:m].cpu().numpy().view(np.uint64)
         h_len = ln[:m].cpu().numpy().view(np.uint32)
         end = int(h_off[-1] + h_len[-1])
@@ -783,8 +784,11 @@ class Runner:
         O.cas_batch_simd(host, h_off[:100], h_len[:100], threads)  # warm
         # repeat the sample until about 10 s of CPU work has been timed
         t0 = time.perf_counter()
-        O.cas_batch_simd(host, h_off, h_len, threads)
+        cpu_cas8 = O.cas_batch_simd(host, h_off, h_len, threads)
         t1 = time.perf_counter() - t0
+        # the headline step's GPU cas ids of the same files (parity in the bench)
+        sample_mism = int(np.count_nonzero(np.any(cpu_cas8 != gpu_cas8, axis=1)))
+        assert sample_mism == 0, f"config 2: {sample_mism} GPU cas ids differ from the CPU port"
         reps = int(min(60, max(1, np.ceil(self.args.cpu_seconds / max(t1, 1e-3)))))
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -858,7 +862,7 @@ class Runner:
                         ts.append(time.perf_counter() - t0)
                     single[f"{fn_name}_{name}_us"] = float(np.median(ts) * 1e6)
         return {"value": reps * m / dt, "unit": "files/s", "cores": threads, "kind": "port",
-                "cores_note": cores_note,
+                "cores_note": cores_note, "gpu_cas_id_mismatches": sample_mism,
                 "value_1thread": one, "scalar_value": scalar,
                 "config1_dir": dir_res, "config3_checksum": ck,
                 "single_file_1thread": single,
