@@ -41,6 +41,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "b3_device.hpp"
 #include "internal.hpp"
@@ -649,12 +650,19 @@ hipError_t small_host_launch(const uint8_t* h_arena, const uint64_t* h_off, cons
   const uint32_t nch = max_len <= B3_CHUNK_LEN ? 1u : (max_len + B3_CHUNK_LEN - 1) / B3_CHUNK_LEN;
   const uint32_t threads = std::max<uint32_t>(256, (nch + 63) / 64 * 64);
   const size_t lds = (static_cast<size_t>(max_len) + 15) / 16 * 16 + 16;
-  static const bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(k_small_host),
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               static_cast<int>(kHostStageMax + 16)) == hipSuccess;
-  }();
-  if (!attr) return hipErrorInvalidValue;
+  // the dynamic-LDS limit is a per-device attribute of the loaded kernel: set
+  // once for each device this process launches on
+  static std::atomic<uint64_t> attr_set{0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint64_t bit = 1ull << (dev & 63);
+  if (!(attr_set.load(std::memory_order_acquire) & bit)) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_small_host),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             static_cast<int>(kHostStageMax + 16));
+    if (e != hipSuccess) return e;
+    attr_set.fetch_or(bit, std::memory_order_release);
+  }
   KScope k(timer, "cas_small_host", s);
   k_small_host<<<n, threads, lds, s>>>(h_arena, h_off, h_len, out_words,
                                        reinterpret_cast<uint32_t*>(h_out));
