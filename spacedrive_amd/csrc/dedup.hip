@@ -306,13 +306,18 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
                          in.row_of(q, u));
     }
     lds_barrier();
-    if (threadIdx.x == 0) {
-      uint32_t run = 0;
-      for (uint32_t b = 0; b < nbins; ++b) {
-        base[b] = run;
-        run += cnt[b];
+    if (threadIdx.x < 64) {  // the (<= 64) run starts: one wave's shuffle scan
+      static_assert(kRunMaxBins <= 64, "one wave scans the run starts");
+      const uint32_t lane = threadIdx.x;
+      const uint32_t v = lane < nbins ? cnt[lane] : 0u;
+      uint32_t inc = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d);
+        if (lane >= static_cast<uint32_t>(d)) inc += o;
       }
-      base[nbins] = run;
+      if (lane < nbins) base[lane] = inc - v;
+      if (lane == nbins - 1) base[nbins] = inc;
     }
     lds_barrier();
 #pragma unroll
