@@ -105,14 +105,17 @@ __global__ __launch_bounds__(kThreads) void k_orphan_write(const int32_t* __rest
     if (lane == 0) off[k][w] = __popcll(b);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // (k, wave) order is list order
-    uint32_t run = offs[blockIdx.x];
-    for (int k = 0; k < kORows; ++k)
-      for (int v = 0; v < kOWaves; ++v) {
-        const uint32_t a = off[k][v];
-        off[k][v] = run;
-        run += a;
-      }
+  static_assert(kORows * kOWaves == 64, "one wave scans the (row step, wave) counts");
+  if (threadIdx.x < 64) {  // (k, wave) order -- k-major, the array's order -- is list order
+    uint32_t* f = &off[0][0];
+    const uint32_t a = f[lane];
+    uint32_t inc = a;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t x = __shfl_up(inc, d);
+      if (lane >= static_cast<uint32_t>(d)) inc += x;
+    }
+    f[lane] = offs[blockIdx.x] + inc - a;
   }
   __syncthreads();
 #pragma unroll

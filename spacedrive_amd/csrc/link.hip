@@ -114,16 +114,22 @@ __global__ __launch_bounds__(kThreads) void k_link_write(
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // (k, wave) order is row order
-    uint32_t rc = cnt[blockIdx.x], rl = cnt[nb + blockIdx.x] - total_c;
-    for (int k = 0; k < kRows; ++k)
-      for (int v = 0; v < kWaves; ++v) {
-        const uint32_t a = oc[k][v], b = ol[k][v];
-        oc[k][v] = rc;
-        ol[k][v] = rl;
-        rc += a;
-        rl += b;
+  static_assert(kRows * kWaves == 64, "one wave scans the (row step, wave) counts");
+  if (threadIdx.x < 64) {  // (k, wave) order -- k-major, the array's order -- is row order
+    uint32_t* fc = &oc[0][0];
+    uint32_t* fl = &ol[0][0];
+    const uint32_t a = fc[lane], b = fl[lane];
+    uint32_t ic = a, il = b;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t xc = __shfl_up(ic, d), xl = __shfl_up(il, d);
+      if (lane >= static_cast<uint32_t>(d)) {
+        ic += xc;
+        il += xl;
       }
+    }
+    fc[lane] = cnt[blockIdx.x] + ic - a;
+    fl[lane] = cnt[nb + blockIdx.x] - total_c + il - b;
   }
   __syncthreads();
 #pragma unroll
