@@ -17,8 +17,9 @@ inline uint32_t tiles_for(uint64_t n) { return static_cast<uint32_t>((n + kTile 
 __global__ __launch_bounds__(kThreads) static void k_tiles(const uint32_t* __restrict__ in,
                                                            uint64_t n, uint32_t* __restrict__ out,
                                                            uint32_t* __restrict__ tile_sums) {
-  __shared__ uint32_t sh[kThreads];
+  __shared__ uint32_t wsum[kThreads / 64];
   const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x * 4;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
   uint32_t v[4];
   uint32_t s = 0;
 #pragma unroll
@@ -26,21 +27,29 @@ __global__ __launch_bounds__(kThreads) static void k_tiles(const uint32_t* __res
     v[k] = base + k < n ? in[base + k] : 0u;
     s += v[k];
   }
-  sh[threadIdx.x] = s;
-  __syncthreads();
-  for (int d = 1; d < kThreads; d <<= 1) {
-    const uint32_t t = threadIdx.x >= d ? sh[threadIdx.x - d] : 0u;
-    __syncthreads();
-    sh[threadIdx.x] += t;
-    __syncthreads();
+  // wave shuffles, then the 4 wave totals (one barrier instead of 16)
+  uint32_t inc = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d);
+    if (lane >= static_cast<uint32_t>(d)) inc += o;
   }
-  uint32_t run = sh[threadIdx.x] - s;
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kThreads / 64; ++k) {
+    const uint32_t x = wsum[k];
+    pre += static_cast<uint32_t>(k) < w ? x : 0u;
+    tot += x;
+  }
+  uint32_t run = pre + inc - s;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (base + k < n) out[base + k] = run;
     run += v[k];
   }
-  if (threadIdx.x == kThreads - 1) tile_sums[blockIdx.x] = sh[threadIdx.x];
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
 }
 
 // Single block of kSumThreads: exclusive scan of the tile sums (wave shuffles,
