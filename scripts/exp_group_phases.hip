@@ -155,8 +155,11 @@ int main(int argc, char** argv) {
   (void)hipDeviceSynchronize();
   uint8_t* w = static_cast<uint8_t*>(ws);
   const uint4* rec = reinterpret_cast<const uint4*>(w + L.rec);
-  const uint32_t* hist = reinterpret_cast<const uint32_t*>(w + L.hist);
-  const uint32_t P = bucket_part_blocks(), nb = 1u << L.bits;
+  // bucket starts: the fine-count paths (12-bit one-level, two-level) publish
+  // them with stride 1 (round 2); narrower partitions use the digit-major scan
+  const bool fine = L.cbits || L.bits == kStageBits;
+  const uint32_t* hist = reinterpret_cast<const uint32_t*>(w + (fine ? L.fbase : L.hist));
+  const uint32_t P = fine ? 1u : bucket_part_blocks(), nb = 1u << L.bits;
   const ChunkOf c = ChunkOf::make(100);
   printf("n %llu buckets %u\n", (unsigned long long)n, nb);
   printf("full grouping          %.4f ms\n",
