@@ -18,6 +18,11 @@ using namespace sdgpu;
 
 namespace {
 
+// linear probing, as the product kernel used before round 2's double hashing
+__device__ __forceinline__ uint32_t lin_next(uint32_t h) {
+  return h + 1 == kLdsSlots ? 0u : h + 1;
+}
+
 __global__ void k_rows(uint64_t* key, uint32_t* rank, uint64_t n, uint64_t distinct) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
     const uint64_t j = (i * 0x9E3779B1ull) % n;  // a permutation of the rows (n odd multiple ok)
@@ -75,7 +80,7 @@ __global__ __launch_bounds__(kGroupThreads, 8) void g0(const uint4* __restrict__
         atomicMin(&lmin[h[j]], q[j].z);
         pend &= ~(1u << j);
       } else {
-        h[j] = next_slot(h[j]);
+        h[j] = lin_next(h[j]);
       }
     }
   }

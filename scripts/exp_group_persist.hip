@@ -11,6 +11,7 @@
 //        only duplicate rows take a ds_min (after a barrier)
 //   GR2/GR4  read-ahead probing: read 2 / 4 slots per round, CAS only the
 //        first empty-or-equal one (fewer probe rounds, more registers)
+//   GD   double hashing instead of linear probing (shorter longest chains)
 // On the product's own records: 12.5 M rows (one-level) and 100 M rows (two-level).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_group_persist.hip -o build/exp_group_persist
 #include "../spacedrive_amd/csrc/dedup.hip"
@@ -22,6 +23,11 @@
 using namespace sdgpu;
 
 namespace {
+
+// linear probing, as the product kernel used before round 2's double hashing
+__device__ __forceinline__ uint32_t lin_next(uint32_t h) {
+  return h + 1 == kLdsSlots ? 0u : h + 1;
+}
 
 __global__ void k_rows(uint64_t* key, uint32_t* rank, uint8_t* has, uint64_t n, uint64_t distinct) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
@@ -87,7 +93,7 @@ __device__ __forceinline__ void group_lds(const uint4 (&q)[kP], uint32_t start, 
         atomicMin(&lmin[h[j]], q[j].z);
         pend &= ~(1u << j);
       } else {
-        h[j] = next_slot(h[j]);
+        h[j] = lin_next(h[j]);
       }
     }
   }
@@ -208,7 +214,7 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_winner(
         dup |= 1u << j;
         pend &= ~(1u << j);
       } else {
-        h[j] = next_slot(h[j]);
+        h[j] = lin_next(h[j]);
       }
     }
   }
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_lookahead(
 #pragma unroll
       for (int t = 0; t < kLook; ++t) {
         look[j][t] = lkey[s];
-        s = next_slot(s);
+        s = lin_next(s);
       }
     }
     uint64_t prev[kPer];
@@ -300,13 +306,13 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_lookahead(
         if (look[j][t] == kEmpty || look[j][t] == k) t0 = t;
       if (t0 == kLook) {  // all kLook slots hold other keys: skip past them
 #pragma unroll
-        for (int t = 0; t < kLook; ++t) h[j] = next_slot(h[j]);
+        for (int t = 0; t < kLook; ++t) h[j] = lin_next(h[j]);
         skip |= 1u << j;
         continue;
       }
 #pragma unroll
       for (int t = 0; t < kLook; ++t)
-        if (t < t0) h[j] = next_slot(h[j]);
+        if (t < t0) h[j] = lin_next(h[j]);
       if (look[j][t0] == k) {
         prev[j] = k;  // already there: no CAS needed
       } else {
@@ -323,10 +329,91 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_lookahead(
         atomicMin(&lmin[h[j]], q[j].z);
         pend &= ~(1u << j);
       } else {
-        h[j] = next_slot(h[j]);
+        h[j] = lin_next(h[j]);
       }
     }
   }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if (!(live >> j & 1u)) continue;
+    const uint32_t r = q[j].z;
+    const uint32_t f = (keyed >> j & 1u) ? lmin[h[j]] : special_min;
+    if (chunk_of(r) != chunk_of(f)) rep[q[j].w] = f;
+  }
+}
+
+
+// GD: the product kernel with double hashing in place of linear probing: a
+// record's probe step is 1 + 6 * ((h >> 40) % 1024) (coprime with the 6144
+// slots), so probe sequences of different keys no longer run in clusters and
+// a wave's longest probe chain -- the number of CAS rounds it makes -- shrinks.
+__global__ __launch_bounds__(kGroupThreads, 8) void k_group_double(
+    const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P, ChunkOf chunk_of,
+    uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin, uint32_t* __restrict__ rep,
+    uint32_t* __restrict__ rounds_max) {
+  __shared__ uint64_t lkey[kLdsSlots];
+  __shared__ uint32_t lmin[kLdsSlots];
+  __shared__ uint32_t special_min;
+  const uint32_t b = blockIdx.x;
+  const uint32_t start = offs[static_cast<uint64_t>(b) * P];
+  const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];
+  uint4 q[kPer];
+  load_bucket(rec, start, end, q);
+  if (end - start > kLdsCap) {
+    group_bucket(rec, start, end, q, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
+    return;
+  }
+  if (end == start) return;
+  for (uint32_t s = threadIdx.x; s < kLdsSlots; s += kGroupThreads) {
+    lkey[s] = kEmpty;
+    lmin[s] = 0xFFFFFFFFu;
+  }
+  if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
+  __syncthreads();
+  uint32_t h[kPer], step[kPer];
+  uint32_t live = 0, pend = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+    h[j] = lds_slot(k);
+    step[j] = 1u + 6u * static_cast<uint32_t>((k >> 40) & 1023u);
+    if (start + threadIdx.x + j * kGroupThreads < end) {
+      live |= 1u << j;
+      if (k == kEmpty)
+        atomicMin(&special_min, q[j].z);
+      else
+        pend |= 1u << j;
+    }
+  }
+  const uint32_t keyed = pend;
+  uint32_t rounds = 0;
+  while (pend) {
+    ++rounds;
+    uint64_t prev[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+      prev[j] = (pend >> j & 1u)
+                    ? atomicCAS(reinterpret_cast<unsigned long long*>(&lkey[h[j]]),
+                                static_cast<unsigned long long>(kEmpty),
+                                static_cast<unsigned long long>(k))
+                    : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      if (!(pend >> j & 1u)) continue;
+      const uint64_t k = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+      if (prev[j] == kEmpty || prev[j] == k) {
+        atomicMin(&lmin[h[j]], q[j].z);
+        pend &= ~(1u << j);
+      } else {
+        const uint32_t s = h[j] + step[j];
+        h[j] = s >= kLdsSlots ? s - kLdsSlots : s;
+      }
+    }
+  }
+  if (rounds_max) atomicMax(rounds_max, rounds);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
@@ -404,7 +491,8 @@ void run(uint64_t n) {
   auto gw = [&] { k_group_winner<<<nb, kGroupThreads>>>(rec, offs, P, c, gkey, gmin, rep2); };
   auto gr2 = [&] { k_group_lookahead<2><<<nb, kGroupThreads>>>(rec, offs, P, c, gkey, gmin, rep2); };
   auto gr4 = [&] { k_group_lookahead<4><<<nb, kGroupThreads>>>(rec, offs, P, c, gkey, gmin, rep2); };
-  for (int v = 0; v < 6; ++v) {
+  auto gd = [&] { k_group_double<<<nb, kGroupThreads>>>(rec, offs, P, c, gkey, gmin, rep2, nullptr); };
+  for (int v = 0; v < 7; ++v) {
     (void)hipMemcpy(rep2, rank, 4 * n, hipMemcpyDeviceToDevice);  // rows keep their rank
     // (keyless rows: rank; the product's init_rep wrote rank for every row)
     if (v == 0) g0();
@@ -412,9 +500,10 @@ void run(uint64_t n) {
     else if (v == 2) gp5();
     else if (v == 3) gw();
     else if (v == 4) gr2();
-    else gr4();
+    else if (v == 5) gr4();
+    else gd();
     (void)hipDeviceSynchronize();
-    printf("%s mismatches vs product grouping: %llu\n", v == 0 ? "G0 " : v == 1 ? "GP4" : v == 2 ? "GP5" : v == 3 ? "GW " : v == 4 ? "GR2" : "GR4",
+    printf("%s mismatches vs product grouping: %llu\n", v == 0 ? "G0 " : v == 1 ? "GP4" : v == 2 ? "GP5" : v == 3 ? "GW " : v == 4 ? "GR2" : v == 5 ? "GR4" : "GD ",
            (unsigned long long)mismatches(rep, rep2, n));
   }
   for (int r = 0; r < 2; ++r) {
@@ -424,6 +513,17 @@ void run(uint64_t n) {
     printf("GW  winner-store         %.4f ms\n", time_ms(gw, 9));
     printf("GR2 read-ahead 2 slots   %.4f ms\n", time_ms(gr2, 9));
     printf("GR4 read-ahead 4 slots   %.4f ms\n", time_ms(gr4, 9));
+    printf("GD  double hashing       %.4f ms\n", time_ms(gd, 9));
+  }
+  {  // longest probe chain (CAS rounds of a thread) with double hashing
+    uint32_t* rm;
+    (void)hipMalloc(&rm, 4);
+    (void)hipMemset(rm, 0, 4);
+    k_group_double<<<nb, kGroupThreads>>>(rec, offs, P, c, gkey, gmin, rep2, rm);
+    uint32_t h_rm = 0;
+    (void)hipMemcpy(&h_rm, rm, 4, hipMemcpyDeviceToHost);
+    printf("GD  max CAS rounds of a thread: %u\n", h_rm);
+    (void)hipFree(rm);
   }
   (void)hipFree(ws);
   (void)hipFree(key);
