@@ -127,7 +127,7 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_persist(
       group_lds<kP>(q, s, e, chunk_of, rep, lkey, lmin, special_min);
     } else {  // the product's global-table path (its own __syncthreads)
       uint4 none[kPer];
-      group_bucket(rec, s, e, none, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
+      group_bucket(Rec16Src{rec}, s, e, none, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
     }
     lds_barrier();  // the table is re-initialised for the next bucket
   };
@@ -168,9 +168,9 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_winner(
   const uint32_t start = offs[static_cast<uint64_t>(b) * P];
   const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];
   uint4 q[kPer];
-  load_bucket(rec, start, end, q);
+  load_bucket(Rec16Src{rec}, start, end, q);
   if (end - start > kLdsCap) {
-    group_bucket(rec, start, end, q, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
+    group_bucket(Rec16Src{rec}, start, end, q, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
     return;
   }
   if (end == start) return;
@@ -252,9 +252,9 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_lookahead(
   const uint32_t start = offs[static_cast<uint64_t>(b) * P];
   const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];
   uint4 q[kPer];
-  load_bucket(rec, start, end, q);
+  load_bucket(Rec16Src{rec}, start, end, q);
   if (end - start > kLdsCap) {
-    group_bucket(rec, start, end, q, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
+    group_bucket(Rec16Src{rec}, start, end, q, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
     return;
   }
   if (end == start) return;
@@ -359,9 +359,9 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_double(
   const uint32_t start = offs[static_cast<uint64_t>(b) * P];
   const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];
   uint4 q[kPer];
-  load_bucket(rec, start, end, q);
+  load_bucket(Rec16Src{rec}, start, end, q);
   if (end - start > kLdsCap) {
-    group_bucket(rec, start, end, q, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
+    group_bucket(Rec16Src{rec}, start, end, q, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
     return;
   }
   if (end == start) return;

@@ -51,6 +51,7 @@
 #include "scan_device.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace sdgpu {
@@ -452,14 +453,20 @@ constexpr uint32_t kStage2Bits = 9;
 constexpr uint32_t kStage2Slots = 16;
 constexpr int kStage2Rows = 4;
 constexpr uint32_t kStage2Blocks = 64;
-template <typename In, bool kInitRep, uint32_t kBits = kStageBits, uint32_t kSlots = 2, int kRows = 2>
+// kRec12: 12-byte records {hash lo, hash hi, row} for rows whose rank is
+// rank_base + row (RowsIn without a rank array): a quarter less to write here
+// and to read in the group kernel (k_bucket_group12).
+template <typename In, bool kInitRep, uint32_t kBits = kStageBits, uint32_t kSlots = 2, int kRows = 2,
+          bool kRec12 = false>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     In in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ offs, uint4* __restrict__ rec,
     uint32_t* __restrict__ rep, const uint32_t* __restrict__ seg, uint32_t P1,
     const uint32_t* __restrict__ ftot = nullptr, uint32_t* __restrict__ fbase = nullptr,
     uint32_t R = 1) {
   constexpr uint32_t nbins = 1u << kBits;
-  __shared__ uint4 stage[nbins][kSlots];
+  using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
+  __shared__ RecT stage[nbins][kSlots];
+  RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
   __shared__ uint32_t fill[nbins];
   __shared__ uint32_t cur[nbins];
   const uint32_t c = blockIdx.y;
@@ -550,13 +557,16 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       if (!in.valid_of(q, u)) continue;
       const uint64_t h = in_hash<In>(in.key_of(q, u));
       const uint32_t b = digit_of(h, skip, kBits);
-      const uint4 rq = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r,
-                                  in.row_of(q, u));
+      RecT rq;
+      if constexpr (kRec12)
+        rq = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), in.row_of(q, u));
+      else
+        rq = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r, in.row_of(q, u));
       const uint32_t sl = atomicAdd(&fill[b], 1u);
       if (sl < kSlots) {
         stage[b][sl] = rq;
       } else {
-        rec[atomicAdd(&cur[b], 1u)] = rq;
+        out[atomicAdd(&cur[b], 1u)] = rq;
       }
     }
     lds_barrier();
@@ -571,7 +581,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
           const uint32_t p = cur[b];
           cur[b] = p + kSlots;
 #pragma unroll
-          for (uint32_t k = 0; k < kSlots; ++k) rec[p + k] = stage[b][k];
+          for (uint32_t k = 0; k < kSlots; ++k) out[p + k] = stage[b][k];
           fill[b] = 0;
         }
       }
@@ -584,7 +594,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       const uint32_t f = fill[b], p = cur[b];
       if (f >= kSlots) {
 #pragma unroll
-        for (uint32_t k = part; k < kSlots; k += T) rec[p + k] = stage[b][k];
+        for (uint32_t k = part; k < kSlots; k += T) out[p + k] = stage[b][k];
         if (part == 0) {
           cur[b] = p + kSlots;
           fill[b] = 0;
@@ -611,7 +621,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     }
   }
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
-    for (uint32_t k = 0; k < fill[b]; ++k) rec[cur[b] + k] = stage[b][k];
+    for (uint32_t k = 0; k < fill[b]; ++k) out[cur[b] + k] = stage[b][k];
 }
 
 // First probe slot of a record in the LDS table (kLdsSlots, any size): the
@@ -643,21 +653,38 @@ __device__ __forceinline__ uint64_t global_slot(uint64_t h, uint64_t tsize) {
 
 constexpr int kPer = (kLdsCap + kGroupThreads - 1) / kGroupThreads;
 
+// Bucket records as {hash lo, hash hi, rank, row}: 16-byte records as stored,
+// or 12-byte ones {hash lo, hash hi, row} with rank = rank_base + row.
+struct Rec16Src {
+  const uint4* __restrict__ p;
+  __device__ __forceinline__ uint4 operator()(uint32_t i) const { return p[i]; }
+};
+struct Rec12Src {
+  const uint3* __restrict__ p;
+  uint32_t rank_base;
+  __device__ __forceinline__ uint4 operator()(uint32_t i) const {
+    const uint3 v = p[i];
+    return make_uint4(v.x, v.y, rank_base + v.z, v.z);
+  }
+};
+
 // LDS-sized bucket: every thread loads its (at most kPer) records at once and
 // keeps them in registers for both phases.
-__device__ __forceinline__ void load_bucket(const uint4* __restrict__ rec, uint32_t start,
-                                            uint32_t end, uint4 (&q_reg)[kPer]) {
+template <typename Src>
+__device__ __forceinline__ void load_bucket(Src rec, uint32_t start, uint32_t end,
+                                            uint4 (&q_reg)[kPer]) {
   if (end - start > kLdsCap) return;
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const uint32_t i = start + threadIdx.x + j * kGroupThreads;
-    q_reg[j] = i < end ? rec[i] : make_uint4(0, 0, 0, 0);
+    q_reg[j] = i < end ? rec(i) : make_uint4(0, 0, 0, 0);
   }
 }
 
 // Group-by of one bucket, rows [start, end) of rec (q_reg preloaded by
 // load_bucket when the bucket fits the LDS table).
-__device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint32_t start,
+template <typename Src>
+__device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
                                              uint32_t end, const uint4 (&q_reg)[kPer],
                                              ChunkOf chunk_of, uint64_t* __restrict__ gkey,
                                              uint32_t* __restrict__ gmin,
@@ -747,7 +774,7 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
     return;
   }
   for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
-    const uint4 q = rec[i];
+    const uint4 q = rec(i);
     const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
     const uint32_t r = q.z;
     if (k == kEmpty) {
@@ -768,7 +795,7 @@ __device__ __forceinline__ void group_bucket(const uint4* __restrict__ rec, uint
   }
   __syncthreads();
   for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
-    const uint4 q = rec[i];
+    const uint4 q = rec(i);
     const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
     const uint32_t r = q.z;
     uint32_t f;
@@ -801,8 +828,25 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
   const uint32_t start = offs[static_cast<uint64_t>(b) * P];
   const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];  // offs[nb*P] = total
   uint4 q_reg[kPer];
-  load_bucket(rec, start, end, q_reg);
-  group_bucket(rec, start, end, q_reg, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
+  load_bucket(Rec16Src{rec}, start, end, q_reg);
+  group_bucket(Rec16Src{rec}, start, end, q_reg, chunk_of, gkey, gmin, rep, lkey, lmin,
+               special_min);
+}
+
+// k_bucket_group over 12-byte records (rank = rank_base + row).
+__global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12(
+    const uint3* __restrict__ rec, uint32_t rank_base, const uint32_t* __restrict__ offs,
+    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
+    uint32_t* __restrict__ rep) {
+  __shared__ uint64_t lkey[kLdsSlots];
+  __shared__ uint32_t lmin[kLdsSlots];
+  __shared__ uint32_t special_min;
+  const uint32_t b = blockIdx.x;
+  const uint32_t start = offs[b], end = offs[b + 1];
+  const Rec12Src src{rec, rank_base};
+  uint4 q_reg[kPer];
+  load_bucket(src, start, end, q_reg);
+  group_bucket(src, start, end, q_reg, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
 }
 
 __global__ __launch_bounds__(256) void k_fill_init(uint32_t* __restrict__ dst, uint64_t n,
@@ -1009,6 +1053,24 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
       KScope k(timer, "bucket_hist", s);
       k_part_hist<In><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, 0, fine, nullptr, true);
       k_fine_scan<kPartBlocks, 1><<<nb / 64, 1024, 0, s>>>(fine, nb, fE, ftot, ovf);
+    }
+    if constexpr (std::is_same<In, RowsIn>::value) {
+      if (!in.rank) {  // rank = rank_base + row: 12-byte records
+        {
+          KScope k(timer, "bucket_scatter", s);
+          if (init_rep)
+            k_part_scatter_rec_staged<In, true, kStageBits, 2, 2, true><<<P, kPartThreads, 0, s>>>(
+                in, n, kShardBits, fE, rec, rep, nullptr, 0, ftot, fbase);
+          else
+            k_part_scatter_rec_staged<In, false, kStageBits, 2, 2, true><<<P, kPartThreads, 0, s>>>(
+                in, n, kShardBits, fE, rec, rep, nullptr, 0, ftot, fbase);
+        }
+        KScope k(timer, "bucket_group", s);
+        k_bucket_group12<<<nb, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
+                                                      in.rank_base, fbase,
+                                                      ChunkOf::make(chunk_rows), gkey, gmin, rep);
+        return hipGetLastError();
+      }
     }
     {
       KScope k(timer, "bucket_scatter", s);

@@ -281,3 +281,25 @@ def test_two_level_fine_count_overflow(ctx):
     np.testing.assert_array_equal(dedup.group_reps(key, has, 100, ctx), ref)
     key2 = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)  # no overflow now
     np.testing.assert_array_equal(dedup.group_reps(key2, has, 100, ctx), O.group_reps(key2, has, 100))
+
+
+@pytest.mark.parametrize("n,chunk", [(12_500_000, 100), (7_000_000, 7)])
+def test_implicit_rank_12_byte_records(ctx, n, chunk):
+    """Rows without a rank array (rank = row): the 12-bit path moves 12-byte
+    records {hash, row}.  Same reps as with the explicit rank array (16-byte
+    records) and as the oracle; sentinel-valued keys and keyless rows included."""
+    import torch
+    from spacedrive_amd import dedup
+    rng = np.random.default_rng(n)
+    pool = rng.integers(0, 2**64 - 1, int(n * 0.8), dtype=np.uint64, endpoint=True)
+    pool[0] = np.uint64(2**64 - 1)
+    key = pool[rng.integers(0, pool.size, n)]
+    has = (rng.random(n) > 0.001).astype(np.uint8)
+    ops = dedup.HipOps(ctx)
+    dk = torch.from_numpy(key.view(np.int64)).cuda()
+    dh = torch.from_numpy(has).cuda()
+    dr = torch.arange(n, dtype=torch.int32, device="cuda")
+    implicit = ops.group_rows(dk, dh, None, chunk, 0).cpu().numpy().view(np.uint32)
+    explicit = ops.group_rows(dk, dh, dr, chunk, 0).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(implicit, explicit)
+    np.testing.assert_array_equal(implicit, O.group_reps(key, has, chunk))
