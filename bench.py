@@ -529,7 +529,7 @@ class Runner:
         self.group(key, has, grank)  # first launches (lazy code-object loads) untimed
         t, kt = self.timed_kernels(lambda: self.group(key, has, grank), steps, warmup)
         explicit_ms = None
-        if implicit:
+        if implicit and not self.args.no_explicit_rank:
             self.group(key, has, rank)
             explicit_ms = 1e3 * self.timed(lambda: self.group(key, has, rank), steps, warmup) / steps
         xchg = None
@@ -596,7 +596,7 @@ class Runner:
             self._cpu_dedup = self.cpu_grouping(key, has, rank, grank)
         # K7 Object link batch over the same 12.5 M rows: the
         # create list and the (row, creator) connect pairs as dense arrays
-        repv = self.group(key, has, rank)
+        repv = self.group(key, has, grank)
         link_t, link_kt = self.timed_kernels(
             lambda: dedup.link_batch_device(repv, rank, has, 0, ctx=self.ctx, trim=False),
             steps, warmup)
@@ -652,11 +652,19 @@ class Runner:
         total = self.args.dedup_full_rows
         key, has, rank = corpus.synth_dedup_rows_device(4, total, int(total * 0.8), 0, total,
                                                         device=self.local, ctx=self.ctx)
-        self.ops.group_rows(key, has, rank, 100, 0)  # two-level kernels' first launches
+        # rows in rank order (synth rank[i] = i): no rank array, 12-byte records;
+        # the explicit-rank call timed beside it
+        assert bool((rank == torch.arange(total, dtype=rank.dtype, device=rank.device)).all())
+        self.ops.group_rows(key, has, None, 100, 0)  # two-level kernels' first launches
         torch.cuda.synchronize()
-        t, kt = self.timed_kernels(lambda: self.ops.group_rows(key, has, rank, 100, 0), steps,
+        t, kt = self.timed_kernels(lambda: self.ops.group_rows(key, has, None, 100, 0), steps,
                                    warmup)
-        rep = self.ops.group_rows(key, has, rank, 100, 0)
+        explicit_ms = None
+        if not self.args.no_explicit_rank:
+            self.ops.group_rows(key, has, rank, 100, 0)
+            explicit_ms = 1e3 * self.timed(lambda: self.ops.group_rows(key, has, rank, 100, 0),
+                                           steps, warmup) / steps
+        rep = self.ops.group_rows(key, has, None, 100, 0)
         nk = int(has.sum())
         linked = int((rep != rank).sum())
         del key, has, rank, rep
@@ -667,14 +675,15 @@ class Runner:
         # and the fine counts (2^15 buckets x 256 blocks x 4 B); the fine scan reads
         # those and writes the 64 block starts per bucket; the second pass moves every
         # record once more; the group-by as in the one-level path
+        # (implicit rank: no rank array read, 12-byte records)
         nfine = 1 << 15
         alg = {"bucket_hist": 9 * total,
-               "bucket_scatter1": 17 * total + 16 * nk + 4 * nfine * 256,
+               "bucket_scatter1": 13 * total + 12 * nk + 4 * nfine * 256,
                "bucket_fine_scan": 4 * nfine * 256 + 4 * nfine * 64 + 4 * nfine,
-               "bucket_scatter": 32 * nk,
-               "bucket_group": 16 * nk + 4 * linked}
+               "bucket_scatter": 24 * nk,
+               "bucket_group": 12 * nk + 4 * linked}
         pmc_names = {"bucket_hist": "k_part_hist", "bucket_scatter1": "k_part_scatter_runs",
-                     "bucket_scatter": "k_part_scatter_rec_staged", "bucket_group": "k_bucket_group"}
+                     "bucket_scatter": "k_part_scatter_rec_staged", "bucket_group": "k_bucket_group12"}
         step_s = t / steps
         roof = {"bound": "hbm", "peak": HBM_PEAK / 1e9, "unit": "GB/s", "linked_rows": linked,
                 "kernels": {}, "note": "algorithmic bytes of the two-level partition + group-by "
@@ -694,7 +703,8 @@ class Runner:
                         "frac": 16 * total / step_s / HBM_PEAK, "design_bytes": sum(alg.values()),
                         "pmc_source": src}
         return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * step_s,
-                "rows": total, "roofline": roof, "kernels": kernels}
+                "rows": total, "rank": "implicit (row order, 12-byte records)",
+                "explicit_rank_ms_per_step": explicit_ms, "roofline": roof, "kernels": kernels}
 
     def verify_sharded(self, key, has, rank):
         """--verify: the sharded grouping over all ranks (the exchange path the
@@ -922,6 +932,9 @@ def main():
     ap.add_argument("--components", default="cas,dedup,consumers,checksum,staged,dir,single")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-explicit-rank", action="store_true",
+                    help="skip the explicit-rank grouping timed beside the implicit one "
+                         "(PMC passes: one variant per kernel name)")
     ap.add_argument("--verify", action="store_true",
                     help="check the sharded grouping against the one-GPU grouping first")
     args = ap.parse_args()

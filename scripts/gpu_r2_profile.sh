@@ -19,13 +19,13 @@ for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CY
 done
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $C -d "$OUT/dedup/pmc_$C" -o pmc --output-format csv \
-    -- python3 bench.py --steps 2 --warmup 1 --no-cpu --components dedup --dedup-full-rows 0 \
+    -- python3 bench.py --steps 2 --warmup 1 --no-cpu --components dedup --dedup-full-rows 0 --no-explicit-rank \
     > "$OUT/dedup_pmc_$C.log" 2>&1 || exit 1
 done
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $C -d "$OUT/dedup_full/pmc_$C" -o pmc --output-format csv \
     -- python3 bench.py --steps 2 --warmup 1 --no-cpu --components dedup --dedup-rows 100000000 \
-    --dedup-full-rows 0 > "$OUT/dedup_full_pmc_$C.log" 2>&1 || exit 1
+    --dedup-full-rows 0 --no-explicit-rank > "$OUT/dedup_full_pmc_$C.log" 2>&1 || exit 1
 done
 python3 scripts/pmc_summary.py "$OUT/cas" "$OUT/pmc_cas.json" > "$OUT/pmc_cas.txt" || exit 1
 python3 scripts/pmc_summary.py "$OUT/dedup" "$OUT/pmc_dedup.json" > "$OUT/pmc_dedup.txt" || exit 1

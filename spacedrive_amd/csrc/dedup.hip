@@ -267,15 +267,18 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec(
 // needs no pass over the records of its own.  A counter that would pass 65535
 // (one key filling more than 64 Ki rows of a block's tile) sets *ovf, and
 // k_fine_recount rebuilds the counts from the records instead.
+// kRec12: 12-byte records {hash lo, hash hi, row} (rank = rank_base + row).
 constexpr uint32_t kRunMaxBins = 64;
-template <typename In, bool kInitRep>
+template <typename In, bool kInitRep, bool kRec12 = false>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
     In in, uint64_t n, uint32_t skip, uint32_t bits, const uint32_t* __restrict__ offs,
     uint4* __restrict__ rec, uint32_t* __restrict__ rep, uint32_t fbits,
     uint32_t* __restrict__ fine, uint32_t* __restrict__ ovf) {
   constexpr int U = 4;
   constexpr uint32_t R = U * kPartThreads;
-  __shared__ uint4 buf[R];
+  using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
+  __shared__ RecT buf[R];
+  RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
   __shared__ uint32_t cnt[kRunMaxBins], base[kRunMaxBins + 1], cur[kRunMaxBins];
   __shared__ uint32_t fc[1u << (kMaxBucketBits - 1)];  // 2 x 16-bit counters per word
   const uint32_t nbins = 1u << bits, nfine = 1u << fbits;
@@ -289,7 +292,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
     if (threadIdx.x < nbins) cnt[threadIdx.x] = 0;
     lds_barrier();
     uint32_t dg[U], lr[U];
-    uint4 rq[U];
+    RecT rq[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads;
@@ -303,8 +306,11 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
       lr[u] = atomicAdd(&cnt[dg[u]], 1u);
       const uint32_t fb = digit_of(h, skip, fbits), sh = (fb & 1u) << 4;
       over |= ((atomicAdd(&fc[fb >> 1], 1u << sh) >> sh) & 0xFFFFu) == 0xFFFFu;
-      rq[u] = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r,
-                         in.row_of(q, u));
+      if constexpr (kRec12)
+        rq[u] = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), in.row_of(q, u));
+      else
+        rq[u] = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), r,
+                           in.row_of(q, u));
     }
     lds_barrier();
     if (threadIdx.x < 64) {  // the (<= 64) run starts: one wave's shuffle scan
@@ -327,9 +333,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
     lds_barrier();
     const uint32_t total = base[nbins];
     for (uint32_t k = threadIdx.x; k < total; k += kPartThreads) {
-      const uint4 v = buf[k];
+      const RecT v = buf[k];
       const uint32_t b = digit_of((static_cast<uint64_t>(v.y) << 32) | v.x, skip, bits);
-      rec[cur[b] + (k - base[b])] = v;
+      out[cur[b] + (k - base[b])] = v;
     }
     lds_barrier();
     if (threadIdx.x < nbins) cur[threadIdx.x] += cnt[threadIdx.x];
@@ -358,8 +364,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
 // every (coarse block j, segment c) -- a grid-stride loop, so the usual call
 // costs one small launch -- recount the records j wrote to segment c
 // ([seg[c * P + j], seg[c * P + j + 1])) on the kB2 second-pass digit bits.
-template <uint32_t kB2>
-__global__ __launch_bounds__(kPartThreads) void k_fine_recount(const uint4* __restrict__ rec,
+template <uint32_t kB2, typename RecT = uint4>
+__global__ __launch_bounds__(kPartThreads) void k_fine_recount(const RecT* __restrict__ rec,
                                                                 uint32_t skip,
                                                                 const uint32_t* __restrict__ seg,
                                                                 uint32_t P, uint32_t nseg,
@@ -376,7 +382,7 @@ __global__ __launch_bounds__(kPartThreads) void k_fine_recount(const uint4* __re
     const uint32_t s0 = seg[static_cast<uint64_t>(c) * P + j];
     const uint32_t s1 = seg[static_cast<uint64_t>(c) * P + j + 1];
     for (uint32_t i = s0 + threadIdx.x; i < s1; i += kPartThreads) {
-      const uint4 v = rec[i];
+      const RecT v = rec[i];
       atomicAdd(&cnt[digit_of((static_cast<uint64_t>(v.y) << 32) | v.x, skip, kB2)], 1u);
     }
     __syncthreads();
@@ -961,9 +967,13 @@ void allow_lds(K kernel, size_t bytes) {
 // rows per thread per round, kP2 blocks per segment.  The second pass's offsets
 // come from the coarse pass's fine counts (k_fine_scan; bucket starts scanned
 // in the second pass's prologue): no histogram pass over the coarse records.
-template <typename In, uint32_t kB2, uint32_t kS2, int kR2, uint32_t kP2>
+// kRec12: rows without a rank array (rank = rank_base + row), 12-byte records
+// in both passes.
+template <typename In, uint32_t kB2, uint32_t kS2, int kR2, uint32_t kP2, bool kRec12 = false>
 hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t chunk_rows,
-                            uint32_t* rep, bool init_rep, void* ws, hipStream_t s, KTimer* timer) {
+                            uint32_t* rep, bool init_rep, void* ws, hipStream_t s, KTimer* timer,
+                            uint32_t rank_base = 0) {
+  using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(w + L.tiles);
   uint4* rec = reinterpret_cast<uint4*>(w + L.rec);
@@ -994,30 +1004,41 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
   {
     KScope k(timer, "bucket_scatter1", s);
     if (init_rep)
-      k_part_scatter_runs<In, true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, L.cbits, hist1,
-                                                               rec1, rep, bits, fine, ovf);
+      k_part_scatter_runs<In, true, kRec12><<<P, kPartThreads, 0, s>>>(
+          in, n, kShardBits, L.cbits, hist1, rec1, rep, bits, fine, ovf);
     else
-      k_part_scatter_runs<In, false><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, L.cbits, hist1,
-                                                                rec1, rep, bits, fine, ovf);
+      k_part_scatter_runs<In, false, kRec12><<<P, kPartThreads, 0, s>>>(
+          in, n, kShardBits, L.cbits, hist1, rec1, rep, bits, fine, ovf);
   }
   // pass 2: kB2 bits below, per coarse segment, staged in kS2-record runs
-  const Rec16In in2{rec1};
+  using In2 = typename std::conditional<kRec12, Rec12In, Rec16In>::type;
+  In2 in2;
+  if constexpr (kRec12)
+    in2 = Rec12In{reinterpret_cast<const uint3*>(rec1), rank_base};
+  else
+    in2 = Rec16In{rec1};
   constexpr uint32_t P2 = kP2;
   {
     KScope k(timer, "bucket_fine_scan", s);
-    k_fine_recount<kB2><<<kPartBlocks, kPartThreads, 0, s>>>(rec1, skip2, hist1, P, nseg, bits,
-                                                             fine, ovf);
+    k_fine_recount<kB2, RecT><<<kPartBlocks, kPartThreads, 0, s>>>(
+        reinterpret_cast<const RecT*>(rec1), skip2, hist1, P, nseg, bits, fine, ovf);
     k_fine_scan<P2, kPartBlocks / kP2><<<(nfine + 63) / 64, 1024, 0, s>>>(fine, nfine, fE, ftot,
                                                                           ovf);
   }
   {
     KScope k(timer, "bucket_scatter", s);
-    k_part_scatter_rec_staged<Rec16In, false, kB2, kS2, kR2><<<dim3(P2, nseg), kPartThreads, 0, s>>>(
-        in2, 0, skip2, fE, rec, nullptr, hist1, P, ftot, fbase, kPartBlocks / kP2);
+    k_part_scatter_rec_staged<In2, false, kB2, kS2, kR2, kRec12>
+        <<<dim3(P2, nseg), kPartThreads, 0, s>>>(in2, 0, skip2, fE, rec, nullptr, hist1, P, ftot,
+                                                 fbase, kPartBlocks / kP2);
   }
   KScope k(timer, "bucket_group", s);
-  k_bucket_group<<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, ChunkOf::make(chunk_rows), gkey,
-                                                 gmin, rep);
+  if constexpr (kRec12)
+    k_bucket_group12<<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec), rank_base,
+                                                     fbase, ChunkOf::make(chunk_rows), gkey, gmin,
+                                                     rep);
+  else
+    k_bucket_group<<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, ChunkOf::make(chunk_rows), gkey,
+                                                   gmin, rep);
   return hipGetLastError();
 }
 
@@ -1035,9 +1056,15 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   const uint32_t P = bucket_part_blocks();
   const uint64_t nh = (static_cast<uint64_t>(1) << bits) * P;
   const size_t lds = sizeof(uint32_t) << bits;
-  if (L.cbits)
+  if (L.cbits) {
+    if constexpr (std::is_same<In, RowsIn>::value) {
+      if (!in.rank)  // rank = rank_base + row: 12-byte records
+        return two_level_launch<In, kStage2Bits, kStage2Slots, kStage2Rows, kStage2Blocks, true>(
+            in, n, L, chunk_rows, rep, init_rep, ws, s, timer, in.rank_base);
+    }
     return two_level_launch<In, kStage2Bits, kStage2Slots, kStage2Rows, kStage2Blocks>(
         in, n, L, chunk_rows, rep, init_rep, ws, s, timer);
+  }
   if (bits == kStageBits) {
     // 12-bit digits: block-major counts, k_fine_scan for every block's start
     // inside every bucket (one launch instead of the 3-launch scan), bucket

@@ -200,6 +200,37 @@ struct Rec16In {
   __device__ __forceinline__ uint32_t row_of(const RowBatch<U>& q, int u) const { return q.b[u]; }
 };
 
+// Rec12In: 12-byte bucket records {hash lo, hash hi, row} of a first pass over
+// rows without a rank array (rank = rank_base + row).
+struct Rec12In {
+  static constexpr bool kHashed = true;
+  const uint3* rec;
+  uint32_t rank_base;
+  template <int U>
+  __device__ __forceinline__ void load_many(uint64_t i0, uint64_t stride, uint64_t end,
+                                            uint64_t safe, RowBatch<U>& q) const {
+    batch_index(i0, stride, end, safe, q);
+    uint3 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = rec[q.row[u]];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      q.k[u] = (static_cast<uint64_t>(t[u].y) << 32) | t[u].x;
+      q.b[u] = t[u].z;
+    }
+  }
+  template <int U>
+  __device__ __forceinline__ uint64_t key_of(const RowBatch<U>& q, int u) const { return q.k[u]; }
+  template <int U>
+  __device__ __forceinline__ uint32_t rank_of(const RowBatch<U>& q, int u) const {
+    return rank_base + q.b[u];
+  }
+  template <int U>
+  __device__ __forceinline__ bool valid_of(const RowBatch<U>& q, int u) const { return q.in[u]; }
+  template <int U>
+  __device__ __forceinline__ uint32_t row_of(const RowBatch<U>& q, int u) const { return q.b[u]; }
+};
+
 template <typename In>
 __device__ __forceinline__ uint64_t in_hash(uint64_t k) {
   if constexpr (In::kHashed) return k;

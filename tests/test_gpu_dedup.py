@@ -283,10 +283,10 @@ def test_two_level_fine_count_overflow(ctx):
     np.testing.assert_array_equal(dedup.group_reps(key2, has, 100, ctx), O.group_reps(key2, has, 100))
 
 
-@pytest.mark.parametrize("n,chunk", [(12_500_000, 100), (7_000_000, 7)])
+@pytest.mark.parametrize("n,chunk", [(12_500_000, 100), (7_000_000, 7), (13_000_000, 100)])
 def test_implicit_rank_12_byte_records(ctx, n, chunk):
-    """Rows without a rank array (rank = row): the 12-bit path moves 12-byte
-    records {hash, row}.  Same reps as with the explicit rank array (16-byte
+    """Rows without a rank array (rank = row): the 12-bit and the two-level
+    (13 M rows) paths move 12-byte records {hash, row}.  Same reps as with the explicit rank array (16-byte
     records) and as the oracle; sentinel-valued keys and keyless rows included."""
     import torch
     from spacedrive_amd import dedup
