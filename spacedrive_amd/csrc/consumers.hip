@@ -28,14 +28,32 @@ uint32_t grid_for(uint64_t n, uint64_t per = kThreads) {
   return static_cast<uint32_t>(g == 0 ? 1 : (g < 65535 ? g : 65535));
 }
 
-// mark[o] = 1: some file_path references Object o (negative = NULL object_id)
+// mark[o] = 1: some file_path references Object o (negative = NULL object_id).
+// Workgroups go to the 8 XCDs round-robin (block b on XCD b % 8), so block b
+// marks only the ids of range b % 8 and every XCD's stores stay inside one
+// eighth of the map, which its L2 holds (10 M ids: 1.25 MB of 4 MB) until the
+// lines leave whole.  Every file_path id is read once per range (8 times in
+// all, the repeats from the shared last-level cache): one scattered byte store
+// per row into the whole map left each store a partial-line write of its own.
+constexpr uint32_t kMarkRanges = 8;
 __global__ __launch_bounds__(kThreads) void k_mark(const int32_t* __restrict__ fp_obj, uint64_t n,
-                                                   uint8_t* __restrict__ mark, uint32_t max_id) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n;
-       i += stride) {
-    const int32_t o = fp_obj[i];
-    if (o >= 0 && static_cast<uint32_t>(o) <= max_id) mark[o] = 1;
+                                                   uint8_t* __restrict__ mark, uint32_t max_id,
+                                                   uint32_t span) {
+  const uint32_t r = blockIdx.x % kMarkRanges, g = blockIdx.x / kMarkRanges;
+  const uint32_t lo = r * span;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x / kMarkRanges) * kThreads * 4;
+  for (uint64_t i0 = static_cast<uint64_t>(g) * kThreads * 4 + threadIdx.x; i0 < n; i0 += stride) {
+    int32_t o[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t i = i0 + static_cast<uint64_t>(u) * kThreads;
+      o[u] = i < n ? fp_obj[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t d = static_cast<uint32_t>(o[u]) - lo;  // negative ids wrap past span
+      if (o[u] >= 0 && d < span && static_cast<uint32_t>(o[u]) <= max_id) mark[o[u]] = 1;
+    }
   }
 }
 
@@ -219,7 +237,12 @@ hipError_t orphan_objects_launch(const int32_t* obj, uint64_t n_obj, const int32
   uint32_t* cnt = reinterpret_cast<uint32_t*>(bits + map);
   uint32_t* tiles = cnt + blocks + 1;
   (void)hipMemsetAsync(bits, 0, map, s);
-  if (n_fp) k_mark<<<grid_for(n_fp, 4 * kThreads), kThreads, 0, s>>>(fp_obj, n_fp, bits, max_id);
+  if (n_fp) {
+    const uint32_t span = static_cast<uint32_t>((static_cast<uint64_t>(max_id) + kMarkRanges) / kMarkRanges);
+    const uint64_t per = (n_fp + 4 * kThreads - 1) / (4 * kThreads);  // 1024-row groups
+    const uint32_t groups = static_cast<uint32_t>(per < 256 ? per : 256);
+    k_mark<<<groups * kMarkRanges, kThreads, 0, s>>>(fp_obj, n_fp, bits, max_id, span);
+  }
   if (blocks) {
     k_orphan_count<<<static_cast<uint32_t>(blocks), kThreads, 0, s>>>(obj, n_obj, bits, max_id,
                                                                       cnt);
