@@ -184,7 +184,9 @@ int sdgpu_group_pairs_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint32
                              void *stream);
 /* Device-resident, one GPU, whole rows: rep[i] for every row i; rows with
  * d_has_key[i] == 0 get rep[i] = rank[i].  d_has_key NULL = every row keyed;
- * d_rank NULL = rank i (rows already in id order).  skip_bits ignored. */
+ * d_rank NULL = rank i (rows already in id order; the partition then moves
+ * 12-byte bucket records instead of 16-byte ones, ~10 % faster).  skip_bits
+ * ignored. */
 int sdgpu_group_rows_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t *d_has_key,
                             const uint32_t *d_rank, uint64_t n, uint32_t chunk_rows,
                             uint32_t skip_bits, uint32_t *d_rep, void *stream);
