@@ -149,6 +149,45 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
   __syncthreads();
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
+  if constexpr (std::is_same<In, RowsIn>::value) {
+    // Row order does not matter to a histogram: the keys of row pairs as one
+    // 16-B load per lane (8-B loads run at ~0.6x the 16-B rate), has_key as
+    // one 2-B load; the odd rows at the tile's ends one by one.
+    if (!world && (reinterpret_cast<uintptr_t>(in.key) & 15u) == 0 &&
+        (reinterpret_cast<uintptr_t>(in.valid) & 1u) == 0) {
+      auto count = [&](uint64_t k, bool v) {
+        if (v) atomicAdd(&cnt[part_digit(row_hash(k), skip, bits, 0)], 1u);
+      };
+      const uint64_t p0 = (t0 + 1) / 2, p1 = t1 / 2;  // whole pairs: rows [2 p0, 2 p1)
+      if (threadIdx.x == 0 && (t0 & 1u) && t0 < t1) count(in.key[t0], !in.valid || in.valid[t0]);
+      if (threadIdx.x == 1 && (t1 & 1u) && t1 - 1 >= 2 * p0)
+        count(in.key[t1 - 1], !in.valid || in.valid[t1 - 1]);
+      const uint4* __restrict__ k4 = reinterpret_cast<const uint4*>(in.key);
+      const uint16_t* __restrict__ v2 = reinterpret_cast<const uint16_t*>(in.valid);
+      constexpr int kP = kUnroll / 2;
+      for (uint64_t q0 = p0 + threadIdx.x; q0 < p1; q0 += kP * kPartThreads) {
+        uint4 kk[kP];
+        uint32_t vv[kP];
+#pragma unroll
+        for (int u = 0; u < kP; ++u) {
+          const uint64_t q = q0 + static_cast<uint64_t>(u) * kPartThreads;
+          kk[u] = k4[q < p1 ? q : q0];
+          vv[u] = v2 ? v2[q < p1 ? q : q0] : 0x0101u;
+        }
+#pragma unroll
+        for (int u = 0; u < kP; ++u) {
+          if (q0 + static_cast<uint64_t>(u) * kPartThreads >= p1) continue;
+          count((static_cast<uint64_t>(kk[u].y) << 32) | kk[u].x, (vv[u] & 0xFFu) != 0);
+          count((static_cast<uint64_t>(kk[u].w) << 32) | kk[u].z, (vv[u] >> 8) != 0);
+        }
+      }
+      __syncthreads();
+      for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
+        hist[blk_major ? static_cast<uint64_t>(part_block()) * nbins + b
+                       : static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
+      return;
+    }
+  }
   for (uint64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += kUnroll * kPartThreads) {
     RowBatch<kUnroll> q;
     in.template load_many<kUnroll>(i0, kPartThreads, t1, i0, q);
