@@ -303,3 +303,24 @@ def test_implicit_rank_12_byte_records(ctx, n, chunk):
     explicit = ops.group_rows(dk, dh, dr, chunk, 0).cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(implicit, explicit)
     np.testing.assert_array_equal(implicit, O.group_reps(key, has, chunk))
+
+
+@pytest.mark.parametrize("key_off,has_off", [(0, 0), (1, 0), (0, 1), (1, 1)])
+def test_histogram_alignment_paths(ctx, key_off, has_off):
+    """k_part_hist reads row pairs with 16-B key / 2-B has_key loads when both
+    arrays are so aligned, else row by row: 7 M rows (12-bit path, odd tile
+    starts) from views that start 1 element in, same reps as the oracle."""
+    import torch
+    from spacedrive_amd import dedup
+    n = 7_000_001
+    rng = np.random.default_rng(77 + key_off * 2 + has_off)
+    pool = rng.integers(0, 2**64 - 1, n // 2, dtype=np.uint64, endpoint=True)
+    key = pool[rng.integers(0, pool.size, n)]
+    has = (rng.random(n) > 0.01).astype(np.uint8)
+    kbuf = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    hbuf = torch.zeros(n + 1, dtype=torch.uint8, device="cuda")
+    kbuf[key_off:key_off + n] = torch.from_numpy(key.view(np.int64)).cuda()
+    hbuf[has_off:has_off + n] = torch.from_numpy(has).cuda()
+    dk, dh = kbuf[key_off:key_off + n], hbuf[has_off:has_off + n]
+    rep = dedup.HipOps(ctx).group_rows(dk, dh, None, 100, 0).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(rep, O.group_reps(key, has, 100))
