@@ -157,12 +157,16 @@ class Runner:
         self.backend = backend if self.world > 1 else None
         self.ops = dedup.HipOps(self.ctx)
         self.comm = None
+        # every wait on an RCCL peer inside libsdgpu is bounded by this (a
+        # rank that never joins or dies mid-exchange: -ETIMEDOUT, not a hang)
+        self.comm_timeout_ms = int(os.environ.get("SDGPU_COMM_TIMEOUT_MS", "120000"))
         # SD_BENCH_FORCE_COMM=1: also at N = 1 through a one-rank RCCL
         # communicator (rehearses the N > 1 code path on a one-GPU box)
         force = os.environ.get("SD_BENCH_FORCE_COMM") == "1" and self.world == 1
         if force:
             self.backend = "nccl (one-rank rehearsal)"
-            self.comm = dedup.Comm.init_rank(self.ctx, 1, 0, dedup.Comm.unique_id())
+            self.comm = dedup.Comm.init_rank(self.ctx, 1, 0, dedup.Comm.unique_id(),
+                                             timeout_ms=self.comm_timeout_ms)
         if self.world > 1 and backend == "nccl":
             # the grouping's exchange runs INSIDE libsdgpu over RCCL (what the
             # Rust host calls): rank 0's communicator id travels over the
@@ -171,7 +175,8 @@ class Runner:
             dist.broadcast_object_list(obj, src=0)
             err = None
             try:
-                self.comm = dedup.Comm.init_rank(self.ctx, self.world, self.rank, obj[0])
+                self.comm = dedup.Comm.init_rank(self.ctx, self.world, self.rank, obj[0],
+                                                 timeout_ms=self.comm_timeout_ms)
             except Exception as e:  # reported, and every rank takes the same path
                 err = e
             ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=self.dev)
@@ -182,6 +187,44 @@ class Runner:
                 if self.comm is not None:
                     self.comm.close()
                     self.comm = None
+
+    def world_info(self) -> dict:
+        """Launched world and, with a libsdgpu communicator, its RCCL world
+        size and this rank's exchange volume / host time so far."""
+        w = {"dist_world_size": self.dist.get_world_size() if self.world > 1 else 1,
+             "devices_visible": self.torch.cuda.device_count(),
+             "backend": self.backend, "exchange": self.exchange_name()}
+        if self.comm is not None:
+            try:
+                nr, rk, tr = self.comm.info()
+                w["rccl"] = {"nranks": nr, "rank": rk, "transport": tr,
+                             "stats_rank": self.comm.stats()}
+            except Exception as e:  # noqa: BLE001 -- e.g. an aborted communicator
+                w["rccl"] = {"error": repr(e)[:200]}
+        return w
+
+    def free(self):
+        self.torch.cuda.empty_cache()
+
+    def drop_samples(self):
+        """Releases the CPU leg's samples and the temporary files of the
+        latency / config-1 legs."""
+        import shutil
+        self._cpu_sample = None
+        if getattr(self, "_single_root", None):
+            shutil.rmtree(self._single_root, ignore_errors=True)
+            self._single_root = self._single_sample = None
+        if getattr(self, "_dir_sample", None):  # ranks > 0, or --no-cpu
+            shutil.rmtree(self._dir_sample[2], ignore_errors=True)
+            self._dir_sample = None
+        self.free()
+
+    def shutdown(self):
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None
+        if self.world > 1:
+            self.dist.destroy_process_group()
 
     def exchange_name(self) -> str:
         if self.comm is not None:
@@ -200,6 +243,11 @@ class Runner:
         return dedup.sharded_group_reps(key, has, rank, 100, ops=self.ops, timings=timings)
 
     def barrier(self):
+        if self.comm is not None:
+            # the last exchange's reps, waited for against the communicator's
+            # deadline (a dead peer raises -ETIMEDOUT here instead of hanging
+            # the torch synchronisation below)
+            self.comm.wait()
         if self.world > 1:
             self.dist.barrier()
 
@@ -384,7 +432,7 @@ class Runner:
         # row, next to the step's ~42 KB of windows per file) so
         # the run can be checked after timing against ONE grouping of all its
         # rows: batching through the Object index must equal the whole-run rule
-        verify = W == 1 and index is not None
+        verify = W == 1 and index is not None and not self.args.no_cpu
         if verify:
             keys_all = torch.empty(nsteps * n, dtype=torch.int64, device=self.dev)
             reps_all = torch.empty(nsteps * n, dtype=torch.int32, device=self.dev)
@@ -400,13 +448,14 @@ class Runner:
         t = self.timed(run, 1, 0)
         whole = None
         if verify:
-            has_all = has.repeat(nsteps)
-            rank_all = torch.arange(nsteps * n, dtype=torch.int64, device=self.dev).to(torch.int32)
-            ref = self.ops.group_rows(keys_all, has_all, rank_all, 100, 0)
-            whole = {"rows": nsteps * n, "mismatches": int((ref != reps_all).sum()),
-                     "note": "reps of the batched run (Object index) vs one grouping of all "
-                             "its rows on the GPU (the canonical rule over global ranks)"}
-            del keys_all, reps_all, has_all, rank_all, ref
+            # checked after the timing against the ORACLE's grouping of all the
+            # run's rows (staged_oracle leg, rank 0 at N = 1): batching through
+            # the Object index must equal the whole-run rule
+            self._staged_verify = (keys_all.cpu().numpy().view(np.uint64),
+                                   np.tile(has.cpu().numpy(), nsteps),
+                                   reps_all.cpu().numpy().view(np.uint32))
+            whole = {"rows": nsteps * n, "checked_by": "staged_oracle leg (O.group_reps)"}
+            del keys_all, reps_all
         assert int(st.abs().sum()) == 0
         last = self._staged_last
         linked_last = int((last != ranks[nsteps - 1]).sum())
@@ -623,6 +672,24 @@ class Runner:
                 "config": {"workload": "config4: 80% distinct u64 keys + 20% dups, 0.1% keyless",
                            "rows_per_gpu": per, "rows_total": total},
                 "kernels": kernels}
+
+    def staged_oracle(self):
+        """Config 5's parity at full size: the reps of the batched 50 M-file run
+        (grouped step by step through the Object index on the GPU) against the
+        oracle's grouping of ALL its rows at once (orc_group_reps, C, one
+        thread; the canonical rule over global ranks, file_identifier/mod.rs:
+        168-241)."""
+        from oracle import oracle as O
+        keys, has, reps = self._staged_verify
+        self._staged_verify = None
+        t0 = time.perf_counter()
+        ref = O.group_reps(keys, has, 100)
+        dt = time.perf_counter() - t0
+        bad = int(np.count_nonzero(ref != reps))
+        return {"rows": int(keys.size), "mismatches": bad, "oracle_rows_per_s": keys.size / dt,
+                "oracle_seconds": dt,
+                "note": "reps of the batched run (Object index, step by step) vs the oracle's "
+                        "one grouping of all its rows (oracle orc_group_reps, one thread)"}
 
     def cpu_grouping(self, key, has, rank, grank):
         """CPU leg of config 4: the oracle's C grouping (orc_group_reps, one
@@ -914,7 +981,81 @@ def self_launch(n: int) -> int:
     return subprocess.run(cmd).returncode
 
 
-def main():
+class LineWriter:
+    """The bench's one JSON line, guarded so it is printed exactly once: at the
+    end of a normal run, or by the watchdog when the deadline passes first
+    (an auxiliary leg that fails or hangs must not take the
+    headline, roofline and cpu_baseline with it)."""
+
+    def __init__(self, out, rank: int):
+        import threading
+        self.out, self.rank = out, rank
+        self.lock = threading.Lock()
+        self.done = False
+        self.line = {"metric": METRIC, "value": None, "components": {}}
+
+    def emit(self, **extra) -> None:
+        with self.lock:
+            if self.done:
+                return
+            self.done = True
+            if self.rank == 0:
+                line = dict(self.line)
+                line.update(extra)
+                print(json.dumps(line, default=str), file=self.out, flush=True)
+
+
+def start_watchdog(writer: LineWriter, seconds: float, state: dict):
+    """Prints the line with what was measured so far and ends the process if
+    the run is still going after `seconds` (a hung leg, e.g. a collective whose
+    peer died).  Daemon timer thread: ctypes / HIP waits release the GIL."""
+    import threading
+
+    def fire():
+        leg = state.get("leg")
+        log(f"bench: deadline of {seconds:.0f} s passed inside leg {leg!r}; "
+            "printing what was measured and exiting")
+        comp = writer.line.setdefault("components", {})
+        if leg:
+            comp.setdefault(leg, {})["error"] = f"deadline: still running after {seconds:.0f} s"
+        writer.line["incomplete"] = {"leg": leg, "deadline_s": seconds}
+        writer.emit()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0 if writer.line.get("value") is not None else 3)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def build_roofline(c, compress_peak, valu_peak, classes):
+    """The dominant kernel's roofline (K1 k_leaves3): algorithmic int32 ops per
+    launch / its event-timed average duration, against the spec VALU peak."""
+    ri = c["roofline_inputs"]
+    ops = ri["leaf_compressions"] * ISA_PER_COMPRESSION
+    t_leaf = ri["avg_leaves_s"]
+    achieved = ops / t_leaf if t_leaf > 0 else 0.0
+    traffic, traffic_src = pmc_traffic("k_leaves3")
+    return {"bound": "valu", "kernel": "cas_leaves (K1 k_leaves3)",
+            "achieved": achieved / 1e12, "peak": VALU_PEAK_SPEC / 1e12, "unit": "Tops/s",
+            "frac": achieved / VALU_PEAK_SPEC, "traffic": traffic,
+            "traffic_source": traffic_src,
+            "peak_measured": compress_peak / 1e12 if compress_peak else None,
+            "peak_measured_note": "register-only BLAKE3 compressions (same 680-VALU stream, no "
+                                  "memory traffic): the attainable issue roof of this mix",
+            "peak_g_mix_probe": valu_peak / 1e12 if valu_peak else None,
+            "peak_by_class_measured": classes,
+            "frac_of_measured": achieved / compress_peak if compress_peak else None,
+            "algorithmic_per_launch": {"compressions": ri["leaf_compressions"],
+                                       "int32_ops": ops, "window_bytes": ri["bytes"]},
+            "compressions_per_s": ri["leaf_compressions"] / t_leaf if t_leaf else None,
+            "hbm_GBps": ri["bytes"] / t_leaf / 1e9 if t_leaf else None,
+            "hbm_frac": ri["bytes"] / t_leaf / HBM_PEAK if t_leaf else None}
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -931,137 +1072,154 @@ def main():
     ap.add_argument("--dir-files", type=int, default=10_000)
     ap.add_argument("--components", default="cas,dedup,consumers,checksum,staged,dir,single")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--deadline", type=float,
+                    default=float(os.environ.get("SD_BENCH_DEADLINE_S", "480")),
+                    help="seconds after which the line is printed with what was measured "
+                         "and the process ends (the driver's limit is 600 s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-explicit-rank", action="store_true",
                     help="skip the explicit-rank grouping timed beside the implicit one "
                          "(PMC passes: one variant per kernel name)")
     ap.add_argument("--verify", action="store_true",
                     help="check the sharded grouping against the one-GPU grouping first")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main(argv=None, runner_cls=None, out=None):
+    """Runs the legs; every leg but the headline is guarded (a failure becomes
+    components.<leg>.error), and the line is printed once -- at the end, or by
+    the watchdog at --deadline."""
+    import traceback
+    args = parse_args(argv)
     comps = set(args.components.split(","))
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(self_launch(args.gpus))
-    # stdout carries exactly one JSON line: everything else the process (or a
-    # library it loads -- RCCL prints a version banner on communicator init)
-    # writes to fd 1 goes to stderr
-    sys.stdout.flush()
-    json_out = os.fdopen(os.dup(1), "w")
-    os.dup2(2, 1)
+    if runner_cls is None:
+        if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+            sys.exit(self_launch(args.gpus))
+        runner_cls = Runner
+    if out is None:
+        # stdout carries exactly one JSON line: everything else the process (or
+        # a library it loads -- RCCL prints a version banner on communicator
+        # init) writes to fd 1 goes to stderr
+        sys.stdout.flush()
+        out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
     if args.gpus != int(os.environ.get("WORLD_SIZE", "1")):
         log(f"bench: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}: "
             "reporting the launched world size")
+    t_begin = time.perf_counter()
+    state = {"leg": "init"}
+    writer = LineWriter(out, int(os.environ.get("RANK", "0")))
+    start_watchdog(writer, args.deadline, state)
+    line = writer.line
+    comp = line["components"]
+    walls = {}
+    line["leg_wall_s"] = walls
 
-    R = Runner(args)
-    torch = R.torch
-    valu_peak = R.ctx.valu_peak()
-    compress_peak = R.ctx.valu_peak(5)  # register-only compressions, 680 VALU each
-    classes = {name: R.ctx.valu_peak(k) / 1e12 for k, name in
-               [(1, "v_xor_b32"), (2, "v_add3_u32"), (3, "v_alignbit_b32"), (4, "v_add_u32")]}
-    log(f"measured int32 VALU peak: {valu_peak / 1e12:.1f} T lane-ops/s "
-        f"(spec {VALU_PEAK_SPEC / 1e12:.1f}); per class {json.dumps(classes)}")
+    def leg(name, fn, guarded=True):
+        state["leg"] = name
+        t0 = time.perf_counter()
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001 -- reported in the line, the run goes on
+            if not guarded:
+                raise
+            log(f"bench: leg {name} failed: {e!r}\n{traceback.format_exc()}")
+            comp.setdefault(name, {})["error"] = repr(e)[:400]
+            return None
+        finally:
+            walls[name] = round(time.perf_counter() - t0, 2)
+            state["leg"] = None
+
+    R = leg("init", lambda: runner_cls(args), guarded=False)
+    writer.rank = R.rank
+    line.update({"unit": "files/s", "n_gpus": R.world, "steps": args.steps,
+                 "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+                 "vs_baseline": None, "dtype": "u32",
+                 "data": "synthetic (BASELINE configs 2/3/4 shapes, generated in HBM)",
+                 "config": {"workload": "identifier job step: config2 (1M files/GPU) cas_id + "
+                                        "sharded cas_id->Object grouping + Object link batch",
+                            "files_per_gpu": args.files, "global_files": args.files * R.world,
+                            "parallelism": f"dp{R.world} (files) + hash-sharded dedup, "
+                                           "RCCL all-to-all"},
+                 "world": R.world_info()})
+
+    def peaks():
+        v = R.ctx.valu_peak()
+        cp = R.ctx.valu_peak(5)  # register-only compressions, 680 VALU each
+        cl = {name: R.ctx.valu_peak(k) / 1e12 for k, name in
+              [(1, "v_xor_b32"), (2, "v_add3_u32"), (3, "v_alignbit_b32"), (4, "v_add_u32")]}
+        log(f"measured int32 VALU peak: {v / 1e12:.1f} T lane-ops/s "
+            f"(spec {VALU_PEAK_SPEC / 1e12:.1f}); per class {json.dumps(cl)}")
+        return v, cp, cl
+    pk = leg("valu_probe", peaks) or (None, None, None)
+
     c = None
     if "cas" in comps:  # the headline step; only profiling passes leave it out
-        c = R.run_cas(args.steps, args.warmup)
-        log("cas:", json.dumps(c["cas"]), json.dumps(c["kernels"]))
-    single = None
+        c = leg("cas", lambda: R.run_cas(args.steps, args.warmup))
+        if c:
+            log("cas:", json.dumps(c["cas"]), json.dumps(c["kernels"]))
+            comp["cas"] = c["cas"]
+            comp["identifier_job"] = c["job"]
+            line["value"] = c["job"]["value"]
+            line["ms_per_step"] = c["job"]["ms_per_step"]
+            line["kernels"] = c["kernels"]
+            line["roofline"] = leg("roofline", lambda: build_roofline(c, pk[1], pk[0], pk[2]))
     if "single" in comps:
-        single = R.run_single()
-        log("single:", json.dumps(single))
-    dir_comp = None
+        single = leg("single_file_latency", R.run_single)
+        if single:
+            log("single:", json.dumps(single))
+            comp["single_file_latency"] = single
     if "dir" in comps:
-        dir_comp = R.run_dir(max(1, min(args.steps, 3)))
-        log("dir:", json.dumps(dir_comp))
+        d = leg("dir", lambda: R.run_dir(max(1, min(args.steps, 3))))
+        if d:
+            log("dir:", json.dumps(d))
+            comp["dir"] = d
     cpu = None
-    if R.rank == 0 and R.world == 1 and not args.no_cpu:  # the CPU leg: rank 0 at N = 1 only
-        cpu = R.cpu_baseline()
-        log("cpu:", json.dumps(cpu))
-    R._cpu_sample = None
-    if getattr(R, "_single_root", None):
-        import shutil
-        shutil.rmtree(R._single_root, ignore_errors=True)
-        R._single_root = R._single_sample = None
-    if getattr(R, "_dir_sample", None):  # ranks > 0, or --no-cpu: drop the config-1 files
-        import shutil
-        shutil.rmtree(R._dir_sample[2], ignore_errors=True)
-        R._dir_sample = None
-    torch.cuda.empty_cache()
-    R._cpu_dedup = None
-    comp = {"cas": c["cas"], "identifier_job": c["job"]} if c else {}
-    if dir_comp:
-        comp["dir"] = dir_comp
-    if single:
-        comp["single_file_latency"] = single
+    if R.rank == 0 and R.world == 1 and not args.no_cpu and c:  # rank 0 at N = 1 only
+        cpu = leg("cpu_baseline", R.cpu_baseline)
+        if cpu:
+            log("cpu:", json.dumps(cpu))
+    line["cpu_baseline"] = cpu
+    leg("cleanup", R.drop_samples)
     if "dedup" in comps:
-        d = R.run_dedup(args.steps, args.warmup)
-        log("dedup:", json.dumps(d))
-        comp["dedup"] = d
-        if cpu is not None and R._cpu_dedup:
-            cpu["config4_grouping"] = R._cpu_dedup
-        torch.cuda.empty_cache()
+        d = leg("dedup", lambda: R.run_dedup(args.steps, args.warmup))
+        if d:
+            log("dedup:", json.dumps(d))
+            comp["dedup"] = d
+            if cpu is not None and getattr(R, "_cpu_dedup", None):
+                cpu["config4_grouping"] = R._cpu_dedup
+        R._cpu_dedup = None
+        R.free()
     if "consumers" in comps:
-        k = R.run_consumers(args.steps, args.warmup)
-        log("consumers:", json.dumps(k))
-        comp["consumers"] = k
-        torch.cuda.empty_cache()
+        k = leg("consumers", lambda: R.run_consumers(args.steps, args.warmup))
+        if k:
+            log("consumers:", json.dumps(k))
+            comp["consumers"] = k
+        R.free()
     if "staged" in comps:
-        g = R.run_staged()
-        log("staged:", json.dumps(g))
-        comp["staged"] = g
-        torch.cuda.empty_cache()
+        g = leg("staged", R.run_staged)
+        if g:
+            log("staged:", json.dumps(g))
+            comp["staged"] = g
+        R.free()
+        if g and getattr(R, "_staged_verify", None) is not None:
+            v = leg("staged_oracle", R.staged_oracle)
+            if v:
+                log("staged_oracle:", json.dumps(v))
+                g["verify_whole_run"] = v
+        R._staged_verify = None
     if "checksum" in comps:
-        k = R.run_checksum(args.steps, args.warmup)
-        log("checksum:", json.dumps(k))
-        comp["checksum"] = k
-        torch.cuda.empty_cache()
-
-    if c is None:  # profiling pass over some components: no headline value
-        if R.rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "components": comp,
-                              "note": "--components without cas: profiling pass, no headline"}),
-                  file=json_out, flush=True)
-        if R.comm is not None:
-            R.comm.close()
-        if R.world > 1:
-            R.dist.destroy_process_group()
-        return
-    ri = c["roofline_inputs"]
-    ops = ri["leaf_compressions"] * ISA_PER_COMPRESSION
-    t_leaf = ri["avg_leaves_s"]
-    achieved = ops / t_leaf if t_leaf > 0 else 0.0
-    traffic, traffic_src = pmc_traffic("k_leaves3")
-    roof = {"bound": "valu", "kernel": "cas_leaves (K1 k_leaves3)",
-            "achieved": achieved / 1e12, "peak": VALU_PEAK_SPEC / 1e12, "unit": "Tops/s",
-            "frac": achieved / VALU_PEAK_SPEC, "traffic": traffic,
-            "traffic_source": traffic_src,
-            "peak_measured": compress_peak / 1e12,
-            "peak_measured_note": "register-only BLAKE3 compressions (same 680-VALU stream, no "
-                                  "memory traffic): the attainable issue roof of this mix",
-            "peak_g_mix_probe": valu_peak / 1e12, "peak_by_class_measured": classes,
-            "frac_of_measured": achieved / compress_peak if compress_peak else None,
-            "algorithmic_per_launch": {"compressions": ri["leaf_compressions"],
-                                       "int32_ops": ops, "window_bytes": ri["bytes"]},
-            "compressions_per_s": ri["leaf_compressions"] / t_leaf if t_leaf else None,
-            "hbm_GBps": ri["bytes"] / t_leaf / 1e9 if t_leaf else None,
-            "hbm_frac": ri["bytes"] / t_leaf / HBM_PEAK if t_leaf else None}
-    job = c["job"]
-    line = {"metric": METRIC, "value": job["value"], "unit": "files/s", "n_gpus": R.world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": job["ms_per_step"],
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (BASELINE configs 2/3/4 shapes, generated in HBM)",
-            "config": {"workload": "identifier job step: config2 (1M files/GPU) cas_id + "
-                                   "sharded cas_id->Object grouping + Object link batch",
-                       "files_per_gpu": args.files, "global_files": args.files * R.world,
-                       "parallelism": f"dp{R.world} (files) + hash-sharded dedup, RCCL all-to-all"},
-            "components": comp, "kernels": c["kernels"], "roofline": roof, "cpu_baseline": cpu,
-            "world": {"dist_world_size": R.dist.get_world_size() if R.world > 1 else 1,
-                      "devices_visible": torch.cuda.device_count(),
-                      "backend": R.backend, "exchange": R.exchange_name()}}
-    if R.rank == 0:
-        print(json.dumps(line), file=json_out, flush=True)
-    if R.comm is not None:
-        R.comm.close()
-    if R.world > 1:
-        R.dist.destroy_process_group()
+        k = leg("checksum", lambda: R.run_checksum(args.steps, args.warmup))
+        if k:
+            log("checksum:", json.dumps(k))
+            comp["checksum"] = k
+        R.free()
+    line["world"] = R.world_info()  # after the legs: exchange volume of the run
+    if c is None and "cas" not in comps:
+        line["note"] = "--components without cas: profiling pass, no headline"
+    walls["total"] = round(time.perf_counter() - t_begin, 2)
+    writer.emit()
+    leg("shutdown", R.shutdown)
 
 
 if __name__ == "__main__":

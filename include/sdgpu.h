@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SDGPU_ABI_VERSION 2
+#define SDGPU_ABI_VERSION 3
 
 /* cas.rs:10-15 */
 #define SDGPU_CAS_SAMPLE_COUNT 4u
@@ -198,8 +198,12 @@ int sdgpu_group_rows_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t
  * A device hash table key -> value lives with one context.  Values are either
  * a row rank (the Object created by that row in an earlier batch of the same
  * run) or SDGPU_REP_EXISTING | handle for an Object registered by the caller
- * (handle < 2^31, e.g. the Object's database id).  A key keeps the minimum
- * value inserted for it (the canonical "first" Object).
+ * (handle < 2^31, e.g. the Object's database id).  A key keeps the canonical
+ * "first" Object: a registered (pre-existing) Object before any
+ * Object created during the run, whatever the order of the calls (find_many,
+ * mod.rs:168-185, returns Objects already in the database); the lowest handle
+ * among registered ones, the lowest rank among created ones.  Row ranks must
+ * be < 2^31 (SDGPU_REP_EXISTING is the top bit).
  * Grouping batches in id order through one index yields exactly the grouping
  * of the whole run (tests/test_gpu_index.py). */
 #define SDGPU_REP_EXISTING 0x80000000u
@@ -245,18 +249,47 @@ int sdgpu_dedup_batch(sdgpu_ctx *ctx, sdgpu_index *idx, const uint64_t *key,
 #define SDGPU_TRANSPORT_RCCL 1
 #define SDGPU_TRANSPORT_PEER 2
 typedef struct sdgpu_comm sdgpu_comm;
-/* One process per GPU: rank 0 creates the id, every rank receives it
- * out of band and joins (blocks until all nranks have joined). */
+/* Failure model (ABI 3).  RCCL communicators are created non-blocking; every
+ * wait on a peer (joining, the count exchange's one synchronisation,
+ * sdgpu_comm_wait) is bounded by the communicator's timeout.  When it passes,
+ * or a local step of the exchange fails, the communicator is aborted (its
+ * queued kernels exit) and the call returns -ETIMEDOUT (or the local error);
+ * the peers then time out too, so a missing or failed rank ends the job with
+ * an error on every rank instead of a hang.  An aborted communicator returns
+ * -ECONNABORTED from every later exchange; destroy it. */
 int sdgpu_comm_unique_id(uint8_t id[SDGPU_COMM_ID_BYTES]);
+/* One process per GPU: rank 0 creates the id, every rank receives it out of
+ * band and joins; returns when all nranks have joined, or -ETIMEDOUT after
+ * timeout_ms (> 0).  The timeout also bounds the communicator's exchanges. */
+int sdgpu_comm_init_rank_timeout(sdgpu_ctx *ctx, int nranks, int rank,
+                                 const uint8_t id[SDGPU_COMM_ID_BYTES], int timeout_ms,
+                                 sdgpu_comm **out);
+/* The same with the timeout from env SDGPU_COMM_TIMEOUT_MS (default 300 s). */
 int sdgpu_comm_init_rank(sdgpu_ctx *ctx, int nranks, int rank,
                          const uint8_t id[SDGPU_COMM_ID_BYTES], sdgpu_comm **out);
 /* One process driving ngpu contexts: out[r] is rank r's communicator. */
 int sdgpu_comm_init_all(sdgpu_ctx *const *ctx, int ngpu, int transport, sdgpu_comm **out);
 int sdgpu_comm_destroy(sdgpu_comm *comm);
 int sdgpu_comm_info(sdgpu_comm *comm, int *nranks, int *rank, int *transport);
+int sdgpu_comm_set_timeout(sdgpu_comm *comm, int timeout_ms);
+/* Waits, bounded by the timeout, until `stream` (NULL: the stream of the
+ * communicator's last exchange) has drained -- i.e. the reps of the last
+ * sdgpu_group_sharded_device are written.  -ETIMEDOUT (communicator aborted)
+ * if a peer never completes its side. */
+int sdgpu_comm_wait(sdgpu_comm *comm, void *stream);
+/* Cumulative exchange volume of this rank (bytes = 12-B records + 4-B reps). */
+typedef struct sdgpu_comm_stats_t {
+  uint64_t calls;
+  uint64_t rows_sent, rows_received;      /* keyed rows to / from every rank incl. self */
+  uint64_t bytes_sent, bytes_received;    /* payload incl. the self share */
+  uint64_t bytes_remote;                  /* payload that crossed to / from other ranks */
+  double count_wait_ms;                   /* host ms until the counts were known */
+  double host_ms;                         /* host ms inside the exchange calls */
+} sdgpu_comm_stats_t;
+int sdgpu_comm_stats(sdgpu_comm *comm, sdgpu_comm_stats_t *out);
 /* Collective, one process per GPU (RCCL): every rank calls it with its own
- * rows (global ranks in d_rank, required); rep for each of its rows.  idx
- * (may be NULL) is this rank's share of the Object index. */
+ * rows (global ranks in d_rank, required, each < 2^31); rep for each of its
+ * rows.  idx (may be NULL) is this rank's share of the Object index. */
 int sdgpu_group_sharded_device(sdgpu_ctx *ctx, sdgpu_comm *comm, sdgpu_index *idx,
                                const uint64_t *d_key, const uint8_t *d_has_key,
                                const uint32_t *d_rank, uint64_t n, uint32_t chunk_rows,

@@ -355,3 +355,28 @@ def thumbnail_shards(cas8: np.ndarray, valid=None):
     rows = np.arange(first.size) if valid is None else np.flatnonzero(np.asarray(valid))
     order = rows[np.argsort(first[rows], kind="stable")]
     return order.astype(np.int32), np.bincount(first[rows], minlength=256).astype(np.int32)
+
+
+def mix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finalizer (the bijection csrc/rows_device.hpp uses for row
+    hashes and the config-5 key variation)."""
+    z = np.asarray(x, np.uint64).copy()
+    with np.errstate(over="ignore"):
+        z ^= z >> np.uint64(30)
+        z *= np.uint64(0xBF58476D1CE4E5B9)
+        z ^= z >> np.uint64(27)
+        z *= np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return z
+
+
+def vary_keys(key: np.ndarray, vary: np.ndarray, step: int) -> np.ndarray:
+    """Keys of step `step` of the bench's config-5 run (synthetic-corpus
+    convention, not a reference function): rows marked `vary` stand for files
+    with new content, key' = mix64(key ^ step * phi64); step 0 unchanged."""
+    key = np.asarray(key, np.uint64)
+    if step == 0:
+        return key.copy()
+    with np.errstate(over="ignore"):
+        s = np.uint64((step * 0x9E3779B97F4A7C15) & (2**64 - 1))
+    return np.where(np.asarray(vary) != 0, mix64(key ^ s), key)

@@ -14,8 +14,13 @@
 // linear probing from row_hash(key) & (cap - 1) (four slots per 64-B line, so a
 // probe is one line read at load <= 1/2).  Empty slot: key == ~0; the key ~0
 // itself lives in a separate special slot.  Inserts: 64-bit agent-scope CAS
-// on the key, then atomicMin on the value, so one key keeps the MINIMUM value
-// inserted for it.
+// on the key, then atomicMin on the value's slot encoding, so one key keeps
+// the first Object in this order: any pre-existing Object (lowest handle)
+// before any Object created during the run (lowest rank) -- the reference's
+// find_many (mod.rs:168-185) returns Objects already in the database, so an
+// Object registered with add_objects wins whatever the call order.  Slot
+// encoding: enc = value ^ EXISTING (existing handles map below 2^31, ranks
+// above; the empty value 0xFFFFFFFF stays above both).
 //
 // Values: a row rank r (< 2^31) -- the Object created by row r of this or an
 // earlier batch of the same run -- or SDGPU_REP_EXISTING | handle for an
@@ -40,11 +45,15 @@ __device__ __forceinline__ uint64_t slot_key(const uint4& q) {
   return (static_cast<uint64_t>(q.y) << 32) | q.x;
 }
 
-// Insert (k, v): value = min over inserts.  Returns nothing; counts new keys.
+__device__ __forceinline__ uint32_t enc_value(uint32_t v) { return v ^ kRepExisting; }
+
+// Insert (k, v): keeps the minimum enc_value over inserts (existing Objects
+// first).  Returns nothing; counts new keys.
 __device__ __forceinline__ void index_insert(const IndexRef& t, uint64_t k, uint32_t v) {
+  const uint32_t e = enc_value(v);
   if (k == kEmptyKey) {
     atomicMax(&t.special[0], 1u);
-    atomicMin(&t.special[1], v);
+    atomicMin(&t.special[1], e);
     return;
   }
   uint64_t h = row_hash(k) & (t.cap - 1);
@@ -54,7 +63,7 @@ __device__ __forceinline__ void index_insert(const IndexRef& t, uint64_t k, uint
         atomicCAS(kp, static_cast<unsigned long long>(kEmptyKey), static_cast<unsigned long long>(k));
     if (prev == kEmptyKey || prev == k) {
       if (prev == kEmptyKey) atomicAdd(t.count, 1ull);
-      atomicMin(&t.slots[h].z, v);
+      atomicMin(&t.slots[h].z, e);
       return;
     }
     h = (h + 1) & (t.cap - 1);
@@ -64,7 +73,7 @@ __device__ __forceinline__ void index_insert(const IndexRef& t, uint64_t k, uint
 // Value of k, or false.
 __device__ __forceinline__ bool index_find(const IndexRef& t, uint64_t k, uint32_t& v) {
   if (k == kEmptyKey) {
-    v = t.special[1];
+    v = enc_value(t.special[1]);
     return t.special[0] != 0;
   }
   uint64_t h = row_hash(k) & (t.cap - 1);
@@ -72,7 +81,7 @@ __device__ __forceinline__ bool index_find(const IndexRef& t, uint64_t k, uint32
     const uint4 q = t.slots[h];
     const uint64_t sk = slot_key(q);
     if (sk == k) {
-      v = q.z;
+      v = enc_value(q.z);
       return true;
     }
     if (sk == kEmptyKey) return false;
@@ -98,7 +107,7 @@ __global__ __launch_bounds__(kThreads) void k_index_rehash(IndexRef from, IndexR
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < from.cap;
        i += stride) {
     const uint4 q = from.slots[i];
-    if (slot_key(q) != kEmptyKey) index_insert(to, slot_key(q), q.z);
+    if (slot_key(q) != kEmptyKey) index_insert(to, slot_key(q), enc_value(q.z));
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && from.special[0]) {
     to.special[0] = 1;

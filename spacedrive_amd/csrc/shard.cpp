@@ -22,9 +22,12 @@
 // sdgpu_comm_init_all), and, for contexts that share a device (RCCL refuses
 // two ranks on one GPU: the one-GPU test box), device-to-device peer copies
 // ordered by events.  Both move the same buffers in the same pattern.
+#include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -39,6 +42,13 @@ struct sdgpu_comm {
   int transport = SDGPU_TRANSPORT_RCCL;
   int device = 0;
   ncclComm_t nccl = nullptr;
+  // RCCL communicators are non-blocking (config.blocking = 0): every wait on
+  // a peer is polled against this deadline and the communicator is aborted
+  // when it passes, so a rank that never arrives costs -ETIMEDOUT, not a hang
+  int timeout_ms = 0;
+  bool aborted = false;
+  hipStream_t last_stream = nullptr;  // stream of the last exchange (sdgpu_comm_wait)
+  sdgpu_comm_stats_t stats{};
 };
 
 struct sdgpu_index {
@@ -59,6 +69,79 @@ int nccl_err(ncclResult_t r) { return r == ncclSuccess ? 0 : -EIO; }
     const int rc_ = nccl_err(expr);            \
     if (rc_ != 0) return rc_;                  \
   } while (0)
+
+constexpr int kDefaultCommTimeoutMs = 300000;
+
+// SDGPU_COMM_TIMEOUT_MS, read once per communicator (init), else 300 s.
+int default_timeout_ms() {
+  const char* e = getenv("SDGPU_COMM_TIMEOUT_MS");
+  if (e && *e) {
+    const long v = strtol(e, nullptr, 10);
+    if (v > 0 && v < (1l << 30)) return static_cast<int>(v);
+  }
+  return kDefaultCommTimeoutMs;
+}
+
+using Clock = std::chrono::steady_clock;
+
+Clock::time_point deadline_of(int timeout_ms) {
+  return Clock::now() + std::chrono::milliseconds(timeout_ms);
+}
+
+// Spin briefly (the count exchange is on the step's critical path), then back off.
+void backoff(int& spins) {
+  if (++spins < 2000) {
+    std::this_thread::yield();
+  } else {
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+// Abort an RCCL communicator after a local failure or an expired deadline:
+// its kernels still queued on the device exit, its peers see their own
+// deadline pass (a local error becomes a bounded job-wide failure, never a
+// hang).  The communicator is unusable afterwards (-ECONNABORTED).
+int comm_fail(sdgpu_comm* m, int rc) {
+  if (m && m->nccl && !m->aborted) {
+    (void)hipSetDevice(m->device);
+    (void)ncclCommAbort(m->nccl);
+    m->nccl = nullptr;
+    m->aborted = true;
+  }
+  return rc;
+}
+
+// Waits until the communicator's non-blocking operation settles.
+int nccl_settle(sdgpu_comm* m, Clock::time_point deadline) {
+  int spins = 0;
+  for (;;) {
+    ncclResult_t a = ncclSuccess;
+    if (ncclCommGetAsyncError(m->nccl, &a) != ncclSuccess) return comm_fail(m, -EIO);
+    if (a == ncclSuccess) return 0;
+    if (a != ncclInProgress) return comm_fail(m, -EIO);
+    if (Clock::now() > deadline) return comm_fail(m, -ETIMEDOUT);
+    backoff(spins);
+  }
+}
+
+// Waits for stream s to drain while the communicator's peers may still be
+// missing: polled, with the communicator's asynchronous error checked, up to
+// the deadline.
+int stream_wait(sdgpu_comm* m, hipStream_t s, Clock::time_point deadline) {
+  if (!m->nccl) return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
+  int spins = 0;
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return comm_fail(m, map_err(q));
+    ncclResult_t a = ncclSuccess;
+    if (ncclCommGetAsyncError(m->nccl, &a) != ncclSuccess ||
+        (a != ncclSuccess && a != ncclInProgress))
+      return comm_fail(m, -EIO);
+    if (Clock::now() > deadline) return comm_fail(m, -ETIMEDOUT);
+    backoff(spins);
+  }
+}
 
 // ---- Object index ------------------------------------------------------------
 
@@ -154,32 +237,48 @@ struct RankJob {
 // One all-to-all round: rank j sends bytes(j, p) from sendp(j, p) to every p
 // and receives rbytes(j, p) into recvp(j, p) from every p.
 template <typename SP, typename RP, typename SB, typename RB>
-int alltoallv(std::vector<RankJob>& J, int W, SP sendp, RP recvp, SB sbytes, RB rbytes) {
+int alltoallv(std::vector<RankJob>& J, int W, Clock::time_point deadline, SP sendp, RP recvp,
+              SB sbytes, RB rbytes) {
   const int transport = J[0].comm->transport;
   if (transport == SDGPU_TRANSPORT_RCCL) {
-    SD_NCCL(ncclGroupStart());
+    // non-blocking communicators: calls inside the group may report
+    // ncclInProgress; ncclGroupEnd's completion is polled per communicator
+    auto ok = [](ncclResult_t r) { return r == ncclSuccess || r == ncclInProgress; };
+    if (!ok(ncclGroupStart())) return comm_fail(J[0].comm, -EIO);
+    bool fail = false;
     for (auto& j : J) {
-      for (int p = 0; p < W; ++p) {
-        SD_NCCL(ncclSend(sendp(j, p), sbytes(j, p), ncclUint8, p, j.comm->nccl, j.s));
-        SD_NCCL(ncclRecv(recvp(j, p), rbytes(j, p), ncclUint8, p, j.comm->nccl, j.s));
+      for (int p = 0; p < W && !fail; ++p) {
+        fail |= !ok(ncclSend(sendp(j, p), sbytes(j, p), ncclUint8, p, j.comm->nccl, j.s));
+        fail |= !ok(ncclRecv(recvp(j, p), rbytes(j, p), ncclUint8, p, j.comm->nccl, j.s));
       }
     }
-    SD_NCCL(ncclGroupEnd());
+    const ncclResult_t e = ncclGroupEnd();
+    if (fail || !ok(e)) {
+      for (auto& j : J) comm_fail(j.comm, -EIO);
+      return -EIO;
+    }
+    for (auto& j : J) SD_TRY_RC(nccl_settle(j.comm, deadline));
     return 0;
   }
-  // peer copies: all ranks live in this process (J holds every rank, J[r] is rank r)
+  // peer copies: all ranks live in this process (J holds every rank, J[r] is rank r).
+  // An event belongs to the device current at its creation and may only be
+  // recorded on a stream of that device (waits may cross devices), so rank r's
+  // events are created -- and recorded -- with rank r's device current.
   if (static_cast<int>(J.size()) != W) return -EINVAL;
-  std::vector<hipEvent_t> ready(W), done(W);
+  std::vector<hipEvent_t> ready(W, nullptr), done(W, nullptr);
   int rc = 0;
   for (int r = 0; r < W && rc == 0; ++r) {
-    if (hipEventCreateWithFlags(&ready[r], hipEventDisableTiming) != hipSuccess ||
+    if (hipSetDevice(J[r].c->device) != hipSuccess ||
+        hipEventCreateWithFlags(&ready[r], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&done[r], hipEventDisableTiming) != hipSuccess)
       rc = -EIO;
   }
   for (int r = 0; r < W && rc == 0; ++r)
-    if (hipEventRecord(ready[r], J[r].s) != hipSuccess) rc = -EIO;
+    if (hipSetDevice(J[r].c->device) != hipSuccess || hipEventRecord(ready[r], J[r].s) != hipSuccess)
+      rc = -EIO;
   for (int d = 0; d < W && rc == 0; ++d) {  // receiver d pulls from every source
     RankJob& jd = J[d];
+    if (hipSetDevice(jd.c->device) != hipSuccess) rc = -EIO;
     for (int src = 0; src < W && rc == 0; ++src) {
       const size_t b = rbytes(jd, src);
       if (b != sbytes(J[src], d)) {
@@ -195,17 +294,37 @@ int alltoallv(std::vector<RankJob>& J, int W, SP sendp, RP recvp, SB sbytes, RB 
     if (rc == 0 && hipEventRecord(done[d], jd.s) != hipSuccess) rc = -EIO;
   }
   // a source may reuse its send buffer only after every receiver copied it
-  for (int src = 0; src < W && rc == 0; ++src)
+  for (int src = 0; src < W && rc == 0; ++src) {
+    if (hipSetDevice(J[src].c->device) != hipSuccess) rc = -EIO;
     for (int d = 0; d < W && rc == 0; ++d)
       if (hipStreamWaitEvent(J[src].s, done[d], 0) != hipSuccess) rc = -EIO;
+  }
   for (int r = 0; r < W; ++r) {
+    (void)hipSetDevice(J[r].c->device);
     if (ready[r]) (void)hipEventDestroy(ready[r]);
     if (done[r]) (void)hipEventDestroy(done[r]);
   }
   return rc;
 }
 
+int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows);
+
+// One exchange step; any failure on an RCCL rank aborts its communicator
+// (bounded failure for the peers) and is returned.
 int run_sharded(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
+  for (auto& j : J)
+    if (j.comm->aborted || (j.comm->transport == SDGPU_TRANSPORT_RCCL && !j.comm->nccl))
+      return -ECONNABORTED;
+  const int rc = run_sharded_impl(J, W, chunk_rows);
+  if (rc != 0)
+    for (auto& j : J)
+      if (j.comm->transport == SDGPU_TRANSPORT_RCCL) comm_fail(j.comm, rc);
+  return rc;
+}
+
+int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
+  const auto t_start = Clock::now();
+  const Clock::time_point deadline = deadline_of(J[0].comm->timeout_ms);
   // 1. send side: packed records by owner + per-owner counts, on each GPU
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
@@ -227,7 +346,7 @@ int run_sharded(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
   }
   // 2. counts all-to-all, then the one host synchronisation
   SD_TRY_RC(alltoallv(
-      J, W, [](RankJob& j, int p) -> void* { return j.dcnt + p; },
+      J, W, deadline, [](RankJob& j, int p) -> void* { return j.dcnt + p; },
       [](RankJob& j, int p) -> void* { return j.rcnt_d + p; },
       [](RankJob&, int) -> size_t { return 8; }, [](RankJob&, int) -> size_t { return 8; }));
   for (auto& j : J) {
@@ -237,7 +356,11 @@ int run_sharded(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
   }
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
-    SD_TRY(hipStreamSynchronize(j.s));
+    if (j.comm->transport == SDGPU_TRANSPORT_RCCL) {
+      SD_TRY_RC(stream_wait(j.comm, j.s, deadline));
+    } else {
+      SD_TRY(hipStreamSynchronize(j.s));
+    }
     j.scnt.assign(W, 0);
     j.rcnt.assign(W, 0);
     j.soff.assign(W + 1, 0);
@@ -262,9 +385,11 @@ int run_sharded(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
     j.rvalid = r + o_val;
     j.back = static_cast<uint32_t*>(j.c->xs_back.p);
   }
+  const double count_ms =
+      std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
   // 3. the rows, one message per (source, owner) pair
   SD_TRY_RC(alltoallv(
-      J, W, [](RankJob& j, int p) -> void* { return j.srec + 3 * j.soff[p]; },
+      J, W, deadline, [](RankJob& j, int p) -> void* { return j.srec + 3 * j.soff[p]; },
       [](RankJob& j, int p) -> void* { return j.rrec + 3 * j.roff[p]; },
       [](RankJob& j, int p) -> size_t { return 12 * j.scnt[p]; },
       [](RankJob& j, int p) -> size_t { return 12 * j.rcnt[p]; }));
@@ -278,13 +403,29 @@ int run_sharded(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
   }
   // 5. reps back to their sources, gathered to row order
   SD_TRY_RC(alltoallv(
-      J, W, [](RankJob& j, int p) -> void* { return j.rrep + j.roff[p]; },
+      J, W, deadline, [](RankJob& j, int p) -> void* { return j.rrep + j.roff[p]; },
       [](RankJob& j, int p) -> void* { return j.back + j.soff[p]; },
       [](RankJob& j, int p) -> size_t { return 4 * j.rcnt[p]; },
       [](RankJob& j, int p) -> size_t { return 4 * j.scnt[p]; }));
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
     SD_TRY(gather_rep_launch(j.back, j.spos, j.rank, j.n, j.rep, j.s));
+  }
+  const double call_ms =
+      std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
+  for (auto& j : J) {
+    // payload of this rank: records out + reps back, and what it received
+    const uint64_t self_rows = j.scnt[j.comm->rank];
+    sdgpu_comm_stats_t& st = j.comm->stats;
+    st.calls += 1;
+    st.rows_sent += j.total;
+    st.rows_received += j.m;
+    st.bytes_sent += 16 * j.total;      // 12-B records out, 4-B reps back
+    st.bytes_received += 16 * j.m;
+    st.bytes_remote += 16 * (j.total - self_rows) + 16 * (j.m - j.rcnt[j.comm->rank]);
+    st.count_wait_ms += count_ms;
+    st.host_ms += call_ms;
+    j.comm->last_stream = j.s;
   }
   return 0;
 }
@@ -311,28 +452,68 @@ int sdgpu_comm_unique_id(uint8_t id[SDGPU_COMM_ID_BYTES]) {
   return 0;
 }
 
-int sdgpu_comm_init_rank(sdgpu_ctx* c, int nranks, int rank, const uint8_t id[SDGPU_COMM_ID_BYTES],
-                         sdgpu_comm** out) {
-  if (!c || !id || !out || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks)
+int sdgpu_comm_init_rank_timeout(sdgpu_ctx* c, int nranks, int rank,
+                                 const uint8_t id[SDGPU_COMM_ID_BYTES], int timeout_ms,
+                                 sdgpu_comm** out) {
+  if (!c || !id || !out || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks ||
+      timeout_ms <= 0)
     return -EINVAL;
   *out = nullptr;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
-  ncclUniqueId u;
-  memcpy(&u, id, sizeof u);
-  ncclComm_t nc = nullptr;
-  SD_NCCL(ncclCommInitRank(&nc, nranks, u, rank));
   sdgpu_comm* m = new (std::nothrow) sdgpu_comm;
-  if (!m) {
-    (void)ncclCommDestroy(nc);
-    return -ENOMEM;
-  }
+  if (!m) return -ENOMEM;
   m->nranks = nranks;
   m->rank = rank;
   m->transport = SDGPU_TRANSPORT_RCCL;
   m->device = c->device;
-  m->nccl = nc;
+  m->timeout_ms = timeout_ms;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  // non-blocking init: the bootstrap runs while this thread polls the
+  // deadline; a rank that never joins aborts the init (-ETIMEDOUT)
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  const ncclResult_t r = ncclCommInitRankConfig(&m->nccl, nranks, u, rank, &cfg);
+  int rc = 0;
+  if (r != ncclSuccess && r != ncclInProgress) {
+    rc = m->nccl ? comm_fail(m, -EIO) : -EIO;
+  } else {
+    rc = nccl_settle(m, deadline_of(timeout_ms));
+  }
+  if (rc != 0) {
+    delete m;
+    return rc;
+  }
   *out = m;
+  return 0;
+}
+
+int sdgpu_comm_init_rank(sdgpu_ctx* c, int nranks, int rank, const uint8_t id[SDGPU_COMM_ID_BYTES],
+                         sdgpu_comm** out) {
+  return sdgpu_comm_init_rank_timeout(c, nranks, rank, id, default_timeout_ms(), out);
+}
+
+int sdgpu_comm_set_timeout(sdgpu_comm* m, int timeout_ms) {
+  if (!m || timeout_ms <= 0) return -EINVAL;
+  m->timeout_ms = timeout_ms;
+  return 0;
+}
+
+int sdgpu_comm_wait(sdgpu_comm* m, void* stream) {
+  if (!m) return -EINVAL;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : m->last_stream;
+  if (!s) return 0;
+  if (m->aborted) return -ECONNABORTED;
+  SD_TRY(hipSetDevice(m->device));
+  if (m->transport != SDGPU_TRANSPORT_RCCL || !m->nccl)
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
+  return stream_wait(m, s, deadline_of(m->timeout_ms));
+}
+
+int sdgpu_comm_stats(sdgpu_comm* m, sdgpu_comm_stats_t* out) {
+  if (!m || !out) return -EINVAL;
+  *out = m->stats;
   return 0;
 }
 
@@ -359,14 +540,24 @@ int sdgpu_comm_init_all(sdgpu_ctx* const* ctx, int ngpu, int transport, sdgpu_co
           (void)hipGetLastError();
         }
   }
+  const int tmo = default_timeout_ms();
   for (int i = 0; i < ngpu; ++i) {
     sdgpu_comm* m = new (std::nothrow) sdgpu_comm;
-    if (!m) return -ENOMEM;
+    if (!m) {
+      for (int q = 0; q < i; ++q) {
+        delete out[q];
+        out[q] = nullptr;
+      }
+      for (int q = i; q < ngpu; ++q)
+        if (nc[q]) (void)ncclCommDestroy(nc[q]);
+      return -ENOMEM;
+    }
     m->nranks = ngpu;
     m->rank = i;
     m->transport = transport;
     m->device = ctx[i]->device;
     m->nccl = nc[i];
+    m->timeout_ms = tmo;
     out[i] = m;
   }
   return 0;
@@ -376,7 +567,21 @@ int sdgpu_comm_destroy(sdgpu_comm* m) {
   if (!m) return -EINVAL;
   if (m->nccl) {
     (void)hipSetDevice(m->device);
-    (void)ncclCommDestroy(m->nccl);
+    // non-blocking communicator: finalize (may report ncclInProgress while
+    // peers flush) is settled against the deadline, then destroyed; a peer
+    // that never finishes gets the communicator aborted instead
+    const ncclResult_t r = ncclCommFinalize(m->nccl);
+    bool settled = r == ncclSuccess;
+    if (r == ncclInProgress) settled = nccl_settle(m, deadline_of(m->timeout_ms > 0
+                                                                        ? m->timeout_ms
+                                                                        : 10000)) == 0;
+    if (m->nccl) {  // nccl_settle aborts (and clears) on failure
+      if (settled)
+        (void)ncclCommDestroy(m->nccl);
+      else
+        (void)ncclCommAbort(m->nccl);
+    }
+    m->nccl = nullptr;
   }
   delete m;
   return 0;
@@ -467,6 +672,9 @@ int sdgpu_group_rows_indexed_device(sdgpu_ctx* c, sdgpu_index* x, const uint64_t
       (n && (!d_key || !d_rep)))
     return -EINVAL;
   if (n >= (1ull << 32)) return -EINVAL;
+  // index values are ranks < 2^31 (the top bit marks existing Objects): with
+  // implicit ranks (d_rank NULL, rank = i) that bounds n
+  if (!d_rank && n > kRepExisting) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
   hipStream_t s = pick(c, stream);

@@ -18,6 +18,7 @@ built from libsdgpu's single steps.
 """
 from __future__ import annotations
 
+import ctypes
 
 import numpy as np
 
@@ -273,6 +274,14 @@ def dedup_batch(key, has_key, first_rank: int, index: ObjectIndex | None = None,
 TRANSPORT_AUTO, TRANSPORT_RCCL, TRANSPORT_PEER = 0, 1, 2
 
 
+class CommStats(ctypes.Structure):
+    """sdgpu_comm_stats_t (include/sdgpu.h)."""
+    _fields_ = [("calls", ctypes.c_uint64), ("rows_sent", ctypes.c_uint64),
+                ("rows_received", ctypes.c_uint64), ("bytes_sent", ctypes.c_uint64),
+                ("bytes_received", ctypes.c_uint64), ("bytes_remote", ctypes.c_uint64),
+                ("count_wait_ms", ctypes.c_double), ("host_ms", ctypes.c_double)]
+
+
 class Comm:
     """A libsdgpu communicator (sdgpu_comm_*)."""
 
@@ -287,14 +296,37 @@ class Comm:
         return bytes(buf)
 
     @classmethod
-    def init_rank(cls, ctx, nranks: int, rank: int, uid: bytes) -> "Comm":
-        """One process per GPU (RCCL): every rank joins with rank 0's id."""
+    def init_rank(cls, ctx, nranks: int, rank: int, uid: bytes,
+                  timeout_ms: int | None = None) -> "Comm":
+        """One process per GPU (RCCL): every rank joins with rank 0's id.
+        Raises SdgpuError(-ETIMEDOUT) when not every rank joins within
+        timeout_ms (None: SDGPU_COMM_TIMEOUT_MS or 300 s), which also bounds
+        every later exchange of the communicator."""
         import ctypes
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         h = ctypes.c_void_p()
-        check(ctx.lib.sdgpu_comm_init_rank(ctx.h, nranks, rank, buf, ctypes.byref(h)),
-              "sdgpu_comm_init_rank")
+        if timeout_ms is None:
+            check(ctx.lib.sdgpu_comm_init_rank(ctx.h, nranks, rank, buf, ctypes.byref(h)),
+                  "sdgpu_comm_init_rank")
+        else:
+            check(ctx.lib.sdgpu_comm_init_rank_timeout(ctx.h, nranks, rank, buf, int(timeout_ms),
+                                                       ctypes.byref(h)),
+                  "sdgpu_comm_init_rank_timeout")
         return cls(ctx, h)
+
+    def set_timeout(self, timeout_ms: int):
+        check(self.ctx.lib.sdgpu_comm_set_timeout(self.h, int(timeout_ms)),
+              "sdgpu_comm_set_timeout")
+
+    def wait(self, stream=None):
+        """Bounded wait for the last exchange's stream (sdgpu_comm_wait)."""
+        check(self.ctx.lib.sdgpu_comm_wait(self.h, stream), "sdgpu_comm_wait")
+
+    def stats(self) -> dict:
+        """Cumulative exchange volume / host time of this rank (sdgpu_comm_stats)."""
+        st = CommStats()
+        check(self.ctx.lib.sdgpu_comm_stats(self.h, ctypes.byref(st)), "sdgpu_comm_stats")
+        return {f: getattr(st, f) for f, _ in CommStats._fields_}
 
     @classmethod
     def init_all(cls, ctxs, transport: int = TRANSPORT_AUTO) -> list:
@@ -354,7 +386,8 @@ def group_sharded_all(keys, hass, ranks, comms, indexes=None, chunk_rows: int = 
     check(ctxs[0].lib.sdgpu_group_sharded_all_device(
         arr([c.h.value for c in ctxs]), arr([c.h.value for c in comms]),
         arr([i.h.value for i in indexes]) if indexes else None, W,
-        arr([k.data_ptr() for k in keys]), arr([h.data_ptr() for h in hass]) if hass else None,
+        arr([k.data_ptr() for k in keys]),
+        arr([h.data_ptr() if h is not None else None for h in hass]) if hass else None,
         arr([r.data_ptr() for r in ranks]), n, chunk_rows, arr([r.data_ptr() for r in reps]),
         arr([torch.cuda.current_stream(k.device).cuda_stream for k in keys])),
         "sdgpu_group_sharded_all_device")

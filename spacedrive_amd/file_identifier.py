@@ -146,6 +146,9 @@ class FilePaths:
         self.cas_id: list[str | None] = []
         self.object_id: list[int | None] = []
         self.next_object_id = 1
+        # per location, the ids of its non-directory rows (ascending: ids are
+        # appended in order) -- the index the orphan query walks from the cursor
+        self._file_rows: dict[int, list[int]] = {}
 
     def add(self, location_id: int, materialized_path: str, name: str,
             is_dir: bool = False) -> int:
@@ -156,7 +159,10 @@ class FilePaths:
         self.is_dir.append(is_dir)
         self.cas_id.append(None)
         self.object_id.append(None)
-        return len(self.name)
+        fid = len(self.name)
+        if not is_dir:
+            self._file_rows.setdefault(location_id, []).append(fid)
+        return fid
 
     def __len__(self):
         return len(self.name)
@@ -166,18 +172,22 @@ class FilePaths:
         return self.materialized_path[i].lstrip("/") + self.name[i]
 
     def orphans(self, location_id: int, cursor: int | None = None,
-                children_of: str | None = None, under: str | None = None) -> list[int]:
+                children_of: str | None = None, under: str | None = None,
+                limit: int | None = None) -> list[int]:
         """ids of orphan rows in ascending id (orphan_path_filters,
         file_identifier_job.rs:245-268 / shallow.rs:121-139): object_id NULL,
         !is_dir, the location, id >= cursor, and either a subtree
-        (materialized_path starts with `under`) or one directory's children."""
+        (materialized_path starts with `under`) or one directory's children;
+        at most `limit` of them (the query's LIMIT, :286-309).  Walks the
+        location's file rows from the cursor (bisect), so a job step costs
+        about its own rows, not a scan of the table."""
+        import bisect
+        rows = self._file_rows.get(location_id, [])
         out = []
-        start = max(1, cursor or 1)
-        for fid in range(start, len(self.name) + 1):
+        for j in range(bisect.bisect_left(rows, max(1, cursor or 1)), len(rows)):
+            fid = rows[j]
             i = fid - 1
-            if self.object_id[i] is not None or self.is_dir[i]:
-                continue
-            if self.location_id[i] != location_id:
+            if self.object_id[i] is not None:
                 continue
             mp = self.materialized_path[i]
             if children_of is not None and mp != children_of:
@@ -185,6 +195,8 @@ class FilePaths:
             if under is not None and not mp.startswith(under):
                 continue
             out.append(fid)
+            if limit is not None and len(out) >= limit:
+                break
         return out
 
     def existing_objects(self):
@@ -260,8 +272,8 @@ class FileIdentifierJob:
         self._open_index()
         return self
 
-    def _orphans(self, cursor):
-        return self.table.orphans(self.location_id, cursor, self._children_of, self._under)
+    def _orphans(self, cursor, limit=None):
+        return self.table.orphans(self.location_id, cursor, self._children_of, self._under, limit)
 
     def _open_index(self):
         import torch
@@ -280,7 +292,7 @@ class FileIdentifierJob:
         if self.done():
             return self.meta
         nchunks = min(self.chunks_per_step, self.task_count - self.step_number)
-        cand = self._orphans(self.meta.cursor)[:nchunks * CHUNK_SIZE + nchunks]
+        cand = self._orphans(self.meta.cursor, nchunks * CHUNK_SIZE + nchunks)
         if not cand:
             raise EarlyFinish("Expected orphan Paths not returned from database query for this chunk")
         paths = [os.path.join(self.location_path, self.table.rel_path(f)) for f in cand]

@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     lib = _native.load()
-    assert lib.sdgpu_abi_version() == 2
+    assert lib.sdgpu_abi_version() == 3
     assert lib.sdgpu_strerror(0) == b"success"
     assert lib.sdgpu_strerror(-22) == b"Invalid argument"
 
@@ -68,3 +68,41 @@ def test_product_path_has_no_oracle_dependency():
     out = subprocess.run(["ldd", _native.LIB_PATH], capture_output=True, text=True).stdout
     assert "liboracle" not in out
     assert ctypes.CDLL(_native.LIB_PATH)
+
+
+def test_rust_sys_crate_matches_header():
+    """crates/sdgpu-sys/src/lib.rs (the Rust FFI block of INTEGRATION.md §1) is
+    exactly what scripts/gen_rust_sys.py derives from include/sdgpu.h: one
+    `extern "C"` item per declared function, same names, same arity."""
+    import os
+    import re
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "gen_rust_sys.py"),
+                        "--check"])
+    assert r.returncode == 0, "crates/sdgpu-sys/src/lib.rs is stale: run scripts/gen_rust_sys.py"
+    rs = open(os.path.join(root, "crates", "sdgpu-sys", "src", "lib.rs")).read()
+    fns = dict(re.findall(r"pub fn (sdgpu_\w+)\(([^)]*)\)", rs))
+    assert sorted(fns) == _native.declared_symbols()
+    hdr = open(_native.HEADER_PATH).read()
+    for name, args in fns.items():
+        m = re.search(r"\b" + name + r"\s*\(([^;]*?)\)\s*;", hdr, re.S)
+        c_args = [a for a in m.group(1).split(",") if a.strip() not in ("", "void")]
+        assert len([a for a in args.split(",") if a.strip()]) == len(c_args), name
+
+
+def test_rust_wrappers_call_only_declared_symbols():
+    """The sd-core wrapper bodies (crates/sd-core-gpu: generate_cas_id,
+    file_checksum, the batched identifier step) call only entry points the
+    header declares, and keep the reference signatures."""
+    import os
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(root, "crates", "sd-core-gpu", "src")
+    text = "".join(open(os.path.join(src, f)).read() for f in sorted(os.listdir(src)))
+    used = set(re.findall(r"sys::(sdgpu_\w+)\(", text))
+    assert used and used <= set(_native.declared_symbols()), used - set(_native.declared_symbols())
+    assert ("pub async fn generate_cas_id(path: impl AsRef<Path>, size: u64) -> "
+            "Result<String, io::Error>") in text            # core/src/object/cas.rs:23
+    assert ("pub async fn file_checksum(path: impl AsRef<Path>) -> "
+            "Result<String, io::Error>") in text            # validation/hash.rs:10

@@ -80,6 +80,30 @@ def test_preexisting_objects(ctx):
     assert np.count_nonzero(rep & np.uint32(dedup.REP_EXISTING)) > 5000
 
 
+def test_objects_registered_after_a_batch_win(ctx):
+    """Objects registered AFTER a batch already created Objects for the same
+    cas_ids: later rows still link to the registered Objects, as
+    the reference's find_many (mod.rs:168-185) returns Objects already in the
+    database; the first batch's reps are unchanged and the other rows follow
+    the in-run rule over the whole run."""
+    import torch
+    from spacedrive_amd import dedup
+    key, has = _rows(31, 120_000, 50_000)
+    idx = dedup.ObjectIndex(ctx, 4096)
+    rep1 = dedup.dedup_batch(key[:60_000], has[:60_000], 0, idx, 100, ctx)
+    whole = O.group_reps(key, has, 100)
+    np.testing.assert_array_equal(rep1, whole[:60_000])
+    rng = np.random.default_rng(32)
+    ek = rng.choice(key[:60_000][has[:60_000] == 1], 4000)   # keys the first batch inserted
+    eh = rng.permutation(ek.size).astype(np.uint32) + 3
+    idx.add_objects(torch.from_numpy(ek.view(np.int64)).cuda(),
+                    torch.from_numpy(eh.view(np.int32)).cuda())
+    rep2 = dedup.dedup_batch(key[60_000:], has[60_000:], 60_000, idx, 100, ctx)
+    ref2 = O.group_reps_existing(key, has, 100, ek, eh)[60_000:]
+    np.testing.assert_array_equal(rep2, ref2)
+    assert np.count_nonzero(rep2 & np.uint32(dedup.REP_EXISTING)) > 1000
+
+
 def test_device_api_matches_host_api(ctx):
     import torch
     from spacedrive_amd import dedup

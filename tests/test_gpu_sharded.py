@@ -107,7 +107,51 @@ def test_rccl_transport_one_rank(ctx):
     for a, b in ((0, 200_000), (200_000, 500_000)):
         out.append(dedup.group_sharded(dk[a:b], dh[a:b], dr[a:b], comm, idx, 100).cpu().numpy())
     np.testing.assert_array_equal(np.concatenate(out).view(np.uint32), ref)
+    comm.wait()                       # bounded wait for the last exchange's stream
+    st = comm.stats()
+    keyed = int(h.sum())
+    assert st["calls"] == 5
+    assert st["rows_sent"] == st["rows_received"] == 4 * keyed   # 3 whole + 2 halves
+    assert st["bytes_sent"] == 16 * st["rows_sent"]
+    assert st["bytes_remote"] == 0    # one rank: every record is a self-send
     comm.close()
+
+
+_MISSING_PEER = r'''
+import errno, json, sys, time
+sys.path.insert(0, sys.argv[1])
+import torch
+from spacedrive_amd import dedup
+from spacedrive_amd._native import Context, SdgpuError
+ctx = Context(0)
+uid = dedup.Comm.unique_id()
+t0 = time.monotonic()
+try:
+    dedup.Comm.init_rank(ctx, 2, 0, uid, timeout_ms=int(sys.argv[2]))
+    rc = 0
+except SdgpuError as e:
+    rc = e.rc
+print(json.dumps({"rc": rc, "s": time.monotonic() - t0}), flush=True)
+'''
+
+
+def test_rccl_missing_peer_times_out():
+    """VERDICT r2 item 3: a 2-rank communicator whose second rank never
+    joins returns -ETIMEDOUT within the deadline instead of blocking forever
+    (non-blocking ncclCommInitRankConfig polled, ncclCommAbort on expiry).
+    Run in a fresh child process so an abort cannot disturb this one."""
+    import errno
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _MISSING_PEER, root, "4000"], capture_output=True,
+                       text=True, timeout=150)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert res["rc"] == -errno.ETIMEDOUT, res
+    assert 3.5 < res["s"] < 60, res
 
 
 def test_config4_100m_rows_one_gpu_and_8_ranks(ctx, ctxs):

@@ -111,3 +111,48 @@ def test_stage_pinned_piece_split_by_file_count(ctx):
     torch.cuda.synchronize()
     assert int(st.abs().sum()) == 0
     np.testing.assert_array_equal(out.cpu().numpy(), O.cas_batch(arena, off, lens, threads=16))
+
+
+def test_identifier_run_chain_vs_oracle(ctx):
+    """the config-5 chain as the bench runs it --
+    sdgpu_cas_stage_pinned -> sdgpu_synth_vary_keys_device ->
+    sdgpu_group_rows_indexed_device (one Object index for the run) ->
+    sdgpu_link_batch_device -- over 3 steps of 100 k files, every step against
+    the oracle: cas ids (O.cas_batch), reps of the whole run (O.group_reps over
+    all steps' rows in id order, file_identifier/mod.rs:168-241) and the
+    create / connect lists (O.link_batch, mod.rs:189-333)."""
+    import torch
+    from spacedrive_amd import cas, corpus, dedup
+    n, steps = 100_000, 3
+    sizes, seeds = corpus.config2_files(n, seed=41)
+    h, arena, off, ln = _pinned_arena(sizes, seeds)
+    cas_ref = O.cas_batch(arena, off, ln, threads=16)
+    key0 = np.ascontiguousarray(cas_ref).view(np.uint64).ravel()
+    has = (sizes != 0).astype(np.uint8)
+    vary = corpus.config5_vary_mask(sizes, seeds)
+    keys_ref = [O.vary_keys(key0, vary, s) for s in range(steps)]
+    whole = O.group_reps(np.concatenate(keys_ref), np.tile(has, steps), 100)
+    d_has = torch.from_numpy(has).cuda()
+    d_vary = torch.from_numpy(vary).cuda()
+    idx = dedup.ObjectIndex(ctx, 1000)        # grows on the way
+    linked_earlier = 0
+    for s in range(steps):
+        out, st = cas.cas_stage_pinned(h, off, ln, ctx=ctx)
+        torch.cuda.synchronize()
+        assert int(st.abs().sum()) == 0
+        np.testing.assert_array_equal(out.cpu().numpy(), cas_ref)
+        key = out.view(torch.int64).view(-1)
+        corpus.vary_keys_device(key, d_vary, s, ctx=ctx)
+        np.testing.assert_array_equal(key.cpu().numpy().view(np.uint64), keys_ref[s])
+        rank = torch.arange(s * n, (s + 1) * n, dtype=torch.int64).to(torch.int32).cuda()
+        rep = dedup.group_rows_indexed(key, d_has, rank, idx, 100)
+        got = rep.cpu().numpy().view(np.uint32)
+        ref = whole[s * n:(s + 1) * n]
+        np.testing.assert_array_equal(got, ref)
+        c, lr, lo = dedup.link_batch_device(rep, rank, None, 0, ctx=ctx)
+        rc, rlr, rlo = O.link_batch(ref, np.arange(s * n, (s + 1) * n, dtype=np.uint32), None, 0)
+        np.testing.assert_array_equal(c.cpu().numpy().view(np.uint32), rc)
+        np.testing.assert_array_equal(lr.cpu().numpy().view(np.uint32), rlr)
+        np.testing.assert_array_equal(lo.cpu().numpy().view(np.uint32), rlo)
+        linked_earlier += int(np.count_nonzero(ref < s * n))
+    assert linked_earlier > 20_000    # later steps link to earlier steps' Objects
