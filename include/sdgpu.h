@@ -143,6 +143,17 @@ int sdgpu_subtree_device(sdgpu_ctx *ctx, const uint8_t *d_bytes, uint64_t len,
  * GPU computes its slices' CVs, one GPU combines them. */
 int sdgpu_combine_subtrees_device(sdgpu_ctx *ctx, const uint8_t *d_cvs, uint64_t n,
                                   uint8_t *d_out32, void *stream);
+/* Latency service for the single-file callers (watcher/utils.rs:236,411,467,
+ * non_indexed.rs:161): with enable != 0, sdgpu_generate_cas_id and
+ * sdgpu_file_checksum hash messages of at most 112 KiB (every cas message;
+ * files up to 112 KiB for the checksum) on a workgroup that stays resident
+ * on the device and polls a mailbox in pinned memory -- no launch, copy
+ * command or stream synchronisation per call.  The workgroup occupies part
+ * of one CU until 20 ms after the last such call (then it ends itself; the
+ * next call restarts it) and is stopped before any other call of the context
+ * launches work.  Below ~2 KiB one CPU thread is still faster (the hash of
+ * one chunk is 16 dependent compressions). */
+int sdgpu_latency_service(sdgpu_ctx *ctx, int enable);
 /* Path-based drop-in for file_checksum(path): streams the file in 64 MiB
  * power-of-two slices through double-buffered pinned memory; out_hex = 64
  * lowercase hex chars + NUL. */

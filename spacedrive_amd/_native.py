@@ -58,6 +58,7 @@ def _proto(L):
         "sdgpu_combine_subtrees_device": (i32, [ctx, c_vp, u64, c_vp, c_vp]),
         "sdgpu_checksum_files": (i32, [ctx, c_vp, u32, c_vp, c_vp]),
         "sdgpu_file_checksum": (i32, [ctx, ctypes.c_char_p, ctypes.c_char_p]),
+        "sdgpu_latency_service": (i32, [ctx, i32]),
         "sdgpu_dedup": (i32, [ctx, c_vp, c_vp, u32, u32, c_vp]),
         "sdgpu_group_pairs_device": (i32, [ctx, c_vp, c_vp, u64, u32, u32, c_vp, c_vp]),
         "sdgpu_group_rows_device": (i32, [ctx, c_vp, c_vp, c_vp, u64, u32, u32, c_vp, c_vp]),
@@ -176,6 +177,11 @@ class Context:
     @property
     def stream(self) -> int:
         return self.lib.sdgpu_stream(self.h) or 0
+
+    def latency_service(self, enable: bool = True):
+        """Single-file calls through the resident latency kernel
+        (sdgpu_latency_service)."""
+        check(self.lib.sdgpu_latency_service(self.h, 1 if enable else 0), "sdgpu_latency_service")
 
     def set_timing(self, enable: bool = True):
         check(self.lib.sdgpu_set_timing(self.h, 1 if enable else 0), "sdgpu_set_timing")

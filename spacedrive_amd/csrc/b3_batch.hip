@@ -585,6 +585,129 @@ __global__ __launch_bounds__(1024) void k_small_host(const uint8_t* __restrict__
   }
 }
 
+// The resident latency service (internal.hpp SvcMailbox).  Thread 0 polls
+// the request number with system-scope acquire loads (the message area and
+// the mailbox are coherent pinned memory, so every load reads the host's
+// current bytes); the workgroup then hashes the message exactly as
+// k_small_host and thread 0 publishes the digest words, then the request
+// number (system-scope release).  Every wave reaches the loop's exit: the
+// stop request, the idle deadline and the lifetime deadline are decided by
+// thread 0 and broadcast through LDS.
+constexpr uint32_t kSvcThreads = 256;
+static_assert(kSvcThreads >= kHostStageChunks, "one thread per chunk of the largest message");
+
+__global__ __launch_bounds__(kSvcThreads) void k_service(SvcMailbox* __restrict__ mb,
+                                                         const uint8_t* __restrict__ msg,
+                                                         uint32_t last_seq, uint64_t idle_ticks,
+                                                         uint64_t life_ticks) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
+  __shared__ uint32_t cv[8][kHostStageChunks];
+  __shared__ uint32_t s_go, s_len, s_words;
+  const uint32_t t = threadIdx.x;
+  const uint64_t t_start = wall_clock64();
+  uint64_t t_last = t_start;
+  for (;;) {
+    if (t == 0) {
+      uint32_t go = 0;
+      for (;;) {
+        const uint32_t seq = __hip_atomic_load(&mb->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (seq != last_seq) {
+          const uint32_t op = __hip_atomic_load(&mb->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          go = op == kSvcHash ? seq : 0u;
+          s_len = __hip_atomic_load(&mb->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          s_words = __hip_atomic_load(&mb->out_words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (go == 0) last_seq = seq;  // stop
+          break;
+        }
+        const uint64_t now = wall_clock64();
+        if (now - t_last > idle_ticks || now - t_start > life_ticks) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_go = go;
+    }
+    __syncthreads();
+    const uint32_t go = s_go;
+    if (go == 0) break;  // uniform: stop, idle or lifetime deadline
+    const uint32_t l = min(s_len, kHostStageMax), out_words = min(s_words, 16u);
+    {
+      const uint32_t nvec = (l + 15) / 16;
+      const uint4* src = reinterpret_cast<const uint4*>(msg);
+      uint4* dst = reinterpret_cast<uint4*>(stage);
+      constexpr int kU = 8;
+      for (uint32_t i0 = t; i0 < nvec; i0 += kU * kSvcThreads) {
+        uint4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const uint32_t i = i0 + u * kSvcThreads;
+          v[u] = i < nvec ? src[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const uint32_t i = i0 + u * kSvcThreads;
+          if (i < nvec) dst[i] = v[u];
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t nch = n_chunks_of(l);
+    uint32_t c[8];
+    if (nch == 1) {
+      if (t == 0) b3_chunk(stage, l, 0, B3_ROOT, c);
+    } else {
+      if (t < nch) {
+        chunk_any(stage, l, t, 0u, c);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
+      }
+      __syncthreads();
+      uint32_t cnt = nch;
+      while (cnt > 2) {
+        const uint32_t half = cnt >> 1;
+        uint32_t a[8], b[8];
+        const bool merge = t < half;
+        const bool carry = (cnt & 1u) && t == half;
+        if (merge) {
+#pragma unroll
+          for (int w = 0; w < 8; ++w) {
+            a[w] = cv[w][2 * t];
+            b[w] = cv[w][2 * t + 1];
+          }
+          b3_parent(c, a, b, 0u);
+        } else if (carry) {
+#pragma unroll
+          for (int w = 0; w < 8; ++w) c[w] = cv[w][cnt - 1];
+        }
+        __syncthreads();
+        if (merge || carry) {
+#pragma unroll
+          for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
+        }
+        __syncthreads();
+        cnt = half + (cnt & 1u);
+      }
+      if (t == 0) {
+        uint32_t a[8], b[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+          a[w] = cv[w][0];
+          b[w] = cv[w][1];
+        }
+        b3_parent(c, a, b, B3_ROOT);
+      }
+    }
+    if (t == 0) {
+      for (uint32_t w = 0; w < out_words; ++w)
+        __hip_atomic_store(&mb->digest[w], w < 8 ? c[w] : 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->done, go, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      last_seq = go;
+    }
+    t_last = wall_clock64();
+    __syncthreads();  // LDS (stage, cv, s_*) reused by the next request
+  }
+  if (t == 0) __hip_atomic_store(&mb->state, kSvcExited, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
 
 hipError_t batch_hash_launch(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* off,
@@ -666,6 +789,27 @@ hipError_t small_host_launch(const uint8_t* h_arena, const uint64_t* h_off, cons
   KScope k(timer, "cas_small_host", s);
   k_small_host<<<n, threads, lds, s>>>(h_arena, h_off, h_len, out_words,
                                        reinterpret_cast<uint32_t*>(h_out));
+  return hipGetLastError();
+}
+
+}  // namespace sdgpu
+
+namespace sdgpu {
+
+hipError_t service_launch(SvcMailbox* mb, const uint8_t* msg, uint32_t last_seq,
+                          uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s) {
+  static std::atomic<uint64_t> attr_set{0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint64_t bit = 1ull << (dev & 63);
+  if (!(attr_set.load(std::memory_order_acquire) & bit)) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_service),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             static_cast<int>(kHostStageMax + 16));
+    if (e != hipSuccess) return e;
+    attr_set.fetch_or(bit, std::memory_order_release);
+  }
+  k_service<<<1, kSvcThreads, kHostStageMax + 16, s>>>(mb, msg, last_seq, idle_ticks, life_ticks);
   return hipGetLastError();
 }
 

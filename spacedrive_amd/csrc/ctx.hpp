@@ -166,6 +166,14 @@ struct sdgpu_ctx {
   bool timing = false;
   EventTimer timer;
   KTimer* kt() { return timing ? &timer : nullptr; }
+  // resident latency service (f3, sdgpu_latency_service): mailbox + message
+  // area in coherent pinned memory, the kernel's own stream
+  sdgpu::SvcMailbox* svc_mb = nullptr;
+  uint8_t* svc_msg = nullptr;
+  hipStream_t svc_stream = nullptr;
+  bool svc_enabled = false, svc_launched = false;
+  uint32_t svc_seq = 0;
+  uint64_t svc_idle_ticks = 0, svc_life_ticks = 0;
 };
 
 namespace sdgpu {
@@ -174,7 +182,18 @@ namespace sdgpu {
 // workspaces are shared by every call, so when a call moves to a different
 // stream than the previous one it first waits (on the device) for the work
 // already queued on that previous stream.
+// Ends the resident latency kernel (if any) and waits for it: a bulk call
+// gets every CU (K1's persistent grid is sized to the resident capacity).
+inline void service_stop(sdgpu_ctx* c) {
+  if (!c->svc_launched) return;
+  __atomic_store_n(&c->svc_mb->op, kSvcStop, __ATOMIC_RELAXED);
+  __atomic_store_n(&c->svc_mb->seq, ++c->svc_seq, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(c->svc_stream);
+  c->svc_launched = false;
+}
+
 inline hipStream_t pick(sdgpu_ctx* c, void* stream) {
+  service_stop(c);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
   if (c->last && s != c->last) {
     if (!c->handover) (void)hipEventCreateWithFlags(&c->handover, hipEventDisableTiming);

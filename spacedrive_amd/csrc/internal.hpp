@@ -75,6 +75,31 @@ hipError_t small_host_launch(const uint8_t* h_arena, const uint64_t* h_off, cons
                              uint32_t n, uint32_t max_len, uint32_t out_words, uint8_t* h_out,
                              hipStream_t s, KTimer* timer = nullptr);
 
+// Resident latency service (the single-file callers, f3): ONE workgroup that
+// stays on the device and polls a mailbox in coherent pinned host memory;
+// each request's message (<= kHostStageMax bytes, already in the pinned
+// message area) is copied into LDS, hashed like k_small_host, and its digest
+// words and sequence number written back -- a call costs no launch, no copy
+// command and no stream synchronisation.  The kernel returns on a stop
+// request, after idle_ticks of wall clock without a request, or after
+// life_ticks in total (so it always ends, whatever the host does), setting
+// state = kSvcExited first.  Fields sit on separate 64-B lines.
+struct alignas(64) SvcMailbox {
+  uint32_t seq;        // host: request number, written last (release)
+  uint32_t op;         // kSvcHash / kSvcStop
+  uint32_t len;        // message bytes at the message area
+  uint32_t out_words;  // digest words to return (2: cas_id, 8: checksum)
+  uint32_t pad0[12];
+  uint32_t done;       // device: the last request number answered (release)
+  uint32_t state;      // kSvcRunning (host, before a launch) / kSvcExited (device)
+  uint32_t pad1[14];
+  uint32_t digest[16];
+};
+constexpr uint32_t kSvcHash = 0, kSvcStop = 1;
+constexpr uint32_t kSvcRunning = 1, kSvcExited = 2;
+hipError_t service_launch(SvcMailbox* mb, const uint8_t* msg, uint32_t last_seq,
+                          uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);
+
 // ---- tree BLAKE3 of large segments (file_checksum, K2/K3) -------------------
 // TreeSeg: tree_plan.hpp
 // cv_input: every segment's `data` holds `len` 32-byte chaining values of

@@ -70,3 +70,58 @@ def test_generate_cas_id_small_files(ctx, tmp_path):
         p = os.path.join(tmp_path, f"g{n}")
         rng.integers(0, 256, n, dtype=np.uint8).tofile(p)
         assert cas.generate_cas_id(p, n, ctx) == O.cas_id_path(p, n), n
+
+
+@pytest.fixture()
+def svc_ctx():
+    """A separate context with the resident latency service on (f3): the
+    single-file drop-ins go through k_service's mailbox."""
+    from spacedrive_amd._native import Context
+    c = Context(0)
+    c.latency_service(True)
+    yield c
+    c.latency_service(False)
+    c.close()
+
+
+def test_service_generate_cas_id_and_checksum(svc_ctx, tmp_path):
+    """Every size class through the resident kernel: empty (size 0 hashes the
+    8 zero bytes, non_indexed.rs:161), one chunk, chunk boundaries, the
+    100 KiB cas limit, sampled files (57 352-B messages), files up to the
+    112 KiB message area and just past it (one-shot fallback)."""
+    from spacedrive_amd import cas, validation
+    rng = np.random.default_rng(17)
+    sizes = [0, 1, 63, 64, 65, 1023, 1024, 1025, 4096, 65536, 102399, 102400, 102401, 114_688 - 1,
+             114_688, 114_689, 500_000, 3 << 20]
+    for n in sizes:
+        p = os.path.join(tmp_path, f"s{n}")
+        rng.integers(0, 256, n, dtype=np.uint8).tofile(p)
+        assert cas.generate_cas_id(p, n, svc_ctx) == O.cas_id_path(p, n), n
+        assert validation.file_checksum(p, svc_ctx) == O.file_checksum_path(p), n
+
+
+def test_service_survives_idle_exit_and_bulk_calls(svc_ctx, tmp_path):
+    """The resident kernel ends itself after 20 ms without a request and is
+    stopped by any bulk call; the next single-file call relaunches it.  Both
+    orders, repeated, stay bit-exact; a missing file still reports ENOENT."""
+    import time
+    from spacedrive_amd import cas, validation
+    from spacedrive_amd._native import SdgpuError
+    rng = np.random.default_rng(18)
+    p = os.path.join(tmp_path, "f")
+    rng.integers(0, 256, 4096, dtype=np.uint8).tofile(p)
+    want_cas, want_ck = O.cas_id_path(p, 4096), O.file_checksum_path(p)
+    arena, off, ln = _arena([4096, 57352, 1], 3)
+    for it in range(6):
+        assert cas.generate_cas_id(p, 4096, svc_ctx) == want_cas
+        if it % 2:
+            time.sleep(0.05)                                  # idle exit
+        else:
+            out, st = cas.cas_batch(arena, off, ln, svc_ctx)   # bulk call stops it
+            assert np.all(st == 0)
+        assert validation.file_checksum(p, svc_ctx) == want_ck
+    with pytest.raises(SdgpuError) as ei:
+        cas.generate_cas_id(os.path.join(tmp_path, "missing"), 10, svc_ctx)
+    assert ei.value.errno == 2
+    for _ in range(200):                                      # back-to-back requests
+        assert cas.generate_cas_id(p, 4096, svc_ctx) == want_cas
