@@ -164,6 +164,7 @@ struct sdgpu_ctx {
   DevBuf xs_send, xs_recv, xs_back;
   PinBuf xs_counts;
   bool timing = false;
+  bool io_uring = false;  // sdgpu_identify_files reads through io_uring (uring.hpp)
   EventTimer timer;
   KTimer* kt() { return timing ? &timer : nullptr; }
   // resident latency service (f3, sdgpu_latency_service): mailbox + message

@@ -30,6 +30,7 @@
 #include "../../include/sdgpu.h"
 #include "ctx.hpp"
 #include "host_io.hpp"
+#include "uring.hpp"
 #include "internal.hpp"
 #include "scan_device.hpp"
 
@@ -123,8 +124,11 @@ int pipe_slot(sdgpu_ctx* c, int k, size_t bytes) {
 // meaning "no message for this file" (size 0).  est(i) = bytes to reserve.
 // Slabs are sized for this call (at most kSlabBytes / kSlabFiles): a single
 // file costs one ~60 KiB slab, not 256 MiB.
-template <typename Est, typename Produce, typename Finish>
-int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&& finish) {
+// fill_batch (optional): fill_batch(first, cnt, off, cap_end, hb, len, pst) fills
+// a whole slab's messages at once (the io_uring reader) instead of produce().
+template <typename Est, typename Produce, typename Finish, typename FillBatch = std::nullptr_t>
+int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&& finish,
+                 FillBatch&& fill_batch = nullptr) {
   (void)pick(c, nullptr);  // runs on the context stream, after earlier work on others
   constexpr int S = sdgpu_ctx::kPipeSlabs;
   uint64_t want = 0, biggest = 0;
@@ -184,10 +188,7 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     sl.count = cnt;
     // fill (pool threads): message bytes + per-file pre-status
     const auto t_fill = now();
-    parallel_for(cnt, [&](uint32_t j) {
-      const uint64_t cap =
-          (j + 1 < cnt ? off[j + 1] : std::min<uint64_t>(pos, L.arena_cap)) - off[j];
-      const int64_t r = produce(sl.first + j, hb + off[j], static_cast<size_t>(cap));
+    auto settle = [&](uint32_t j, int64_t r) {
       if (r >= 0 && r != 0x7fffffff) {
         len[j] = static_cast<uint32_t>(r);
         pst[j] = 0;
@@ -195,7 +196,16 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
         len[j] = 0;  // hashed as an empty message; status says why it is void
         pst[j] = r == 0x7fffffff ? 1 : static_cast<int32_t>(r);
       }
-    });
+    };
+    bool filled = false;
+    if constexpr (!std::is_same_v<std::decay_t<FillBatch>, std::nullptr_t>)
+      filled = fill_batch(sl.first, cnt, off, std::min<uint64_t>(pos, L.arena_cap), hb, settle);
+    if (!filled)
+      parallel_for(cnt, [&](uint32_t j) {
+        const uint64_t cap =
+            (j + 1 < cnt ? off[j + 1] : std::min<uint64_t>(pos, L.arena_cap)) - off[j];
+        settle(j, produce(sl.first + j, hb + off[j], static_cast<size_t>(cap)));
+      });
     if (ht) ht->host("stage_fill", ms_since(t_fill));
     // device: copy, hash, copy back.  A few messages of <= 1 MiB take the
     // one-launch latency kernel and one H2D copy of the whole slab prefix.
@@ -286,6 +296,10 @@ int sdgpu_open(int device, sdgpu_ctx** out) {
   sdgpu_ctx* c = new (std::nothrow) sdgpu_ctx;
   if (!c) return -ENOMEM;
   c->device = device;
+  {  // staging reads through io_uring (SDGPU_IO=uring) instead of pread
+    const char* io = getenv("SDGPU_IO");
+    c->io_uring = io && strcmp(io, "uring") == 0;
+  }
   // A BLOCKING stream: callers that pass NULL (e.g. torch's legacy default
   // stream, whose handle is 0) get work ordered with the null stream both ways.
   if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess ||
@@ -548,6 +562,38 @@ int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t*
           if (has_key) has_key[first + j] = ok ? 1 : 0;
           if (status) status[first + j] = sj == 1 ? 0 : sj;
         }
+      },
+      [&](uint32_t first, uint32_t cnt, const uint64_t* off, uint64_t end, uint8_t* hb,
+          auto&& settle) -> bool {
+        // batched io_uring chains (csrc/uring.hpp), one ring per pool thread:
+        // the same bytes and statuses as read_cas_message
+        if (!c->io_uring) return false;
+        constexpr uint32_t kGrain = uring::kBatchFiles;
+        parallel_for((cnt + kGrain - 1) / kGrain, [&](uint32_t g) {
+          thread_local uring::Ring ring;
+          thread_local int ring_ok = -1;
+          if (ring_ok < 0) ring_ok = ring.open_ring() ? 1 : 0;
+          const uint32_t j0 = g * kGrain, j1 = std::min(cnt, j0 + kGrain);
+          uring::FileJob jobs[kGrain];
+          uint32_t idx[kGrain], m = 0;
+          for (uint32_t j = j0; j < j1; ++j) {
+            const uint32_t i = first + j;
+            if (size[i] == 0) {
+              settle(j, 0x7fffffff);  // cas_id None (file_identifier/mod.rs:80-88)
+              continue;
+            }
+            const uint64_t cap = (j + 1 < cnt ? off[j + 1] : end) - off[j];
+            jobs[m] = uring::FileJob{paths[i], size[i], hb + off[j], static_cast<size_t>(cap), 0};
+            idx[m++] = j;
+          }
+          if (ring_ok)
+            uring::read_cas_batch(ring, jobs, m);
+          else
+            for (uint32_t k = 0; k < m; ++k)
+              jobs[k].result = read_cas_message(jobs[k].path, jobs[k].size, jobs[k].dst, jobs[k].cap);
+          for (uint32_t k = 0; k < m; ++k) settle(idx[k], jobs[k].result);
+        });
+        return true;
       });
   if (rc) return rc;
   for (const uint32_t i : grown) {

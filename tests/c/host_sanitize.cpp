@@ -16,6 +16,7 @@
 
 #include "../../spacedrive_amd/csrc/host_io.hpp"
 #include "../../spacedrive_amd/csrc/tree_plan.hpp"
+#include "../../spacedrive_amd/csrc/uring.hpp"
 
 using namespace sdgpu;
 
@@ -96,6 +97,42 @@ static void test_cas_reads() {
   CHECK(memcmp(r.data(), w.data(), 4096) == 0, "whole bytes");
   CHECK(hostio::read_whole((dir + "/whole").c_str(), r.data(), 4095) == -EFBIG, "whole efbig");
   CHECK(hostio::read_whole((dir + "/f0").c_str(), r.data(), 16) == 0, "whole empty");
+}
+
+// The io_uring reader (uring.hpp) gives read_cas_message's exact bytes and
+// statuses for every case above, over several batches of one ring (or, where
+// io_uring is unavailable, reports so and is skipped).
+static void test_uring_reads() {
+  uring::Ring ring;
+  if (!ring.open_ring()) {
+    printf("io_uring unavailable: uring reader not exercised\n");
+    return;
+  }
+  std::vector<std::string> names = {"f1", "f100", "f1024", "f102399", "f102400", "f102401",
+                                    "f200000", "f1048576", "grown", "short", "missing", "whole"};
+  std::vector<uint64_t> sz = {1, 100, 1024, 102399, 102400, 102401, 200000, 1 << 20, 5000,
+                              400000, 10, 4096};
+  std::vector<std::string> paths;
+  std::vector<uring::FileJob> jobs;
+  std::vector<std::vector<uint8_t>> a, b;
+  for (int rep = 0; rep < 7; ++rep)  // 84 files: three batches of the ring
+    for (size_t k = 0; k < names.size(); ++k) paths.push_back(dir + "/" + names[k]);
+  for (size_t i = 0; i < paths.size(); ++i) {
+    const uint64_t s = sz[i % sz.size()];
+    const size_t cap = s <= 102400 ? 8 + s + 4096 : 57352;
+    a.emplace_back(cap, 0);
+    b.emplace_back(cap, 0);
+    jobs.push_back(uring::FileJob{paths[i].c_str(), s, b.back().data(), cap, 0});
+  }
+  uring::read_cas_batch(ring, jobs.data(), static_cast<uint32_t>(jobs.size()));
+  for (size_t i = 0; i < paths.size(); ++i) {
+    const int64_t want = hostio::read_cas_message(paths[i].c_str(), jobs[i].size, a[i].data(),
+                                                  a[i].size());
+    CHECK(jobs[i].result == want, "uring %s: %lld vs %lld", paths[i].c_str(),
+          (long long)jobs[i].result, (long long)want);
+    if (want > 0) CHECK(memcmp(a[i].data(), b[i].data(), want) == 0, "uring bytes %s",
+                        paths[i].c_str());
+  }
 }
 
 static void test_parallel_for() {
@@ -201,6 +238,7 @@ int main(int argc, char** argv) {
   char tmpl[] = "/tmp/sdgpu_san_XXXXXX";
   dir = argc > 1 ? argv[1] : mkdtemp(tmpl);
   test_cas_reads();
+  test_uring_reads();
   test_parallel_for();
   test_parallel_for_after_fork();
   test_slab_layout();
