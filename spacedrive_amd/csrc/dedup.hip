@@ -71,6 +71,7 @@ constexpr uint64_t kBucketRows = 3072; // target mean rows per bucket (bucket_bi
 constexpr uint32_t kMaxBucketBits = 15;  // 2^15 buckets: 100 M rows stay in LDS
 constexpr uint32_t kShardBits = 8;       // multi-GPU shards: h >> 56
 constexpr uint64_t kEmpty = ~0ull;
+constexpr uint32_t kPadRow = 0xFFFFFFFFu;  // a record's row field: padding, not a row
 
 // `bits` hash bits below the top `skip` bits of h.
 __device__ __forceinline__ uint32_t digit_of(uint64_t h, uint32_t skip, uint32_t bits) {
@@ -726,6 +727,69 @@ __device__ __forceinline__ void load_bucket(Src rec, uint32_t start, uint32_t en
   }
 }
 
+// Group-by of one bucket too large for LDS: a private region of the global
+// table (4 slots per row, agent-scope atomics).  Records with row ~0 are pads.
+template <typename Src>
+__device__ __forceinline__ void group_bucket_global(Src rec, uint32_t start, uint32_t end,
+                                                    ChunkOf chunk_of, uint64_t* __restrict__ gkey,
+                                                    uint32_t* __restrict__ gmin,
+                                                    uint32_t* __restrict__ rep,
+                                                    uint32_t& special_min) {
+  const uint32_t m = end - start;
+  uint64_t tsize = 1;
+  while (tsize * 2 <= 4ull * m) tsize *= 2;  // 2m < tsize <= 4m (64-bit: no wrap)
+  uint64_t* tk = gkey + 4ull * start;
+  uint32_t* tm = gmin + 4ull * start;
+  for (uint64_t s = threadIdx.x; s < tsize; s += kGroupThreads) {
+    tk[s] = kEmpty;
+    tm[s] = 0xFFFFFFFFu;
+  }
+  if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
+  __syncthreads();
+  for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
+    const uint4 q = rec(i);
+    if (q.w == kPadRow) continue;
+    const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
+    const uint32_t r = q.z;
+    if (k == kEmpty) {
+      atomicMin(&special_min, r);
+      continue;
+    }
+    uint64_t h = global_slot(k, tsize);
+    for (;;) {
+      const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tk[h]),
+                                      static_cast<unsigned long long>(kEmpty),
+                                      static_cast<unsigned long long>(k));
+      if (prev == kEmpty || prev == k) {
+        atomicMin(&tm[h], r);
+        break;
+      }
+      h = (h + 1) & (tsize - 1);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
+    const uint4 q = rec(i);
+    if (q.w == kPadRow) continue;
+    const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
+    const uint32_t r = q.z;
+    uint32_t f;
+    if (k == kEmpty) {
+      f = special_min;
+    } else {
+      uint64_t h = global_slot(k, tsize);
+      for (;;) {
+        const uint64_t kk =
+            __hip_atomic_load(&tk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (kk == k) break;
+        h = (h + 1) & (tsize - 1);
+      }
+      f = __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (chunk_of(r) != chunk_of(f)) rep[q.w] = f;
+  }
+}
+
 // Group-by of one bucket, rows [start, end) of rec (q_reg preloaded by
 // load_bucket when the bucket fits the LDS table).
 template <typename Src>
@@ -737,32 +801,19 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
                                              uint32_t* lmin, uint32_t& special_min) {
   const uint32_t m = end - start;
   if (m == 0) return;
-  const bool in_lds = m <= kLdsCap;
-  uint64_t tsize = kLdsSlots;
-  uint64_t* tk = lkey;
-  uint32_t* tm = lmin;
-  if (!in_lds) {
-    tsize = 1;
-    while (tsize * 2 <= 4ull * m) tsize *= 2;  // 2m < tsize <= 4m (64-bit: no wrap)
-    tk = gkey + 4ull * start;
-    tm = gmin + 4ull * start;
+  if (m > kLdsCap) {
+    group_bucket_global(rec, start, end, chunk_of, gkey, gmin, rep, special_min);
+    return;
   }
-  // (the LDS branch names lkey / lmin directly: through the generic tk / tm
-  // pointers the compiler emits FLAT atomics, ~30 % slower than ds_* here)
-  if (in_lds) {
-    for (uint32_t s = threadIdx.x; s < kLdsSlots; s += kGroupThreads) {
-      lkey[s] = kEmpty;
-      lmin[s] = 0xFFFFFFFFu;
-    }
-  } else {
-    for (uint64_t s = threadIdx.x; s < tsize; s += kGroupThreads) {
-      tk[s] = kEmpty;
-      tm[s] = 0xFFFFFFFFu;
-    }
+  // (the LDS code names lkey / lmin directly: through generic pointers shared
+  // with the global table the compiler emits FLAT atomics, ~30 % slower)
+  for (uint32_t s = threadIdx.x; s < kLdsSlots; s += kGroupThreads) {
+    lkey[s] = kEmpty;
+    lmin[s] = 0xFFFFFFFFu;
   }
   if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
   __syncthreads();
-  if (in_lds) {
+  {
     // A thread's records probe in lock step: every pass issues the LDS
     // round trips of all its pending records back to back and only then
     // inspects the results, so their latencies overlap (the probe loops are
@@ -816,47 +867,102 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
       const uint32_t f = (keyed >> j & 1u) ? lmin[h[j]] : special_min;
       if (chunk_of(r) != chunk_of(f)) rep[q_reg[j].w] = f;  // others keep rank
     }
+  }
+}
+
+// K5 with a PACKED 8-byte LDS table, for buckets of >= 12 digit bits (the
+// one-level 12-bit path and the two-level 15-bit path).  Inside a bucket the
+// digit bits of h are implied, so a key is known by its other 64 - bits
+// (<= 52) bits; with the record's index in the bucket + 1 (12 bits, 0 =
+// empty) a slot is ONE 64-bit word.  The CAS that places or finds a key also
+// names the record that owns it, the group minimum lives per owner
+// (lmin[4096]), and 7680 slots fit where 6144 twelve-byte ones did: load
+// ~0.4 instead of ~0.5, shorter probe chains.  scripts/exp_group_packed.hip:
+// 12.5 M rows 0.078 -> 0.072 ms (profiles/r3/exp_group_packed/run.log).
+// Buckets above 4095 records take the global table; pads (row ~0) are skipped.
+constexpr uint32_t kPkSlots = 7680;  // 2^9 * 15: probe steps odd and prime to 3 and 5
+constexpr uint32_t kPkCap = 4095;
+
+// h without its `bits` digit bits [64 - kShardBits - bits, 64 - kShardBits)
+__device__ __forceinline__ uint64_t key_rest(uint64_t h, uint32_t bits) {
+  const uint32_t lo = 64 - kShardBits - bits;
+  return (h & ((1ull << lo) - 1)) | ((h >> (64 - kShardBits)) << lo);
+}
+
+template <typename Src>
+__device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uint32_t end,
+                                                    uint32_t bits, ChunkOf chunk_of,
+                                                    uint64_t* __restrict__ gkey,
+                                                    uint32_t* __restrict__ gmin,
+                                                    uint32_t* __restrict__ rep, uint64_t* tab,
+                                                    uint32_t* lmin, uint32_t& special_min) {
+  constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
+  const uint32_t m = end - start;
+  if (m == 0) return;
+  if (m > kPkCap) {
+    group_bucket_global(rec, start, end, chunk_of, gkey, gmin, rep, special_min);
     return;
   }
-  for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
-    const uint4 q = rec(i);
-    const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
-    const uint32_t r = q.z;
-    if (k == kEmpty) {
-      atomicMin(&special_min, r);
-      continue;
-    }
-    uint64_t h = global_slot(k, tsize);
-    for (;;) {
-      const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tk[h]),
-                                      static_cast<unsigned long long>(kEmpty),
-                                      static_cast<unsigned long long>(k));
-      if (prev == kEmpty || prev == k) {
-        atomicMin(&tm[h], r);
-        break;
+  uint4 q[kP];
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    const uint32_t i = start + threadIdx.x + j * kGroupThreads;
+    q[j] = i < end ? rec(i) : make_uint4(0, 0, kPadRow, kPadRow);
+  }
+  for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
+  for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
+  __syncthreads();
+  uint32_t slot[kP], step[kP], owner[kP];
+  uint64_t mine[kP];
+  uint32_t pend = 0;
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    const uint64_t h = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+    const uint32_t idx = threadIdx.x + j * kGroupThreads;
+    mine[j] = (key_rest(h, bits) << 12) | (idx + 1);
+    slot[j] = static_cast<uint32_t>((static_cast<uint64_t>(static_cast<uint32_t>(h)) * kPkSlots) >> 32);
+    // double hashing: an odd step prime to 3 and 5 is coprime with 2^9 * 15
+    uint32_t st = 1u + 2u * static_cast<uint32_t>((h >> 40) & 1023u);
+    st += (st % 3u == 0) ? 2u : 0u;
+    st += (st % 5u == 0) ? 2u : 0u;
+    st += (st % 3u == 0) ? 2u : 0u;
+    step[j] = st;
+    owner[j] = idx;
+    if (q[j].w != kPadRow) pend |= 1u << j;
+  }
+  const uint32_t live = pend;
+  // the records of a thread probe in lock step (their LDS round trips overlap)
+  while (pend) {
+    uint64_t prev[kP];
+#pragma unroll
+    for (int j = 0; j < kP; ++j)
+      prev[j] = (pend >> j & 1u)
+                    ? atomicCAS(reinterpret_cast<unsigned long long*>(&tab[slot[j]]), 0ull,
+                                static_cast<unsigned long long>(mine[j]))
+                    : 0ull;
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      if (!(pend >> j & 1u)) continue;
+      if (prev[j] == 0ull) {
+        pend &= ~(1u << j);  // placed: owns its key
+      } else if ((prev[j] >> 12) == (mine[j] >> 12)) {
+        owner[j] = static_cast<uint32_t>(prev[j] & 0xFFFu) - 1;
+        pend &= ~(1u << j);
+      } else {
+        const uint32_t sn = slot[j] + step[j];
+        slot[j] = sn >= kPkSlots ? sn - kPkSlots : sn;
       }
-      h = (h + 1) & (tsize - 1);
     }
   }
+#pragma unroll
+  for (int j = 0; j < kP; ++j)
+    if (live >> j & 1u) atomicMin(&lmin[owner[j]], q[j].z);
   __syncthreads();
-  for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
-    const uint4 q = rec(i);
-    const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
-    const uint32_t r = q.z;
-    uint32_t f;
-    if (k == kEmpty) {
-      f = special_min;
-    } else {
-      uint64_t h = global_slot(k, tsize);
-      for (;;) {
-        const uint64_t kk =
-            __hip_atomic_load(&tk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (kk == k) break;
-        h = (h + 1) & (tsize - 1);
-      }
-      f = __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (chunk_of(r) != chunk_of(f)) rep[q.w] = f;
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    if (!(live >> j & 1u)) continue;
+    const uint32_t r = q[j].z, f = lmin[owner[j]];
+    if (chunk_of(r) != chunk_of(f)) rep[q[j].w] = f;  // others keep rank
   }
 }
 
@@ -892,6 +998,32 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12(
   uint4 q_reg[kPer];
   load_bucket(src, start, end, q_reg);
   group_bucket(src, start, end, q_reg, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
+}
+
+// Packed-table K5 (>= 12 digit bits): rows of bucket b in [offs[b*P], offs[(b+1)*P]).
+__global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group_pk(
+    const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P, uint32_t bits,
+    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
+    uint32_t* __restrict__ rep) {
+  __shared__ uint64_t tab[kPkSlots];
+  __shared__ uint32_t lmin[kPkCap + 1];
+  __shared__ uint32_t special_min;
+  const uint32_t b = blockIdx.x;
+  group_bucket_packed(Rec16Src{rec}, offs[static_cast<uint64_t>(b) * P],
+                      offs[static_cast<uint64_t>(b + 1) * P], bits, chunk_of, gkey, gmin, rep, tab,
+                      lmin, special_min);
+}
+
+__global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12_pk(
+    const uint3* __restrict__ rec, uint32_t rank_base, const uint32_t* __restrict__ offs,
+    uint32_t bits, ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
+    uint32_t* __restrict__ rep) {
+  __shared__ uint64_t tab[kPkSlots];
+  __shared__ uint32_t lmin[kPkCap + 1];
+  __shared__ uint32_t special_min;
+  const uint32_t b = blockIdx.x;
+  group_bucket_packed(Rec12Src{rec, rank_base}, offs[b], offs[b + 1], bits, chunk_of, gkey, gmin,
+                      rep, tab, lmin, special_min);
 }
 
 __global__ __launch_bounds__(256) void k_fill_init(uint32_t* __restrict__ dst, uint64_t n,
@@ -1072,12 +1204,12 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
   }
   KScope k(timer, "bucket_group", s);
   if constexpr (kRec12)
-    k_bucket_group12<<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec), rank_base,
-                                                     fbase, ChunkOf::make(chunk_rows), gkey, gmin,
-                                                     rep);
+    k_bucket_group12_pk<<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
+                                                        rank_base, fbase, bits,
+                                                        ChunkOf::make(chunk_rows), gkey, gmin, rep);
   else
-    k_bucket_group<<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, ChunkOf::make(chunk_rows), gkey,
-                                                   gmin, rep);
+    k_bucket_group_pk<<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits, ChunkOf::make(chunk_rows),
+                                                      gkey, gmin, rep);
   return hipGetLastError();
 }
 
@@ -1132,9 +1264,9 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
                 in, n, kShardBits, fE, rec, rep, nullptr, 0, ftot, fbase);
         }
         KScope k(timer, "bucket_group", s);
-        k_bucket_group12<<<nb, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
-                                                      in.rank_base, fbase,
-                                                      ChunkOf::make(chunk_rows), gkey, gmin, rep);
+        k_bucket_group12_pk<<<nb, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
+                                                         in.rank_base, fbase, kStageBits,
+                                                         ChunkOf::make(chunk_rows), gkey, gmin, rep);
         return hipGetLastError();
       }
     }
@@ -1148,8 +1280,8 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
             in, n, kShardBits, fE, rec, rep, nullptr, 0, ftot, fbase);
     }
     KScope k(timer, "bucket_group", s);
-    k_bucket_group<<<nb, kGroupThreads, 0, s>>>(rec, fbase, 1, ChunkOf::make(chunk_rows), gkey,
-                                                gmin, rep);
+    k_bucket_group_pk<<<nb, kGroupThreads, 0, s>>>(rec, fbase, 1, kStageBits,
+                                                   ChunkOf::make(chunk_rows), gkey, gmin, rep);
     return hipGetLastError();
   }
   {
