@@ -556,6 +556,11 @@ class Runner:
                             fn()
                             ts.append(time.perf_counter() - t0)
                         res[f"{fn_name}_{name}{tag}_us"] = float(np.median(ts) * 1e6)
+            # where one resident-service call's time goes (device wall clock
+            # for the copy and the hash; host clock for the read and the wait)
+            p4 = os.path.join(root, "4KiB")
+            cas.generate_cas_id(p4, 4096, self.ctx)
+            res["service_breakdown_4KiB_cas"] = self.ctx.latency_service_diag()
             self.ctx.latency_service(False)
             self._single_sample = [(os.path.join(root, n), s) for n, s in
                                    (("4KiB", 4096), ("1MiB", 1 << 20))]

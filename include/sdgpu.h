@@ -417,6 +417,11 @@ int sdgpu_valu_probe(sdgpu_ctx *ctx, double *lane_ops_per_s);
  * 3 v_alignbit_b32, 4 v_add_u32; 5 = whole BLAKE3 compressions with everything
  * in registers (680 VALU each): the attainable roof of K1/K2's stream. */
 int sdgpu_valu_probe_kind(sdgpu_ctx *ctx, int kind, double *lane_ops_per_s);
+/* Latency breakdown of the last service request (sdgpu_latency_service) in
+ * microseconds: [0] message copied into LDS, [1] hashed and digest written
+ * (device wall clock), [2] host: post -> answer seen, [3] host: the file read
+ * (the last two for sdgpu_generate_cas_id). */
+int sdgpu_latency_service_diag(sdgpu_ctx *ctx, double out_us[4]);
 
 #ifdef __cplusplus
 }

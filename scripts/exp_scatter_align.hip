@@ -287,6 +287,129 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter_fixed_stores(
     for (uint32_t k = 0; k < fill[b]; ++k) out[cur[b] + k] = stage[b][k];
 }
 
+// W: warp-specialised staged scatter (implicit rank).  Waves 0-7 only LOAD and
+// stage (their next rows are prefetched two rounds ahead and they never
+// store, so their waits cover loads only); waves 8-15 only STORE: the full
+// pairs, the rows that met a full slot (an LDS overflow list) and rep = rank
+// of the round's rows (computed, no load).  Two barriers per round.
+constexpr uint32_t kWProd = 512;  // producer threads
+constexpr int kWU = 4;            // rows per producer thread per round
+__global__ __launch_bounds__(kPartThreads) void k_scatter_warpspec(
+    RowsIn in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ offs,
+    const uint32_t* __restrict__ ftot, uint3* __restrict__ out, uint32_t* __restrict__ rep,
+    uint32_t* __restrict__ fbase) {
+  constexpr uint32_t nbins = kNb;
+  constexpr uint32_t kRound = kWProd * kWU;  // 2048 rows
+  __shared__ uint3 stage[nbins][2];
+  __shared__ uint32_t fill[nbins], cur[nbins];
+  __shared__ uint3 ovf[kRound];
+  __shared__ uint32_t ovf_n;
+  constexpr uint32_t kPerT = nbins / kPartThreads;
+  const uint32_t t = threadIdx.x, lane = __lane_id();
+  uint32_t v[kPerT], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPerT; ++k) {
+    v[k] = ftot[t * kPerT + k];
+    sum += v[k];
+  }
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d);
+    if (lane >= static_cast<uint32_t>(d)) inc += o;
+  }
+  if (lane == 63) fill[t >> 6] = inc;
+  __syncthreads();
+  uint32_t base = inc - sum, total = 0;
+  for (uint32_t w = 0; w < kPartThreads / 64; ++w) {
+    if (w < (t >> 6)) base += fill[w];
+    total += fill[w];
+  }
+  __syncthreads();
+  const uint32_t j = part_block();
+#pragma unroll
+  for (uint32_t k = 0; k < kPerT; ++k) {
+    const uint32_t b = t * kPerT + k;
+    cur[b] = base + offs[static_cast<uint64_t>(j) * nbins + b];
+    fill[b] = 0;
+    if (j == 0) fbase[b] = base;
+    base += v[k];
+  }
+  if (j == 0 && t == 0) fbase[nbins] = total;
+  if (t == 0) ovf_n = 0;
+  __syncthreads();
+  uint64_t t0, t1;
+  tile_of(n, gridDim.x, t0, t1);
+  const uint32_t rounds = t1 > t0 ? static_cast<uint32_t>((t1 - t0 + kRound - 1) / kRound) : 0u;
+  if (t < kWProd) {
+    // producers
+    RowBatch<kWU> qa, qb;
+    in.template load_many<kWU>(t0 + t, kWProd, t1, t0, qa);
+    in.template load_many<kWU>(t0 + kRound + t, kWProd, t1, t0, qb);
+    auto stage_round = [&](const RowBatch<kWU>& q) {
+#pragma unroll
+      for (int u = 0; u < kWU; ++u) {
+        if (!in.valid_of(q, u)) continue;
+        const uint64_t h = row_hash(in.key_of(q, u));
+        const uint32_t b = digit_of(h, skip, kStageBits);
+        const uint3 rq = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), in.row_of(q, u));
+        const uint32_t sl = atomicAdd(&fill[b], 1u);
+        if (sl < 2) stage[b][sl] = rq;
+        else ovf[atomicAdd(&ovf_n, 1u)] = rq;
+      }
+    };
+    // per round exactly the consumers' three barriers: A (staged), M, B (flushed)
+    for (uint32_t r = 0; r < rounds; r += 2) {
+      stage_round(qa);
+      lds_barrier();  // A
+      in.template load_many<kWU>(t0 + (r + 2) * static_cast<uint64_t>(kRound) + t, kWProd, t1, t0, qa);
+      lds_barrier();  // M
+      lds_barrier();  // B
+      if (r + 1 >= rounds) break;
+      stage_round(qb);
+      lds_barrier();  // A
+      in.template load_many<kWU>(t0 + (r + 3) * static_cast<uint64_t>(kRound) + t, kWProd, t1, t0, qb);
+      lds_barrier();  // M
+      lds_barrier();  // B
+    }
+  } else {
+    // consumers
+    const uint32_t c = t - kWProd;
+    for (uint32_t r = 0; r < rounds; ++r) {
+      lds_barrier();  // A
+      const uint64_t r0 = t0 + static_cast<uint64_t>(r) * kRound;
+#pragma unroll
+      for (uint32_t u = 0; u < kRound / kWProd; ++u) {  // rep = rank of the round's rows
+        const uint64_t i = r0 + c + u * kWProd;
+        if (i < t1) rep[i] = in.rank_base + static_cast<uint32_t>(i);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < nbins / kWProd; ++k) {
+        const uint32_t b = c + k * kWProd;
+        if (fill[b] >= 2) {
+          const uint32_t p = cur[b];
+          out[p] = stage[b][0];
+          out[p + 1] = stage[b][1];
+          cur[b] = p + 2;
+          fill[b] = 0;
+        }
+      }
+      const uint32_t no = ovf_n;
+      lds_barrier();  // M: every consumer read ovf_n and the fills; overflow rows next
+      for (uint32_t o = c; o < no; o += kWProd) {
+        const uint3 rq = ovf[o];
+        const uint32_t b = digit_of((static_cast<uint64_t>(rq.y) << 32) | rq.x, skip, kStageBits);
+        out[atomicAdd(&cur[b], 1u)] = rq;
+      }
+      if (c == 0) ovf_n = 0;
+      lds_barrier();  // B
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
+    for (uint32_t k = 0; k < fill[b]; ++k) out[cur[b] + k] = stage[b][k];
+}
+
 // h without its `bits` digit bits [56 - bits, 56): 64 - bits bits
 __device__ __forceinline__ uint64_t key_rest(uint64_t h, uint32_t bits) {
   const uint32_t lo = 56 - bits;
@@ -514,6 +637,9 @@ int main(int argc, char** argv) {
     k_scatter_fixed_stores<<<P, kPartThreads>>>(in, n, kShardBits, fE, ftot, rec, rep1, fbase, dummy,
                                                 dummy_rep);
   };
+  auto w_scatter = [&] {
+    k_scatter_warpspec<<<P, kPartThreads>>>(in, n, kShardBits, fE, ftot, rec, rep1, fbase);
+  };
   struct V {
     const char* name;
     std::function<void()> scan, scatter, group;
@@ -521,7 +647,8 @@ int main(int argc, char** argv) {
   std::vector<V> vs = {{"P0 product 12-B pairs + group12", p0_scan, p0_scatter, p0_group},
                        {"PK product scatter + packed group", p0_scan, p0_scatter, pk_group},
                        {"A2 aligned 16-B pairs + packed group", a2_scan, a2_scatter, a2_group},
-                       {"U0 fixed-count stores + group12", p0_scan, u0_scatter, p0_group}};
+                       {"U0 fixed-count stores + group12", p0_scan, u0_scatter, p0_group},
+                       {"W  warp-specialised + group12", p0_scan, w_scatter, p0_group}};
   for (auto& v : vs) {
     (void)hipMemset(rep1, 0xFF, 4 * n);
     hist();

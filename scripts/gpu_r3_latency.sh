@@ -1,0 +1,10 @@
+# Latency service check: its GPU tests, then the bench's single-file leg alone.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu \
+  tests/test_gpu_latency.py tests/test_gpu_paths.py > gpurun_out/${TAG}_pytest.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest.log; exit 1; }
+tail -2 gpurun_out/${TAG}_pytest.log
+timeout -k 10 300 python -u bench.py --components single --steps 3 --warmup 1 --no-cpu \
+  > gpurun_out/${TAG}_single.json 2> gpurun_out/${TAG}_single.err || exit 1
+python3 -c "import json; print(json.dumps(json.load(open('gpurun_out/${TAG}_single.json'))['components']['single_file_latency'], indent=1))"

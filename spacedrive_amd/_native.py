@@ -59,6 +59,7 @@ def _proto(L):
         "sdgpu_checksum_files": (i32, [ctx, c_vp, u32, c_vp, c_vp]),
         "sdgpu_file_checksum": (i32, [ctx, ctypes.c_char_p, ctypes.c_char_p]),
         "sdgpu_latency_service": (i32, [ctx, i32]),
+        "sdgpu_latency_service_diag": (i32, [ctx, c_vp]),
         "sdgpu_dedup": (i32, [ctx, c_vp, c_vp, u32, u32, c_vp]),
         "sdgpu_group_pairs_device": (i32, [ctx, c_vp, c_vp, u64, u32, u32, c_vp, c_vp]),
         "sdgpu_group_rows_device": (i32, [ctx, c_vp, c_vp, c_vp, u64, u32, u32, c_vp, c_vp]),
@@ -182,6 +183,13 @@ class Context:
         """Single-file calls through the resident latency kernel
         (sdgpu_latency_service)."""
         check(self.lib.sdgpu_latency_service(self.h, 1 if enable else 0), "sdgpu_latency_service")
+
+    def latency_service_diag(self) -> dict:
+        """Breakdown (us) of the last service request."""
+        v = (ctypes.c_double * 4)()
+        check(self.lib.sdgpu_latency_service_diag(self.h, v), "sdgpu_latency_service_diag")
+        return {"copy_to_lds_us": v[0], "hash_us": v[1], "host_post_to_answer_us": v[2],
+                "host_read_us": v[3]}
 
     def set_timing(self, enable: bool = True):
         check(self.lib.sdgpu_set_timing(self.h, 1 if enable else 0), "sdgpu_set_timing")

@@ -628,6 +628,7 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcMailbox* __restrict_
     __syncthreads();
     const uint32_t go = s_go;
     if (go == 0) break;  // uniform: stop, idle or lifetime deadline
+    const uint64_t t_seen = wall_clock64();
     const uint32_t l = min(s_len, kHostStageMax), out_words = min(s_words, 16u);
     {
       const uint32_t nvec = (l + 15) / 16;
@@ -649,6 +650,7 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcMailbox* __restrict_
       }
     }
     __syncthreads();
+    const uint64_t t_loaded = wall_clock64();
     const uint32_t nch = n_chunks_of(l);
     uint32_t c[8];
     if (nch == 1) {
@@ -699,6 +701,9 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcMailbox* __restrict_
       for (uint32_t w = 0; w < out_words; ++w)
         __hip_atomic_store(&mb->digest[w], w < 8 ? c[w] : 0u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->t_seen, t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->t_loaded, t_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->t_done, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&mb->done, go, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       last_seq = go;
     }

@@ -175,6 +175,7 @@ struct sdgpu_ctx {
   bool svc_enabled = false, svc_launched = false;
   uint32_t svc_seq = 0;
   uint64_t svc_idle_ticks = 0, svc_life_ticks = 0;
+  double svc_host_read_us = 0, svc_host_post_us = 0;  // last generate_cas_id (diag)
 };
 
 namespace sdgpu {

@@ -670,6 +670,147 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     for (uint32_t k = 0; k < fill[b]; ++k) out[cur[b] + k] = stage[b][k];
 }
 
+// The 12-bit staged scatter of rows in rank order (RowsIn without a rank
+// array: 12-byte records, rank = rank_base + row), WARP-SPECIALISED.  Waves
+// 0-7 only load and stage: their rows are prefetched two rounds ahead and they
+// never store, so the compiler's waits before a round cover their loads only
+// (in k_part_scatter_rec_staged the conditional record stores sit between a
+// round's prefetch and its use, and the waits there drain them too).  Waves
+// 8-15 only store: the full slot pairs, the rows that met a full slot (an LDS
+// overflow list, kept in arrival order per bucket by an LDS cursor) and, with
+// kInitRep, rep = rank of the round's rows (computed, nothing loaded).  Three
+// barriers per round: staged (A), fills read (M), flushed (B).
+// scripts/exp_scatter_align.hip: 12.5 M rows 0.136 -> 0.123 ms
+// (profiles/r3/exp_scatter_align/run.log).
+constexpr uint32_t kWsProd = 512;   // producer threads (waves 0-7)
+constexpr int kWsRows = 4;          // rows per producer thread per round
+template <bool kInitRep>
+__global__ __launch_bounds__(kPartThreads) void k_part_scatter_ws(
+    RowsIn in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ offs,
+    const uint32_t* __restrict__ ftot, uint3* __restrict__ out, uint32_t* __restrict__ rep,
+    uint32_t* __restrict__ fbase) {
+  constexpr uint32_t nbins = 1u << kStageBits;
+  constexpr uint32_t kRound = kWsProd * kWsRows;  // 2048 rows
+  static_assert(2 * kWsProd == kPartThreads, "half producers, half consumers");
+  __shared__ uint3 stage[nbins][2];
+  __shared__ uint32_t fill[nbins], cur[nbins];
+  __shared__ uint3 ovf[kRound];
+  __shared__ uint32_t ovf_n;
+  // bucket starts: the segment's sizes scanned here, block 0 publishes them
+  constexpr uint32_t kPerT = nbins / kPartThreads;
+  const uint32_t t = threadIdx.x, lane = __lane_id();
+  uint32_t v[kPerT], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPerT; ++k) {
+    v[k] = ftot[t * kPerT + k];
+    sum += v[k];
+  }
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d);
+    if (lane >= static_cast<uint32_t>(d)) inc += o;
+  }
+  if (lane == 63) fill[t >> 6] = inc;
+  __syncthreads();
+  uint32_t base = inc - sum, total = 0;
+  for (uint32_t w = 0; w < kPartThreads / 64; ++w) {
+    if (w < (t >> 6)) base += fill[w];
+    total += fill[w];
+  }
+  __syncthreads();
+  const uint32_t j = part_block();
+#pragma unroll
+  for (uint32_t k = 0; k < kPerT; ++k) {
+    const uint32_t b = t * kPerT + k;
+    cur[b] = base + offs[static_cast<uint64_t>(j) * nbins + b];
+    fill[b] = 0;
+    if (j == 0) fbase[b] = base;
+    base += v[k];
+  }
+  if (j == 0 && t == 0) fbase[nbins] = total;
+  if (t == 0) ovf_n = 0;
+  __syncthreads();
+  uint64_t t0, t1;
+  tile_of(n, gridDim.x, t0, t1);
+  const uint32_t rounds = t1 > t0 ? static_cast<uint32_t>((t1 - t0 + kRound - 1) / kRound) : 0u;
+  if (t < kWsProd) {
+    RowBatch<kWsRows> qa, qb;
+    in.template load_many<kWsRows>(t0 + t, kWsProd, t1, t0, qa);
+    in.template load_many<kWsRows>(t0 + kRound + t, kWsProd, t1, t0, qb);
+    auto stage_round = [&](const RowBatch<kWsRows>& q) {
+#pragma unroll
+      for (int u = 0; u < kWsRows; ++u) {
+        if (!in.valid_of(q, u)) continue;
+        const uint64_t h = row_hash(in.key_of(q, u));
+        const uint32_t b = digit_of(h, skip, kStageBits);
+        const uint3 rq = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32),
+                                    in.row_of(q, u));
+        const uint32_t sl = atomicAdd(&fill[b], 1u);
+        if (sl < 2)
+          stage[b][sl] = rq;
+        else
+          ovf[atomicAdd(&ovf_n, 1u)] = rq;
+      }
+    };
+    // per round exactly the consumers' three barriers (A, M, B); the loads
+    // of round r + 2 go out between A and B, while the consumers store
+    for (uint32_t r = 0; r < rounds; r += 2) {
+      stage_round(qa);
+      lds_barrier();  // A
+      in.template load_many<kWsRows>(t0 + (r + 2) * static_cast<uint64_t>(kRound) + t, kWsProd, t1,
+                                     t0, qa);
+      lds_barrier();  // M
+      lds_barrier();  // B
+      if (r + 1 >= rounds) break;
+      stage_round(qb);
+      lds_barrier();  // A
+      in.template load_many<kWsRows>(t0 + (r + 3) * static_cast<uint64_t>(kRound) + t, kWsProd, t1,
+                                     t0, qb);
+      lds_barrier();  // M
+      lds_barrier();  // B
+    }
+  } else {
+    const uint32_t c = t - kWsProd;
+    for (uint32_t r = 0; r < rounds; ++r) {
+      lds_barrier();  // A
+      if constexpr (kInitRep) {
+        // every row starts as its own Object: rows without a key stay so
+        // (mod.rs:238-239); K5 overwrites only the rows that link
+        const uint64_t r0 = t0 + static_cast<uint64_t>(r) * kRound;
+#pragma unroll
+        for (uint32_t u = 0; u < kRound / kWsProd; ++u) {
+          const uint64_t i = r0 + c + u * kWsProd;
+          if (i < t1) rep[i] = in.rank_base + static_cast<uint32_t>(i);
+        }
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < nbins / kWsProd; ++k) {
+        const uint32_t b = c + k * kWsProd;
+        if (fill[b] >= 2) {
+          const uint32_t p = cur[b];
+          out[p] = stage[b][0];
+          out[p + 1] = stage[b][1];
+          cur[b] = p + 2;
+          fill[b] = 0;
+        }
+      }
+      const uint32_t no = ovf_n;
+      lds_barrier();  // M: fills and ovf_n read by every consumer
+      for (uint32_t o = c; o < no; o += kWsProd) {
+        const uint3 rq = ovf[o];
+        out[atomicAdd(&cur[digit_of((static_cast<uint64_t>(rq.y) << 32) | rq.x, skip, kStageBits)],
+                      1u)] = rq;
+      }
+      if (c == 0) ovf_n = 0;
+      lds_barrier();  // B
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
+    for (uint32_t k = 0; k < fill[b]; ++k) out[cur[b] + k] = stage[b][k];
+}
+
 // First probe slot of a record in the LDS table (kLdsSlots, any size): the
 // low 32 bits of its hash, scaled.  The digit bits (the top ones) are constant
 // inside a bucket, the low ones are not.
@@ -1256,12 +1397,13 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
       if (!in.rank) {  // rank = rank_base + row: 12-byte records
         {
           KScope k(timer, "bucket_scatter", s);
+          uint3* rec12 = reinterpret_cast<uint3*>(rec);
           if (init_rep)
-            k_part_scatter_rec_staged<In, true, kStageBits, 2, 2, true><<<P, kPartThreads, 0, s>>>(
-                in, n, kShardBits, fE, rec, rep, nullptr, 0, ftot, fbase);
+            k_part_scatter_ws<true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, fE, ftot, rec12,
+                                                               rep, fbase);
           else
-            k_part_scatter_rec_staged<In, false, kStageBits, 2, 2, true><<<P, kPartThreads, 0, s>>>(
-                in, n, kShardBits, fE, rec, rep, nullptr, 0, ftot, fbase);
+            k_part_scatter_ws<false><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, fE, ftot, rec12,
+                                                                rep, fbase);
         }
         KScope k(timer, "bucket_group", s);
         k_bucket_group12_pk<<<nb, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),

@@ -94,6 +94,9 @@ struct alignas(64) SvcMailbox {
   uint32_t state;      // kSvcRunning (host, before a launch) / kSvcExited (device)
   uint32_t pad1[14];
   uint32_t digest[16];
+  // device wall clock (s_memrealtime) of the last request: seen, message in
+  // LDS, digest written -- the latency breakdown (sdgpu_latency_service_diag)
+  uint64_t t_seen, t_loaded, t_done;
 };
 constexpr uint32_t kSvcHash = 0, kSvcStop = 1;
 constexpr uint32_t kSvcRunning = 1, kSvcExited = 2;

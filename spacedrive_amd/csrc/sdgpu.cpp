@@ -683,6 +683,22 @@ int service_hash(sdgpu_ctx* c, uint32_t len, uint32_t out_words, uint32_t* diges
 
 }  // namespace
 
+int sdgpu_latency_service_diag(sdgpu_ctx* c, double out_us[4]) {
+  if (!c || !out_us) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->svc_mb) return -ENOENT;
+  SvcMailbox* mb = c->svc_mb;
+  const double tick_us = 1000.0 / static_cast<double>(c->svc_idle_ticks / 20);  // ticks per ms
+  const uint64_t a = __atomic_load_n(&mb->t_seen, __ATOMIC_RELAXED);
+  const uint64_t b = __atomic_load_n(&mb->t_loaded, __ATOMIC_RELAXED);
+  const uint64_t d = __atomic_load_n(&mb->t_done, __ATOMIC_RELAXED);
+  out_us[0] = static_cast<double>(b - a) * tick_us;  // message copied into LDS
+  out_us[1] = static_cast<double>(d - b) * tick_us;  // hashed, digest written
+  out_us[2] = c->svc_host_post_us;                   // host: read + post -> answer seen
+  out_us[3] = c->svc_host_read_us;                   // host: the file read
+  return 0;
+}
+
 int sdgpu_latency_service(sdgpu_ctx* c, int enable) {
   if (!c) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -706,11 +722,16 @@ int sdgpu_generate_cas_id(sdgpu_ctx* c, const char* path, uint64_t size, char ou
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
   if (c->svc_enabled) {
+    const auto t0 = std::chrono::steady_clock::now();
     const int64_t r = read_cas_message(path, size, c->svc_msg, kHostStageMax);
+    const auto t1 = std::chrono::steady_clock::now();
     if (r < 0 && r != -EFBIG) return static_cast<int>(r);
     if (r >= 0) {
       uint32_t d[2];
       const int rc = service_hash(c, static_cast<uint32_t>(r), 2, d);
+      c->svc_host_read_us = std::chrono::duration<double, std::micro>(t1 - t0).count();
+      c->svc_host_post_us =
+          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count();
       if (rc == 0) {
         memcpy(out, d, 8);
         to_hex(out, 8, out_hex);
