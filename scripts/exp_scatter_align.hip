@@ -410,6 +410,149 @@ __global__ __launch_bounds__(kPartThreads) void k_scatter_warpspec(
     for (uint32_t k = 0; k < fill[b]; ++k) out[cur[b] + k] = stage[b][k];
 }
 
+// AW: warp-specialised AND aligned: 16-B records in even-padded (block,
+// bucket) regions, pairs flushed by two adjacent consumer lanes as one aligned
+// 32-B sector, rows that met a full slot to the back of their region (through
+// a 1024-entry LDS list; a producer writes directly only when the list is
+// full -- rare, so its loads' waits stay store-free in the usual round).
+constexpr uint32_t kAwOvf = 1024;
+__global__ __launch_bounds__(kPartThreads) void k_scatter_aw(
+    RowsIn in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ fine,
+    const uint32_t* __restrict__ E, const uint32_t* __restrict__ ftot, uint4* __restrict__ out,
+    uint32_t* __restrict__ rep, uint32_t* __restrict__ fbase) {
+  constexpr uint32_t nbins = kNb;
+  constexpr uint32_t kRound = kWProd * kWU;  // 2048 rows
+  __shared__ uint3 stage[nbins][2];
+  __shared__ uint32_t fill[nbins], front[nbins], back[nbins];
+  __shared__ uint3 ovf[kAwOvf];
+  __shared__ uint32_t ovf_n;
+  constexpr uint32_t kPerT = nbins / kPartThreads;
+  const uint32_t t = threadIdx.x, lane = __lane_id();
+  uint32_t v[kPerT], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPerT; ++k) {
+    v[k] = ftot[t * kPerT + k];
+    sum += v[k];
+  }
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d);
+    if (lane >= static_cast<uint32_t>(d)) inc += o;
+  }
+  if (lane == 63) fill[t >> 6] = inc;
+  __syncthreads();
+  uint32_t base = inc - sum, total = 0;
+  for (uint32_t w = 0; w < kPartThreads / 64; ++w) {
+    if (w < (t >> 6)) base += fill[w];
+    total += fill[w];
+  }
+  __syncthreads();
+  const uint32_t j = part_block();
+#pragma unroll
+  for (uint32_t k = 0; k < kPerT; ++k) {
+    const uint32_t b = t * kPerT + k;
+    const uint32_t f0 = base + E[static_cast<uint64_t>(j) * nbins + b];
+    front[b] = f0;
+    back[b] = f0 + ((fine[static_cast<uint64_t>(j) * nbins + b] + 1u) & ~1u);
+    fill[b] = 0;
+    if (j == 0) fbase[b] = base;
+    base += v[k];
+  }
+  if (j == 0 && t == 0) fbase[nbins] = total;
+  if (t == 0) ovf_n = 0;
+  __syncthreads();
+  uint64_t t0, t1;
+  tile_of(n, gridDim.x, t0, t1);
+  const uint32_t rb = in.rank_base;
+  const uint32_t rounds = t1 > t0 ? static_cast<uint32_t>((t1 - t0 + kRound - 1) / kRound) : 0u;
+  if (t < kWProd) {
+    RowBatch<kWU> qa, qb;
+    in.template load_many<kWU>(t0 + t, kWProd, t1, t0, qa);
+    in.template load_many<kWU>(t0 + kRound + t, kWProd, t1, t0, qb);
+    auto stage_round = [&](const RowBatch<kWU>& q) {
+#pragma unroll
+      for (int u = 0; u < kWU; ++u) {
+        if (!in.valid_of(q, u)) continue;
+        const uint64_t h = row_hash(in.key_of(q, u));
+        const uint32_t b = digit_of(h, skip, kStageBits);
+        const uint32_t row = in.row_of(q, u);
+        const uint32_t sl = atomicAdd(&fill[b], 1u);
+        if (sl < 2) {
+          stage[b][sl] = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), row);
+        } else {
+          const uint32_t o = atomicAdd(&ovf_n, 1u);
+          if (o < kAwOvf)
+            ovf[o] = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), row);
+          else  // list full (many rows of one key in a round): directly
+            out[atomicSub(&back[b], 1u) - 1u] =
+                make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), rb + row, row);
+        }
+      }
+    };
+    for (uint32_t r = 0; r < rounds; r += 2) {
+      stage_round(qa);
+      lds_barrier();  // A
+      in.template load_many<kWU>(t0 + (r + 2) * static_cast<uint64_t>(kRound) + t, kWProd, t1, t0, qa);
+      lds_barrier();  // M
+      lds_barrier();  // B
+      if (r + 1 >= rounds) break;
+      stage_round(qb);
+      lds_barrier();  // A
+      in.template load_many<kWU>(t0 + (r + 3) * static_cast<uint64_t>(kRound) + t, kWProd, t1, t0, qb);
+      lds_barrier();  // M
+      lds_barrier();  // B
+    }
+  } else {
+    const uint32_t c = t - kWProd, slot = c & 1u;
+    for (uint32_t r = 0; r < rounds; ++r) {
+      lds_barrier();  // A
+      const uint64_t r0 = t0 + static_cast<uint64_t>(r) * kRound;
+#pragma unroll
+      for (uint32_t u = 0; u < kRound / kWProd; ++u) {
+        const uint64_t i = r0 + c + u * kWProd;
+        if (i < t1) rep[i] = rb + static_cast<uint32_t>(i);
+      }
+      // lanes 2m, 2m+1: slot 0 / 1 of one bucket -> one aligned 32-B sector
+#pragma unroll
+      for (uint32_t k = 0; k < 2 * nbins / kWProd; ++k) {
+        const uint32_t b = (c >> 1) + k * (kWProd / 2);
+        if (fill[b] >= 2) {
+          const uint32_t p = front[b];
+          const uint3 rr = stage[b][slot];
+          out[p + slot] = make_uint4(rr.x, rr.y, rb + rr.z, rr.z);
+        }
+      }
+      const uint32_t no = min(ovf_n, kAwOvf);
+      lds_barrier();  // M: every consumer has read the fills, front and ovf_n
+#pragma unroll
+      for (uint32_t k = 0; k < nbins / kWProd; ++k) {
+        const uint32_t b = c + k * kWProd;
+        if (fill[b] >= 2) {
+          front[b] += 2;
+          fill[b] = 0;
+        }
+      }
+      for (uint32_t o = c; o < no; o += kWProd) {
+        const uint3 rr = ovf[o];
+        const uint32_t b = digit_of((static_cast<uint64_t>(rr.y) << 32) | rr.x, skip, kStageBits);
+        out[atomicSub(&back[b], 1u) - 1u] = make_uint4(rr.x, rr.y, rb + rr.z, rr.z);
+      }
+      if (c == 0) ovf_n = 0;
+      lds_barrier();  // B
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) {
+    uint32_t p = front[b];
+    if (fill[b] == 1) {
+      const uint3 rr = stage[b][0];
+      out[p++] = make_uint4(rr.x, rr.y, rb + rr.z, rr.z);
+    }
+    if (p < back[b]) out[p] = make_uint4(0u, 0u, kPad, kPad);
+  }
+}
+
 // h without its `bits` digit bits [56 - bits, 56): 64 - bits bits
 __device__ __forceinline__ uint64_t key_rest(uint64_t h, uint32_t bits) {
   const uint32_t lo = 56 - bits;
@@ -637,6 +780,9 @@ int main(int argc, char** argv) {
     k_scatter_fixed_stores<<<P, kPartThreads>>>(in, n, kShardBits, fE, ftot, rec, rep1, fbase, dummy,
                                                 dummy_rep);
   };
+  auto aw_scatter = [&] {
+    k_scatter_aw<<<P, kPartThreads>>>(in, n, kShardBits, fine, fE, ftot, rec16, rep1, fbase);
+  };
   auto w_scatter = [&] {
     k_scatter_warpspec<<<P, kPartThreads>>>(in, n, kShardBits, fE, ftot, rec, rep1, fbase);
   };
@@ -648,7 +794,9 @@ int main(int argc, char** argv) {
                        {"PK product scatter + packed group", p0_scan, p0_scatter, pk_group},
                        {"A2 aligned 16-B pairs + packed group", a2_scan, a2_scatter, a2_group},
                        {"U0 fixed-count stores + group12", p0_scan, u0_scatter, p0_group},
-                       {"W  warp-specialised + group12", p0_scan, w_scatter, p0_group}};
+                       {"W  warp-specialised + group12", p0_scan, w_scatter, p0_group},
+                       {"WP warp-specialised + packed group", p0_scan, w_scatter, pk_group},
+                       {"AW aligned warp-spec. + packed group", a2_scan, aw_scatter, a2_group}};
   for (auto& v : vs) {
     (void)hipMemset(rep1, 0xFF, 4 * n);
     hist();
