@@ -44,8 +44,10 @@ class FakeRunner:
     def run_cas(self, steps, warmup):
         if MODE == "cas_raises":
             raise RuntimeError("injected K1 failure")
+        job = ({"error": "SdgpuError(-110, 'sdgpu_group_sharded_device: timed out')"}
+               if MODE == "job_fails" else {"value": 7.4e7, "ms_per_step": 13.5})
         return {"cas": {"value": 7.5e7, "unit": "files/s", "ms_per_step": 13.3},
-                "job": {"value": 7.4e7, "ms_per_step": 13.5},
+                "job": job,
                 "kernels": {"cas_leaves": {"avg_ms": 13.0, "launches": 20}},
                 "roofline_inputs": {"chunk_blocks": 1, "parents": 0,
                                     "leaf_compressions": 685_757_283, "fold_compressions": 0,
@@ -121,3 +123,14 @@ def test_failed_headline_still_prints_a_line():
     d = json.loads(lines[0])
     assert d["value"] is None and "injected K1" in d["components"]["cas"]["error"]
     assert d["components"]["checksum"]["value"] == 3100.0
+
+
+def test_failed_exchange_keeps_a_cas_headline():
+    """The identifier step's exchange fails (e.g. -ETIMEDOUT from a dead peer):
+    the line reports K1's cas_id rate as value, says so, and keeps roofline."""
+    p, lines, _ = _run("job_fails")
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(lines[0])
+    assert d["value"] == 7.5e7 and "job step failed" in d["headline_note"]
+    assert "timed out" in d["components"]["identifier_job"]["error"]
+    assert d["roofline"]["bound"] == "valu" and d["cpu_baseline"]["kind"] == "port"
