@@ -648,8 +648,10 @@ class Runner:
             # PMC HBM bytes per launch (committed FETCH_SIZE / WRITE_SIZE passes of
             # this 12.5 M-row grouping) beside the algorithmic bytes, and the whole
             # step against SURVEY 8(d)'s 16 B per row
-            pmc_names = {"bucket_hist": "k_part_hist", "bucket_scatter": "k_part_scatter_rec_staged",
-                         "bucket_group": "k_bucket_group12" if implicit else "k_bucket_group"}
+            pmc_names = {"bucket_hist": "k_part_hist",
+                         "bucket_scatter": ("k_part_scatter_ws" if implicit
+                                            else "k_part_scatter_rec_staged"),
+                         "bucket_group": "k_bucket_group12_pk" if implicit else "k_bucket_group_pk"}
             src = None
             for k, kn in pmc_names.items():
                 b_, src_ = pmc_traffic(kn, "dedup")
@@ -774,7 +776,8 @@ class Runner:
                "bucket_scatter": 24 * nk,
                "bucket_group": 12 * nk + 4 * linked}
         pmc_names = {"bucket_hist": "k_part_hist", "bucket_scatter1": "k_part_scatter_runs",
-                     "bucket_scatter": "k_part_scatter_rec_staged", "bucket_group": "k_bucket_group12"}
+                     "bucket_scatter": "k_part_scatter_rec_staged",
+                     "bucket_group": "k_bucket_group12_pk"}
         step_s = t / steps
         roof = {"bound": "hbm", "peak": HBM_PEAK / 1e9, "unit": "GB/s", "linked_rows": linked,
                 "kernels": {}, "note": "algorithmic bytes of the two-level partition + group-by "
