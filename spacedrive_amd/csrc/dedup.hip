@@ -515,6 +515,19 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
   RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
   __shared__ uint32_t fill[nbins];
   __shared__ uint32_t cur[nbins];
+  // Fewer buckets than threads (the two-level second pass): the row that
+  // fills a bucket's kSlots slots lists the bucket, and the flush writes each
+  // listed bucket's run with kSlots ADJACENT lanes, so a store instruction
+  // covers 64 / kSlots whole runs.  (Two lanes per bucket, each writing every
+  // other record, touched 32 runs per instruction: the store pattern, not the
+  // bytes, set the pass's time -- scripts/exp_stores.hip, runs of 2 vs 16:
+  // 0.133 vs 0.033 ms for 201 MB.)  full_n by round parity: the count of
+  // round r + 1 is cleared during round r's flush, when nothing reads it.
+  constexpr bool kCoop = nbins < kPartThreads;
+  static_assert(!kCoop || (64 % kSlots == 0 && kPartThreads % kSlots == 0),
+                "a bucket's run is written by lanes of one wave");
+  __shared__ uint16_t full[kCoop ? nbins : 1];
+  __shared__ uint32_t full_n[2];
   const uint32_t c = blockIdx.y;
   uint64_t t0 = 0, t1 = 0;
   if (ftot) {
@@ -577,6 +590,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       fill[b] = 0;
     }
   }
+  if (threadIdx.x == 0) full_n[0] = full_n[1] = 0;
   __syncthreads();
   if (ftot) {
     // tile set above
@@ -593,7 +607,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
   // one round: stage (or write) the batch's rows, then flush the full slots.
   // The round barriers wait for LDS only (lds_barrier), so the next round's
   // loads and this round's record stores stay in flight across them.
-  auto round = [&](const RowBatch<U>& q, uint64_t i0) {
+  auto round = [&](const RowBatch<U>& q, uint64_t i0, uint32_t par) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t i = i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads;
@@ -611,6 +625,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       const uint32_t sl = atomicAdd(&fill[b], 1u);
       if (sl < kSlots) {
         stage[b][sl] = rq;
+        if constexpr (kCoop)
+          if (sl == kSlots - 1) full[atomicAdd(&full_n[par], 1u)] = static_cast<uint16_t>(b);
       } else {
         out[atomicAdd(&cur[b], 1u)] = rq;
       }
@@ -632,16 +648,17 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
         }
       }
     } else {
-      // T adjacent lanes of one wave per bin, each writing every T-th record;
-      // the wave reads fill / cur before its first lane updates them
-      constexpr uint32_t T = kPartThreads / nbins;
-      static_assert(kPartThreads % nbins == 0 && T <= 64 && kSlots % T == 0, "flush lanes per bin");
-      const uint32_t b = threadIdx.x / T, part = threadIdx.x % T;
-      const uint32_t f = fill[b], p = cur[b];
-      if (f >= kSlots) {
-#pragma unroll
-        for (uint32_t k = part; k < kSlots; k += T) out[p + k] = stage[b][k];
-        if (part == 0) {
+      // lane group x / kSlots writes listed bucket e's record x % kSlots; the
+      // group's lanes read cur[b] in the same instruction, before its first
+      // lane advances it
+      const uint32_t nf = full_n[par];
+      if (threadIdx.x == 0) full_n[par ^ 1u] = 0;
+      for (uint32_t x = threadIdx.x; x < nf * kSlots; x += kPartThreads) {
+        const uint32_t e = x / kSlots, k = x % kSlots;
+        const uint32_t b = full[e];
+        const uint32_t p = cur[b];
+        out[p + k] = stage[b][k];
+        if (k == 0) {
           cur[b] = p + kSlots;
           fill[b] = 0;
         }
@@ -659,10 +676,10 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     in.template load_many<U>(t0 + threadIdx.x, kPartThreads, t1, t0, qa);
     for (uint64_t i0 = t0;; i0 += 2 * kStep) {  // uniform trip count
       in.template load_many<U>(i0 + kStep + threadIdx.x, kPartThreads, t1, t0, qb);
-      round(qa, i0);
+      round(qa, i0, 0u);
       if (i0 + kStep >= t1) break;
       in.template load_many<U>(i0 + 2 * kStep + threadIdx.x, kPartThreads, t1, t0, qa);
-      round(qb, i0 + kStep);
+      round(qb, i0 + kStep, 1u);
       if (i0 + 2 * kStep >= t1) break;
     }
   }
