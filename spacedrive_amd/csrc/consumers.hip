@@ -44,11 +44,13 @@ __global__ __launch_bounds__(kThreads) void k_mark(const int32_t* __restrict__ f
   const uint64_t stride = static_cast<uint64_t>(gridDim.x / kMarkRanges) * kThreads * 4;
   for (uint64_t i0 = static_cast<uint64_t>(g) * kThreads * 4 + threadIdx.x; i0 < n; i0 += stride) {
     int32_t o[4];
+    // loads unconditional (clamped), the tail masked after: a guarded load
+    // made the compiler wait out each load's latency in turn
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint64_t i = i0 + static_cast<uint64_t>(u) * kThreads;
-      o[u] = i < n ? fp_obj[i] : -1;
-    }
+    for (int u = 0; u < 4; ++u) o[u] = fp_obj[min(i0 + static_cast<uint64_t>(u) * kThreads, n - 1)];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + static_cast<uint64_t>(u) * kThreads >= n) o[u] = -1;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint32_t d = static_cast<uint32_t>(o[u]) - lo;  // negative ids wrap past span
@@ -57,9 +59,15 @@ __global__ __launch_bounds__(kThreads) void k_mark(const int32_t* __restrict__ f
   }
 }
 
-// Object o is an orphan: no file_path marked it (ids past max_id are never marked)
-__device__ __forceinline__ bool orphan(int32_t o, const uint8_t* mark, uint32_t max_id) {
-  return o >= 0 && (static_cast<uint32_t>(o) > max_id || mark[o] == 0);
+// Object o is an orphan: no file_path marked it (ids past max_id are never
+// marked).  m = mark[o] read beforehand for every id (mark_of), so the kRows
+// gathers of a thread are in flight together.
+__device__ __forceinline__ bool orphan(int32_t o, uint8_t m, uint32_t max_id) {
+  return o >= 0 && (static_cast<uint32_t>(o) > max_id || m == 0);
+}
+__device__ __forceinline__ uint8_t mark_of(int32_t o, const uint8_t* mark, uint32_t max_id) {
+  const uint32_t c = o < 0 ? 0u : min(static_cast<uint32_t>(o), max_id);  // any in-range byte
+  return mark[c];
 }
 
 // The Object list in tiles of kORows x kThreads ids: id tile + k * kThreads + t
@@ -69,9 +77,18 @@ constexpr int kORows = 16;
 constexpr uint64_t kOTile = static_cast<uint64_t>(kORows) * kThreads;
 constexpr int kOWaves = kThreads / 64;
 
-__device__ __forceinline__ int32_t obj_at(const int32_t* __restrict__ obj, uint64_t n,
-                                          uint64_t i) {
-  return i < n ? obj[i] : -1;
+// the kORows ids of a thread (loads unconditional, tail masked after), then
+// their mark bytes
+__device__ __forceinline__ void obj_tile(const int32_t* __restrict__ obj, uint64_t n, uint64_t tile,
+                                         const uint8_t* __restrict__ bits, uint32_t max_id,
+                                         int32_t (&o)[kORows], uint8_t (&m)[kORows]) {
+#pragma unroll
+  for (int k = 0; k < kORows; ++k) o[k] = obj[min(tile + k * kThreads + threadIdx.x, n - 1)];
+#pragma unroll
+  for (int k = 0; k < kORows; ++k)
+    if (tile + k * kThreads + threadIdx.x >= n) o[k] = -1;
+#pragma unroll
+  for (int k = 0; k < kORows; ++k) m[k] = mark_of(o[k], bits, max_id);
 }
 
 // orphans per tile
@@ -83,11 +100,11 @@ __global__ __launch_bounds__(kThreads) void k_orphan_count(const int32_t* __rest
   __shared__ uint32_t sw[kOWaves];
   const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * kOTile;
   int32_t o[kORows];
-#pragma unroll
-  for (int k = 0; k < kORows; ++k) o[k] = obj_at(obj, n, tile + k * kThreads + threadIdx.x);
+  uint8_t m[kORows];
+  obj_tile(obj, n, tile, bits, max_id, o, m);
   uint32_t c = 0;
 #pragma unroll
-  for (int k = 0; k < kORows; ++k) c += orphan(o[k], bits, max_id) ? 1u : 0u;
+  for (int k = 0; k < kORows; ++k) c += orphan(o[k], m[k], max_id) ? 1u : 0u;
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
   if (__lane_id() == 0) sw[threadIdx.x >> 6] = c;
@@ -111,12 +128,12 @@ __global__ __launch_bounds__(kThreads) void k_orphan_write(const int32_t* __rest
   const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
   int32_t o[kORows];
+  uint8_t m[kORows];
   uint32_t pre[kORows], f = 0;
-#pragma unroll
-  for (int k = 0; k < kORows; ++k) o[k] = obj_at(obj, n, tile + k * kThreads + threadIdx.x);
+  obj_tile(obj, n, tile, bits, max_id, o, m);
 #pragma unroll
   for (int k = 0; k < kORows; ++k) {
-    const bool is = orphan(o[k], bits, max_id);
+    const bool is = orphan(o[k], m[k], max_id);
     f |= (is ? 1u : 0u) << k;
     const uint64_t b = __ballot(is);
     pre[k] = __popcll(b & lt);

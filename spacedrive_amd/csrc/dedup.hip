@@ -877,12 +877,13 @@ struct Rec12Src {
 template <typename Src>
 __device__ __forceinline__ void load_bucket(Src rec, uint32_t start, uint32_t end,
                                             uint4 (&q_reg)[kPer]) {
-  if (end - start > kLdsCap) return;
+  if (end - start > kLdsCap || end == start) return;
+  // unconditional loads, selected after (see group_bucket_packed)
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const uint32_t i = start + threadIdx.x + j * kGroupThreads;
-    q_reg[j] = i < end ? rec(i) : make_uint4(0, 0, 0, 0);
-  }
+  for (int j = 0; j < kPer; ++j) q_reg[j] = rec(min(start + threadIdx.x + j * kGroupThreads, end - 1));
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if (start + threadIdx.x + j * kGroupThreads >= end) q_reg[j] = make_uint4(0, 0, 0, 0);
 }
 
 // Group-by of one bucket too large for LDS: a private region of the global
@@ -1061,12 +1062,16 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
     group_bucket_global(rec, start, end, chunk_of, gkey, gmin, rep, special_min);
     return;
   }
+  // every load issued unconditionally (past the end: the bucket's last record)
+  // and the pad selected after: a guarded `i < end ? rec(i) : pad` made the
+  // compiler branch around each load and wait out its latency before the
+  // next one (four serial memory latencies per workgroup)
   uint4 q[kP];
 #pragma unroll
-  for (int j = 0; j < kP; ++j) {
-    const uint32_t i = start + threadIdx.x + j * kGroupThreads;
-    q[j] = i < end ? rec(i) : make_uint4(0, 0, kPadRow, kPadRow);
-  }
+  for (int j = 0; j < kP; ++j) q[j] = rec(min(start + threadIdx.x + j * kGroupThreads, end - 1));
+#pragma unroll
+  for (int j = 0; j < kP; ++j)
+    if (start + threadIdx.x + j * kGroupThreads >= end) q[j] = make_uint4(0, 0, kPadRow, kPadRow);
   for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
   for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
   __syncthreads();

@@ -34,15 +34,38 @@ struct LinkRow {
   bool c, l;  // creates an Object / connects to one
 };
 
-__device__ __forceinline__ LinkRow link_row(const uint32_t* __restrict__ rep,
-                                            const uint32_t* __restrict__ rank,
-                                            const uint8_t* __restrict__ valid, uint32_t first_rank,
-                                            uint64_t n, uint64_t i) {
-  LinkRow x{0, 0, false, false};
-  if (i >= n) return x;
-  x.r = rank ? rank[i] : first_rank + static_cast<uint32_t>(i);
-  x.p = rep[i];
-  const bool v = valid ? valid[i] != 0 : true;
+// The kRows rows of a thread: every load issued first and unconditionally
+// (rows past the end read row n - 1; a null rank / valid array is replaced by
+// the rep array, whose lines are loaded anyway), the rows resolved at use.  A
+// guarded load -- `i < n`, or a select on the null pointer -- made the
+// compiler branch around each load and wait out its latency in turn.
+struct LinkRows {
+  uint32_t a[kRows], p[kRows], b[kRows];
+};
+
+__device__ __forceinline__ void link_load(const uint32_t* __restrict__ rep,
+                                          const uint32_t* __restrict__ rank,
+                                          const uint8_t* __restrict__ valid, uint64_t n,
+                                          uint64_t tile, LinkRows& q) {
+  const uint32_t* rs = rank ? rank : rep;
+  const uint8_t* vs = valid ? valid : reinterpret_cast<const uint8_t*>(rep);
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const uint64_t i = tile + k * kThreads + threadIdx.x;
+    const uint64_t j = i < n ? i : n - 1;
+    q.p[k] = rep[j];
+    q.a[k] = rs[j];
+    q.b[k] = vs[j];
+  }
+}
+
+__device__ __forceinline__ LinkRow link_row(const LinkRows& q, int k, const uint32_t* rank,
+                                            const uint8_t* valid, uint32_t first_rank, uint64_t n,
+                                            uint64_t i) {
+  LinkRow x;
+  x.r = rank ? q.a[k] : first_rank + static_cast<uint32_t>(i);
+  x.p = q.p[k];
+  const bool v = i < n && (!valid || (q.b[k] & 0xFFu) != 0);
   x.c = v && x.p == x.r;
   x.l = v && x.p != x.r;
   return x;
@@ -57,9 +80,11 @@ __global__ __launch_bounds__(kThreads) void k_link_count(const uint32_t* __restr
   __shared__ uint32_t sc[kWaves], sl[kWaves];
   const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * kTile;
   uint32_t c = 0, l = 0;
+  LinkRows q;
+  link_load(rep, rank, valid, n, tile, q);
 #pragma unroll
   for (int k = 0; k < kRows; ++k) {
-    const LinkRow x = link_row(rep, rank, valid, first_rank, n, tile + k * kThreads + threadIdx.x);
+    const LinkRow x = link_row(q, k, rank, valid, first_rank, n, tile + k * kThreads + threadIdx.x);
     c += x.c;
     l += x.l;
   }
@@ -102,9 +127,11 @@ __global__ __launch_bounds__(kThreads) void k_link_write(
   }
   LinkRow x[kRows];
   uint32_t pc[kRows], pl[kRows];
+  LinkRows q;
+  link_load(rep, rank, valid, n, tile, q);
 #pragma unroll
   for (int k = 0; k < kRows; ++k) {
-    x[k] = link_row(rep, rank, valid, first_rank, n, tile + k * kThreads + threadIdx.x);
+    x[k] = link_row(q, k, rank, valid, first_rank, n, tile + k * kThreads + threadIdx.x);
     const uint64_t bc = __ballot(x[k].c), bl = __ballot(x[k].l);
     pc[k] = __popcll(bc & lt);
     pl[k] = __popcll(bl & lt);
