@@ -526,8 +526,10 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
   constexpr bool kCoop = nbins < kPartThreads;
   static_assert(!kCoop || (64 % kSlots == 0 && kPartThreads % kSlots == 0),
                 "a bucket's run is written by lanes of one wave");
+  // (absent from the 12-bit 16-byte variant, whose stage, fill and cur fill
+  // the 160 KiB exactly: referenced only under kCoop)
   __shared__ uint16_t full[kCoop ? nbins : 1];
-  __shared__ uint32_t full_n[2];
+  __shared__ uint32_t full_n[kCoop ? 2 : 1];
   const uint32_t c = blockIdx.y;
   uint64_t t0 = 0, t1 = 0;
   if (ftot) {
@@ -590,7 +592,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       fill[b] = 0;
     }
   }
-  if (threadIdx.x == 0) full_n[0] = full_n[1] = 0;
+  if constexpr (kCoop)
+    if (threadIdx.x == 0) full_n[0] = full_n[1] = 0;
   __syncthreads();
   if (ftot) {
     // tile set above
@@ -626,7 +629,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       if (sl < kSlots) {
         stage[b][sl] = rq;
         if constexpr (kCoop)
-          if (sl == kSlots - 1) full[atomicAdd(&full_n[par], 1u)] = static_cast<uint16_t>(b);
+          if (sl == kSlots - 1)
+            full[atomicAdd(&full_n[par & (kCoop ? 1u : 0u)], 1u)] = static_cast<uint16_t>(b);
       } else {
         out[atomicAdd(&cur[b], 1u)] = rq;
       }
@@ -651,8 +655,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       // lane group x / kSlots writes listed bucket e's record x % kSlots; the
       // group's lanes read cur[b] in the same instruction, before its first
       // lane advances it
-      const uint32_t nf = full_n[par];
-      if (threadIdx.x == 0) full_n[par ^ 1u] = 0;
+      const uint32_t nf = full_n[par & (kCoop ? 1u : 0u)];
+      if (threadIdx.x == 0) full_n[(par ^ 1u) & (kCoop ? 1u : 0u)] = 0;
       for (uint32_t x = threadIdx.x; x < nf * kSlots; x += kPartThreads) {
         const uint32_t e = x / kSlots, k = x % kSlots;
         const uint32_t b = full[e];

@@ -7,6 +7,8 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <stddef.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -110,8 +112,33 @@ inline int64_t read_cas_message(const char* path, uint64_t size, uint8_t* dst, s
 }
 
 
+// CPUs' worth of time the process may use: cgroup v2 cpu.max ("max" or
+// "<quota> <period>"), 0 when unlimited or unreadable.
+inline uint32_t cgroup_cpus() {
+  FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r");
+  if (!f) return 0;
+  char q[32] = {0};
+  unsigned long long period = 0;
+  const int got = fscanf(f, "%31s %llu", q, &period);
+  fclose(f);
+  if (got != 2 || period == 0 || q[0] < '0' || q[0] > '9') return 0;
+  return static_cast<uint32_t>(strtoull(q, nullptr, 10) / period);
+}
+
+// File-read threads: SDGPU_IO_THREADS if set, else min(16, hardware threads,
+// the cgroup's CPU quota).
 inline uint32_t io_threads() {
-  return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  static const uint32_t n = [] {
+    if (const char* e = getenv("SDGPU_IO_THREADS")) {
+      const unsigned long v = strtoul(e, nullptr, 10);
+      if (v >= 1 && v <= 256) return static_cast<uint32_t>(v);
+    }
+    uint32_t t = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    const uint32_t q = cgroup_cpus();
+    if (q) t = std::min(t, q);
+    return std::max(1u, t);
+  }();
+  return n;
 }
 
 // Persistent workers for the per-slab file reads: a staging call fills many
