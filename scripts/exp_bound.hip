@@ -1003,10 +1003,10 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group11(const uint3* __res
   if (threadIdx.x < 2) scnt[threadIdx.x] = 0;
   uint3 q[kG2Per];
 #pragma unroll
-  for (int j = 0; j < kG2Per; ++j) {
-    const uint32_t i = start + threadIdx.x + j * kGroupThreads;
-    q[j] = i < end ? rec[i] : make_uint3(0, 0, kPadRow);
-  }
+  for (int j = 0; j < kG2Per; ++j) q[j] = rec[min(start + threadIdx.x + j * kGroupThreads, end - 1)];
+#pragma unroll
+  for (int j = 0; j < kG2Per; ++j)
+    if (start + threadIdx.x + j * kGroupThreads >= end) q[j] = make_uint3(0, 0, kPadRow);
   __syncthreads();  // scnt
   uint64_t mine[kG2Per];
   uint32_t row[kG2Per], sub1 = 0, live = 0;
@@ -1111,10 +1111,10 @@ __global__ __launch_bounds__(kGroupThreads, 4) void k_group11b(const uint3* __re
   if (threadIdx.x < 2) scnt[threadIdx.x] = 0;
   uint3 q[kG2Per];
 #pragma unroll
-  for (int j = 0; j < kG2Per; ++j) {
-    const uint32_t i = start + threadIdx.x + j * kGroupThreads;
-    q[j] = i < end ? rec[i] : make_uint3(0, 0, kPadRow);
-  }
+  for (int j = 0; j < kG2Per; ++j) q[j] = rec[min(start + threadIdx.x + j * kGroupThreads, end - 1)];
+#pragma unroll
+  for (int j = 0; j < kG2Per; ++j)
+    if (start + threadIdx.x + j * kGroupThreads >= end) q[j] = make_uint3(0, 0, kPadRow);
   for (uint32_t s = threadIdx.x; s < 2 * kPkSlots; s += kGroupThreads) (&tab[0][0])[s] = 0ull;
   for (uint32_t s = threadIdx.x; s < 2 * (kPkCap + 1); s += kGroupThreads) (&lmin[0][0])[s] = 0xFFFFFFFFu;
   __syncthreads();  // scnt, tables
@@ -1286,6 +1286,185 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_pers(const uint3* __
     }
     __syncthreads();
   }
+}
+
+// Asynchronous producer / consumer rounds: no workgroup barrier per round.
+// Producers stage round r and, the last of their waves to finish, publish
+// pround = r + 1; consumers flush round r's LISTED full buckets (and its
+// overflow list) once pround > r, the last of their waves publishing
+// cround = r + 1 after clearing round r's list counts.  A producer stages
+// round r only after cround >= r - 1 (list buffers by round parity), so the
+// producers run up to two rounds ahead instead of alternating with the
+// consumers.  A flushed bucket's cursor is taken by an atomic (producers take
+// cursors too when the overflow list is full) and its fill reset after its
+// slots are read: a row arriving meanwhile saw fill >= 2 and went to the
+// overflow list.  Every poll is bounded (kSpinCap): a broken protocol gives
+// wrong rows, not a hung device.
+constexpr uint32_t kAsyncOvf = 256;
+constexpr uint32_t kSpinCap = 1u << 22;
+__device__ __forceinline__ void spin_until(const uint32_t* ctr, uint32_t target, uint32_t* err) {
+  uint32_t it = 0;
+  while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++it > kSpinCap) {
+      *err = 1u;
+      break;
+    }
+  }
+}
+template <bool kStore>
+__global__ __launch_bounds__(kPartThreads) void k_ws_async(RowsIn in, uint64_t n, uint32_t skip,
+                                                           const uint32_t* __restrict__ offs,
+                                                           const uint32_t* __restrict__ ftot,
+                                                           uint3* __restrict__ out,
+                                                           uint32_t* __restrict__ rep,
+                                                           uint32_t* __restrict__ fbase,
+                                                           uint32_t* __restrict__ err) {
+  constexpr uint32_t nbins = kNb;
+  constexpr uint32_t kRound = kWsProd * kWsRows;
+  constexpr uint32_t kPW = kWsProd / 64;  // producer waves
+  __shared__ uint3 stage[nbins][2];
+  __shared__ uint32_t fill[nbins], cur[nbins];
+  __shared__ uint16_t flist[2][nbins];
+  __shared__ uint3 ovf[2][kAsyncOvf];
+  __shared__ uint32_t fn[2], on[2], pc[2], cc[2], pround, cround;
+  constexpr uint32_t kPerT = nbins / kPartThreads;
+  const uint32_t t = threadIdx.x, lane = __lane_id();
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(&flist[0][0]);  // prologue scratch
+  uint32_t v[kPerT], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPerT; ++k) {
+    v[k] = ftot[t * kPerT + k];
+    sum += v[k];
+  }
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d);
+    if (lane >= static_cast<uint32_t>(d)) inc += o;
+  }
+  if (lane == 63) wsum[t >> 6] = inc;
+  __syncthreads();
+  uint32_t base = inc - sum, total = 0;
+  for (uint32_t w = 0; w < kPartThreads / 64; ++w) {
+    if (w < (t >> 6)) base += wsum[w];
+    total += wsum[w];
+  }
+  __syncthreads();
+  const uint32_t j = part_block();
+#pragma unroll
+  for (uint32_t k = 0; k < kPerT; ++k) {
+    const uint32_t b = t * kPerT + k;
+    cur[b] = base + offs[static_cast<uint64_t>(j) * nbins + b];
+    fill[b] = 0;
+    if (j == 0) fbase[b] = base;
+    base += v[k];
+  }
+  if (j == 0 && t == 0) fbase[nbins] = total;
+  if (t == 0) {
+    fn[0] = fn[1] = on[0] = on[1] = 0;
+    pc[0] = pc[1] = cc[0] = cc[1] = 0;
+    pround = cround = 0;
+  }
+  __syncthreads();
+  uint64_t t0, t1;
+  tile_of(n, gridDim.x, t0, t1);
+  const uint32_t rounds = t1 > t0 ? static_cast<uint32_t>((t1 - t0 + kRound - 1) / kRound) : 0u;
+  if (t < kWsProd) {
+    RowBatch<kWsRows> qa, qb;
+    in.template load_many<kWsRows>(t0 + t, kWsProd, t1, t0, qa);
+    in.template load_many<kWsRows>(t0 + kRound + t, kWsProd, t1, t0, qb);
+    auto stage_round = [&](const RowBatch<kWsRows>& q, uint32_t r) {
+      const uint32_t par = r & 1u;
+      if (r >= 2) spin_until(&cround, r - 1, err);  // round r - 2's lists consumed
+#pragma unroll
+      for (int u = 0; u < kWsRows; ++u) {
+        if (!in.valid_of(q, u)) continue;
+        const uint64_t h = row_hash(in.key_of(q, u));
+        const uint32_t b = digit_of(h, skip, kStageBits);
+        const uint3 rq = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32),
+                                    in.row_of(q, u));
+        const uint32_t sl = atomicAdd(&fill[b], 1u);
+        if (sl < 2) {
+          stage[b][sl] = rq;
+          if (sl == 1) flist[par][atomicAdd(&fn[par], 1u)] = static_cast<uint16_t>(b);
+        } else {
+          const uint32_t o = atomicAdd(&on[par], 1u);
+          if (o < kAsyncOvf) {
+            ovf[par][o] = rq;
+          } else {
+            const uint32_t p = atomicAdd(&cur[b], 1u);
+            if constexpr (kStore) out[p] = rq;
+          }
+        }
+      }
+      // publish: every LDS write of this wave done, then one arrival per wave
+      // on the round's (parity) counter; its last arriver resets the counter
+      // and advances pround (atomic max: waves may be a round apart)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        const uint32_t a = __hip_atomic_fetch_add(&pc[par], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (a == kPW - 1) {
+          pc[par] = 0;
+          __hip_atomic_fetch_max(&pround, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    };
+    for (uint32_t r = 0; r < rounds; r += 2) {
+      stage_round(qa, r);
+      in.template load_many<kWsRows>(t0 + (r + 2) * static_cast<uint64_t>(kRound) + t, kWsProd, t1,
+                                     t0, qa);
+      if (r + 1 >= rounds) break;
+      stage_round(qb, r + 1);
+      in.template load_many<kWsRows>(t0 + (r + 3) * static_cast<uint64_t>(kRound) + t, kWsProd, t1,
+                                     t0, qb);
+    }
+  } else {
+    const uint32_t c = t - kWsProd;
+    constexpr uint32_t kCW = (kPartThreads - kWsProd) / 64;
+    for (uint32_t r = 0; r < rounds; ++r) {
+      const uint32_t par = r & 1u;
+      {
+        const uint64_t r0 = t0 + static_cast<uint64_t>(r) * kRound;
+#pragma unroll
+        for (uint32_t u = 0; u < kRound / kWsProd; ++u) {
+          const uint64_t i = r0 + c + u * kWsProd;
+          if (i < t1) rep[i] = in.rank_base + static_cast<uint32_t>(i);
+        }
+      }
+      spin_until(&pround, r + 1, err);
+      const uint32_t nf = fn[par], no = min(on[par], kAsyncOvf);
+      for (uint32_t e = c; e < nf; e += kWsProd) {
+        const uint32_t b = flist[par][e];
+        const uint3 x0 = stage[b][0], x1 = stage[b][1];
+        const uint32_t p = atomicAdd(&cur[b], 2u);
+        fill[b] = 0;  // after the slots were read (same wave, in order)
+        if constexpr (kStore) {
+          out[p] = x0;
+          out[p + 1] = x1;
+        }
+      }
+      for (uint32_t o = c; o < no; o += kWsProd) {
+        const uint3 rq = ovf[par][o];
+        const uint32_t p = atomicAdd(&cur[digit_of((static_cast<uint64_t>(rq.y) << 32) | rq.x, skip,
+                                                   kStageBits)], 1u);
+        if constexpr (kStore) out[p] = rq;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        const uint32_t a = __hip_atomic_fetch_add(&cc[par], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (a == kCW - 1) {  // the round's last consumer wave: clear its lists
+          cc[par] = 0;
+          fn[par] = 0;
+          on[par] = 0;
+          __hip_atomic_fetch_max(&cround, r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
+    for (uint32_t k = 0; k < min(fill[b], 2u); ++k) out[cur[b] + k] = stage[b][k];
 }
 
 // group: kMode 0 product, 1 no rep writes, 2 loads only (records summed)
@@ -1507,6 +1686,15 @@ int main(int argc, char** argv) {
   };
   auto gp0 = [&] { k_group_pers<false><<<512, kGroupThreads>>>(rec, 0, fbase, kNb, c, gkey, gmin, rep1); };
   auto gp1 = [&] { k_group_pers<true><<<512, kGroupThreads>>>(rec, 0, fbase, kNb, c, gkey, gmin, rep1); };
+  uint32_t* d_err;
+  (void)hipMalloc(&d_err, 4);
+  (void)hipMemset(d_err, 0, 4);
+  auto sa = [&] {
+    k_ws_async<true><<<P, kPartThreads>>>(in, n, kShardBits, fE, ftot, rec, rep1, fbase, d_err);
+  };
+  auto san = [&] {
+    k_ws_async<false><<<P, kPartThreads>>>(in, n, kShardBits, fE, ftot, rec, rep1, fbase, d_err);
+  };
   auto g0 = [&] {
     k_bucket_group12_pk<<<kNb, kGroupThreads>>>(rec, 0, fbase, kStageBits, c, gkey, gmin, rep1);
   };
@@ -1584,6 +1772,21 @@ int main(int argc, char** argv) {
       printf("P11b 11-bit pipeline (two tables) vs product: %llu mismatches (%s)\n",
              (unsigned long long)bad, hipGetErrorString(hipGetLastError()));
     }
+    {
+      (void)hipMemset(rep1, 0xFF, 4 * n);
+      h0();
+      scan();
+      sa();
+      g0v();
+      (void)hipDeviceSynchronize();
+      (void)hipMemcpy(b.data(), rep1, 4 * n, hipMemcpyDeviceToHost);
+      bad = 0;
+      for (uint64_t i = 0; i < n; ++i) bad += a[i] != b[i];
+      uint32_t e = 0;
+      (void)hipMemcpy(&e, d_err, 4, hipMemcpyDeviceToHost);
+      printf("SA async scatter + group vs product: %llu mismatches, spin cap hit %u (%s)\n",
+             (unsigned long long)bad, e, hipGetErrorString(hipGetLastError()));
+    }
     for (int gg = 0; gg < 2; ++gg) {
       (void)hipMemset(rep1, 0xFF, 4 * n);
       h0();
@@ -1632,7 +1835,9 @@ int main(int argc, char** argv) {
                           {"S6 ws asm loads, counted waits", h0, s6},
                           {"S7 ws asm loads, no rec stores", h0, s7},
                           {"S8 ws batched LDS trips", h0, s8},
-                          {"S9 ws batched, no rec stores", h0, s9}};
+                          {"S9 ws batched, no rec stores", h0, s9},
+                          {"SA ws async rounds", h0, sa},
+                          {"SAn ws async, no rec stores", h0, san}};
     for (auto& v : ss) {
       v.hist();
       scan();
