@@ -1467,6 +1467,110 @@ __global__ __launch_bounds__(kPartThreads) void k_ws_async(RowsIn in, uint64_t n
     for (uint32_t k = 0; k < min(fill[b], 2u); ++k) out[cur[b] + k] = stage[b][k];
 }
 
+// kB buckets per workgroup: every bucket's records loaded up front (one
+// memory latency for all of them), then the buckets grouped one after the
+// other through the same table.  kLminInit: each record writes its own rank
+// into lmin[its index] instead of the 4096-entry clear (only owners' entries
+// are read).
+template <int kB, bool kLminInit>
+__global__ __launch_bounds__(kGroupThreads, 8) void k_group_multi(const uint3* __restrict__ rec,
+                                                                  uint32_t rank_base,
+                                                                  const uint32_t* __restrict__ offs,
+                                                                  ChunkOf chunk_of,
+                                                                  uint64_t* __restrict__ gkey,
+                                                                  uint32_t* __restrict__ gmin,
+                                                                  uint32_t* __restrict__ rep) {
+  __shared__ uint64_t tab[kPkSlots];
+  __shared__ uint32_t lmin[kPkCap + 1];
+  __shared__ uint32_t special_min;
+  constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
+  uint3 q[kB][kP];
+  uint32_t st[kB], en[kB];
+#pragma unroll
+  for (int bb = 0; bb < kB; ++bb) {
+    const uint32_t b = blockIdx.x * kB + bb;
+    st[bb] = offs[b];
+    en[bb] = offs[b + 1];
+  }
+#pragma unroll
+  for (int bb = 0; bb < kB; ++bb)
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      const uint32_t i = st[bb] + threadIdx.x + j * kGroupThreads;
+      q[bb][j] = rec[min(i, max(en[bb], st[bb] + 1) - 1)];
+    }
+#pragma unroll
+  for (int bb = 0; bb < kB; ++bb) {
+    const uint32_t start = st[bb], end = en[bb];
+    if (end - start > kPkCap) {  // uniform
+      if (bb) __syncthreads();
+      group_bucket_global(Rec12Src{rec, rank_base}, start, end, chunk_of, gkey, gmin, rep, special_min);
+      continue;
+    }
+    if (bb) __syncthreads();  // the previous bucket's lookups done
+    for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
+    if constexpr (!kLminInit)
+      for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
+    uint32_t slot[kP], owner[kP];
+    uint64_t mine[kP];
+    uint32_t pend = 0;
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      const uint3 v = q[bb][j];
+      const uint64_t h = (static_cast<uint64_t>(v.y) << 32) | v.x;
+      const uint32_t idx = threadIdx.x + j * kGroupThreads;
+      mine[j] = (key_rest(h, kStageBits) << 12) | (idx + 1);
+      slot[j] = static_cast<uint32_t>((static_cast<uint64_t>(v.x) * kPkSlots) >> 32);
+      owner[j] = idx;
+      if (start + idx < end) {
+        pend |= 1u << j;
+        if constexpr (kLminInit) lmin[idx] = rank_base + v.z;
+      }
+    }
+    __syncthreads();
+    const uint32_t live = pend;
+    while (pend) {
+      uint64_t prev[kP];
+#pragma unroll
+      for (int j = 0; j < kP; ++j)
+        prev[j] = (pend >> j & 1u)
+                      ? atomicCAS(reinterpret_cast<unsigned long long*>(&tab[slot[j]]), 0ull,
+                                  static_cast<unsigned long long>(mine[j]))
+                      : 0ull;
+#pragma unroll
+      for (int j = 0; j < kP; ++j) {
+        if (!(pend >> j & 1u)) continue;
+        if (prev[j] == 0ull) {
+          pend &= ~(1u << j);
+        } else if ((prev[j] >> 12) == (mine[j] >> 12)) {
+          owner[j] = static_cast<uint32_t>(prev[j] & 0xFFFu) - 1;
+          pend &= ~(1u << j);
+        } else {
+          const uint3 v = q[bb][j];
+          const uint64_t h = (static_cast<uint64_t>(v.y) << 32) | v.x;
+          uint32_t stp = 1u + 2u * static_cast<uint32_t>((h >> 40) & 1023u);
+          stp += (stp % 3u == 0) ? 2u : 0u;
+          stp += (stp % 5u == 0) ? 2u : 0u;
+          stp += (stp % 3u == 0) ? 2u : 0u;
+          const uint32_t sn = slot[j] + stp;
+          slot[j] = sn >= kPkSlots ? sn - kPkSlots : sn;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kP; ++j)
+      if ((live >> j & 1u) && (!kLminInit || owner[j] != threadIdx.x + j * kGroupThreads))
+        atomicMin(&lmin[owner[j]], rank_base + q[bb][j].z);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      if (!(live >> j & 1u)) continue;
+      const uint32_t r = rank_base + q[bb][j].z, f = lmin[owner[j]];
+      if (chunk_of(r) != chunk_of(f)) rep[q[bb][j].z] = f;
+    }
+  }
+}
+
 // group: kMode 0 product, 1 no rep writes, 2 loads only (records summed)
 template <int kMode>
 __global__ __launch_bounds__(kGroupThreads, 8) void k_group_var(const uint3* __restrict__ rec,
@@ -1695,6 +1799,9 @@ int main(int argc, char** argv) {
   auto san = [&] {
     k_ws_async<false><<<P, kPartThreads>>>(in, n, kShardBits, fE, ftot, rec, rep1, fbase, d_err);
   };
+  auto gm1 = [&] { k_group_multi<1, true><<<kNb, kGroupThreads>>>(rec, 0, fbase, c, gkey, gmin, rep1); };
+  auto gm2 = [&] { k_group_multi<2, false><<<kNb / 2, kGroupThreads>>>(rec, 0, fbase, c, gkey, gmin, rep1); };
+  auto gm2i = [&] { k_group_multi<2, true><<<kNb / 2, kGroupThreads>>>(rec, 0, fbase, c, gkey, gmin, rep1); };
   auto g0 = [&] {
     k_bucket_group12_pk<<<kNb, kGroupThreads>>>(rec, 0, fbase, kStageBits, c, gkey, gmin, rep1);
   };
@@ -1787,17 +1894,18 @@ int main(int argc, char** argv) {
       printf("SA async scatter + group vs product: %llu mismatches, spin cap hit %u (%s)\n",
              (unsigned long long)bad, e, hipGetErrorString(hipGetLastError()));
     }
-    for (int gg = 0; gg < 2; ++gg) {
+    for (int gg = 0; gg < 5; ++gg) {
       (void)hipMemset(rep1, 0xFF, 4 * n);
       h0();
       scan();
       s0();
-      if (gg == 0) gp0(); else gp1();
+      if (gg == 0) gp0(); else if (gg == 1) gp1(); else if (gg == 2) gm1(); else if (gg == 3) gm2(); else gm2i();
       (void)hipDeviceSynchronize();
       (void)hipMemcpy(b.data(), rep1, 4 * n, hipMemcpyDeviceToHost);
       bad = 0;
       for (uint64_t i = 0; i < n; ++i) bad += a[i] != b[i];
-      printf("GP%d persistent group vs product: %llu mismatches (%s)\n", gg, (unsigned long long)bad,
+      printf("G%s group vs product: %llu mismatches (%s)\n",
+             gg == 0 ? "P0" : gg == 1 ? "P1" : gg == 2 ? "M1" : gg == 3 ? "M2" : "M2i", (unsigned long long)bad,
              hipGetErrorString(hipGetLastError()));
     }
     for (int rr = 0; rr < 2; ++rr) {
@@ -1884,6 +1992,9 @@ int main(int argc, char** argv) {
     s0();
     std::vector<V> gs = {{"G0 group product", g0}, {"Gv group copy", g0v},
                          {"G1 group no rep writes", g1}, {"G2 group loads only", g2},
+                         {"GM1 1 bucket, lmin by records", gm1},
+                         {"GM2 2 buckets per workgroup", gm2},
+                         {"GM2i 2 buckets, lmin by records", gm2i},
                          {"GP0 persistent, targeted clear", gp0},
                          {"GP1 persistent + prefetch", gp1}};
     for (auto& v : gs) printf("%-32s %.4f ms\n", v.name, time_ms(v.f, reps));
