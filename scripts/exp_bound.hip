@@ -1571,6 +1571,126 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_multi(const uint3* _
   }
 }
 
+// 11-bit buckets grouped as two 12-bit sub-buckets at TWO workgroups per CU:
+// the 7 records per thread are loaded, then REDISTRIBUTED through LDS (the
+// table's memory, not yet in use) into per-sub-bucket lists, and read back
+// so that each thread holds at most 4 records of each sub-bucket; the two
+// sub-buckets are then grouped one after the other exactly as the 12-bit
+// kernel groups a bucket.
+constexpr int kC4 = 4;  // records per thread per sub-bucket (4096 capacity)
+struct SubRec {
+  uint32_t lo, hi, row;  // h, row (h's low word first)
+};
+__global__ __launch_bounds__(kGroupThreads, 8) void k_group11c(const uint3* __restrict__ rec,
+                                                               uint32_t rank_base,
+                                                               const uint32_t* __restrict__ offs,
+                                                               ChunkOf chunk_of,
+                                                               uint64_t* __restrict__ gkey,
+                                                               uint32_t* __restrict__ gmin,
+                                                               uint32_t* __restrict__ rep) {
+  __shared__ uint64_t tab[kPkSlots];    // 61440 B
+  __shared__ uint32_t lmin[kPkCap + 1];  // 16384 B
+  __shared__ uint32_t scnt[2];
+  __shared__ uint32_t special_min;
+  const uint32_t start = offs[blockIdx.x], end = offs[blockIdx.x + 1];
+  const uint32_t m = end - start;
+  if (m == 0) return;
+  if (m > kG2Cap) {
+    group_bucket_global(Rec12Src{rec, rank_base}, start, end, chunk_of, gkey, gmin, rep, special_min);
+    return;
+  }
+  // scratch lists in the table's memory: sub-bucket s's records at
+  // lst + s * 4096 (12 B each: 2 x 4096 x 12 = 96 KiB > 76 KiB, so the
+  // capacity per sub-bucket here is (76 KiB / 2) / 12 B = 3276 records;
+  // larger sub-buckets take the global table)
+  constexpr uint32_t kLst = (sizeof(tab) + sizeof(lmin)) / 2 / sizeof(SubRec);  // 3276
+  SubRec* lst = reinterpret_cast<SubRec*>(tab);
+  if (threadIdx.x < 2) scnt[threadIdx.x] = 0;
+  uint3 q[kG2Per];
+#pragma unroll
+  for (int j = 0; j < kG2Per; ++j) q[j] = rec[min(start + threadIdx.x + j * kGroupThreads, end - 1)];
+  __syncthreads();  // scnt
+#pragma unroll
+  for (int j = 0; j < kG2Per; ++j) {
+    if (start + threadIdx.x + j * kGroupThreads >= end) continue;
+    const uint64_t h = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+    const uint32_t sb = digit_of(h, kShardBits + 11, 1);
+    const uint32_t idx = atomicAdd(&scnt[sb], 1u);
+    if (idx < kLst) lst[sb * kLst + idx] = SubRec{q[j].x, q[j].y, q[j].z};
+  }
+  __syncthreads();
+  const uint32_t n0 = scnt[0], n1 = scnt[1];
+  if (n0 > kLst || n1 > kLst) {  // uniform
+    group_bucket_global(Rec12Src{rec, rank_base}, start, end, chunk_of, gkey, gmin, rep, special_min);
+    return;
+  }
+  SubRec r2[2][kC4];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int j = 0; j < kC4; ++j) {
+      const uint32_t i = threadIdx.x + j * kGroupThreads;
+      r2[s2][j] = lst[s2 * kLst + min(i, kLst - 1)];
+    }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const uint32_t cnt = s2 ? n1 : n0;
+    __syncthreads();  // the lists read (s2 = 0) / the previous lookups done
+    for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
+    for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
+    __syncthreads();
+    uint32_t slot[kC4], owner[kC4];
+    uint64_t mine[kC4];
+    uint32_t pend = 0;
+#pragma unroll
+    for (int j = 0; j < kC4; ++j) {
+      const uint64_t h = (static_cast<uint64_t>(r2[s2][j].hi) << 32) | r2[s2][j].lo;
+      const uint32_t idx = threadIdx.x + j * kGroupThreads;
+      mine[j] = (key_rest(h, 12) << 12) | ((idx + 1) & 0xFFFu);
+      slot[j] = static_cast<uint32_t>((static_cast<uint64_t>(r2[s2][j].lo) * kPkSlots) >> 32);
+      owner[j] = idx;
+      if (idx < cnt) pend |= 1u << j;
+    }
+    const uint32_t live = pend;
+    while (pend) {
+      uint64_t prev[kC4];
+#pragma unroll
+      for (int j = 0; j < kC4; ++j)
+        prev[j] = (pend >> j & 1u)
+                      ? atomicCAS(reinterpret_cast<unsigned long long*>(&tab[slot[j]]), 0ull,
+                                  static_cast<unsigned long long>(mine[j]))
+                      : 0ull;
+#pragma unroll
+      for (int j = 0; j < kC4; ++j) {
+        if (!(pend >> j & 1u)) continue;
+        if (prev[j] == 0ull) {
+          pend &= ~(1u << j);
+        } else if ((prev[j] >> 12) == (mine[j] >> 12)) {
+          owner[j] = static_cast<uint32_t>(prev[j] & 0xFFFu) - 1;
+          pend &= ~(1u << j);
+        } else {
+          uint32_t st = 1u + 2u * static_cast<uint32_t>((r2[s2][j].hi >> 8) & 1023u);  // h bits [40, 50)
+          st += (st % 3u == 0) ? 2u : 0u;
+          st += (st % 5u == 0) ? 2u : 0u;
+          st += (st % 3u == 0) ? 2u : 0u;
+          const uint32_t sn = slot[j] + st;
+          slot[j] = sn >= kPkSlots ? sn - kPkSlots : sn;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kC4; ++j)
+      if (live >> j & 1u) atomicMin(&lmin[owner[j]], rank_base + r2[s2][j].row);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kC4; ++j) {
+      if (!(live >> j & 1u)) continue;
+      const uint32_t r = rank_base + r2[s2][j].row, f = lmin[owner[j]];
+      if (chunk_of(r) != chunk_of(f)) rep[r2[s2][j].row] = f;
+    }
+  }
+}
+
 // group: kMode 0 product, 1 no rep writes, 2 loads only (records summed)
 template <int kMode>
 __global__ __launch_bounds__(kGroupThreads, 8) void k_group_var(const uint3* __restrict__ rec,
@@ -1613,7 +1733,9 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_var(const uint3* __r
     const uint32_t idx = threadIdx.x + j * kGroupThreads;
     mine[j] = (key_rest(h, kStageBits) << 12) | (idx + 1);
     slot[j] = static_cast<uint32_t>((static_cast<uint64_t>(static_cast<uint32_t>(h)) * kPkSlots) >> 32);
-    uint32_t st = 1u + 2u * static_cast<uint32_t>((h >> 40) & 1023u);
+    // kMode 4: the probe step from h bits [32, 42) (bits 44-55 are the digit,
+    // constant in a bucket: (h >> 40) & 1023 varies in 4 bits only)
+    uint32_t st = 1u + 2u * static_cast<uint32_t>((h >> (kMode == 4 ? 32 : 40)) & 1023u);
     st += (st % 3u == 0) ? 2u : 0u;
     st += (st % 5u == 0) ? 2u : 0u;
     st += (st % 3u == 0) ? 2u : 0u;
@@ -1654,7 +1776,7 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_var(const uint3* __r
     if (!(live >> j & 1u)) continue;
     const uint32_t r = q[j].z, f = lmin[owner[j]];
     if (chunk_of(r) != chunk_of(f)) {
-      if constexpr (kMode == 0) rep[q[j].w] = f;
+      if constexpr (kMode == 0 || kMode == 4) rep[q[j].w] = f;
       else acc += f;
     }
   }
@@ -1802,12 +1924,16 @@ int main(int argc, char** argv) {
   auto gm1 = [&] { k_group_multi<1, true><<<kNb, kGroupThreads>>>(rec, 0, fbase, c, gkey, gmin, rep1); };
   auto gm2 = [&] { k_group_multi<2, false><<<kNb / 2, kGroupThreads>>>(rec, 0, fbase, c, gkey, gmin, rep1); };
   auto gm2i = [&] { k_group_multi<2, true><<<kNb / 2, kGroupThreads>>>(rec, 0, fbase, c, gkey, gmin, rep1); };
+  auto gr11c = [&] {
+    k_group11c<<<2048, kGroupThreads>>>(rec, 0, fbase, c, gkey, gmin, rep1);
+  };
   auto g0 = [&] {
     k_bucket_group12_pk<<<kNb, kGroupThreads>>>(rec, 0, fbase, kStageBits, c, gkey, gmin, rep1);
   };
   auto g0v = [&] { k_group_var<0><<<kNb, kGroupThreads>>>(rec, fbase, c, rep1); };
   auto g1 = [&] { k_group_var<1><<<kNb, kGroupThreads>>>(rec, fbase, c, rep1); };
   auto g2 = [&] { k_group_var<2><<<kNb, kGroupThreads>>>(rec, fbase, c, rep1); };
+  auto g4 = [&] { k_group_var<4><<<kNb, kGroupThreads>>>(rec, fbase, c, rep1); };
 
 
   // correctness of the product-equivalent copies (hv, sv, g0v)
@@ -1878,6 +2004,16 @@ int main(int argc, char** argv) {
       for (uint64_t i = 0; i < n; ++i) bad += a[i] != b[i];
       printf("P11b 11-bit pipeline (two tables) vs product: %llu mismatches (%s)\n",
              (unsigned long long)bad, hipGetErrorString(hipGetLastError()));
+      (void)hipMemset(rep1, 0xFF, 4 * n);
+      hb(11);
+      d11();
+      gr11c();
+      (void)hipDeviceSynchronize();
+      (void)hipMemcpy(b.data(), rep1, 4 * n, hipMemcpyDeviceToHost);
+      bad = 0;
+      for (uint64_t i = 0; i < n; ++i) bad += a[i] != b[i];
+      printf("P11c 11-bit pipeline (LDS redistribution) vs product: %llu mismatches (%s)\n",
+             (unsigned long long)bad, hipGetErrorString(hipGetLastError()));
     }
     {
       (void)hipMemset(rep1, 0xFF, 4 * n);
@@ -1894,18 +2030,18 @@ int main(int argc, char** argv) {
       printf("SA async scatter + group vs product: %llu mismatches, spin cap hit %u (%s)\n",
              (unsigned long long)bad, e, hipGetErrorString(hipGetLastError()));
     }
-    for (int gg = 0; gg < 5; ++gg) {
+    for (int gg = 0; gg < 6; ++gg) {
       (void)hipMemset(rep1, 0xFF, 4 * n);
       h0();
       scan();
       s0();
-      if (gg == 0) gp0(); else if (gg == 1) gp1(); else if (gg == 2) gm1(); else if (gg == 3) gm2(); else gm2i();
+      if (gg == 0) gp0(); else if (gg == 1) gp1(); else if (gg == 2) gm1(); else if (gg == 3) gm2(); else if (gg == 4) gm2i(); else g4();
       (void)hipDeviceSynchronize();
       (void)hipMemcpy(b.data(), rep1, 4 * n, hipMemcpyDeviceToHost);
       bad = 0;
       for (uint64_t i = 0; i < n; ++i) bad += a[i] != b[i];
       printf("G%s group vs product: %llu mismatches (%s)\n",
-             gg == 0 ? "P0" : gg == 1 ? "P1" : gg == 2 ? "M1" : gg == 3 ? "M2" : "M2i", (unsigned long long)bad,
+             gg == 0 ? "P0" : gg == 1 ? "P1" : gg == 2 ? "M1" : gg == 3 ? "M2" : gg == 4 ? "M2i" : "4 (step bits)", (unsigned long long)bad,
              hipGetErrorString(hipGetLastError()));
     }
     for (int rr = 0; rr < 2; ++rr) {
@@ -1981,6 +2117,9 @@ int main(int argc, char** argv) {
     d11();
     printf("%-32s %.4f ms\n", "G11 group 11-bit buckets", time_ms(gr11, reps));
     printf("%-32s %.4f ms\n", "G11b group 11-bit, two tables", time_ms(gr11b, reps));
+    printf("%-32s %.4f ms\n", "G11c group 11-bit, redistributed", time_ms(gr11c, reps));
+    printf("%-32s %.4f ms\n", "P11c whole 11-bit (redistributed)",
+           time_ms([&] { hb(11); d11(); gr11c(); }, reps));
     printf("%-32s %.4f ms\n", "P11b whole 11-bit (two tables)",
            time_ms([&] { hb(11); d11(); gr11b(); }, reps));
     printf("%-32s %.4f ms\n", "P11 whole 11-bit pipeline",
@@ -1992,6 +2131,7 @@ int main(int argc, char** argv) {
     s0();
     std::vector<V> gs = {{"G0 group product", g0}, {"Gv group copy", g0v},
                          {"G1 group no rep writes", g1}, {"G2 group loads only", g2},
+                         {"G4 group, step from h bits 32-41", g4},
                          {"GM1 1 bucket, lmin by records", gm1},
                          {"GM2 2 buckets per workgroup", gm2},
                          {"GM2i 2 buckets, lmin by records", gm2i},
