@@ -400,6 +400,113 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
     f[b] = (fc[b >> 1] >> ((b & 1u) << 4)) & 0xFFFFu;
 }
 
+// The coarse pass WITHOUT a histogram pass before it (round 3): each block
+// writes its keyed rows into its own tile's range of the record array,
+// [t0, t0 + keyed rows), round after round, each round counting-sorted by
+// coarse digit in LDS and stored as ONE contiguous chunk; a run table records
+// where every (block, round, digit) run starts and how long it is, and the
+// block adds its per-digit totals to segtot (the segment sizes).  The second
+// pass (k_part2_runs) reads a segment's records as those runs, so no global
+// offsets -- and no k_part_hist pass over all rows -- are needed.  Fine
+// counts per final bucket as in k_part_scatter_runs.
+template <typename In, bool kInitRep, bool kRec12 = false>
+__global__ __launch_bounds__(kPartThreads) void k_part_private(
+    In in, uint64_t n, uint32_t skip, uint32_t bits, uint4* __restrict__ rec,
+    uint32_t* __restrict__ rep, uint32_t fbits, uint32_t* __restrict__ fine,
+    uint32_t* __restrict__ ovf, uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_len,
+    uint32_t max_rounds, uint32_t* __restrict__ segtot) {
+  constexpr int U = 4;
+  constexpr uint32_t R = U * kPartThreads;
+  using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
+  __shared__ RecT buf[R];
+  RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
+  __shared__ uint32_t cnt[kRunMaxBins], base[kRunMaxBins + 1];
+  __shared__ uint32_t fc[1u << (kMaxBucketBits - 1)];  // 2 x 16-bit counters per word
+  const uint32_t nbins = 1u << bits, nfine = 1u << fbits;
+  const uint32_t blk = part_block();
+  for (uint32_t b = threadIdx.x; b < nfine / 2; b += kPartThreads) fc[b] = 0;
+  bool over = false;
+  uint64_t t0, t1;
+  tile_of(n, gridDim.x, t0, t1);
+  uint32_t acc = 0, r = 0, dsum = 0;  // records written, rounds done; wave 0: its digit's total
+  auto round = [&](const RowBatch<U>& q, uint64_t i0) {
+    if (threadIdx.x < nbins) cnt[threadIdx.x] = 0;
+    lds_barrier();
+    uint32_t dg[U], lr[U];
+    RecT rq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads;
+      dg[u] = ~0u;
+      if (!q.in[u]) continue;
+      const uint32_t rk = in.rank_of(q, u);
+      if (kInitRep) rep[i] = rk;
+      if (!in.valid_of(q, u)) continue;
+      const uint64_t h = in_hash<In>(in.key_of(q, u));
+      dg[u] = digit_of(h, skip, bits);
+      lr[u] = atomicAdd(&cnt[dg[u]], 1u);
+      const uint32_t fb = digit_of(h, skip, fbits), sh = (fb & 1u) << 4;
+      over |= ((atomicAdd(&fc[fb >> 1], 1u << sh) >> sh) & 0xFFFFu) == 0xFFFFu;
+      if constexpr (kRec12)
+        rq[u] = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), in.row_of(q, u));
+      else
+        rq[u] = make_uint4(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), rk,
+                           in.row_of(q, u));
+    }
+    lds_barrier();
+    if (threadIdx.x < 64) {  // run starts (one wave's shuffle scan) and the run table row
+      static_assert(kRunMaxBins <= 64, "one wave scans the run starts");
+      const uint32_t lane = threadIdx.x;
+      const uint32_t v = lane < nbins ? cnt[lane] : 0u;
+      uint32_t inc = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d);
+        if (lane >= static_cast<uint32_t>(d)) inc += o;
+      }
+      if (lane < nbins) base[lane] = inc - v;
+      if (lane == nbins - 1) base[nbins] = inc;
+      const uint64_t e = (static_cast<uint64_t>(blk) * max_rounds + r) * kRunMaxBins + lane;
+      run_start[e] = static_cast<uint32_t>(t0) + acc + inc - v;
+      run_len[e] = v;
+      dsum += v;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (dg[u] != ~0u) buf[base[dg[u]] + lr[u]] = rq[u];
+    lds_barrier();
+    const uint32_t total = base[nbins];
+    for (uint32_t k = threadIdx.x; k < total; k += kPartThreads) out[t0 + acc + k] = buf[k];
+    acc += total;
+    ++r;
+    lds_barrier();
+  };
+  constexpr uint64_t kStep = R;
+  if (t0 < t1) {
+    RowBatch<U> qa, qb;
+    in.template load_many<U>(t0 + threadIdx.x, kPartThreads, t1, t0, qa);
+    for (uint64_t i0 = t0;; i0 += 2 * kStep) {  // uniform trip count
+      in.template load_many<U>(i0 + kStep + threadIdx.x, kPartThreads, t1, t0, qb);
+      round(qa, i0);
+      if (i0 + kStep >= t1) break;
+      in.template load_many<U>(i0 + 2 * kStep + threadIdx.x, kPartThreads, t1, t0, qa);
+      round(qb, i0 + kStep);
+      if (i0 + 2 * kStep >= t1) break;
+    }
+  }
+  if (threadIdx.x < 64) {  // rounds this tile did not have: empty runs
+    for (uint32_t rr = r; rr < max_rounds; ++rr)
+      run_len[(static_cast<uint64_t>(blk) * max_rounds + rr) * kRunMaxBins + threadIdx.x] = 0u;
+    if (threadIdx.x < nbins && dsum) atomicAdd(&segtot[threadIdx.x], dsum);
+  }
+  if (over) *ovf = 1u;
+  __syncthreads();
+  uint32_t* f = fine + static_cast<uint64_t>(blk) * nfine;
+  for (uint32_t b = threadIdx.x; b < nfine; b += kPartThreads)
+    f[b] = (fc[b >> 1] >> ((b & 1u) << 4)) & 0xFFFFu;
+}
+
 // Only after a 16-bit counter overflow in k_part_scatter_runs (*ovf): for
 // every (coarse block j, segment c) -- a grid-stride loop, so the usual call
 // costs one small launch -- recount the records j wrote to segment c
@@ -424,6 +531,35 @@ __global__ __launch_bounds__(kPartThreads) void k_fine_recount(const RecT* __res
     for (uint32_t i = s0 + threadIdx.x; i < s1; i += kPartThreads) {
       const RecT v = rec[i];
       atomicAdd(&cnt[digit_of((static_cast<uint64_t>(v.y) << 32) | v.x, skip, kB2)], 1u);
+    }
+    __syncthreads();
+    uint32_t* f = fine + static_cast<uint64_t>(j) * (1u << fbits) + (static_cast<uint64_t>(c) << kB2);
+    for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads) f[b] = cnt[b];
+    __syncthreads();
+  }
+}
+
+// k_fine_recount for the run layout of k_part_private: the records coarse
+// block j wrote to segment c are its runs (j, r, c), r < max_rounds.
+template <uint32_t kB2, typename RecT = uint4>
+__global__ __launch_bounds__(kPartThreads) void k_fine_recount_runs(
+    const RecT* __restrict__ rec, uint32_t skip, const uint32_t* __restrict__ run_start,
+    const uint32_t* __restrict__ run_len, uint32_t max_rounds, uint32_t P, uint32_t nseg,
+    uint32_t fbits, uint32_t* __restrict__ fine, const uint32_t* __restrict__ ovf) {
+  if (*ovf == 0) return;
+  constexpr uint32_t nb = 1u << kB2;
+  __shared__ uint32_t cnt[nb];
+  for (uint32_t jc = blockIdx.x; jc < P * nseg; jc += gridDim.x) {
+    const uint32_t j = jc % P, c = jc / P;
+    for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads) cnt[b] = 0;
+    __syncthreads();
+    for (uint32_t r = 0; r < max_rounds; ++r) {
+      const uint64_t e = (static_cast<uint64_t>(j) * max_rounds + r) * kRunMaxBins + c;
+      const uint32_t s0 = run_start[e], len = run_len[e];
+      for (uint32_t i = threadIdx.x; i < len; i += kPartThreads) {
+        const RecT v = rec[s0 + i];
+        atomicAdd(&cnt[digit_of((static_cast<uint64_t>(v.y) << 32) | v.x, skip, kB2)], 1u);
+      }
     }
     __syncthreads();
     uint32_t* f = fine + static_cast<uint64_t>(j) * (1u << fbits) + (static_cast<uint64_t>(c) << kB2);
@@ -688,6 +824,164 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     }
   }
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
+    for (uint32_t k = 0; k < fill[b]; ++k) out[cur[b] + k] = stage[b][k];
+}
+
+// Second pass of the two-level partition over k_part_private's runs: block
+// (j, c) takes the runs coarse blocks [R j, R (j + 1)) wrote for segment c --
+// up to kMaxRuns (block, round) runs, listed with their exclusive prefix in LDS
+// -- and stages their records exactly as k_part_scatter_rec_staged's second
+// pass does (kS2-record slots, listed full buckets flushed by adjacent lanes).
+// Record k of the block's virtual range is found by a 9-step binary search
+// of the run prefix.  Segment starts from segtot (sizes summed by the first
+// pass); bucket starts from the fine scan's sizes as before.
+constexpr uint32_t kMaxRuns = 512;  // R x max_rounds (host: two_level_runs_ok)
+template <bool kRec12, uint32_t kB2, uint32_t kS2, int kRows>
+__global__ __launch_bounds__(kPartThreads) void k_part2_runs(
+    const uint4* __restrict__ rec1, uint32_t skip, const uint32_t* __restrict__ offs,
+    uint4* __restrict__ rec, const uint32_t* __restrict__ run_start,
+    const uint32_t* __restrict__ run_len, uint32_t max_rounds, uint32_t P1, uint32_t R,
+    const uint32_t* __restrict__ segtot, const uint32_t* __restrict__ ftot,
+    uint32_t* __restrict__ fbase) {
+  constexpr uint32_t nbins = 1u << kB2;
+  using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
+  static_assert(nbins < kPartThreads && 64 % kS2 == 0 && kPartThreads % kS2 == 0,
+                "listed buckets flushed by adjacent lanes of one wave");
+  static_assert(kMaxRuns < kPartThreads, "one run per thread in the prologue");
+  __shared__ RecT stage[nbins][kS2];
+  __shared__ uint32_t fill[nbins], cur[nbins];
+  __shared__ uint16_t full[nbins];
+  __shared__ uint32_t full_n[2];
+  __shared__ uint32_t rpre[kMaxRuns + 1], rst[kMaxRuns];
+  __shared__ uint32_t wsum[kPartThreads / 64];
+  __shared__ uint32_t s_segbase, s_all;
+  const RecT* __restrict__ in = reinterpret_cast<const RecT*>(rec1);
+  RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
+  const uint32_t c = blockIdx.y, j = part_block(), t = threadIdx.x, lane = __lane_id();
+  const uint32_t nseg = gridDim.y;
+  if (t < 64) {  // this segment's start and the total, from the (<= 64) segment sizes
+    const uint32_t v = t < nseg ? segtot[t] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
+    }
+    if (t == c) s_segbase = inc - v;
+    if (t == 63) s_all = inc;
+  }
+  {  // the block's runs and their exclusive prefix (block scan)
+    const uint32_t nr = R * max_rounds;
+    uint32_t len = 0, st = 0;
+    if (t < nr) {
+      const uint32_t cb = R * j + t / max_rounds, rr = t % max_rounds;
+      if (cb < P1) {
+        const uint64_t e = (static_cast<uint64_t>(cb) * max_rounds + rr) * kRunMaxBins + c;
+        len = run_len[e];
+        st = run_start[e];
+      }
+    }
+    uint32_t inc = len;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
+    }
+    if (lane == 63) wsum[t >> 6] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < (t >> 6); ++w) before += wsum[w];
+    if (t <= kMaxRuns) rpre[t] = before + inc - len;  // rpre[kMaxRuns] = the block's total
+    if (t < kMaxRuns) rst[t] = st;
+  }
+  __syncthreads();  // s_segbase, wsum reused below
+  {  // bucket starts: segment start + the segment's bucket sizes scanned
+    constexpr uint32_t kPerT = 1;
+    static_assert(nbins <= kPartThreads, "one bucket per thread");
+    const uint64_t nfine = static_cast<uint64_t>(nseg) << kB2, b0 = static_cast<uint64_t>(c) << kB2;
+    const uint32_t v = t < nbins ? ftot[b0 + t] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
+    }
+    if (lane == 63) wsum[t >> 6] = inc;
+    __syncthreads();
+    uint32_t base = s_segbase + inc - v;
+    for (uint32_t w = 0; w < (t >> 6); ++w) base += wsum[w];
+    (void)kPerT;
+    if (t < nbins) {
+      cur[t] = base + offs[static_cast<uint64_t>(j) * nfine + b0 + t];
+      fill[t] = 0;
+      if (j == 0) fbase[b0 + t] = base;
+    }
+    if (j == 0 && c == nseg - 1 && t == 0) fbase[nfine] = s_all;
+    if (t == 0) full_n[0] = full_n[1] = 0;
+  }
+  __syncthreads();
+  const uint32_t T = rpre[kMaxRuns];
+  constexpr uint32_t kStep = static_cast<uint32_t>(kRows) * kPartThreads;
+  // record k of the block's runs (k < T): the run whose prefix is the last <= k
+  auto src_of = [&](uint32_t k) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t s = kMaxRuns / 2; s >= 1; s >>= 1)
+      if (rpre[pos + s] <= k) pos += s;
+    return rst[pos] + (k - rpre[pos]);
+  };
+  struct Batch {
+    RecT v[kRows];
+  };
+  auto load = [&](uint32_t k0, Batch& q) {
+    uint32_t s[kRows];
+#pragma unroll
+    for (int u = 0; u < kRows; ++u) s[u] = src_of(min(k0 + t + u * kPartThreads, T - 1));
+#pragma unroll
+    for (int u = 0; u < kRows; ++u) q.v[u] = in[s[u]];
+  };
+  auto round = [&](const Batch& q, uint32_t k0, uint32_t par) {
+#pragma unroll
+    for (int u = 0; u < kRows; ++u) {
+      if (k0 + t + u * kPartThreads >= T) continue;
+      const RecT rq = q.v[u];
+      const uint32_t b = digit_of((static_cast<uint64_t>(rq.y) << 32) | rq.x, skip, kB2);
+      const uint32_t sl = atomicAdd(&fill[b], 1u);
+      if (sl < kS2) {
+        stage[b][sl] = rq;
+        if (sl == kS2 - 1) full[atomicAdd(&full_n[par], 1u)] = static_cast<uint16_t>(b);
+      } else {
+        out[atomicAdd(&cur[b], 1u)] = rq;
+      }
+    }
+    lds_barrier();
+    const uint32_t nf = full_n[par];
+    if (t == 0) full_n[par ^ 1u] = 0;
+    for (uint32_t x = t; x < nf * kS2; x += kPartThreads) {
+      const uint32_t e = x / kS2, k = x % kS2;
+      const uint32_t b = full[e];
+      const uint32_t p = cur[b];
+      out[p + k] = stage[b][k];
+      if (k == 0) {
+        cur[b] = p + kS2;
+        fill[b] = 0;
+      }
+    }
+    lds_barrier();
+  };
+  if (T > 0) {  // the next round's records are loaded during the current one
+    Batch qa, qb;
+    load(0, qa);
+    for (uint32_t k0 = 0;; k0 += 2 * kStep) {  // uniform trip count
+      load(k0 + kStep, qb);
+      round(qa, k0, 0u);
+      if (k0 + kStep >= T) break;
+      load(k0 + 2 * kStep, qa);
+      round(qb, k0 + kStep, 1u);
+      if (k0 + 2 * kStep >= T) break;
+    }
+  }
+  for (uint32_t b = t; b < nbins; b += kPartThreads)
     for (uint32_t k = 0; k < fill[b]; ++k) out[cur[b] + k] = stage[b][k];
 }
 
@@ -1193,6 +1487,12 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12_pk(
                       rep, tab, lmin, special_min);
 }
 
+// the segment sizes k_part_private adds to, and the fine-count overflow flag
+__global__ void k_zero_runs(uint32_t* __restrict__ segtot, uint32_t* __restrict__ ovf) {
+  if (threadIdx.x < kRunMaxBins) segtot[threadIdx.x] = 0;
+  if (threadIdx.x == 0) *ovf = 0;
+}
+
 __global__ __launch_bounds__(256) void k_fill_init(uint32_t* __restrict__ dst, uint64_t n,
                                                    const uint32_t* __restrict__ init) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
@@ -1265,6 +1565,10 @@ struct GroupLayout {
   uint32_t bits, cbits;
   size_t hist, tiles, rec, hist1, rec1, gkey, gmin;
   size_t fine, fE, ftot, fbase, ovf;  // two-level only: the coarse pass's fine counts
+  // two-level without a histogram pass (k_part_private / k_part2_runs): the
+  // run table [block][round][digit] (starts, lengths) and the segment sizes
+  uint32_t max_rounds;
+  size_t run_s, run_l, segtot;
   size_t total;
 };
 
@@ -1288,6 +1592,13 @@ GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
   L.ftot = o; o = align_up(o + 4 * nf, 256);
   L.fbase = o; o = align_up(o + 4 * (nf + 1), 256);
   L.ovf = o; o = align_up(o + 4, 256);
+  // rounds of 4096 rows in the largest coarse tile (kPartBlocks tiles)
+  const uint64_t tile = (n + kPartBlocks - 1) / kPartBlocks;
+  L.max_rounds = L.cbits ? static_cast<uint32_t>((tile + 4095) / 4096) : 0u;
+  const uint64_t nrun = static_cast<uint64_t>(kPartBlocks) * L.max_rounds * kRunMaxBins;
+  L.run_s = o; o = align_up(o + 4 * nrun, 256);
+  L.run_l = o; o = align_up(o + 4 * nrun, 256);
+  L.segtot = o; o = align_up(o + 4 * kRunMaxBins, 256);
   L.total = o;
   return L;
 }
@@ -1328,6 +1639,46 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
   static_assert(kMaxBucketBits - kB2 <= 6, "coarse digits fit k_part_scatter_runs");
   static_assert(kP2 <= kPartBlocks && kPartBlocks % kP2 == 0, "second-pass blocks per segment");
   static_assert((1u << kB2) <= kPartThreads, "second-pass bucket starts: one bucket per thread");
+  if (kPartBlocks / kP2 * L.max_rounds <= kMaxRuns) {
+    // no histogram pass: the coarse pass writes each block's records into its
+    // own tile range as runs, the second pass reads segments as run lists
+    uint32_t* run_s = reinterpret_cast<uint32_t*>(w + L.run_s);
+    uint32_t* run_l = reinterpret_cast<uint32_t*>(w + L.run_l);
+    uint32_t* segtot = reinterpret_cast<uint32_t*>(w + L.segtot);
+    uint4* rec1 = reinterpret_cast<uint4*>(w + L.rec1);
+    const uint32_t nseg = 1u << L.cbits;
+    k_zero_runs<<<1, 64, 0, s>>>(segtot, ovf);
+    {
+      KScope k(timer, "bucket_scatter1", s);
+      if (init_rep)
+        k_part_private<In, true, kRec12><<<P, kPartThreads, 0, s>>>(
+            in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, L.max_rounds, segtot);
+      else
+        k_part_private<In, false, kRec12><<<P, kPartThreads, 0, s>>>(
+            in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, L.max_rounds, segtot);
+    }
+    {
+      KScope k(timer, "bucket_fine_scan", s);
+      k_fine_recount_runs<kB2, RecT><<<kPartBlocks, kPartThreads, 0, s>>>(
+          reinterpret_cast<const RecT*>(rec1), skip2, run_s, run_l, L.max_rounds, P, nseg, bits, fine,
+          ovf);
+      k_fine_scan<kP2, kPartBlocks / kP2><<<(nfine + 63) / 64, 1024, 0, s>>>(fine, nfine, fE, ftot, ovf);
+    }
+    {
+      KScope k(timer, "bucket_scatter", s);
+      k_part2_runs<kRec12, kB2, kS2, kR2><<<dim3(kP2, nseg), kPartThreads, 0, s>>>(
+          rec1, skip2, fE, rec, run_s, run_l, L.max_rounds, P, kPartBlocks / kP2, segtot, ftot, fbase);
+    }
+    KScope k(timer, "bucket_group", s);
+    if constexpr (kRec12)
+      k_bucket_group12_pk<<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
+                                                          rank_base, fbase, bits,
+                                                          ChunkOf::make(chunk_rows), gkey, gmin, rep);
+    else
+      k_bucket_group_pk<<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits, ChunkOf::make(chunk_rows),
+                                                        gkey, gmin, rep);
+    return hipGetLastError();
+  }
   // pass 1: coarse partition on the top cbits digit bits (rep initialised
   // here), counting every row's final bucket on the way
   uint32_t* hist1 = reinterpret_cast<uint32_t*>(w + L.hist1);
