@@ -763,20 +763,22 @@ class Runner:
         del key, has, rank, rep
         torch.cuda.empty_cache()
         kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in kt.items()}
-        # algorithmic HBM bytes per launch of the two-level path:
-        # coarse pass reads key + rank + has_key, writes rep, one record per keyed row
-        # and the fine counts (2^15 buckets x 256 blocks x 4 B); the fine scan reads
-        # those and writes the 64 block starts per bucket; the second pass moves every
-        # record once more; the group-by as in the one-level path
-        # (implicit rank: no rank array read, 12-byte records)
+        # algorithmic HBM bytes per launch of the two-level path without a
+        # histogram pass: the coarse pass (k_part_private)
+        # reads key + has_key, writes rep, one record per keyed row into its own
+        # tile range, the run table (start + length per block x 4096-row round x
+        # coarse digit) and the fine counts (2^15 buckets x 256 blocks x 4 B); the
+        # fine scan reads those and writes the 128 block starts per bucket; the
+        # second pass (k_part2_runs) moves every record once more; the group-by as
+        # in the one-level path (implicit rank: no rank array read, 12-byte records)
         nfine = 1 << 15
-        alg = {"bucket_hist": 9 * total,
-               "bucket_scatter1": 13 * total + 12 * nk + 4 * nfine * 256,
-               "bucket_fine_scan": 4 * nfine * 256 + 4 * nfine * 64 + 4 * nfine,
+        tile = -(-total // 256)  # rows per coarse block (ceil)
+        rounds = -(-tile // 4096)
+        alg = {"bucket_scatter1": 13 * total + 12 * nk + 8 * 256 * rounds * 64 + 4 * nfine * 256,
+               "bucket_fine_scan": 4 * nfine * 256 + 4 * nfine * 128 + 4 * nfine,
                "bucket_scatter": 24 * nk,
                "bucket_group": 12 * nk + 4 * linked}
-        pmc_names = {"bucket_hist": "k_part_hist", "bucket_scatter1": "k_part_scatter_runs",
-                     "bucket_scatter": "k_part_scatter_rec_staged",
+        pmc_names = {"bucket_scatter1": "k_part_private", "bucket_scatter": "k_part2_runs",
                      "bucket_group": "k_bucket_group12_pk"}
         step_s = t / steps
         roof = {"bound": "hbm", "peak": HBM_PEAK / 1e9, "unit": "GB/s", "linked_rows": linked,

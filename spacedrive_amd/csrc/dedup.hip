@@ -626,15 +626,18 @@ __global__ __launch_bounds__(1024) void k_fine_scan(const uint32_t* __restrict__
 // [c][digit][block] -- so the group kernel sees 2^(cbits + kBits) buckets.
 constexpr uint32_t kStageBits = 12;
 // Second pass of the two-level partition: 9 digit bits, 16-record runs, 4 rows
-// per thread per round, 64 blocks per coarse segment (each takes what 4
+// per thread per round, 128 blocks per coarse segment (each takes what 2
 // coarse blocks wrote to its segment).  Wider runs write fewer partial lines:
 // on the staged scatter alone 12/2 0.163 ms, 10/8 0.123 ms
 // (profiles/r2/exp_scatter_slots_r2t.log); at 100 M rows the 6 + 9-bit split
 // with 16-record runs beat 5 + 10 with 8 (profiles/r2/exp_twolevel_r2E.log).
+// Blocks per segment at 100 M rows (scripts/exp_twolevel_s2.hip,
+// profiles/r3/exp_twolevel_s2/): 64 -> 128 2.25 -> 2.21 ms, 256 2.40 ms;
+// 8-record runs (two blocks per CU) 2.37 ms; 2 or 8 rows per thread slower.
 constexpr uint32_t kStage2Bits = 9;
 constexpr uint32_t kStage2Slots = 16;
 constexpr int kStage2Rows = 4;
-constexpr uint32_t kStage2Blocks = 64;
+constexpr uint32_t kStage2Blocks = 128;
 // kRec12: 12-byte records {hash lo, hash hi, row} for rows whose rank is
 // rank_base + row (RowsIn without a rank array): a quarter less to write here
 // and to read in the group kernel (k_bucket_group12).
