@@ -1,6 +1,10 @@
 // Experiment: the two-level grouping's second pass (k_part2_runs) at 100 M rows,
 // its staging run length kS2, blocks per segment kP2 and rows per thread kR2.
-// (run r3F: S2 8 / R2 2 / R2 8 all slower, P2 128 faster; run r3G: P2 256.)
+// (run r3F: S2 8 / R2 2 / R2 8 all slower, P2 128 faster; run r3G: P2 256 slower;
+// run r3I: the flush threshold -- buckets with at least kF2 staged records
+// are flushed at every round's end, so fewer arrivals meet a full slot array
+// and leave as single-record stores: ~20 % of records at kF2 = 16 by a
+// Poisson model, ~2 % at 8.)
 // The product stages 16-record runs with 64 blocks per segment at ~106 KiB of
 // LDS, so one block per CU: a block's prologue (segment / run-list / bucket
 // scans, each behind a global load) overlaps no other block's main loop.
@@ -87,16 +91,16 @@ int main(int argc, char** argv) {
   std::vector<V> vs = {
       {"product (S2 16, P2 64, R2 4)",
        [&] { (void)dedup_local_launch(gi, 100, rep1, true, ws, 0, nullptr); }},
-      {"S2 16, P2 128, R2 4",
-       [&] { (void)two_level_launch<RowsIn, 9, 16, 4, 128, true>(in, n, L, 100, rep1, true, ws, 0, nullptr); }},
-      {"S2 16, P2 256, R2 4",
-       [&] { (void)two_level_launch<RowsIn, 9, 16, 4, 256, true>(in, n, L, 100, rep1, true, ws, 0, nullptr); }},
-      {"S2 16, P2 256, R2 2",
-       [&] { (void)two_level_launch<RowsIn, 9, 16, 2, 256, true>(in, n, L, 100, rep1, true, ws, 0, nullptr); }},
-      {"S2 16, P2 128, R2 2",
-       [&] { (void)two_level_launch<RowsIn, 9, 16, 2, 128, true>(in, n, L, 100, rep1, true, ws, 0, nullptr); }},
-      {"S2 16, P2 256, R2 8",
-       [&] { (void)two_level_launch<RowsIn, 9, 16, 8, 256, true>(in, n, L, 100, rep1, true, ws, 0, nullptr); }},
+      {"S2 16, P2 128, R2 4 (flush at 16)",
+       [&] { (void)two_level_launch<RowsIn, 9, 16, 4, 128, true, 16>(in, n, L, 100, rep1, true, ws, 0, nullptr); }},
+      {"flush at 12",
+       [&] { (void)two_level_launch<RowsIn, 9, 16, 4, 128, true, 12>(in, n, L, 100, rep1, true, ws, 0, nullptr); }},
+      {"flush at 10",
+       [&] { (void)two_level_launch<RowsIn, 9, 16, 4, 128, true, 10>(in, n, L, 100, rep1, true, ws, 0, nullptr); }},
+      {"flush at 8",
+       [&] { (void)two_level_launch<RowsIn, 9, 16, 4, 128, true, 8>(in, n, L, 100, rep1, true, ws, 0, nullptr); }},
+      {"flush at 6",
+       [&] { (void)two_level_launch<RowsIn, 9, 16, 4, 128, true, 6>(in, n, L, 100, rep1, true, ws, 0, nullptr); }},
   };
   for (auto& v : vs) {
     (void)hipMemset(rep1, 0xFF, 4 * n);

@@ -837,9 +837,15 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
 // pass does (kS2-record slots, listed full buckets flushed by adjacent lanes).
 // Record k of the block's virtual range is found by a 9-step binary search
 // of the run prefix.  Segment starts from segtot (sizes summed by the first
-// pass); bucket starts from the fine scan's sizes as before.
+// pass); bucket starts from the fine scan's sizes as before.  kF: a bucket is
+// listed for the round-end flush once it holds kF records (kF = kS2: full
+// buckets only).  Flushing from 8 or 12 staged records cuts the arrivals that
+// meet a full slot array (single-record stores, ~20 % of records at kF = 16)
+// but measured slower at 100 M rows (2.02 ms at 16, 2.06 at 12, 2.10 at 8,
+// profiles/r3/exp_twolevel_s2/run_r3I.log): a block's stores into one bucket
+// fill one contiguous range, so the L2 merges the single stores anyway.
 constexpr uint32_t kMaxRuns = 512;  // R x max_rounds (host: two_level_runs_ok)
-template <bool kRec12, uint32_t kB2, uint32_t kS2, int kRows>
+template <bool kRec12, uint32_t kB2, uint32_t kS2, int kRows, uint32_t kF = kS2>
 __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
     const uint4* __restrict__ rec1, uint32_t skip, const uint32_t* __restrict__ offs,
     uint4* __restrict__ rec, const uint32_t* __restrict__ run_start,
@@ -850,6 +856,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
   using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
   static_assert(nbins < kPartThreads && 64 % kS2 == 0 && kPartThreads % kS2 == 0,
                 "listed buckets flushed by adjacent lanes of one wave");
+  static_assert(kF >= 1 && kF <= kS2, "flush threshold within the slots");
   static_assert(kMaxRuns < kPartThreads, "one run per thread in the prologue");
   __shared__ RecT stage[nbins][kS2];
   __shared__ uint32_t fill[nbins], cur[nbins];
@@ -952,7 +959,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
       const uint32_t sl = atomicAdd(&fill[b], 1u);
       if (sl < kS2) {
         stage[b][sl] = rq;
-        if (sl == kS2 - 1) full[atomicAdd(&full_n[par], 1u)] = static_cast<uint16_t>(b);
+        if (sl == kF - 1) full[atomicAdd(&full_n[par], 1u)] = static_cast<uint16_t>(b);
       } else {
         out[atomicAdd(&cur[b], 1u)] = rq;
       }
@@ -963,10 +970,10 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
     for (uint32_t x = t; x < nf * kS2; x += kPartThreads) {
       const uint32_t e = x / kS2, k = x % kS2;
       const uint32_t b = full[e];
-      const uint32_t p = cur[b];
-      out[p + k] = stage[b][k];
+      const uint32_t p = cur[b], len = min(fill[b], kS2);
+      if (k < len) out[p + k] = stage[b][k];
       if (k == 0) {
-        cur[b] = p + kS2;
+        cur[b] = p + len;
         fill[b] = 0;
       }
     }
@@ -1621,7 +1628,8 @@ void allow_lds(K kernel, size_t bytes) {
 // in the second pass's prologue): no histogram pass over the coarse records.
 // kRec12: rows without a rank array (rank = rank_base + row), 12-byte records
 // in both passes.
-template <typename In, uint32_t kB2, uint32_t kS2, int kR2, uint32_t kP2, bool kRec12 = false>
+template <typename In, uint32_t kB2, uint32_t kS2, int kR2, uint32_t kP2, bool kRec12 = false,
+          uint32_t kF2 = kS2>
 hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t chunk_rows,
                             uint32_t* rep, bool init_rep, void* ws, hipStream_t s, KTimer* timer,
                             uint32_t rank_base = 0) {
@@ -1669,7 +1677,7 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
     }
     {
       KScope k(timer, "bucket_scatter", s);
-      k_part2_runs<kRec12, kB2, kS2, kR2><<<dim3(kP2, nseg), kPartThreads, 0, s>>>(
+      k_part2_runs<kRec12, kB2, kS2, kR2, kF2><<<dim3(kP2, nseg), kPartThreads, 0, s>>>(
           rec1, skip2, fE, rec, run_s, run_l, L.max_rounds, P, kPartBlocks / kP2, segtot, ftot, fbase);
     }
     KScope k(timer, "bucket_group", s);
