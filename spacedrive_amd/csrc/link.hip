@@ -48,14 +48,15 @@ __device__ __forceinline__ void link_load(const uint32_t* __restrict__ rep,
                                           const uint8_t* __restrict__ valid, uint64_t n,
                                           uint64_t tile, LinkRows& q) {
   const uint32_t* rs = rank ? rank : rep;
-  const uint8_t* vs = valid ? valid : reinterpret_cast<const uint8_t*>(rep);
 #pragma unroll
   for (int k = 0; k < kRows; ++k) {
     const uint64_t i = tile + k * kThreads + threadIdx.x;
     const uint64_t j = i < n ? i : n - 1;
     q.p[k] = rep[j];
     q.a[k] = rs[j];
-    q.b[k] = vs[j];
+    // null valid: a byte of row j's own rep word (rep indexed as bytes by j
+    // would read another line, the first quarter of the rep array)
+    q.b[k] = *(valid ? valid + j : reinterpret_cast<const uint8_t*>(rep + j));
   }
 }
 

@@ -85,20 +85,25 @@ struct RowsIn {
     get(i, k, r, v);
     row = static_cast<uint32_t>(i);
   }
-  // null rank / valid: the loads read the key array instead (same lines) and
-  // the value is replaced at use, so the batch has no branch
+  // null rank / valid: the load reads the row's own key word instead (the
+  // line its key load brings in) and the value is replaced at use, so the
+  // batch has no branch.  (Indexing the key array as a u32 / u8 array by row
+  // read a DIFFERENT line, the first half / eighth of the key array: +4 B of
+  // HBM per row, 1.30 GB fetched per 100 M-row coarse pass for 0.9 GB of
+  // rows, profiles/r3/prof_r3J/pmc_dedup_full.txt.)
   template <int U>
   __device__ __forceinline__ void load_many(uint64_t i0, uint64_t stride, uint64_t end,
                                             uint64_t safe, RowBatch<U>& q) const {
     batch_index(i0, stride, end, safe, q);
-    const uint32_t* rs = rank ? rank : reinterpret_cast<const uint32_t*>(key);
-    const uint8_t* vs = valid ? valid : reinterpret_cast<const uint8_t*>(key);
+    const uint32_t* ka = reinterpret_cast<const uint32_t*>(key);
 #pragma unroll
     for (int u = 0; u < U; ++u) q.k[u] = key[q.row[u]];
 #pragma unroll
-    for (int u = 0; u < U; ++u) q.a[u] = rs[q.row[u]];
+    for (int u = 0; u < U; ++u)
+      q.a[u] = *(rank ? rank + q.row[u] : ka + 2ull * q.row[u]);
 #pragma unroll
-    for (int u = 0; u < U; ++u) q.b[u] = vs[q.row[u]];
+    for (int u = 0; u < U; ++u)
+      q.b[u] = *(valid ? valid + q.row[u] : reinterpret_cast<const uint8_t*>(ka + 2ull * q.row[u]));
   }
   template <int U>
   __device__ __forceinline__ uint64_t key_of(const RowBatch<U>& q, int u) const { return q.k[u]; }
@@ -134,12 +139,12 @@ struct RecIn {
   __device__ __forceinline__ void load_many(uint64_t i0, uint64_t stride, uint64_t end,
                                             uint64_t safe, RowBatch<U>& q) const {
     batch_index(i0, stride, end, safe, q);
-    const uint8_t* vs = valid ? valid : reinterpret_cast<const uint8_t*>(rec);
     uint3 t[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) t[u] = rec[q.row[u]];
 #pragma unroll
-    for (int u = 0; u < U; ++u) q.b[u] = vs[q.row[u]];
+    for (int u = 0; u < U; ++u)  // null valid: the record's own line (see RowsIn)
+      q.b[u] = *(valid ? valid + q.row[u] : reinterpret_cast<const uint8_t*>(rec + q.row[u]));
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       q.k[u] = (static_cast<uint64_t>(t[u].y) << 32) | t[u].x;
