@@ -492,13 +492,191 @@ __global__ __launch_bounds__(1024) void k_small(const uint8_t* __restrict__ aren
   }
 }
 
+// ---- Quad-lane hashing of an LDS-staged message (the latency paths) ---------
+// A single message is a chain of dependent compressions (16 per chunk, then
+// one per tree level), so its latency is one compression's latency times the
+// chain, and one wave64 lane per chunk spends ~2,800 cycles on each (680
+// VALU instructions, 4 independent G chains).  Here each compression is spread
+// over a QUAD of lanes: lane i holds state column i (a, b, c, d) =
+// (v[i], v[4+i], v[8+i], v[12+i]) and computes G_i of the column step, then,
+// after DPP quad rotations of rows b, c, d, G_i of the diagonal step -- 30
+// instructions per round instead of 96; its 4 message words per round are
+// read from LDS at per-lane offsets of the message schedule.  The outputs
+// cv[i] = a ^ c and cv[4+i] = b ^ d are exactly the next block's a and b.
+// One wave, chained compressions (scripts/exp_chain.hip,
+// profiles/r3/latency/r3L_exp_chain.log): ~1,000 cycles (0.42 us) per
+// compression against ~2,800-2,950 (1.15-1.23 us) for the lane form.
+__device__ __constant__ uint8_t kQuadSched[7][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8},
+    {3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1},
+    {10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6},
+    {12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4},
+    {9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7},
+    {11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13}};
+
+// DPP quad_perm: lane i of each quad reads lane i+1 / i+2 / i+3 (mod 4)
+constexpr int kQuadRot1 = 0x39, kQuadRot2 = 0x4E, kQuadRot3 = 0x93;
+template <int kCtrl>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
+  return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), kCtrl, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ void quad_g(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d,
+                                       uint32_t x, uint32_t y) {
+  SDGPU_G(a, b, c, d, x, y);
+}
+
+// Per-lane state of the quad form: lane i = threadIdx.x & 3.
+struct QuadLane {
+  uint32_t i;            // column
+  uint32_t iv_a, iv_b;   // IV[i], IV[4 + i]
+  uint32_t woff[28];     // byte offsets of this lane's message words, round by round
+  __device__ __forceinline__ void init() {
+    i = threadIdx.x & 3u;
+    const uint32_t iva[4] = {IV0, IV1, IV2, IV3}, ivb[4] = {IV4, IV5, IV6, IV7};
+    iv_a = i == 0 ? iva[0] : i == 1 ? iva[1] : i == 2 ? iva[2] : iva[3];
+    iv_b = i == 0 ? ivb[0] : i == 1 ? ivb[1] : i == 2 ? ivb[2] : ivb[3];
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+      woff[4 * r] = 4u * kQuadSched[r][2 * i];
+      woff[4 * r + 1] = 4u * kQuadSched[r][2 * i + 1];
+      woff[4 * r + 2] = 4u * kQuadSched[r][8 + 2 * i];
+      woff[4 * r + 3] = 4u * kQuadSched[r][9 + 2 * i];
+    }
+  }
+  // (h0, h1) = (cv[i], cv[4+i]) <- compress of the 64-byte block at LDS `blk`
+  // (4-byte aligned, zero padded); d = this lane's word of {counter lo,
+  // counter hi, block length, flags}.
+  __device__ __forceinline__ void compress(uint32_t& h0, uint32_t& h1, const uint8_t* blk,
+                                           uint32_t d) const {
+    uint32_t w[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) w[k] = *reinterpret_cast<const uint32_t*>(blk + woff[k]);
+    uint32_t a = h0, b = h1, c = iv_a;
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+      quad_g(a, b, c, d, w[4 * r], w[4 * r + 1]);  // column step
+      b = quad_perm<kQuadRot1>(b);
+      c = quad_perm<kQuadRot2>(c);
+      d = quad_perm<kQuadRot3>(d);
+      quad_g(a, b, c, d, w[4 * r + 2], w[4 * r + 3]);  // diagonal step
+      b = quad_perm<kQuadRot3>(b);
+      c = quad_perm<kQuadRot2>(c);
+      d = quad_perm<kQuadRot1>(d);
+    }
+    h0 = a ^ c;
+    h1 = b ^ d;
+  }
+  __device__ __forceinline__ uint32_t dword(uint32_t ctr, uint32_t blen, uint32_t flags) const {
+    return i == 0 ? ctr : i == 1 ? 0u : i == 2 ? blen : flags;
+  }
+};
+
+// The BLAKE3 hash of the l-byte message staged at LDS `msg` (zero padded to a
+// 64-byte multiple, at least 64 bytes), by the whole workgroup in quads; chunk
+// CVs in LDS cvr (8 words per chunk, row-major: a parent's 16 message words are
+// its two children's rows, contiguous).  Returns with the digest's words i and
+// 4 + i in lanes i = 0..3 of the first quad (h0, h1); every thread must call it.
+__device__ __forceinline__ void quad_hash_staged(const QuadLane& L, const uint8_t* msg, uint32_t l,
+                                                 uint32_t* cvr, uint32_t& h0, uint32_t& h1) {
+  const uint32_t q = threadIdx.x >> 2, Q = blockDim.x >> 2;
+  const uint32_t nch = n_chunks_of(l);
+  const bool root_chunk = nch == 1;
+  for (uint32_t c = q; c < nch; c += Q) {
+    const uint32_t clen = min(B3_CHUNK_LEN, l - c * B3_CHUNK_LEN);
+    const uint32_t nb = clen == 0 ? 1u : (clen + 63u) >> 6;
+    const uint8_t* cp = msg + c * B3_CHUNK_LEN;
+    uint32_t a = L.iv_a, b = L.iv_b;
+    for (uint32_t j = 0; j < nb; ++j) {
+      const bool last = j + 1 == nb;
+      const uint32_t flags = (j == 0 ? B3_CHUNK_START : 0u) |
+                             (last ? (B3_CHUNK_END | (root_chunk ? B3_ROOT : 0u)) : 0u);
+      L.compress(a, b, cp + 64u * j,
+                 L.dword(root_chunk ? 0u : c, last ? clen - 64u * j : B3_BLOCK_LEN, flags));
+    }
+    if (root_chunk) {
+      h0 = a;
+      h1 = b;
+    } else {
+      cvr[8 * c + L.i] = a;
+      cvr[8 * c + 4 + L.i] = b;
+    }
+  }
+  if (root_chunk) return;  // uniform
+  __syncthreads();
+  uint32_t cnt = nch;
+  while (cnt > 2) {  // one level: parents of (2p, 2p + 1), the odd last CV carried
+    const uint32_t half = cnt >> 1;
+    uint32_t a = 0, b = 0;
+    if (q < half) {
+      a = L.iv_a;
+      b = L.iv_b;
+      L.compress(a, b, reinterpret_cast<const uint8_t*>(cvr + 16 * q),
+                 L.dword(0u, B3_BLOCK_LEN, B3_PARENT));
+    }
+    __syncthreads();
+    if (q < half) {
+      cvr[8 * q + L.i] = a;
+      cvr[8 * q + 4 + L.i] = b;
+    } else if ((cnt & 1u) && q == half) {
+      cvr[8 * half + L.i] = cvr[8 * (cnt - 1) + L.i];
+      cvr[8 * half + 4 + L.i] = cvr[8 * (cnt - 1) + 4 + L.i];
+    }
+    __syncthreads();
+    cnt = half + (cnt & 1u);
+  }
+  if (q == 0) {
+    h0 = L.iv_a;
+    h1 = L.iv_b;
+    L.compress(h0, h1, reinterpret_cast<const uint8_t*>(cvr), L.dword(0u, B3_BLOCK_LEN, B3_PARENT | B3_ROOT));
+  }
+}
+
+// Copies the l-byte message at `src` (16-B aligned, readable up to the next 16
+// bytes) into LDS `dst`, zeroing the bytes past l up to the 64-byte block end
+// (at least one block), as the quad hash reads whole blocks.
+__device__ __forceinline__ void stage_message(uint8_t* dst, const uint8_t* __restrict__ src,
+                                              uint32_t l) {
+  const uint32_t nvec = (l + 15) / 16;
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  constexpr int kU = 8;
+  for (uint32_t i0 = threadIdx.x; i0 < nvec; i0 += kU * blockDim.x) {
+    uint4 v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t i = i0 + u * blockDim.x;
+      v[u] = i < nvec ? s4[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t i = i0 + u * blockDim.x;
+      if (i >= nvec) continue;
+      if (16 * i + 16 > l) {  // the last vector: bytes past l -> 0
+        const uint32_t vb = l - 16 * i;
+        uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint32_t n = vb > 4 * k ? min(vb - 4 * k, 4u) : 0u;
+          w[k] &= n >= 4 ? ~0u : (1u << (8 * n)) - 1u;
+        }
+        v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      d4[i] = v[u];
+    }
+  }
+  const uint32_t end = l == 0 ? 64u : (l + 63u) & ~63u;  // whole blocks
+  for (uint32_t i = nvec + threadIdx.x; i < end / 16; i += blockDim.x) d4[i] = make_uint4(0, 0, 0, 0);
+}
+
 // Host-staged latency path: a few messages of at most kHostStageMax bytes in
 // pinned host memory (the caller's staging slab), one workgroup each, copied
 // into LDS by the workgroup (16 B per lane, eight loads in flight per lane: a couple of PCIe
-// round trips), hashed there exactly as k_small does, and the out_words
-// written straight into pinned host memory -- no H2D / D2H copy commands
-// around the launch (they are ~2/3 of a 4 KiB single-file call's fixed cost,
-// profiles/r2/latency/).
+// round trips), hashed there in quads of lanes (quad_hash_staged), and the
+// out_words written straight into pinned host memory -- no H2D / D2H copy
+// commands around the launch (they are ~2/3 of a 4 KiB single-file call's
+// fixed cost, profiles/r2/latency/).
 constexpr uint32_t kHostStageChunks = kHostStageMax / B3_CHUNK_LEN;
 
 __global__ __launch_bounds__(1024) void k_small_host(const uint8_t* __restrict__ arena,
@@ -507,81 +685,19 @@ __global__ __launch_bounds__(1024) void k_small_host(const uint8_t* __restrict__
                                                      uint32_t out_words,
                                                      uint32_t* __restrict__ out_all) {
   extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
-  __shared__ uint32_t cv[8][kHostStageChunks];
-  const uint32_t t = threadIdx.x, m = blockIdx.x;
-  const uint8_t* __restrict__ msg = arena + off[m];
+  __shared__ __attribute__((aligned(16))) uint32_t cvr[8 * kHostStageChunks];
+  const uint32_t m = blockIdx.x;
   const uint32_t l = len[m];
   uint32_t* __restrict__ out = out_all + static_cast<uint64_t>(m) * out_words;
-  {
-    const uint32_t nvec = (l + 15) / 16;
-    const uint4* src = reinterpret_cast<const uint4*>(msg);
-    uint4* dst = reinterpret_cast<uint4*>(stage);
-    constexpr int kU = 8;
-    for (uint32_t i0 = t; i0 < nvec; i0 += kU * blockDim.x) {
-      uint4 v[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const uint32_t i = i0 + u * blockDim.x;
-        v[u] = i < nvec ? src[i] : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const uint32_t i = i0 + u * blockDim.x;
-        if (i < nvec) dst[i] = v[u];
-      }
-    }
-  }
+  QuadLane L;
+  L.init();
+  stage_message(stage, arena + off[m], l);
   __syncthreads();
-  const uint8_t* p = stage;
-  const uint32_t nch = n_chunks_of(l);
-  uint32_t c[8];
-  if (nch == 1) {
-    if (t == 0) {
-      b3_chunk(p, l, 0, B3_ROOT, c);
-      for (uint32_t w = 0; w < out_words; ++w) out[w] = c[w];
-    }
-    return;
-  }
-  if (t < nch) {
-    chunk_any(p, l, t, 0u, c);
-#pragma unroll
-    for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
-  }
-  __syncthreads();
-  uint32_t cnt = nch;
-  while (cnt > 2) {
-    const uint32_t half = cnt >> 1;
-    uint32_t a[8], b[8];
-    const bool merge = t < half;
-    const bool carry = (cnt & 1u) && t == half;
-    if (merge) {
-#pragma unroll
-      for (int w = 0; w < 8; ++w) {
-        a[w] = cv[w][2 * t];
-        b[w] = cv[w][2 * t + 1];
-      }
-      b3_parent(c, a, b, 0u);
-    } else if (carry) {
-#pragma unroll
-      for (int w = 0; w < 8; ++w) c[w] = cv[w][cnt - 1];
-    }
-    __syncthreads();
-    if (merge || carry) {
-#pragma unroll
-      for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
-    }
-    __syncthreads();
-    cnt = half + (cnt & 1u);
-  }
-  if (t == 0) {
-    uint32_t a[8], b[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      a[w] = cv[w][0];
-      b[w] = cv[w][1];
-    }
-    b3_parent(c, a, b, B3_ROOT);
-    for (uint32_t w = 0; w < out_words; ++w) out[w] = c[w];
+  uint32_t h0 = 0, h1 = 0;
+  quad_hash_staged(L, stage, l, cvr, h0, h1);
+  if (threadIdx.x < 4) {  // digest words i and 4 + i
+    if (L.i < out_words) out[L.i] = h0;
+    if (4 + L.i < out_words) out[4 + L.i] = h1;
   }
 }
 
@@ -589,21 +705,24 @@ __global__ __launch_bounds__(1024) void k_small_host(const uint8_t* __restrict__
 // the request number with system-scope acquire loads (the message area and
 // the mailbox are coherent pinned memory, so every load reads the host's
 // current bytes); the workgroup then hashes the message exactly as
-// k_small_host and thread 0 publishes the digest words, then the request
+// k_small_host (in quads of lanes) and thread 0 publishes the digest words
+// (gathered from the first quad by shuffles), then the request
 // number (system-scope release).  Every wave reaches the loop's exit: the
 // stop request, the idle deadline and the lifetime deadline are decided by
 // thread 0 and broadcast through LDS.
 constexpr uint32_t kSvcThreads = 256;
-static_assert(kSvcThreads >= kHostStageChunks, "one thread per chunk of the largest message");
+static_assert(kSvcThreads / 4 >= kHostStageChunks / 2, "one quad per parent of the first tree level");
 
 __global__ __launch_bounds__(kSvcThreads) void k_service(SvcMailbox* __restrict__ mb,
                                                          const uint8_t* __restrict__ msg,
                                                          uint32_t last_seq, uint64_t idle_ticks,
                                                          uint64_t life_ticks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
-  __shared__ uint32_t cv[8][kHostStageChunks];
+  __shared__ __attribute__((aligned(16))) uint32_t cvr[8 * kHostStageChunks];
   __shared__ uint32_t s_go, s_len, s_words;
   const uint32_t t = threadIdx.x;
+  QuadLane L;
+  L.init();
   const uint64_t t_start = wall_clock64();
   uint64_t t_last = t_start;
   for (;;) {
@@ -630,85 +749,28 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcMailbox* __restrict_
     if (go == 0) break;  // uniform: stop, idle or lifetime deadline
     const uint64_t t_seen = wall_clock64();
     const uint32_t l = min(s_len, kHostStageMax), out_words = min(s_words, 16u);
-    {
-      const uint32_t nvec = (l + 15) / 16;
-      const uint4* src = reinterpret_cast<const uint4*>(msg);
-      uint4* dst = reinterpret_cast<uint4*>(stage);
-      constexpr int kU = 8;
-      for (uint32_t i0 = t; i0 < nvec; i0 += kU * kSvcThreads) {
-        uint4 v[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-          const uint32_t i = i0 + u * kSvcThreads;
-          v[u] = i < nvec ? src[i] : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-          const uint32_t i = i0 + u * kSvcThreads;
-          if (i < nvec) dst[i] = v[u];
-        }
-      }
-    }
+    stage_message(stage, msg, l);
     __syncthreads();
     const uint64_t t_loaded = wall_clock64();
-    const uint32_t nch = n_chunks_of(l);
-    uint32_t c[8];
-    if (nch == 1) {
-      if (t == 0) b3_chunk(stage, l, 0, B3_ROOT, c);
-    } else {
-      if (t < nch) {
-        chunk_any(stage, l, t, 0u, c);
+    uint32_t h0 = 0, h1 = 0;
+    quad_hash_staged(L, stage, l, cvr, h0, h1);
+    if (t < 64) {  // wave 0: thread 0 gathers the digest from lanes 0..3
+      uint32_t dg[8];
 #pragma unroll
-        for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
-      }
-      __syncthreads();
-      uint32_t cnt = nch;
-      while (cnt > 2) {
-        const uint32_t half = cnt >> 1;
-        uint32_t a[8], b[8];
-        const bool merge = t < half;
-        const bool carry = (cnt & 1u) && t == half;
-        if (merge) {
-#pragma unroll
-          for (int w = 0; w < 8; ++w) {
-            a[w] = cv[w][2 * t];
-            b[w] = cv[w][2 * t + 1];
-          }
-          b3_parent(c, a, b, 0u);
-        } else if (carry) {
-#pragma unroll
-          for (int w = 0; w < 8; ++w) c[w] = cv[w][cnt - 1];
-        }
-        __syncthreads();
-        if (merge || carry) {
-#pragma unroll
-          for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
-        }
-        __syncthreads();
-        cnt = half + (cnt & 1u);
-      }
+      for (int w = 0; w < 8; ++w) dg[w] = __shfl(w < 4 ? h0 : h1, w & 3);
       if (t == 0) {
-        uint32_t a[8], b[8];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-          a[w] = cv[w][0];
-          b[w] = cv[w][1];
-        }
-        b3_parent(c, a, b, B3_ROOT);
+        for (uint32_t w = 0; w < out_words; ++w)
+          __hip_atomic_store(&mb->digest[w], w < 8 ? dg[w] : 0u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->t_seen, t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->t_loaded, t_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->t_done, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->done, go, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        last_seq = go;
       }
-    }
-    if (t == 0) {
-      for (uint32_t w = 0; w < out_words; ++w)
-        __hip_atomic_store(&mb->digest[w], w < 8 ? c[w] : 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&mb->t_seen, t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&mb->t_loaded, t_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&mb->t_done, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&mb->done, go, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      last_seq = go;
     }
     t_last = wall_clock64();
-    __syncthreads();  // LDS (stage, cv, s_*) reused by the next request
+    __syncthreads();  // LDS (stage, cvr, s_*) reused by the next request
   }
   if (t == 0) __hip_atomic_store(&mb->state, kSvcExited, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -776,8 +838,10 @@ hipError_t small_host_launch(const uint8_t* h_arena, const uint64_t* h_off, cons
   if (max_len > kHostStageMax || (reinterpret_cast<uintptr_t>(h_arena) & 15u))
     return hipErrorInvalidValue;
   const uint32_t nch = max_len <= B3_CHUNK_LEN ? 1u : (max_len + B3_CHUNK_LEN - 1) / B3_CHUNK_LEN;
-  const uint32_t threads = std::max<uint32_t>(256, (nch + 63) / 64 * 64);
-  const size_t lds = (static_cast<size_t>(max_len) + 15) / 16 * 16 + 16;
+  // quads: >= 64 of them, one per parent of the first tree level
+  const uint32_t threads = std::max<uint32_t>(256, (2 * nch + 63) / 64 * 64);
+  // whole 64-byte blocks (stage_message zero-pads the last one), at least one
+  const size_t lds = std::max<size_t>(64, (static_cast<size_t>(max_len) + 63) / 64 * 64);
   // the dynamic-LDS limit is a per-device attribute of the loaded kernel: set
   // once for each device this process launches on
   static std::atomic<uint64_t> attr_set{0};

@@ -125,3 +125,22 @@ def test_service_survives_idle_exit_and_bulk_calls(svc_ctx, tmp_path):
     assert ei.value.errno == 2
     for _ in range(200):                                      # back-to-back requests
         assert cas.generate_cas_id(p, 4096, svc_ctx) == want_cas
+
+
+@pytest.mark.parametrize("service", [False, True])
+def test_quad_tree_shapes(ctx, svc_ctx, tmp_path, service):
+    """The latency kernels hash in quads of lanes and build the tree level by
+    level (odd CVs carried): every chunk-count class the carries produce --
+    2-9, 15-17, 31-33, 63-65 and 111-112 chunks, ragged and whole last chunks
+    -- through file_checksum (the message is the file) on the launch path
+    (k_small_host) and through the resident service (k_service)."""
+    from spacedrive_amd import validation
+    c = svc_ctx if service else ctx
+    rng = np.random.default_rng(19)
+    chunks = [2, 3, 4, 5, 6, 7, 8, 9, 15, 16, 17, 31, 32, 33, 63, 64, 65, 111, 112]
+    for k in chunks:
+        for n in {1024 * (k - 1) + 1, 1024 * (k - 1) + 700, 1024 * k}:
+            p = os.path.join(tmp_path, f"q{n}")
+            rng.integers(0, 256, n, dtype=np.uint8).tofile(p)
+            assert validation.file_checksum(p, c) == O.file_checksum_path(p), (k, n)
+
