@@ -19,7 +19,7 @@ KERNELS = ["k_leaves3", "k_fold3", "k_tree_level<true>", "k_tree_level<false>",
            "k_part_scatter_ws", "k_part_private", "k_part2_runs", "k_fine_recount_runs",
            "k_fine_scan", "k_bucket_group12_pk", "k_bucket_group_pk",
            "k_bucket_group12", "k_bucket_group", "k_link_count", "k_link_write", "k_small_host",
-           "k_small", "k_service"]
+           "k_small_split", "k_service"]
 LONG_MS = 5.0  # K1 launches over a whole 1 M-file step take ~13 ms; every other K1 launch < 2 ms
 
 

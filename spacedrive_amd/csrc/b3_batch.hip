@@ -412,85 +412,17 @@ uint32_t leaves3_grid() {
 }
 
 // ============================================================================
-// Latency path: one workgroup per message of at most 1024 chunks (1 MiB).
-// Thread t hashes chunk t (16 compressions), then the CVs are folded level by
-// level in LDS (pairwise, odd node carried up: BLAKE3's left-complete tree),
-// one compression per level, ROOT on the last.  A 57-chunk cas message is one
-// pass of 57 lanes + 6 levels: ~22 compression latencies in ONE launch, for
-// the single-file callers (watcher/utils.rs:236,411,467, non_indexed.rs:161)
-// where K1's planning launches would dominate.
+// Latency paths, for the single-file callers (watcher/utils.rs:236,411,467,
+// non_indexed.rs:161) and small batches, where K1's planning launches would
+// dominate: a message's chunks are hashed in parallel, then the CVs folded
+// level by level in LDS (pairwise, odd node carried up: BLAKE3's
+// left-complete tree), one compression per level, ROOT on the last -- each
+// compression spread over a quad of lanes.  k_small_host / k_service: one
+// workgroup per message of <= 112 KiB; k_small_split: messages of <= 1 MiB
+// (1024 chunks) split into 64 KiB groups, one workgroup each.
 // ============================================================================
 
 constexpr uint32_t kSmallMaxChunks = 1024;
-
-__global__ __launch_bounds__(1024) void k_small(const uint8_t* __restrict__ arena,
-                                                const uint64_t* __restrict__ off,
-                                                const uint32_t* __restrict__ len,
-                                                uint32_t max_len, uint32_t out_words,
-                                                uint32_t* __restrict__ out,
-                                                int32_t* __restrict__ status) {
-  __shared__ uint32_t cv[8][kSmallMaxChunks];  // word-major: lane-indexed access is conflict-free
-  const uint32_t m = blockIdx.x;
-  const uint32_t t = threadIdx.x;
-  const uint32_t l = len[m];
-  const bool ok = l <= max_len && (off[m] & 15u) == 0 && l <= kSmallMaxChunks * B3_CHUNK_LEN;
-  if (t == 0 && status) status[m] = ok ? 0 : -EINVAL;
-  if (!ok) {
-    if (t < out_words) out[m * out_words + t] = 0u;
-    return;
-  }
-  const uint32_t nch = n_chunks_of(l);
-  const uint8_t* p = arena + off[m];
-  uint32_t c[8];
-  if (nch == 1) {
-    if (t == 0) {
-      b3_chunk(p, l, 0, B3_ROOT, c);
-      for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = c[w];
-    }
-    return;
-  }
-  if (t < nch) {
-    chunk_any(p, l, t, 0u, c);
-#pragma unroll
-    for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
-  }
-  __syncthreads();
-  uint32_t cnt = nch;
-  while (cnt > 2) {
-    const uint32_t half = cnt >> 1;
-    uint32_t a[8], b[8];
-    const bool merge = t < half;
-    const bool carry = (cnt & 1u) && t == half;
-    if (merge) {
-#pragma unroll
-      for (int w = 0; w < 8; ++w) {
-        a[w] = cv[w][2 * t];
-        b[w] = cv[w][2 * t + 1];
-      }
-      b3_parent(c, a, b, 0u);
-    } else if (carry) {
-#pragma unroll
-      for (int w = 0; w < 8; ++w) c[w] = cv[w][cnt - 1];
-    }
-    __syncthreads();
-    if (merge || carry) {
-#pragma unroll
-      for (int w = 0; w < 8; ++w) cv[w][t] = c[w];
-    }
-    __syncthreads();
-    cnt = half + (cnt & 1u);
-  }
-  if (t == 0) {
-    uint32_t a[8], b[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      a[w] = cv[w][0];
-      b[w] = cv[w][1];
-    }
-    b3_parent(c, a, b, B3_ROOT);
-    for (uint32_t w = 0; w < out_words; ++w) out[m * out_words + w] = c[w];
-  }
-}
 
 // ---- Quad-lane hashing of an LDS-staged message (the latency paths) ---------
 // A single message is a chain of dependent compressions (16 per chunk, then
@@ -573,18 +505,21 @@ struct QuadLane {
   }
 };
 
-// The BLAKE3 hash of the l-byte message staged at LDS `msg` (zero padded to a
-// 64-byte multiple, at least 64 bytes), by the whole workgroup in quads; chunk
-// CVs in LDS cvr (8 words per chunk, row-major: a parent's 16 message words are
-// its two children's rows, contiguous).  Returns with the digest's words i and
-// 4 + i in lanes i = 0..3 of the first quad (h0, h1); every thread must call it.
-__device__ __forceinline__ void quad_hash_staged(const QuadLane& L, const uint8_t* msg, uint32_t l,
-                                                 uint32_t* cvr, uint32_t& h0, uint32_t& h1) {
+// Chunk CVs of the glen bytes staged at LDS `msg` (zero padded to a 64-byte
+// multiple, at least 64 bytes), chunk counters ctr0, ctr0 + 1, ...: lane i of
+// the quad owning chunk j writes cvr[8 j + i] and cvr[8 j + 4 + i] (row-major
+// CVs: a parent's 16 message words are its two children's rows, contiguous).
+// With `whole` (these bytes are the whole message) and a single chunk, that
+// chunk is the ROOT: its output words i and 4 + i are left in (h0, h1) of
+// lanes i = 0..3 and nothing is written.  Every thread must call it.
+__device__ __forceinline__ void quad_chunks(const QuadLane& L, const uint8_t* msg, uint32_t glen,
+                                            uint32_t ctr0, bool whole, uint32_t* cvr, uint32_t& h0,
+                                            uint32_t& h1) {
   const uint32_t q = threadIdx.x >> 2, Q = blockDim.x >> 2;
-  const uint32_t nch = n_chunks_of(l);
-  const bool root_chunk = nch == 1;
+  const uint32_t nch = n_chunks_of(glen);
+  const bool root_chunk = whole && nch == 1;
   for (uint32_t c = q; c < nch; c += Q) {
-    const uint32_t clen = min(B3_CHUNK_LEN, l - c * B3_CHUNK_LEN);
+    const uint32_t clen = min(B3_CHUNK_LEN, glen - c * B3_CHUNK_LEN);
     const uint32_t nb = clen == 0 ? 1u : (clen + 63u) >> 6;
     const uint8_t* cp = msg + c * B3_CHUNK_LEN;
     uint32_t a = L.iv_a, b = L.iv_b;
@@ -593,7 +528,7 @@ __device__ __forceinline__ void quad_hash_staged(const QuadLane& L, const uint8_
       const uint32_t flags = (j == 0 ? B3_CHUNK_START : 0u) |
                              (last ? (B3_CHUNK_END | (root_chunk ? B3_ROOT : 0u)) : 0u);
       L.compress(a, b, cp + 64u * j,
-                 L.dword(root_chunk ? 0u : c, last ? clen - 64u * j : B3_BLOCK_LEN, flags));
+                 L.dword(root_chunk ? 0u : ctr0 + c, last ? clen - 64u * j : B3_BLOCK_LEN, flags));
     }
     if (root_chunk) {
       h0 = a;
@@ -603,10 +538,17 @@ __device__ __forceinline__ void quad_hash_staged(const QuadLane& L, const uint8_
       cvr[8 * c + 4 + L.i] = b;
     }
   }
-  if (root_chunk) return;  // uniform
-  __syncthreads();
-  uint32_t cnt = nch;
-  while (cnt > 2) {  // one level: parents of (2p, 2p + 1), the odd last CV carried
+}
+
+// The tree over the cnt >= 1 CVs in cvr (written before a barrier the caller
+// placed): level by level, parents of (2p, 2p + 1) one per quad, the odd last
+// CV carried; top_flags (ROOT or 0) on the last parent.  cnt == 1: the CV
+// itself.  Leaves the result's words i and 4 + i in (h0, h1) of lanes 0..3;
+// every thread must call it; needs blockDim.x / 4 >= cnt / 2.
+__device__ __forceinline__ void quad_tree(const QuadLane& L, uint32_t* cvr, uint32_t cnt,
+                                          uint32_t top_flags, uint32_t& h0, uint32_t& h1) {
+  const uint32_t q = threadIdx.x >> 2;
+  while (cnt > 2) {
     const uint32_t half = cnt >> 1;
     uint32_t a = 0, b = 0;
     if (q < half) {
@@ -627,10 +569,28 @@ __device__ __forceinline__ void quad_hash_staged(const QuadLane& L, const uint8_
     cnt = half + (cnt & 1u);
   }
   if (q == 0) {
-    h0 = L.iv_a;
-    h1 = L.iv_b;
-    L.compress(h0, h1, reinterpret_cast<const uint8_t*>(cvr), L.dword(0u, B3_BLOCK_LEN, B3_PARENT | B3_ROOT));
+    if (cnt == 1) {
+      h0 = cvr[L.i];
+      h1 = cvr[4 + L.i];
+    } else {
+      h0 = L.iv_a;
+      h1 = L.iv_b;
+      L.compress(h0, h1, reinterpret_cast<const uint8_t*>(cvr),
+                 L.dword(0u, B3_BLOCK_LEN, B3_PARENT | top_flags));
+    }
   }
+}
+
+// The BLAKE3 hash of the l-byte message staged at LDS `msg` (zero padded to a
+// 64-byte multiple, at least 64 bytes), by the whole workgroup in quads; the
+// digest's words i and 4 + i end in lanes i = 0..3 (h0, h1).
+__device__ __forceinline__ void quad_hash_staged(const QuadLane& L, const uint8_t* msg, uint32_t l,
+                                                 uint32_t* cvr, uint32_t& h0, uint32_t& h1) {
+  quad_chunks(L, msg, l, 0u, true, cvr, h0, h1);
+  const uint32_t nch = n_chunks_of(l);
+  if (nch == 1) return;  // uniform
+  __syncthreads();
+  quad_tree(L, cvr, nch, B3_ROOT, h0, h1);
 }
 
 // Copies the l-byte message at `src` (16-B aligned, readable up to the next 16
@@ -698,6 +658,87 @@ __global__ __launch_bounds__(1024) void k_small_host(const uint8_t* __restrict__
   if (threadIdx.x < 4) {  // digest words i and 4 + i
     if (L.i < out_words) out[L.i] = h0;
     if (4 + L.i < out_words) out[4 + L.i] = h1;
+  }
+}
+
+// Messages of up to 1 MiB (SMALL_MAX_BYTES): each split into 64-chunk groups
+// (64 KiB subtrees, complete and power-of-two aligned, so their CVs are nodes
+// of BLAKE3's tree), one 256-thread workgroup per group staging its bytes in
+// LDS and hashing them in quads; the group CVs go to `scratch`, and the
+// workgroup that finishes a message's last group (agent-scope counter) folds
+// them with ROOT.  A 1 MiB message: 16 workgroups of 16 dependent
+// compressions + 6 levels, then 4 levels, instead of one workgroup whose 16
+// waves issue 1024 lanes' compressions on one CU (k_small, ~96 us).  The
+// source may be device or pinned host memory (16-B aligned offsets, readable
+// up to the next 16 bytes).  scratch: small_split_scratch_bytes(), its
+// counters zero (every last workgroup resets its counter); <= 64 messages.
+constexpr uint32_t kSplitThreads = 256;
+constexpr uint32_t kSplitGroupChunks = 64;
+constexpr uint32_t kSplitMaxGroups = SMALL_MAX_BYTES / (kSplitGroupChunks * B3_CHUNK_LEN);
+constexpr uint32_t kSplitMaxMsgs = 64;  // scratch: kSplitMaxMsgs counters, then the group CVs
+static_assert(kSplitThreads / 4 >= kSplitGroupChunks / 2 && kSplitThreads / 4 >= kSplitMaxGroups / 2,
+              "one quad per parent of a first tree level");
+
+__global__ __launch_bounds__(kSplitThreads) void k_small_split(
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, uint32_t max_len, uint32_t gmax, uint32_t out_words,
+    uint32_t* __restrict__ out, int32_t* __restrict__ status, uint32_t* __restrict__ scratch) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kSplitGroupChunks * B3_CHUNK_LEN];
+  __shared__ __attribute__((aligned(16))) uint32_t cvr[8 * kSplitGroupChunks];
+  __shared__ uint32_t s_last;
+  const uint32_t m = blockIdx.x / gmax, g = blockIdx.x % gmax, t = threadIdx.x;
+  const uint32_t l = len[m];
+  const bool ok = l <= max_len && (off[m] & 15u) == 0 && l <= SMALL_MAX_BYTES;
+  if (g == 0 && t == 0 && status) status[m] = ok ? 0 : -EINVAL;
+  uint32_t* __restrict__ o = out + static_cast<uint64_t>(m) * out_words;
+  if (!ok) {
+    if (g == 0 && t < out_words) o[t] = 0u;
+    return;
+  }
+  const uint32_t nch = n_chunks_of(l);
+  const uint32_t G = (nch + kSplitGroupChunks - 1) / kSplitGroupChunks;
+  if (g >= G) return;  // uniform per workgroup
+  constexpr uint32_t kGroupBytes = kSplitGroupChunks * B3_CHUNK_LEN;
+  const uint32_t glen = min(kGroupBytes, l - g * kGroupBytes);
+  QuadLane L;
+  L.init();
+  stage_message(stage, arena + off[m] + static_cast<uint64_t>(g) * kGroupBytes, glen);
+  __syncthreads();
+  const bool whole = G == 1;
+  uint32_t h0 = 0, h1 = 0;
+  quad_chunks(L, stage, glen, g * kSplitGroupChunks, whole, cvr, h0, h1);
+  const uint32_t k = n_chunks_of(glen);
+  if (!(whole && k == 1)) {
+    __syncthreads();
+    quad_tree(L, cvr, k, whole ? B3_ROOT : 0u, h0, h1);
+  }
+  if (!whole) {
+    // counters first (fixed place whatever n is: each stays zero between uses)
+    uint32_t* cnt = scratch;
+    uint32_t* cv = scratch + kSplitMaxMsgs + (static_cast<uint64_t>(m) * kSplitMaxGroups + g) * 8;
+    if (t < 4) {
+      __hip_atomic_store(cv + L.i, h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cv + 4 + L.i, h1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (t == 0) {
+      const uint32_t done =
+          __hip_atomic_fetch_add(cnt + m, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = done + 1 == G;
+      if (s_last) __hip_atomic_store(cnt + m, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;  // uniform
+    // the last group of the message: every group CV is published; fold them
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    const uint32_t* all = scratch + kSplitMaxMsgs + static_cast<uint64_t>(m) * kSplitMaxGroups * 8;
+    if (t < 8 * G) cvr[t] = __hip_atomic_load(all + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    quad_tree(L, cvr, G, B3_ROOT, h0, h1);
+  }
+  if (t < 4) {  // digest words i and 4 + i
+    if (L.i < out_words) o[L.i] = h0;
+    if (4 + L.i < out_words) o[4 + L.i] = h1;
   }
 }
 
@@ -813,18 +854,20 @@ hipError_t batch_hash_launch(const uint8_t* arena, uint64_t arena_bytes, const u
 
 namespace sdgpu {
 
-// One workgroup per message; max_chunks = the largest chunk count of the batch
-// (host-known), which sizes the workgroup.  Messages must be <= 1 MiB.
-hipError_t small_hash_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                             uint32_t n, uint32_t max_len, uint32_t max_chunks,
-                             uint32_t out_words, uint8_t* out, int32_t* status, hipStream_t s,
-                             KTimer* timer) {
+size_t small_split_scratch_bytes() {
+  return (kSplitMaxMsgs + static_cast<size_t>(kSplitMaxMsgs) * kSplitMaxGroups * 8) * 4;
+}
+
+hipError_t small_split_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                              uint32_t n, uint32_t max_len, uint32_t max_chunks,
+                              uint32_t out_words, uint8_t* out, int32_t* status, uint32_t* scratch,
+                              hipStream_t s, KTimer* timer) {
   if (n == 0) return hipSuccess;
-  if (max_chunks > kSmallMaxChunks) return hipErrorInvalidValue;
-  const uint32_t threads = std::max<uint32_t>(64, (max_chunks + 63) / 64 * 64);
-  KScope k(timer, "cas_small", s);
-  k_small<<<n, threads, 0, s>>>(arena, off, len, max_len, out_words,
-                                reinterpret_cast<uint32_t*>(out), status);
+  if (n > kSplitMaxMsgs || max_chunks > kSmallMaxChunks || !scratch) return hipErrorInvalidValue;
+  const uint32_t gmax = std::max<uint32_t>(1, (max_chunks + kSplitGroupChunks - 1) / kSplitGroupChunks);
+  KScope k(timer, "cas_small_split", s);
+  k_small_split<<<n * gmax, kSplitThreads, 0, s>>>(arena, off, len, max_len, gmax, out_words,
+                                                   reinterpret_cast<uint32_t*>(out), status, scratch);
   return hipGetLastError();
 }
 

@@ -143,6 +143,7 @@ struct sdgpu_ctx {
   hipStream_t last = nullptr;
   std::mutex mu;
   DevBuf batch_ws, tree_ws, dedup_ws, shard_ws, io_a, io_b, link_ws, stage_meta;
+  DevBuf small_ws;  // k_small_split's group CVs and per-message counters (zeroed once)
   DevBuf stage_slab[3];
   // host staging of the path / host-buffer entry points (identify_files,
   // cas_batch, generate_cas_id, checksum_files, file_checksum): pinned and
@@ -221,6 +222,17 @@ inline int ensure_dev(sdgpu_ctx* c, DevBuf& b, size_t bytes) {
   SD_TRY(hipMalloc(&b.p, want));
   b.cap = want;
   return 0;
+}
+
+// k_small_split's scratch: allocated and zeroed once per context (the kernel
+// leaves its counters zero), nullptr on failure.
+inline uint32_t* small_scratch(sdgpu_ctx* c, hipStream_t s) {
+  if (!c->small_ws.p) {
+    const size_t bytes = small_split_scratch_bytes();
+    if (ensure_dev(c, c->small_ws, bytes) != 0) return nullptr;
+    if (hipMemsetAsync(c->small_ws.p, 0, bytes, s) != hipSuccess) return nullptr;
+  }
+  return static_cast<uint32_t*>(c->small_ws.p);
 }
 
 // Grow-only device buffer that keeps its first `keep` bytes.

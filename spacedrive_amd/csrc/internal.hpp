@@ -58,14 +58,20 @@ hipError_t batch_hash_launch(const uint8_t* arena, uint64_t arena_bytes, const u
                              uint32_t out_words, uint8_t* out, int32_t* status,
                              const BatchWork& w, hipStream_t s, KTimer* timer = nullptr);
 
-// Latency path for a few messages of at most 1 MiB each: ONE launch, one
-// workgroup per message (thread per chunk, LDS tree).  max_chunks = largest
-// chunk count in the batch.  Same status / out semantics as batch_hash_launch.
+// Latency path for a few messages of at most 1 MiB each (SMALL_MAX_BYTES):
+// ONE launch.  max_chunks = largest chunk count in the batch.  Same status /
+// out semantics as batch_hash_launch.
 constexpr uint32_t SMALL_MAX_BYTES = 1024u * 1024u;
-hipError_t small_hash_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
-                             uint32_t n, uint32_t max_len, uint32_t max_chunks,
-                             uint32_t out_words, uint8_t* out, int32_t* status, hipStream_t s,
-                             KTimer* timer = nullptr);
+// Messages of <= SMALL_MAX_BYTES each (device or pinned host memory, 16-B
+// aligned offsets, readable up to the next 16 bytes), each split into 64 KiB groups hashed by one workgroup apiece and folded by
+// the message's last group: the latency path for messages above one CU's
+// worth of chunks; n <= 64.  scratch: small_split_scratch_bytes() device bytes
+// whose counters (the first 64 words) start zeroed (the kernel leaves them so).
+size_t small_split_scratch_bytes();
+hipError_t small_split_launch(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                              uint32_t n, uint32_t max_len, uint32_t max_chunks,
+                              uint32_t out_words, uint8_t* out, int32_t* status, uint32_t* scratch,
+                              hipStream_t s, KTimer* timer = nullptr);
 // A few messages of at most kHostStageMax bytes read straight from pinned
 // host memory (16-B aligned offsets; off / len in pinned memory too), one
 // workgroup each, digest words written straight to pinned host memory: the

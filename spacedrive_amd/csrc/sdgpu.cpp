@@ -234,9 +234,9 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     const uint64_t* d_off = reinterpret_cast<const uint64_t*>(db + L.off);
     const uint32_t* d_len = reinterpret_cast<const uint32_t*>(db + L.len);
     if (ok && !host1)
-      ok = (small ? small_hash_launch(db, d_off, d_len, cnt, kStageMaxMsg,
-                                      max_msg <= kChunkLen ? 1u : (max_msg + kChunkLen - 1) / kChunkLen,
-                                      2, db + L.out, nullptr, s, c->kt())
+      ok = (small ? small_split_launch(db, d_off, d_len, cnt, kStageMaxMsg,
+                                       max_msg <= kChunkLen ? 1u : (max_msg + kChunkLen - 1) / kChunkLen,
+                                       2, db + L.out, nullptr, small_scratch(c, s), s, c->kt())
                   : batch_hash_launch(db, L.arena_cap, d_off, d_len, cnt, kStageMaxMsg, 2,
                                       db + L.out, nullptr, w, s, c->kt())) == hipSuccess;
     if (!ok ||
@@ -898,41 +898,32 @@ int file_checksum_locked(sdgpu_ctx* c, const char* path, uint8_t digest[32]) {
     }
     if (!s) s = pick(c, nullptr);
     if (fstat(fd, &st) == 0 && static_cast<uint64_t>(st.st_size) <= SMALL_MAX_BYTES) {
-      // latency path: the whole file in one read, one copy, one launch (the
+      // latency path: the whole file in one read and one launch (the
       // reference's 1 MiB read loop, hash.rs:14-20, ends on the short read)
       const size_t cap = SMALL_MAX_BYTES;  // room for growth up to 1 MiB
       if ((rc = pipe_slot(c, 0, cap + 256))) break;
       uint8_t* hb = static_cast<uint8_t*>(hp[0].p);
       const int64_t got = read_whole_fd(fd, hb, cap);
       if (got >= 0) {
-        uint8_t* db = static_cast<uint8_t*>(c->pipe_d[0].p);
-        uint64_t* meta = reinterpret_cast<uint64_t*>(hb + cap);  // {off = 0, len}
-        meta[0] = 0;
-        meta[1] = static_cast<uint64_t>(got);
         const uint32_t nch = got <= 1024 ? 1u : static_cast<uint32_t>((got + 1023) / 1024);
-        if (static_cast<uint64_t>(got) <= kHostStageMax) {
-          // the whole file hashed from the pinned buffer, digest written back
-          // into it by the kernel: no copy commands
-          uint8_t* hout = hb + cap + 64;
-          uint64_t* hoff = reinterpret_cast<uint64_t*>(hb + cap + 128);  // {0}, then the length
-          hoff[0] = 0;
-          hoff[1] = static_cast<uint64_t>(got);
-          if (small_host_launch(hb, hoff, reinterpret_cast<const uint32_t*>(hoff + 1), 1,
-                                static_cast<uint32_t>(got), 8, hout, s, c->kt()) != hipSuccess ||
-              hipStreamSynchronize(s) != hipSuccess)
-            rc = -EIO;
-          else
-            memcpy(out.data(), hout, 32);
-          break;
-        }
-        if (hipMemcpyAsync(db, hb, static_cast<size_t>(got), hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(db + cap, hb + cap, 16, hipMemcpyHostToDevice, s) != hipSuccess ||
-            small_hash_launch(db, reinterpret_cast<const uint64_t*>(db + cap),
-                              reinterpret_cast<const uint32_t*>(db + cap + 8), 1, SMALL_MAX_BYTES,
-                              nch, 8, db + cap + 64, nullptr, s, c->kt()) != hipSuccess ||
-            hipMemcpyAsync(out.data(), db + cap + 64, 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
+        // the whole file hashed from the pinned buffer, digest written back
+        // into it by the kernel: no copy commands (<= 112 KiB: one workgroup;
+        // above: 64 KiB groups on as many workgroups, k_small_split)
+        uint8_t* hout = hb + cap + 64;
+        uint64_t* hoff = reinterpret_cast<uint64_t*>(hb + cap + 128);  // {0}, then the length
+        hoff[0] = 0;
+        hoff[1] = static_cast<uint64_t>(got);
+        const uint32_t* hlen = reinterpret_cast<const uint32_t*>(hoff + 1);
+        hipError_t e;
+        if (static_cast<uint64_t>(got) <= kHostStageMax)
+          e = small_host_launch(hb, hoff, hlen, 1, static_cast<uint32_t>(got), 8, hout, s, c->kt());
+        else
+          e = small_split_launch(hb, hoff, hlen, 1, SMALL_MAX_BYTES, nch, 8, hout, nullptr,
+                                 small_scratch(c, s), s, c->kt());
+        if (e != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
           rc = -EIO;
+        else
+          memcpy(out.data(), hout, 32);
         break;
       }
       if (got != -EFBIG) {

@@ -188,7 +188,7 @@ def test_device_api_workspace_guards(ctx):
 
 @pytest.mark.parametrize("n", [1, 3, 64])
 def test_small_batch_latency_kernel_bit_exact(ctx, n, tmp_path):
-    """Batches of <= 64 messages take the one-launch latency kernel (k_small):
+    """Batches of <= 64 messages take the one-launch latency kernel (k_small_host):
     every chunk-count shape up to 101 chunks, through sdgpu_cas_batch."""
     from spacedrive_amd import cas
     lens = _tree_edge_lengths()

@@ -117,7 +117,8 @@ def test_four_gib_file_bit_exact(ctx):
 @pytest.mark.parametrize("n", [2, 1023, 1025, 4096, 65537, (1 << 19) + 1, (1 << 20) - 1, 1 << 20,
                                (1 << 20) + 1])
 def test_file_checksum_latency_path_boundaries(ctx, tmp_path, n):
-    """Files up to 1 MiB take the one-launch k_small path; 1 MiB + 1 streams."""
+    """Files up to 1 MiB take the one-launch latency path (k_small_host up to
+    112 KiB, k_small_split above); 1 MiB + 1 streams."""
     from spacedrive_amd import validation
     p = tmp_path / "g.bin"
     data = np.random.default_rng(n + 3).integers(0, 256, n, dtype=np.uint8)

@@ -1,8 +1,9 @@
-"""GPU parity of the single-file latency kernel (k_small: one workgroup per
-message, a lane per chunk, the tree level by level in LDS): batches of <= 64
-cas messages (<= 102 408 B), single files through generate_cas_id and
-file_checksum up to 1 MiB (1024 chunks, the kernel's limit); checked
-bit-exact against the oracle."""
+"""GPU parity of the single-file latency kernels (k_small_host / k_service:
+one workgroup per message of <= 112 KiB; k_small_split: messages of <= 1 MiB
+in 64 KiB groups on as many workgroups; every compression spread over a quad
+of lanes, the tree level by level in LDS): batches of <= 64 cas messages
+(<= 102 408 B), single files through generate_cas_id and file_checksum up to
+1 MiB (1024 chunks, the limit); checked bit-exact against the oracle."""
 import os
 
 import numpy as np
@@ -143,4 +144,23 @@ def test_quad_tree_shapes(ctx, svc_ctx, tmp_path, service):
             p = os.path.join(tmp_path, f"q{n}")
             rng.integers(0, 256, n, dtype=np.uint8).tofile(p)
             assert validation.file_checksum(p, c) == O.file_checksum_path(p), (k, n)
+
+
+def test_split_group_shapes(ctx, tmp_path):
+    """file_checksum of files in (112 KiB, 1 MiB]: k_small_split hashes every
+    64 KiB group on its own workgroup and the message's last group folds the
+    group CVs -- 2..16 groups, a last group of 1 chunk (a lone chunk CV, no
+    parent), of a ragged chunk, of 63 / 64 chunks; repeated calls (the group
+    counters reset themselves)."""
+    from spacedrive_amd import validation
+    rng = np.random.default_rng(23)
+    G = 64 * 1024
+    sizes = [112 * 1024 + 1, 2 * G, 2 * G + 1, 2 * G + 1024, 2 * G + 1025, 3 * G - 1024, 3 * G - 1,
+             5 * G + 7, 8 * G, 9 * G + 1, 15 * G + 1024, 16 * G - 1, 16 * G]
+    for n in sizes:
+        p = os.path.join(tmp_path, f"g{n}")
+        rng.integers(0, 256, n, dtype=np.uint8).tofile(p)
+        want = O.file_checksum_path(p)
+        for _ in range(3):
+            assert validation.file_checksum(p, ctx) == want, n
 
