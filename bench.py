@@ -113,6 +113,12 @@ def k1_split(lens: np.ndarray):
     return leaves, blk + par - leaves
 
 
+# single-file latency sizes (the GPU / CPU crossover for the watcher callers,
+# include/sdgpu.h): one chunk chain, 16 / 32 / 64 KiB messages, a sampled file
+SINGLE_SIZES = (("4KiB", 4096), ("16KiB", 16384), ("32KiB", 32768), ("64KiB", 65536),
+                ("1MiB", 1 << 20))
+
+
 def pmc_traffic(kernel: str, section: str = "kernels"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/<round>/pmc_traffic.json, written by scripts/pmc_summary.py from
@@ -553,7 +559,7 @@ class Runner:
             for svc in (False, True):
                 self.ctx.latency_service(svc)
                 tag = "_service" if svc else ""
-                for name, size in (("4KiB", 4096), ("1MiB", 1 << 20)):
+                for name, size in SINGLE_SIZES:
                     p = os.path.join(root, name)
                     if not os.path.exists(p):
                         rng.integers(0, 256, size, dtype=np.uint8).tofile(p)
@@ -575,8 +581,7 @@ class Runner:
             cas.generate_cas_id(p4, 4096, self.ctx)
             res["service_breakdown_4KiB_cas"] = self.ctx.latency_service_diag()
             self.ctx.latency_service(False)
-            self._single_sample = [(os.path.join(root, n), s) for n, s in
-                                   (("4KiB", 4096), ("1MiB", 1 << 20))]
+            self._single_sample = [(os.path.join(root, n), s) for n, s in SINGLE_SIZES]
         finally:
             self._single_root = root
         return res
