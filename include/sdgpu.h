@@ -153,14 +153,13 @@ int sdgpu_combine_subtrees_device(sdgpu_ctx *ctx, const uint8_t *d_cvs, uint64_t
  * next call restarts it) and is stopped before any other call of the context
  * launches work.
  * Crossover for the watcher / non-indexed callers (MI355X, measured,
- * profiles/r3/latency): the workgroup hashes in quads of lanes (one
- * compression spread over 4 lanes), so a call costs ~25 us up to one chunk
- * chain (4 KiB: 24.8 us, of which ~13 us are the 16 + 3 dependent
- * compressions) and ~33 us for a sampled cas message (57 352 B); one CPU
- * thread of the AVX2 port needs 7.7 us for 4 KiB and 80 us for the sampled
- * message.  So: hash on the CPU below ~16 KiB of message, on the GPU above
- * (every file > 100 KiB for generate_cas_id; files > 16 KiB for
- * file_checksum, where 1 MiB takes 0.17 ms vs 1.4 ms). */
+ * profiles/r3/check_r3R_bench.json): the workgroup hashes in quads of lanes
+ * (one compression spread over 4 lanes); generate_cas_id through the service
+ * 23 / 25 / 28 / 35 us at 4 / 16 / 32 / 64 KiB and 32 us for a sampled file
+ * (57 352-B message), against 7.7 / 22 / 40 / 78 / 69 us on one CPU thread
+ * of the AVX2 port.  So: hash on the CPU below ~20 KiB of message, on the
+ * GPU above (every file > 100 KiB for generate_cas_id; files > 20 KiB for
+ * file_checksum, where 1 MiB takes 78 us vs 1.1 ms). */
 int sdgpu_latency_service(sdgpu_ctx *ctx, int enable);
 /* Path-based drop-in for file_checksum(path): streams the file in 64 MiB
  * power-of-two slices through double-buffered pinned memory; out_hex = 64
