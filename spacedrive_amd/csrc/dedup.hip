@@ -685,11 +685,25 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     uint32_t* wsum = fill;  // scratch for the 16 wave sums (LDS is full)
     const uint32_t j = part_block(), t = threadIdx.x, lane = __lane_id();
     const uint64_t nfine = static_cast<uint64_t>(gridDim.y) << kBits, b0 = static_cast<uint64_t>(c) << kBits;
-    uint32_t v[kPerT], sum = 0;
+    // every prologue load issued up front (clamped, selected at use): the
+    // bucket sizes, this block's starts inside them and the segment bounds
+    uint32_t v[kPerT], ov[kPerT], sum = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kPerT; ++k) {
-      const uint32_t b = t * kPerT + k;
-      v[k] = b < nbins ? ftot[b0 + b] : 0u;
+      const uint32_t b = min(t * kPerT + k, nbins - 1);
+      v[k] = ftot[b0 + b];
+      ov[k] = offs[j * nfine + b0 + b];
+    }
+    uint32_t seg_c = 0, seg_t0 = 0, seg_t1 = 0, seg_end = 0;
+    if (seg) {
+      seg_c = seg[static_cast<uint64_t>(c) * P1];
+      seg_t0 = seg[static_cast<uint64_t>(c) * P1 + min(P1, R * j)];
+      seg_t1 = seg[static_cast<uint64_t>(c) * P1 + min(P1, R * (j + 1))];
+      seg_end = seg[static_cast<uint64_t>(gridDim.y) * P1];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPerT; ++k) {
+      if (t * kPerT + k >= nbins) v[k] = 0u;
       sum += v[k];
     }
     uint32_t inc = sum;
@@ -700,7 +714,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     }
     if (lane == 63) wsum[t >> 6] = inc;
     __syncthreads();
-    uint32_t base = (seg ? seg[static_cast<uint64_t>(c) * P1] : 0u) + inc - sum, total = 0;
+    uint32_t base = seg_c + inc - sum, total = 0;
     for (uint32_t w = 0; w < kPartThreads / 64; ++w) {
       if (w < (t >> 6)) base += wsum[w];
       total += wsum[w];
@@ -710,17 +724,17 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
     for (uint32_t k = 0; k < kPerT; ++k) {
       const uint32_t b = t * kPerT + k;
       if (b < nbins) {
-        cur[b] = base + offs[j * nfine + b0 + b];
+        cur[b] = base + ov[k];
         fill[b] = 0;
         if (j == 0) fbase[b0 + b] = base;
       }
       base += v[k];
     }
     if (j == 0 && c == gridDim.y - 1 && t == 0)
-      fbase[nfine] = seg ? seg[static_cast<uint64_t>(gridDim.y) * P1] : total;
+      fbase[nfine] = seg ? seg_end : total;
     if (seg) {
-      t0 = seg[static_cast<uint64_t>(c) * P1 + min(P1, R * j)];
-      t1 = seg[static_cast<uint64_t>(c) * P1 + min(P1, R * (j + 1))];
+      t0 = seg_t0;
+      t1 = seg_t1;
     } else {
       tile_of(n, gridDim.x, t0, t1);
     }
@@ -869,8 +883,21 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
   RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
   const uint32_t c = blockIdx.y, j = part_block(), t = threadIdx.x, lane = __lane_id();
   const uint32_t nseg = gridDim.y;
+  const uint64_t nfine = static_cast<uint64_t>(nseg) << kB2, b0 = static_cast<uint64_t>(c) << kB2;
+  const uint32_t nr = R * max_rounds;
+  // Every prologue load is issued here, up front and unconditionally (clamped
+  // indices, values selected at use): their addresses are independent, so the
+  // block waits out ONE memory latency instead of four in a row (a block's
+  // prologue overlaps nothing else: one block per CU).
+  const uint32_t seg_v = segtot[min(t, nseg - 1)];
+  const uint32_t tr = min(t, nr - 1), cb = R * j + tr / max_rounds, rr = tr % max_rounds;
+  const uint64_t e = (static_cast<uint64_t>(min(cb, P1 - 1)) * max_rounds + rr) * kRunMaxBins + c;
+  const uint32_t len_v = run_len[e], st_v = run_start[e];
+  const uint32_t tb = min(t, nbins - 1);
+  const uint32_t ft_v = ftot[b0 + tb];
+  const uint32_t off_v = offs[static_cast<uint64_t>(j) * nfine + b0 + tb];
   if (t < 64) {  // this segment's start and the total, from the (<= 64) segment sizes
-    const uint32_t v = t < nseg ? segtot[t] : 0u;
+    const uint32_t v = t < nseg ? seg_v : 0u;
     uint32_t inc = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -881,16 +908,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
     if (t == 63) s_all = inc;
   }
   {  // the block's runs and their exclusive prefix (block scan)
-    const uint32_t nr = R * max_rounds;
-    uint32_t len = 0, st = 0;
-    if (t < nr) {
-      const uint32_t cb = R * j + t / max_rounds, rr = t % max_rounds;
-      if (cb < P1) {
-        const uint64_t e = (static_cast<uint64_t>(cb) * max_rounds + rr) * kRunMaxBins + c;
-        len = run_len[e];
-        st = run_start[e];
-      }
-    }
+    const bool has = t < nr && cb < P1;
+    const uint32_t len = has ? len_v : 0u, st = has ? st_v : 0u;
     uint32_t inc = len;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -906,10 +925,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
   }
   __syncthreads();  // s_segbase, wsum reused below
   {  // bucket starts: segment start + the segment's bucket sizes scanned
-    constexpr uint32_t kPerT = 1;
     static_assert(nbins <= kPartThreads, "one bucket per thread");
-    const uint64_t nfine = static_cast<uint64_t>(nseg) << kB2, b0 = static_cast<uint64_t>(c) << kB2;
-    const uint32_t v = t < nbins ? ftot[b0 + t] : 0u;
+    const uint32_t v = t < nbins ? ft_v : 0u;
     uint32_t inc = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -920,9 +937,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
     __syncthreads();
     uint32_t base = s_segbase + inc - v;
     for (uint32_t w = 0; w < (t >> 6); ++w) base += wsum[w];
-    (void)kPerT;
     if (t < nbins) {
-      cur[t] = base + offs[static_cast<uint64_t>(j) * nfine + b0 + t];
+      cur[t] = base + off_v;
       fill[t] = 0;
       if (j == 0) fbase[b0 + t] = base;
     }
@@ -1024,12 +1040,17 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_ws(
   // bucket starts: the segment's sizes scanned here, block 0 publishes them
   constexpr uint32_t kPerT = nbins / kPartThreads;
   const uint32_t t = threadIdx.x, lane = __lane_id();
-  uint32_t v[kPerT], sum = 0;
+  const uint32_t j = part_block();
+  // the block's starts inside its buckets loaded with the bucket sizes (one
+  // memory latency for both, not one after the other around the scan)
+  uint32_t v[kPerT], ov[kPerT], sum = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kPerT; ++k) {
     v[k] = ftot[t * kPerT + k];
-    sum += v[k];
+    ov[k] = offs[static_cast<uint64_t>(j) * nbins + t * kPerT + k];
   }
+#pragma unroll
+  for (uint32_t k = 0; k < kPerT; ++k) sum += v[k];
   uint32_t inc = sum;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -1044,11 +1065,10 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_ws(
     total += fill[w];
   }
   __syncthreads();
-  const uint32_t j = part_block();
 #pragma unroll
   for (uint32_t k = 0; k < kPerT; ++k) {
     const uint32_t b = t * kPerT + k;
-    cur[b] = base + offs[static_cast<uint64_t>(j) * nbins + b];
+    cur[b] = base + ov[k];
     fill[b] = 0;
     if (j == 0) fbase[b] = base;
     base += v[k];
