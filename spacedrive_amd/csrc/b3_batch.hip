@@ -754,8 +754,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_small_split(
 constexpr uint32_t kSvcThreads = 256;
 static_assert(kSvcThreads / 4 >= kHostStageChunks / 2, "one quad per parent of the first tree level");
 
-__global__ __launch_bounds__(kSvcThreads) void k_service(SvcMailbox* __restrict__ mb,
-                                                         const uint8_t* __restrict__ msg,
+// mb and msg carry no const / __restrict__: the host rewrites both between
+// requests within one kernel lifetime, so their loads must not be treated as
+// invariant (hoisted or merged across loop iterations).
+__global__ __launch_bounds__(kSvcThreads) void k_service(SvcMailbox* mb, uint8_t* msg,
                                                          uint32_t last_seq, uint64_t idle_ticks,
                                                          uint64_t life_ticks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
@@ -921,7 +923,8 @@ hipError_t service_launch(SvcMailbox* mb, const uint8_t* msg, uint32_t last_seq,
     if (e != hipSuccess) return e;
     attr_set.fetch_or(bit, std::memory_order_release);
   }
-  k_service<<<1, kSvcThreads, kHostStageMax + 16, s>>>(mb, msg, last_seq, idle_ticks, life_ticks);
+  k_service<<<1, kSvcThreads, kHostStageMax + 16, s>>>(mb, const_cast<uint8_t*>(msg), last_seq,
+                                                        idle_ticks, life_ticks);
   return hipGetLastError();
 }
 

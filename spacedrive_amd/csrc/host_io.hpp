@@ -113,7 +113,7 @@ inline int64_t read_cas_message(const char* path, uint64_t size, uint8_t* dst, s
 
 
 // CPUs' worth of time the process may use: cgroup v2 cpu.max ("max" or
-// "<quota> <period>"), 0 when unlimited or unreadable.
+// "<quota> <period>"), rounded up (at least 1); 0 when unlimited or unreadable.
 inline uint32_t cgroup_cpus() {
   FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r");
   if (!f) return 0;
@@ -122,7 +122,9 @@ inline uint32_t cgroup_cpus() {
   const int got = fscanf(f, "%31s %llu", q, &period);
   fclose(f);
   if (got != 2 || period == 0 || q[0] < '0' || q[0] > '9') return 0;
-  return static_cast<uint32_t>(strtoull(q, nullptr, 10) / period);
+  // a fractional quota below one CPU still allows one (0 means unlimited)
+  const unsigned long long quota = strtoull(q, nullptr, 10);
+  return static_cast<uint32_t>(std::max(1ull, (quota + period - 1) / period));
 }
 
 // File-read threads: SDGPU_IO_THREADS if set, else min(16, hardware threads,

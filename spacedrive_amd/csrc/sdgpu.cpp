@@ -586,9 +586,11 @@ int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t*
             jobs[m] = uring::FileJob{paths[i], size[i], hb + off[j], static_cast<size_t>(cap), 0};
             idx[m++] = j;
           }
-          if (ring_ok)
-            uring::read_cas_batch(ring, jobs, m);
-          else
+          if (ring_ok) {
+            // false: the ring failed (the batch finished through pread or -EIO)
+            // and was closed; this thread reads with pread from now on
+            if (!uring::read_cas_batch(ring, jobs, m)) ring_ok = 0;
+          } else
             for (uint32_t k = 0; k < m; ++k)
               jobs[k].result = read_cas_message(jobs[k].path, jobs[k].size, jobs[k].dst, jobs[k].cap);
           for (uint32_t k = 0; k < m; ++k) settle(idx[k], jobs[k].result);

@@ -127,12 +127,14 @@ class Ring {
     return s;
   }
 
-  // Submits every prepared SQE and waits for `wait` completions.
-  int submit_and_wait(unsigned wait) {
+  // Publishes every prepared SQE and submits them, waiting for `wait`
+  // completions.  `submitted` = the SQEs the kernel consumed (each will post
+  // exactly one CQE: NODROP, no CQE-skip flags), also when an error is returned.
+  int submit_and_wait(unsigned wait, unsigned& submitted) {
     const uint32_t tail = local_tail_;
     const unsigned n = tail - sq_tail_->load(std::memory_order_relaxed);
     sq_tail_->store(tail, std::memory_order_release);
-    unsigned submitted = 0;
+    submitted = 0;
     for (;;) {
       const int r = sys_enter(fd_, n - submitted, wait, IORING_ENTER_GETEVENTS);
       if (r < 0) {
@@ -145,19 +147,51 @@ class Ring {
     }
   }
 
-  // Completions available now, or wait for at least one.
+  // Tests only: publishes the prepared SQEs, submits just the first k of
+  // them, and reports -EBUSY, as a submission that fails part-way would.
+  int submit_partial(unsigned k, unsigned& submitted) {
+    const uint32_t tail = local_tail_;
+    const unsigned n = std::min<unsigned>(k, tail - sq_tail_->load(std::memory_order_relaxed));
+    sq_tail_->store(tail, std::memory_order_release);
+    submitted = 0;
+    while (submitted < n) {
+      const int r = sys_enter(fd_, n - submitted, 0, 0);
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        return -errno;
+      }
+      submitted += static_cast<unsigned>(r);
+    }
+    return -EBUSY;
+  }
+
+  // Withdraws every SQE the kernel has not consumed (prepared, or published
+  // but not yet submitted).  Without SQPOLL the kernel reads the SQ only
+  // inside io_uring_enter, so sq_head is stable here.
+  void retract() {
+    const uint32_t head = sq_head_->load(std::memory_order_acquire);
+    sq_tail_->store(head, std::memory_order_release);
+    local_tail_ = head;
+  }
+
+  // Reaps `want` completions, waiting as needed.  A failing wait is retried a
+  // bounded number of times (EINTR does not count); -errno when it persists.
   template <typename F>
   int reap(unsigned want, F&& on_cqe) {
-    unsigned got = 0;
+    unsigned got = 0, fails = 0;
     while (got < want) {
       uint32_t head = cq_head_->load(std::memory_order_relaxed);
       const uint32_t tail = cq_tail_->load(std::memory_order_acquire);
       if (head == tail) {
         const int r = sys_enter(fd_, 0, 1, IORING_ENTER_GETEVENTS);
-        if (r < 0 && errno != EINTR) return -errno;
+        if (r < 0 && errno != EINTR) {
+          const int e = errno;
+          if (++fails > 64) return -e;
+          usleep(100);
+        }
         continue;
       }
-      for (; head != tail; ++head, ++got) {
+      for (; head != tail && got < want; ++head, ++got) {
         const io_uring_cqe& c = cqes_[head & cq_mask_];
         on_cqe(c.user_data, c.res);
       }
@@ -193,12 +227,22 @@ struct FileJob {
 
 // The cas messages of `n` files through one ring: batches of kBatchFiles.
 // Exactly read_cas_message's bytes and statuses (slow path for anything odd).
-inline void read_cas_batch(Ring& ring, FileJob* f, uint32_t n) {
+//
+// Error model: every SQE the kernel consumed is reaped before any
+// pread fallback touches a file's buffer, SQEs it did not consume are
+// withdrawn, and the statx targets live in thread-local storage, not on this
+// frame.  On a ring error the function finishes the call with pread and
+// returns false: the caller must stop using this ring (it is closed here).
+// If even the drain fails (the kernel would not hand back completions that it
+// owes), the files of the batch and the rest get -EIO instead of a pread into
+// buffers a late READ could still overwrite.  `fail_after` (tests only): the
+// submission reports -EBUSY after that many SQEs of the first batch.
+inline bool read_cas_batch(Ring& ring, FileJob* f, uint32_t n, int fail_after = -1) {
   struct Slot {
     int32_t res[9];
     struct statx sx;
   };
-  Slot slots[kBatchFiles];
+  thread_local Slot slots[kBatchFiles];
   for (uint32_t b0 = 0; b0 < n; b0 += kBatchFiles) {
     const uint32_t nb = std::min(kBatchFiles, n - b0);
     unsigned nsqe = 0;
@@ -253,51 +297,81 @@ inline void read_cas_batch(Ring& ring, FileJob* f, uint32_t n) {
           rd(1 + k, j.dst + 8 + hf + k * ss, ss, hf + k * jump, true);
         rd(5, j.dst + 8 + hf + 4 * ss, hf, j.size - hf, true);  // footer at the STAT size
       }
+      if (!ok) break;
       io_uring_sqe* c = sqe(kOpClose);
       if (!c) break;
       c->opcode = IORING_OP_CLOSE;
       c->file_index = s + 1;
-      if (sampled) {  // confirms the actual end == stat size (SeekFrom::End)
-        io_uring_sqe* x = sqe(kOpStatx);
-        if (!x) break;
-        x->opcode = IORING_OP_STATX;
-        x->fd = AT_FDCWD;
-        x->addr = reinterpret_cast<uint64_t>(j.path);
-        x->len = STATX_SIZE;
-        x->off = reinterpret_cast<uint64_t>(&sl.sx);
-      }
+      // sampled: confirms the actual end == stat size (SeekFrom::End); whole
+      // reads: confirms the one READ reached the end (a short read from FUSE,
+      // NFS or a signal must not pass for the whole file: ADVICE r3)
+      io_uring_sqe* x = sqe(kOpStatx);
+      if (!x) break;
+      x->opcode = IORING_OP_STATX;
+      x->fd = AT_FDCWD;
+      x->addr = reinterpret_cast<uint64_t>(j.path);
+      x->len = STATX_SIZE;
+      x->off = reinterpret_cast<uint64_t>(&sl.sx);
     }
-    int rc = ok && nsqe ? ring.submit_and_wait(nsqe) : (ok ? 0 : -ENOSPC);
-    if (rc == 0 && nsqe)
-      rc = ring.reap(nsqe, [&](uint64_t ud, int32_t res) {
+    unsigned submitted = 0;
+    int rc;
+    if (!ok) {
+      ring.retract();  // the ring was not empty: nothing of this batch went out
+      rc = -ENOSPC;
+    } else if (nsqe == 0) {
+      rc = 0;
+    } else if (fail_after >= 0 && b0 == 0) {
+      rc = ring.submit_partial(static_cast<unsigned>(fail_after), submitted);  // -EBUSY
+      ring.retract();
+    } else {
+      rc = ring.submit_and_wait(nsqe, submitted);
+      if (rc != 0) ring.retract();  // withdraw what the kernel did not take
+    }
+    // every consumed SQE posts one CQE: reap them all before any buffer of
+    // this batch is touched again (statx targets are thread-local)
+    int drain = 0;
+    if (submitted)
+      drain = ring.reap(submitted, [&](uint64_t ud, int32_t res) {
         slots[ud & 0xFF].res[(ud >> 8) & 0xFF] = res;
       });
+    if (drain != 0) {
+      // completions owed by the kernel never came: a READ may still land in
+      // these buffers, so no file of this call is read into them
+      for (uint32_t s = b0; s < n; ++s)
+        if (s >= b0 + nb || f[s].result == INT64_MIN) f[s].result = -EIO;
+      ring.close_ring();
+      return false;
+    }
     for (uint32_t s = 0; s < nb; ++s) {
       FileJob& j = f[b0 + s];
       if (j.result != INT64_MIN) continue;  // set above (-ENOBUFS)
       const Slot& sl = slots[s];
-      bool fast = rc == 0 && sl.res[kOpOpen] >= 0;
+      bool fast = rc == 0 && sl.res[kOpOpen] >= 0 && sl.res[kOpStatx] == 0;
       const uint64_t hf = SDGPU_CAS_HEADER_OR_FOOTER_SIZE, ss = SDGPU_CAS_SAMPLE_SIZE;
       if (fast && j.size <= SDGPU_CAS_MINIMUM_FILE_SIZE) {
         const int32_t got = sl.res[kOpRead0];
-        // a full reservation may hide growth: the slow path decides
-        fast = got >= 0 && static_cast<size_t>(got) < j.cap - 8;
+        // a full reservation may hide growth, and a read shorter than the
+        // file may be a short read: the slow path decides both
+        fast = got >= 0 && static_cast<size_t>(got) < j.cap - 8 &&
+               static_cast<uint64_t>(got) == sl.sx.stx_size;
         if (fast) j.result = 8 + got;
       } else if (fast) {
         fast = sl.res[kOpRead0] == static_cast<int32_t>(hf) && sl.res[kOpRead0 + 5] == static_cast<int32_t>(hf) &&
-               sl.res[kOpStatx] == 0 && sl.sx.stx_size == j.size;
+               sl.sx.stx_size == j.size;
         for (uint32_t k = 0; k < SDGPU_CAS_SAMPLE_COUNT && fast; ++k)
           fast = sl.res[kOpRead0 + 1 + k] == static_cast<int32_t>(ss);
         if (fast) j.result = SDGPU_CAS_SAMPLED_MSG_LEN;
       }
       if (!fast) j.result = hostio::read_cas_message(j.path, j.size, j.dst, j.cap);
     }
-    if (rc != 0) {  // the ring failed as a whole: the rest through pread
+    if (rc != 0) {  // the ring failed: the rest through pread, and no more ring
       for (uint32_t s = b0 + nb; s < n; ++s)
         f[s].result = hostio::read_cas_message(f[s].path, f[s].size, f[s].dst, f[s].cap);
-      return;
+      ring.close_ring();
+      return false;
     }
   }
+  return true;
 }
 
 }  // namespace uring

@@ -124,7 +124,8 @@ static void test_uring_reads() {
     b.emplace_back(cap, 0);
     jobs.push_back(uring::FileJob{paths[i].c_str(), s, b.back().data(), cap, 0});
   }
-  uring::read_cas_batch(ring, jobs.data(), static_cast<uint32_t>(jobs.size()));
+  CHECK(uring::read_cas_batch(ring, jobs.data(), static_cast<uint32_t>(jobs.size())),
+        "uring batch failed");
   for (size_t i = 0; i < paths.size(); ++i) {
     const int64_t want = hostio::read_cas_message(paths[i].c_str(), jobs[i].size, a[i].data(),
                                                   a[i].size());
@@ -132,6 +133,28 @@ static void test_uring_reads() {
           (long long)jobs[i].result, (long long)want);
     if (want > 0) CHECK(memcmp(a[i].data(), b[i].data(), want) == 0, "uring bytes %s",
                         paths[i].c_str());
+  }
+  // a submission that fails part-way (injected -EBUSY after k SQEs
+  // of the first batch) drains what the kernel took, withdraws the rest,
+  // finishes every file through pread with the same bytes and statuses, and
+  // reports the ring as unusable (closed)
+  for (int k : {0, 1, 5, 17, 63}) {
+    uring::Ring r2;
+    CHECK(r2.open_ring(), "second ring");
+    for (size_t i = 0; i < paths.size(); ++i) {
+      std::fill(b[i].begin(), b[i].end(), 0xA5);
+      jobs[i].result = 0;
+    }
+    const bool ok = uring::read_cas_batch(r2, jobs.data(), static_cast<uint32_t>(jobs.size()), k);
+    CHECK(!ok, "injected failure after %d SQEs not reported", k);
+    for (size_t i = 0; i < paths.size(); ++i) {
+      const int64_t want = hostio::read_cas_message(paths[i].c_str(), jobs[i].size, a[i].data(),
+                                                    a[i].size());
+      CHECK(jobs[i].result == want, "uring fail@%d %s: %lld vs %lld", k, paths[i].c_str(),
+            (long long)jobs[i].result, (long long)want);
+      if (want > 0) CHECK(memcmp(a[i].data(), b[i].data(), want) == 0, "uring fail@%d bytes %s",
+                          k, paths[i].c_str());
+    }
   }
 }
 

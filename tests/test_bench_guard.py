@@ -120,17 +120,21 @@ def test_hanging_leg_hits_the_deadline():
 def test_failed_headline_still_prints_a_line():
     p, lines, _ = _run("cas_raises")
     assert len(lines) == 1, p.stdout
+    assert p.returncode == 3
     d = json.loads(lines[0])
     assert d["value"] is None and "injected K1" in d["components"]["cas"]["error"]
     assert d["components"]["checksum"]["value"] == 3100.0
 
 
-def test_failed_exchange_keeps_a_cas_headline():
+def test_failed_exchange_has_no_headline():
     """The identifier step's exchange fails (e.g. -ETIMEDOUT from a dead peer):
-    the line reports K1's cas_id rate as value, says so, and keeps roofline."""
+    the line carries NO headline value (K1 alone is a faster subset of the
+    step), keeps K1's rate under components.cas and the roofline,
+    and the process exits non-zero."""
     p, lines, _ = _run("job_fails")
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode == 3, p.stderr[-3000:]
     d = json.loads(lines[0])
-    assert d["value"] == 7.5e7 and "job step failed" in d["headline_note"]
+    assert d["value"] is None and "job step failed" in d["headline_note"]
+    assert d["components"]["cas"]["value"] == 7.5e7
     assert "timed out" in d["components"]["identifier_job"]["error"]
     assert d["roofline"]["bound"] == "valu" and d["cpu_baseline"]["kind"] == "port"

@@ -170,6 +170,13 @@ def test_config4_100m_rows_one_gpu_and_8_ranks(ctx, ctxs):
     ref = O.group_reps(hk, hh, 100)
     np.testing.assert_array_equal(rep1.cpu().numpy().view(np.uint32), ref)
     del rep1
+    # the variant bench.py times (config4_full_one_gpu): no rank array, so
+    # 12-byte records through k_part_private -> k_part2_runs -> k_bucket_group12_pk
+    # at 2^15 buckets
+    rep0 = ops.group_rows(key, has, None, 100, 0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(rep0.cpu().numpy().view(np.uint32), ref)
+    del rep0
     comms = dedup.Comm.init_all(ctxs)
     per = total // 8
     reps = dedup.group_sharded_all([key[r * per:(r + 1) * per] for r in range(8)],
