@@ -8,8 +8,8 @@
 //   group:   G0 product k_bucket_group12_pk | G1 no rep writes | G2 loads only
 // Only H0/S0/G0 produce the product's result (checked); the others are
 // timing probes.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_bound.hip -o build/exp_bound
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_bound.hip -o build/exp_bound
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

@@ -11,11 +11,11 @@
 //   idle      the chain alone on the device
 //   loaded    the same while every other CU runs a VALU spin kernel
 // and the same chain with each compression spread over a quad of lanes.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_chain.hip -o build/exp_chain
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_chain.hip -o build/exp_chain
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
-#include "../spacedrive_amd/csrc/b3_device.hpp"
+#include "../../spacedrive_amd/csrc/b3_device.hpp"
 
 using namespace sdgpu;
 

@@ -1,7 +1,7 @@
 // Experiment: BLAKE3 compressions per second with everything in registers (no
 // memory), i.e. the compute roof of the exact instruction stream K1/K2 issue,
 // plus the shader clock under that load (s_memtime vs s_memrealtime @100 MHz).
-// Build: hipcc --offload-arch=gfx950 -O3 -I spacedrive_amd/csrc scripts/exp_compress.hip -o build/exp_compress
+// Build: hipcc --offload-arch=gfx950 -O3 -I spacedrive_amd/csrc scripts/exp/exp_compress.hip -o build/exp_compress
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

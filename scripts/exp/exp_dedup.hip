@@ -4,7 +4,7 @@
 //   S1: LDS cursor atomics only (stores to the thread's own sequential slot)
 //   S2: scattered 16-B stores to a hash position, no LDS atomics
 //   S3: scattered 4-B stores (rep-like)
-// Build: hipcc --offload-arch=gfx950 -O3 scripts/exp_dedup.hip -o build/exp_dedup
+// Build: hipcc --offload-arch=gfx950 -O3 scripts/exp/exp_dedup.hip -o build/exp_dedup
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -1,6 +1,6 @@
 """Per-kernel device times of the one-GPU grouping at several table sizes
 (config-4 rows; HIP events on the launch stream).  Usage:
-python scripts/exp_dedup_kernels.py 12500000 100000000"""
+python scripts/exp/exp_dedup_kernels.py 12500000 100000000"""
 import json
 import os
 import sys

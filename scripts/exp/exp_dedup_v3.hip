@@ -11,8 +11,8 @@
 // Result (profiles/r2/exp_dedup_v3_r2C.log): V1 0.311-0.314 vs V0 0.316-0.322 ms
 // -- the device atomics and the memset cost about what the scan did; not
 // adopted.  The histogram alone runs 0.027 ms (4.2 TB/s), at its load floor.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_dedup_v3.hip -o build/exp_dedup_v3
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_dedup_v3.hip -o build/exp_dedup_v3
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

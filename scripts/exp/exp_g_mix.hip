@@ -7,7 +7,7 @@
 //   V2  one of the two add3 split (13 VALU, 5 VOP3 : 8 VOP2)
 //   V3  rotr 16 / rotr 8 as v_perm_b32 byte permutes instead of v_alignbit_b32
 // Each line: compressions/s and VALU lane-ops/s (instructions x 64 lanes).
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_g_mix.hip -o build/exp_g_mix
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_g_mix.hip -o build/exp_g_mix
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -7,8 +7,8 @@
 //   G2  two 512-thread workgroups per bucket, each grouping the half of the
 //       bucket's keys selected by hash bit 32 in a 3072-slot table (4 per CU);
 //       both read the whole bucket (the second from L2: same XCD)
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_group.hip -o build/exp_group
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_group.hip -o build/exp_group
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

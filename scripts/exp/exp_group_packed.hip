@@ -11,8 +11,8 @@
 //   GK16 packed, 16384 slots (128 KiB), load ~0.19, 1 WG/CU
 // Records from the product partition (12.5 M config-4-shaped rows, rank order:
 // 12-byte records); reps must equal the product's.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_group_packed.hip -o build/exp_group_packed
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_group_packed.hip -o build/exp_group_packed
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

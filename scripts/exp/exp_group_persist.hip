@@ -13,8 +13,8 @@
 //        first empty-or-equal one (fewer probe rounds, more registers)
 //   GD   double hashing instead of linear probing (shorter longest chains)
 // On the product's own records: 12.5 M rows (one-level) and 100 M rows (two-level).
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_group_persist.hip -o build/exp_group_persist
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_group_persist.hip -o build/exp_group_persist
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

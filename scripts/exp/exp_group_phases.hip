@@ -8,8 +8,8 @@
 //   E  D + rep writes (the product kernel)
 // plus E with 512 threads per workgroup (same table, 4 workgroups per CU
 // impossible at 72 KiB, so 2) to see the per-thread row count effect.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_group_phases.hip -o build/exp_group_phases
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_group_phases.hip -o build/exp_group_phases
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

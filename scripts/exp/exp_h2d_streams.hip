@@ -2,7 +2,7 @@
 // copy streams in flight (256 MiB pieces of a 4 GiB pinned buffer), to see
 // whether more SDMA engines than the staging ring's one copy stream raise the
 // config-5 bound.  Also D2H and a 64 MiB piece size.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_h2d_streams.hip -o build/exp_h2d_streams
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_h2d_streams.hip -o build/exp_h2d_streams
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 

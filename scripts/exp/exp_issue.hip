@@ -4,7 +4,7 @@
 // mixed stream?  Each mode is a 16-instruction inline-asm block over 8
 // independent registers, looped; throughput in T lane-instr/s at
 // 8 and 1 waves/SIMD.
-// Build: hipcc --offload-arch=gfx950 -O3 scripts/exp_issue.hip -o build/exp_issue
+// Build: hipcc --offload-arch=gfx950 -O3 scripts/exp/exp_issue.hip -o build/exp_issue
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

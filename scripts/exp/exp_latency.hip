@@ -5,7 +5,7 @@
 // (zero-copy, one 16-B load per lane) and writing 32 B to pinned memory + sync;
 // the same with the host spinning on a flag the kernel writes instead of the
 // stream sync.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_latency.hip -o build/exp_latency
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_latency.hip -o build/exp_latency
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

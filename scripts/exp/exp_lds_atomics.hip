@@ -10,7 +10,7 @@
 //   min32     ds_min_u32 (no return)
 //   read64    ds_read_b64
 //   cas64_dep ds_cmpst_rtn_b64 with each result feeding the next address
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_lds_atomics.hip -o build/exp_lds_atomics
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_lds_atomics.hip -o build/exp_lds_atomics
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -3,7 +3,7 @@
 // the library's pool (16 threads) into: (a) one hipHostMalloc'd buffer, (b)
 // one malloc'd buffer (pre-faulted), (c) malloc'd + hipHostRegister'ed, (d)
 // per-thread 128 KiB bounce buffers (what the CPU port does).  Median of 9.
-// Build: hipcc -O2 -std=c++17 scripts/exp_read_dest.cpp -o build/exp_read_dest
+// Build: hipcc -O2 -std=c++17 scripts/exp/exp_read_dest.cpp -o build/exp_read_dest
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -14,8 +14,8 @@
 #include <string>
 #include <vector>
 
-#include "../include/sdgpu.h"
-#include "../spacedrive_amd/csrc/host_io.hpp"
+#include "../../include/sdgpu.h"
+#include "../../spacedrive_amd/csrc/host_io.hpp"
 
 using namespace sdgpu;
 

@@ -1,7 +1,7 @@
 // Experiment (not shipped): config-1 reads into memory pinned by a given HIP
 // runtime (dlopen'ed: /opt/rocm's or the one torch bundles), against malloc'd
 // memory; the same reads as exp_read_dest.cpp.  Host-only build:
-//   g++ -O2 -std=c++17 scripts/exp_read_dest_dl.cpp -ldl -lpthread -o build/exp_read_dest_dl
+//   g++ -O2 -std=c++17 scripts/exp/exp_read_dest_dl.cpp -ldl -lpthread -o build/exp_read_dest_dl
 #include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -12,7 +12,7 @@
 #include <string>
 #include <vector>
 
-#include "../spacedrive_amd/csrc/host_io.hpp"
+#include "../../spacedrive_amd/csrc/host_io.hpp"
 
 using namespace sdgpu;
 

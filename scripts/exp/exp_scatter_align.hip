@@ -18,8 +18,8 @@
 //   P0  product: 12-B records, staged 24-B pairs, k_bucket_group12
 //   PK  product scatter + the packed-table group kernel (12-B records)
 //   A2  aligned 16-B pairs + packed-table group kernel over 16-B records
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_scatter_align.hip -o build/exp_scatter_align
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_scatter_align.hip -o build/exp_scatter_align
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

@@ -3,8 +3,8 @@
 // round): fewer, wider partial-line writes (more slots) against more buckets.
 // Each variant: its own histogram + scan once, then the scatter timed alone
 // (median of 9); records checked by a per-variant checksum.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_scatter_slots.hip -o build/exp_scatter_slots
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_scatter_slots.hip -o build/exp_scatter_slots
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

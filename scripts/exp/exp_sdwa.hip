@@ -1,6 +1,6 @@
 // Experiment: rotr(d ^ a, 16) via two VOP2 SDWA xors vs v_xor + v_alignbit.
 // Checks correctness (with/without s_nop padding) and times each form.
-// Build: hipcc --offload-arch=gfx950 -O3 scripts/exp_sdwa.hip -o build/exp_sdwa
+// Build: hipcc --offload-arch=gfx950 -O3 scripts/exp/exp_sdwa.hip -o build/exp_sdwa
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>

@@ -1,7 +1,7 @@
 /* Experiment (not shipped): single-file call latency from a C host (no Python):
  * open+read+close alone, sdgpu_generate_cas_id, sdgpu_file_checksum on a 4 KiB
  * and a 1 MiB file; median of 2000 calls each.
- * Build: gcc -O2 -Iinclude scripts/exp_single_latency.c -Lspacedrive_amd -lsdgpu
+ * Build: gcc -O2 -Iinclude scripts/exp/exp_single_latency.c -Lspacedrive_amd -lsdgpu
  *        -Wl,-rpath,$PWD/spacedrive_amd -o build/exp_single_latency */
 #include <fcntl.h>
 #include <stdio.h>

@@ -10,7 +10,7 @@
 //      min rank found by walking back/forward over equal keys (segments are
 //      ~1.25 rows), rep scattered to the row's original position.
 // Each timed over 20 launches with HIP events; prints ms per call and rows/s.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_sort_groupby.hip -o build/exp_sort_groupby
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_sort_groupby.hip -o build/exp_sort_groupby
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>

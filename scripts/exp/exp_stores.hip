@@ -11,7 +11,7 @@
 //   W8L runs of 8, eight adjacent lanes
 //   W16L runs of 16
 //   A2L runs of 2 16-byte records (32-B aligned pairs), two lanes
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_stores.hip -o build/exp_stores
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_stores.hip -o build/exp_stores
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

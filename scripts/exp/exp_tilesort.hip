@@ -14,8 +14,8 @@
 // No histogram pass and no cross-block offsets; the scattered accesses move from
 // pair STORES in the partition to short-run LOADS in the group kernel.
 // Records / reps must equal the product's (dedup_local_launch).
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_tilesort.hip -o build/exp_tilesort
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_tilesort.hip -o build/exp_tilesort
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

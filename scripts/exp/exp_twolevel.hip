@@ -2,8 +2,8 @@
 // buckets): digit split and second-pass block count.  The A/B that retired the
 // second pass's histogram kernel (hist2 5+10/8 3.40 ms -> fine counts 6+9/16
 // 2.94 ms) ran against the removed variant: profiles/r2/exp_twolevel_r2E.log.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_twolevel.hip -o build/exp_twolevel
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_twolevel.hip -o build/exp_twolevel
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

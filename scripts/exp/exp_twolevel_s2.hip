@@ -11,8 +11,8 @@
 // 8-record runs halve the staging LDS (two blocks per CU) at the cost of
 // shorter store runs; more blocks per segment shorten each block.
 // Every variant's reps must equal the product's (dedup_local_launch).
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_twolevel_s2.hip -o build/exp_twolevel_s2
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_twolevel_s2.hip -o build/exp_twolevel_s2
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

@@ -2,7 +2,7 @@
 // 3 parents) reading (a) a 40 GiB HBM buffer (lanes 4 KiB apart, as in K1),
 // (b) the same addresses folded into a 256 KiB L2-resident window, and
 // (c) no loads at all.  Reports compressions/s and the in-kernel clock.
-// Build: hipcc --offload-arch=gfx950 -O3 -I spacedrive_amd/csrc scripts/exp_units.hip -o build/exp_units
+// Build: hipcc --offload-arch=gfx950 -O3 -I spacedrive_amd/csrc scripts/exp/exp_units.hip -o build/exp_units
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -2,7 +2,7 @@
 // (host_io.hpp read_cas_message, ~9 syscalls per sampled file) against batched
 // io_uring chains (csrc/uring.hpp), over the config-1 directory, warm page
 // cache, T threads each with its own ring.  Checks the bytes are identical.
-// Build: g++ -O2 -std=c++17 -pthread scripts/exp_uring.cpp -o build/exp_uring
+// Build: g++ -O2 -std=c++17 -pthread scripts/exp/exp_uring.cpp -o build/exp_uring
 // Run:   build/exp_uring <listing: "size path" lines> <threads> <reps>
 #include <chrono>
 #include <cstdio>
@@ -11,8 +11,8 @@
 #include <thread>
 #include <vector>
 
-#include "../spacedrive_amd/csrc/host_io.hpp"
-#include "../spacedrive_amd/csrc/uring.hpp"
+#include "../../spacedrive_amd/csrc/host_io.hpp"
+#include "../../spacedrive_amd/csrc/uring.hpp"
 
 using namespace sdgpu;
 

@@ -17,8 +17,8 @@
 //   X4  X2 with 4 rows per thread per round
 //   X1  same without LDS staging: one global atomic per row
 // Every variant's reps must equal the product's.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp_xcd_scatter.hip -o build/exp_xcd_scatter
-#include "../spacedrive_amd/csrc/dedup.hip"
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_xcd_scatter.hip -o build/exp_xcd_scatter
+#include "../../spacedrive_amd/csrc/dedup.hip"
 
 #include <stdio.h>
 

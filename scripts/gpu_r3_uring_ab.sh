@@ -1,6 +1,6 @@
 # io_uring vs pread A/B for the config-1 staging reads, on
 # the GPU box's host (CPU only; the box's kernel, filesystem and CPU share are
-# what the dir leg runs on).  build/exp_uring is built from scripts/exp_uring.cpp.
+# what the dir leg runs on).  build/exp_uring is built from scripts/exp/exp_uring.cpp.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
