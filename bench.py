@@ -693,13 +693,28 @@ class Runner:
                 "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
                             for k, v in link_kt.items()}}
         del repv
+        # the fused step (sdgpu_group_link_device): the same grouping and write
+        # set without a rep array -- the group kernel emits the lists itself
+        # (valid = has_key, as in the two-call leg above, for the same write set)
+        fused = None
+        if self.world == 1:
+            fz_t, fz_kt = self.timed_kernels(
+                lambda: dedup.group_link_device(key, has, has, grank, 0, 100, ctx=self.ctx,
+                                                trim=False), steps, warmup)
+            fused = {"ms_per_step": 1e3 * fz_t / steps, "value": per * steps / fz_t,
+                     "unit": "rows/s",
+                     "two_call_ms_per_step": 1e3 * t / steps + link["ms_per_step"],
+                     "note": "grouping + Object write set in one pass (no rep array); "
+                             "two_call = group_rows + link_batch_device above",
+                     "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
+                                 for k, v in fz_kt.items()}}
         full = None
         if self.world == 1 and self.args.dedup_full_rows:
             full = self.run_dedup_full(steps, warmup)
         return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
                 "rank": "implicit (row order, 12-byte records)" if implicit else "explicit array",
                 "explicit_rank_ms_per_step": explicit_ms, "exchange": xchg, "roofline": roof, "config4_full_one_gpu": full,
-                "link_batch": link,
+                "link_batch": link, "fused_job": fused,
                 "config": {"workload": "config4: 80% distinct u64 keys + 20% dups, 0.1% keyless",
                            "rows_per_gpu": per, "rows_total": total},
                 "kernels": kernels}
@@ -762,6 +777,15 @@ class Runner:
             self.ops.group_rows(key, has, rank, 100, 0)
             explicit_ms = 1e3 * self.timed(lambda: self.ops.group_rows(key, has, rank, 100, 0),
                                            steps, warmup) / steps
+        from spacedrive_amd import dedup
+        fz_t, fz_kt = self.timed_kernels(
+            lambda: dedup.group_link_device(key, has, None, None, 0, 100, ctx=self.ctx,
+                                            trim=False), steps, warmup)
+        fz_lists = None
+        if not self.args.no_cpu:
+            who, obj, _ = dedup.group_link_device(key, has, None, None, 0, 100, ctx=self.ctx)
+            fz_lists = dedup.split_link_lists(who.cpu().numpy(), obj.cpu().numpy())
+            del who, obj
         rep = self.ops.group_rows(key, has, None, 100, 0)
         nk = int(has.sum())
         linked = int((rep != rank).sum())
@@ -778,7 +802,12 @@ class Runner:
             ref = O.group_reps(hk, hh, 100)
             dt = time.perf_counter() - t0
             parity = int(np.count_nonzero(ref != gpu))
-            del hk, hh, gpu, ref
+            rc, rlr, rlo = O.link_batch(ref, None, None, 0)
+            fc, flr, flo = fz_lists
+            fz_bad = (int(abs(fc.size - rc.size) + abs(flr.size - rlr.size)) or
+                      int(np.count_nonzero(fc != rc) + np.count_nonzero(flr != rlr) +
+                          np.count_nonzero(flo != rlo)))
+            del hk, hh, gpu, ref, rc, rlr, rlo, fc, flr, flo, fz_lists
         del key, has, rank, rep
         torch.cuda.empty_cache()
         kernels = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in kt.items()}
@@ -817,10 +846,18 @@ class Runner:
         roof["step"] = {"survey_8d_bytes": 16 * total, "achieved": 16 * total / step_s / 1e9,
                         "frac": 16 * total / step_s / HBM_PEAK, "design_bytes": sum(alg.values()),
                         "pmc_source": src}
+        fused = {"ms_per_step": 1e3 * fz_t / steps, "value": total * steps / fz_t,
+                 "unit": "rows/s",
+                 "note": "grouping + Object write set (creators / connect pairs) in one pass, "
+                         "no rep array (sdgpu_group_link_device, valid = all rows)",
+                 "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
+                             for k, v in fz_kt.items()}}
+        if parity is not None:
+            fused["list_mismatches_vs_oracle"] = fz_bad
         out = {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * step_s,
                "rows": total, "rank": "implicit (row order, 12-byte records)",
                "explicit_rank_ms_per_step": explicit_ms, "roofline": roof, "kernels": kernels,
-               "gpu_rep_mismatches": parity}
+               "gpu_rep_mismatches": parity, "fused_job": fused}
         if parity is not None:
             out["oracle_seconds"] = round(dt, 2)
             out["parity_note"] = ("reps of the timed implicit-rank call vs oracle orc_group_reps "

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SDGPU_ABI_VERSION 3
+#define SDGPU_ABI_VERSION 4
 
 /* cas.rs:10-15 */
 #define SDGPU_CAS_SAMPLE_COUNT 4u
@@ -367,6 +367,29 @@ int sdgpu_scatter_rep_device(sdgpu_ctx *ctx, const uint32_t *d_src, const uint32
 int sdgpu_link_batch_device(sdgpu_ctx *ctx, const uint32_t *d_rep, const uint32_t *d_rank,
                             const uint8_t *d_valid, uint32_t first_rank, uint64_t n,
                             uint32_t *d_create, uint32_t *d_link_row, uint32_t *d_link_obj,
+                            uint32_t *d_counts, void *stream);
+
+/* Fused grouping + Object write set (ABI 4): the grouping of
+ * sdgpu_group_rows_device and the lists of sdgpu_link_batch_device in one
+ * pass, with no rep array in between (the group kernel writes the lists
+ * directly, coalesced; file_identifier/mod.rs:189-333).  Rows: d_key[i],
+ * d_has_key[i] (NULL = every row keyed), d_valid[i] (NULL = every row valid;
+ * a row with valid == 0 must have has_key == 0 and is in no list: it stays an
+ * orphan, mod.rs:113,127), rank d_rank[i] or first_rank + i (d_rank NULL),
+ * ranks < 2^31.  Output (device), one entry per keyed row and per valid
+ * keyless row, n entries each:
+ *   d_who[e] = rank                  the row creates an Object
+ *   d_who[e] = rank | SDGPU_LINKED   the row connects to the Object created by
+ *                                    the row of rank d_obj[e]
+ * Keyed rows come first, grouped by an internal hash bucket (creators before
+ * linked rows inside a bucket); the valid keyless rows (own Objects,
+ * mod.rs:238-239) follow in row order.  The ORDER of the entries is not
+ * part of the contract (the reference's writes are a set; compare as sets).
+ * d_counts[0] = creators, [1] = linked rows, [2] = entries (= [0] + [1]). */
+#define SDGPU_LINKED 0x80000000u
+int sdgpu_group_link_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t *d_has_key,
+                            const uint8_t *d_valid, const uint32_t *d_rank, uint32_t first_rank,
+                            uint64_t n, uint32_t chunk_rows, uint32_t *d_who, uint32_t *d_obj,
                             uint32_t *d_counts, void *stream);
 
 /* ---- downstream consumers of the grouping ---------------

@@ -1185,6 +1185,140 @@ __device__ __forceinline__ uint64_t global_slot(uint64_t h, uint64_t tsize) {
 
 constexpr int kPer = (kLdsCap + kGroupThreads - 1) / kGroupThreads;
 
+// Ranks of flagged items across a workgroup in record order (record index =
+// thread + step * kGroupThreads, i.e. step-major): pc[j] / pl[j] = creators /
+// linked items of the workgroup before the thread's item of step j, tc / tl
+// = the workgroup's totals.  Per-(step, wave) ballots, then ONE wave scans the
+// 2 x kSteps x 16 wave counts (two per lane).  scr: kListScratch words.  With
+// `reuse`, a leading barrier protects scr from the previous call's readers.
+constexpr int kGroupWaves = kGroupThreads / 64;
+constexpr int kListScratch = 2 * 8 * kGroupWaves + 2;
+template <int kSteps>
+__device__ __forceinline__ void wg_list_ranks(const bool (&c)[kSteps], const bool (&l)[kSteps],
+                                              uint32_t (&pc)[kSteps], uint32_t (&pl)[kSteps],
+                                              uint32_t& tc, uint32_t& tl, uint32_t* scr,
+                                              bool reuse) {
+  constexpr int kE = kSteps * kGroupWaves;  // entries per list
+  static_assert(2 * kE + 2 <= kListScratch && kE <= 128, "two entries per lane of one wave");
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  if (reuse) __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSteps; ++j) {
+    const uint64_t bc = __ballot(c[j]), bl = __ballot(l[j]);
+    pc[j] = __popcll(bc & lt);
+    pl[j] = __popcll(bl & lt);
+    if (lane == 0) {
+      scr[j * kGroupWaves + w] = __popcll(bc);
+      scr[kE + j * kGroupWaves + w] = __popcll(bl);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+#pragma unroll
+    for (int list = 0; list < 2; ++list) {
+      uint32_t* e = scr + list * kE;
+      const uint32_t i0 = 2 * lane;
+      const uint32_t a0 = i0 < kE ? e[i0] : 0u, a1 = i0 + 1 < kE ? e[i0 + 1] : 0u;
+      const uint32_t v = a0 + a1;
+      uint32_t inc = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d);
+        if (lane >= static_cast<uint32_t>(d)) inc += o;
+      }
+      if (i0 < kE) e[i0] = inc - v;
+      if (i0 + 1 < kE) e[i0 + 1] = inc - v + a0;
+      if (lane == 63) scr[2 * kE + list] = inc;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSteps; ++j) {
+    pc[j] += scr[j * kGroupWaves + w];
+    pl[j] += scr[kE + j * kGroupWaves + w];
+  }
+  tc = scr[2 * kE];
+  tl = scr[2 * kE + 1];
+}
+
+// Where K5 puts a bucket's result.  Per record: live (a keyed row of the
+// bucket), r (its rank), w (its row), f (the lowest rank of its key).
+//   RepOut:  rep[w] = f for the rows that link to an earlier chunk (the
+//            partition initialised rep = rank): one scattered 4-B store each.
+//   ListOut: the Object write set itself (round 4; sdgpu_group_link_device),
+//            in the bucket's own record range [start, end) -- one entry per
+//            keyed row, so the positions need no global coordination:
+//            creators from the front in record order, who = rank; linked rows
+//            from the back, who = rank | SDGPU_LINKED, obj = f.  Coalesced;
+//            no rep array.  counts[0] / [1] += the bucket's creators / linked
+//            (one atomic each per workgroup); the last bucket stores the
+//            keyed total in counts[2].
+struct RepOut {
+  static constexpr int kScratch = 1;
+  uint32_t* rep;
+  template <int kSteps>
+  __device__ __forceinline__ void emit(const bool (&live)[kSteps], const bool (&lk)[kSteps],
+                                       const uint32_t (&r)[kSteps], const uint32_t (&w)[kSteps],
+                                       const uint32_t (&f)[kSteps], uint32_t, uint32_t, uint32_t&,
+                                       uint32_t&, uint32_t*, bool) const {
+#pragma unroll
+    for (int j = 0; j < kSteps; ++j)
+      if (lk[j]) rep[w[j]] = f[j];  // others keep rank
+    (void)live;
+    (void)r;
+  }
+};
+constexpr uint32_t kLinkedBit = 0x80000000u;
+struct ListOut {
+  static constexpr int kScratch = kListScratch;
+  uint32_t* who;
+  uint32_t* obj;
+  uint32_t* counts;
+  // c_run / l_run: creators / linked already written for this bucket (the
+  // global-table path emits a bucket in several chunks)
+  template <int kSteps>
+  __device__ __forceinline__ void emit(const bool (&live)[kSteps], const bool (&lk)[kSteps],
+                                       const uint32_t (&r)[kSteps], const uint32_t (&w)[kSteps],
+                                       const uint32_t (&f)[kSteps], uint32_t start, uint32_t end,
+                                       uint32_t& c_run, uint32_t& l_run, uint32_t* scr,
+                                       bool reuse) const {
+    bool c[kSteps], l[kSteps];
+    uint32_t pc[kSteps], pl[kSteps], tc, tl;
+#pragma unroll
+    for (int j = 0; j < kSteps; ++j) {
+      c[j] = live[j] && !lk[j];
+      l[j] = lk[j];
+    }
+    wg_list_ranks<kSteps>(c, l, pc, pl, tc, tl, scr, reuse);
+#pragma unroll
+    for (int j = 0; j < kSteps; ++j) {
+      if (c[j]) who[start + c_run + pc[j]] = r[j];
+      if (l[j]) {
+        const uint32_t p = end - 1 - (l_run + pl[j]);
+        who[p] = r[j] | kLinkedBit;
+        obj[p] = f[j];
+      }
+    }
+    c_run += tc;
+    l_run += tl;
+    (void)w;
+  }
+  // once per bucket, after its last emit
+  __device__ __forceinline__ void done(uint32_t c_run, uint32_t l_run, uint32_t end) const {
+    if (threadIdx.x == 0) {
+      if (c_run) atomicAdd(&counts[0], c_run);
+      if (l_run) atomicAdd(&counts[1], l_run);
+      if (blockIdx.x == gridDim.x - 1) counts[2] = end;
+    }
+  }
+};
+__device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t) {}
+__device__ __forceinline__ void out_done(const ListOut& o, uint32_t c_run, uint32_t l_run,
+                                         uint32_t end) {
+  o.done(c_run, l_run, end);
+}
+
 // Bucket records as {hash lo, hash hi, rank, row}: 16-byte records as stored,
 // or 12-byte ones {hash lo, hash hi, row} with rank = rank_base + row.
 struct Rec16Src {
@@ -1215,13 +1349,14 @@ __device__ __forceinline__ void load_bucket(Src rec, uint32_t start, uint32_t en
 }
 
 // Group-by of one bucket too large for LDS: a private region of the global
-// table (4 slots per row, agent-scope atomics).  Records with row ~0 are pads.
-template <typename Src>
+// table (4 slots per row, agent-scope atomics).  The results leave in chunks of
+// kGroupThreads records (uniform trip count: the list output ranks each chunk
+// across the workgroup).
+template <typename Src, typename Out>
 __device__ __forceinline__ void group_bucket_global(Src rec, uint32_t start, uint32_t end,
                                                     ChunkOf chunk_of, uint64_t* __restrict__ gkey,
-                                                    uint32_t* __restrict__ gmin,
-                                                    uint32_t* __restrict__ rep,
-                                                    uint32_t& special_min) {
+                                                    uint32_t* __restrict__ gmin, const Out& out,
+                                                    uint32_t& special_min, uint32_t* scr) {
   const uint32_t m = end - start;
   uint64_t tsize = 1;
   while (tsize * 2 <= 4ull * m) tsize *= 2;  // 2m < tsize <= 4m (64-bit: no wrap)
@@ -1235,7 +1370,6 @@ __device__ __forceinline__ void group_bucket_global(Src rec, uint32_t start, uin
   __syncthreads();
   for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
     const uint4 q = rec(i);
-    if (q.w == kPadRow) continue;
     const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
     const uint32_t r = q.z;
     if (k == kEmpty) {
@@ -1255,41 +1389,54 @@ __device__ __forceinline__ void group_bucket_global(Src rec, uint32_t start, uin
     }
   }
   __syncthreads();
-  for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
-    const uint4 q = rec(i);
-    if (q.w == kPadRow) continue;
-    const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
-    const uint32_t r = q.z;
-    uint32_t f;
-    if (k == kEmpty) {
-      f = special_min;
-    } else {
-      uint64_t h = global_slot(k, tsize);
-      for (;;) {
-        const uint64_t kk =
-            __hip_atomic_load(&tk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (kk == k) break;
-        h = (h + 1) & (tsize - 1);
+  uint32_t c_run = 0, l_run = 0;
+  for (uint32_t i0 = start; i0 < end; i0 += kGroupThreads) {
+    const uint32_t i = i0 + threadIdx.x;
+    bool live[1] = {false}, lk[1] = {false};
+    uint32_t r[1] = {0}, w[1] = {0}, f[1] = {0};
+    if (i < end) {
+      const uint4 q = rec(i);
+      const uint64_t k = (static_cast<uint64_t>(q.y) << 32) | q.x;
+      uint32_t fv;
+      if (k == kEmpty) {
+        fv = special_min;
+      } else {
+        uint64_t h = global_slot(k, tsize);
+        for (;;) {
+          const uint64_t kk =
+              __hip_atomic_load(&tk[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (kk == k) break;
+          h = (h + 1) & (tsize - 1);
+        }
+        fv = __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      f = __hip_atomic_load(&tm[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      live[0] = true;
+      r[0] = q.z;
+      w[0] = q.w;
+      f[0] = fv;
+      lk[0] = chunk_of(q.z) != chunk_of(fv);
     }
-    if (chunk_of(r) != chunk_of(f)) rep[q.w] = f;
+    out.template emit<1>(live, lk, r, w, f, start, end, c_run, l_run, scr, true);
   }
+  out_done(out, c_run, l_run, end);
 }
 
 // Group-by of one bucket, rows [start, end) of rec (q_reg preloaded by
 // load_bucket when the bucket fits the LDS table).
-template <typename Src>
+template <typename Src, typename Out>
 __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
                                              uint32_t end, const uint4 (&q_reg)[kPer],
                                              ChunkOf chunk_of, uint64_t* __restrict__ gkey,
-                                             uint32_t* __restrict__ gmin,
-                                             uint32_t* __restrict__ rep, uint64_t* lkey,
-                                             uint32_t* lmin, uint32_t& special_min) {
+                                             uint32_t* __restrict__ gmin, const Out& out,
+                                             uint64_t* lkey, uint32_t* lmin, uint32_t& special_min,
+                                             uint32_t* scr) {
   const uint32_t m = end - start;
-  if (m == 0) return;
+  if (m == 0) {
+    out_done(out, 0u, 0u, end);
+    return;
+  }
   if (m > kLdsCap) {
-    group_bucket_global(rec, start, end, chunk_of, gkey, gmin, rep, special_min);
+    group_bucket_global(rec, start, end, chunk_of, gkey, gmin, out, special_min, scr);
     return;
   }
   // (the LDS code names lkey / lmin directly: through generic pointers shared
@@ -1300,61 +1447,65 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
   }
   if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
   __syncthreads();
-  {
-    // A thread's records probe in lock step: every pass issues the LDS
-    // round trips of all its pending records back to back and only then
-    // inspects the results, so their latencies overlap (the probe loops are
-    // latency-bound, not LDS-bandwidth-bound).
-    uint32_t h[kPer], step[kPer];
-    uint32_t live = 0, pend = 0;  // bit j: record j exists / is still probing
+  // A thread's records probe in lock step: every pass issues the LDS
+  // round trips of all its pending records back to back and only then
+  // inspects the results, so their latencies overlap (the probe loops are
+  // latency-bound, not LDS-bandwidth-bound).
+  uint32_t h[kPer], step[kPer];
+  uint32_t live = 0, pend = 0;  // bit j: record j exists / is still probing
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
+    h[j] = lds_slot(k);
+    step[j] = lds_step(k);
+    if (start + threadIdx.x + j * kGroupThreads < end) {
+      live |= 1u << j;
+      if (k == kEmpty)
+        atomicMin(&special_min, q_reg[j].z);
+      else
+        pend |= 1u << j;
+    }
+  }
+  const uint32_t keyed = pend;
+  while (pend) {
+    uint64_t prev[kPer];
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
-      h[j] = lds_slot(k);
-      step[j] = lds_step(k);
-      if (start + threadIdx.x + j * kGroupThreads < end) {
-        live |= 1u << j;
-        if (k == kEmpty)
-          atomicMin(&special_min, q_reg[j].z);
-        else
-          pend |= 1u << j;
-      }
+      prev[j] = (pend >> j & 1u)
+                    ? atomicCAS(reinterpret_cast<unsigned long long*>(&lkey[h[j]]),
+                                static_cast<unsigned long long>(kEmpty),
+                                static_cast<unsigned long long>(k))
+                    : 0ull;
     }
-    const uint32_t keyed = pend;
-    while (pend) {
-      uint64_t prev[kPer];
-#pragma unroll
-      for (int j = 0; j < kPer; ++j) {
-        const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
-        prev[j] = (pend >> j & 1u)
-                      ? atomicCAS(reinterpret_cast<unsigned long long*>(&lkey[h[j]]),
-                                  static_cast<unsigned long long>(kEmpty),
-                                  static_cast<unsigned long long>(k))
-                      : 0ull;
-      }
-#pragma unroll
-      for (int j = 0; j < kPer; ++j) {
-        if (!(pend >> j & 1u)) continue;
-        const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
-        if (prev[j] == kEmpty || prev[j] == k) {
-          atomicMin(&lmin[h[j]], q_reg[j].z);
-          pend &= ~(1u << j);
-        } else {
-          h[j] = next_slot(h[j], step[j]);
-        }
-      }
-    }
-    __syncthreads();
-    // every keyed record's final probe slot h[j] holds its key: read the
-    // group minimum there (no second probe sequence needed)
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      if (!(live >> j & 1u)) continue;
-      const uint32_t r = q_reg[j].z;
-      const uint32_t f = (keyed >> j & 1u) ? lmin[h[j]] : special_min;
-      if (chunk_of(r) != chunk_of(f)) rep[q_reg[j].w] = f;  // others keep rank
+      if (!(pend >> j & 1u)) continue;
+      const uint64_t k = (static_cast<uint64_t>(q_reg[j].y) << 32) | q_reg[j].x;
+      if (prev[j] == kEmpty || prev[j] == k) {
+        atomicMin(&lmin[h[j]], q_reg[j].z);
+        pend &= ~(1u << j);
+      } else {
+        h[j] = next_slot(h[j], step[j]);
+      }
     }
   }
+  __syncthreads();
+  // every keyed record's final probe slot h[j] holds its key: read the
+  // group minimum there (no second probe sequence needed)
+  bool lv[kPer], lk[kPer];
+  uint32_t r[kPer], w[kPer], f[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    lv[j] = live >> j & 1u;
+    r[j] = q_reg[j].z;
+    w[j] = q_reg[j].w;
+    f[j] = lv[j] ? ((keyed >> j & 1u) ? lmin[h[j]] : special_min) : 0u;
+    lk[j] = lv[j] && chunk_of(r[j]) != chunk_of(f[j]);
+  }
+  uint32_t c_run = 0, l_run = 0;
+  out.template emit<kPer>(lv, lk, r, w, f, start, end, c_run, l_run, scr, false);
+  out_done(out, c_run, l_run, end);
 }
 
 // K5 with a PACKED 8-byte LDS table, for buckets of >= 12 digit bits (the
@@ -1364,7 +1515,7 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
 // empty) a slot is ONE 64-bit word.  The CAS that places or finds a key also
 // names the record that owns it, the group minimum lives per owner
 // (lmin[4096]), and 7680 slots fit where 6144 twelve-byte ones did: load
-// ~0.4 instead of ~0.5, shorter probe chains.  scripts/exp_group_packed.hip:
+// ~0.4 instead of ~0.5, shorter probe chains.  scripts/exp/exp_group_packed.hip:
 // 12.5 M rows 0.078 -> 0.072 ms (profiles/r3/exp_group_packed/run.log).
 // Buckets above 4095 records take the global table; pads (row ~0) are skipped.
 constexpr uint32_t kPkSlots = 7680;  // 2^9 * 15: probe steps odd and prime to 3 and 5
@@ -1376,18 +1527,21 @@ __device__ __forceinline__ uint64_t key_rest(uint64_t h, uint32_t bits) {
   return (h & ((1ull << lo) - 1)) | ((h >> (64 - kShardBits)) << lo);
 }
 
-template <typename Src>
+template <typename Src, typename Out>
 __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uint32_t end,
                                                     uint32_t bits, ChunkOf chunk_of,
                                                     uint64_t* __restrict__ gkey,
-                                                    uint32_t* __restrict__ gmin,
-                                                    uint32_t* __restrict__ rep, uint64_t* tab,
-                                                    uint32_t* lmin, uint32_t& special_min) {
+                                                    uint32_t* __restrict__ gmin, const Out& out,
+                                                    uint64_t* tab, uint32_t* lmin,
+                                                    uint32_t& special_min, uint32_t* scr) {
   constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
   const uint32_t m = end - start;
-  if (m == 0) return;
+  if (m == 0) {
+    out_done(out, 0u, 0u, end);
+    return;
+  }
   if (m > kPkCap) {
-    group_bucket_global(rec, start, end, chunk_of, gkey, gmin, rep, special_min);
+    group_bucket_global(rec, start, end, chunk_of, gkey, gmin, out, special_min, scr);
     return;
   }
   // every load issued unconditionally (past the end: the bucket's last record)
@@ -1449,72 +1603,84 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
   for (int j = 0; j < kP; ++j)
     if (live >> j & 1u) atomicMin(&lmin[owner[j]], q[j].z);
   __syncthreads();
+  bool lv[kP], lk[kP];
+  uint32_t r[kP], w[kP], f[kP];
 #pragma unroll
   for (int j = 0; j < kP; ++j) {
-    if (!(live >> j & 1u)) continue;
-    const uint32_t r = q[j].z, f = lmin[owner[j]];
-    if (chunk_of(r) != chunk_of(f)) rep[q[j].w] = f;  // others keep rank
+    lv[j] = live >> j & 1u;
+    r[j] = q[j].z;
+    w[j] = q[j].w;
+    f[j] = lmin[owner[j]];
+    lk[j] = lv[j] && chunk_of(r[j]) != chunk_of(f[j]);
   }
+  uint32_t c_run = 0, l_run = 0;
+  out.template emit<kP>(lv, lk, r, w, f, start, end, c_run, l_run, scr, false);
+  out_done(out, c_run, l_run, end);
 }
 
 
 // One workgroup per bucket.  Rows of bucket b: [offs[b*P], offs[(b+1)*P]).
+template <typename Out>
 __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
     const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P,
-    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
-    uint32_t* __restrict__ rep) {
+    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin, Out out) {
   __shared__ uint64_t lkey[kLdsSlots];
   __shared__ uint32_t lmin[kLdsSlots];
   __shared__ uint32_t special_min;  // min rank of key == kEmpty (sentinel clash)
+  __shared__ uint32_t scr[Out::kScratch];
   const uint32_t b = blockIdx.x;
   const uint32_t start = offs[static_cast<uint64_t>(b) * P];
   const uint32_t end = offs[static_cast<uint64_t>(b + 1) * P];  // offs[nb*P] = total
   uint4 q_reg[kPer];
   load_bucket(Rec16Src{rec}, start, end, q_reg);
-  group_bucket(Rec16Src{rec}, start, end, q_reg, chunk_of, gkey, gmin, rep, lkey, lmin,
-               special_min);
+  group_bucket(Rec16Src{rec}, start, end, q_reg, chunk_of, gkey, gmin, out, lkey, lmin,
+               special_min, scr);
 }
 
 // k_bucket_group over 12-byte records (rank = rank_base + row).
+template <typename Out>
 __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12(
     const uint3* __restrict__ rec, uint32_t rank_base, const uint32_t* __restrict__ offs,
-    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
-    uint32_t* __restrict__ rep) {
+    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin, Out out) {
   __shared__ uint64_t lkey[kLdsSlots];
   __shared__ uint32_t lmin[kLdsSlots];
   __shared__ uint32_t special_min;
+  __shared__ uint32_t scr[Out::kScratch];
   const uint32_t b = blockIdx.x;
   const uint32_t start = offs[b], end = offs[b + 1];
   const Rec12Src src{rec, rank_base};
   uint4 q_reg[kPer];
   load_bucket(src, start, end, q_reg);
-  group_bucket(src, start, end, q_reg, chunk_of, gkey, gmin, rep, lkey, lmin, special_min);
+  group_bucket(src, start, end, q_reg, chunk_of, gkey, gmin, out, lkey, lmin, special_min, scr);
 }
 
 // Packed-table K5 (>= 12 digit bits): rows of bucket b in [offs[b*P], offs[(b+1)*P]).
+template <typename Out>
 __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group_pk(
     const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P, uint32_t bits,
-    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
-    uint32_t* __restrict__ rep) {
+    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin, Out out) {
   __shared__ uint64_t tab[kPkSlots];
   __shared__ uint32_t lmin[kPkCap + 1];
   __shared__ uint32_t special_min;
+  __shared__ uint32_t scr[Out::kScratch];
   const uint32_t b = blockIdx.x;
   group_bucket_packed(Rec16Src{rec}, offs[static_cast<uint64_t>(b) * P],
-                      offs[static_cast<uint64_t>(b + 1) * P], bits, chunk_of, gkey, gmin, rep, tab,
-                      lmin, special_min);
+                      offs[static_cast<uint64_t>(b + 1) * P], bits, chunk_of, gkey, gmin, out, tab,
+                      lmin, special_min, scr);
 }
 
+template <typename Out>
 __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12_pk(
     const uint3* __restrict__ rec, uint32_t rank_base, const uint32_t* __restrict__ offs,
     uint32_t bits, ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
-    uint32_t* __restrict__ rep) {
+    Out out) {
   __shared__ uint64_t tab[kPkSlots];
   __shared__ uint32_t lmin[kPkCap + 1];
   __shared__ uint32_t special_min;
+  __shared__ uint32_t scr[Out::kScratch];
   const uint32_t b = blockIdx.x;
   group_bucket_packed(Rec12Src{rec, rank_base}, offs[b], offs[b + 1], bits, chunk_of, gkey, gmin,
-                      rep, tab, lmin, special_min);
+                      out, tab, lmin, special_min, scr);
 }
 
 // the segment sizes k_part_private adds to, and the fine-count overflow flag
@@ -1649,10 +1815,10 @@ void allow_lds(K kernel, size_t bytes) {
 // kRec12: rows without a rank array (rank = rank_base + row), 12-byte records
 // in both passes.
 template <typename In, uint32_t kB2, uint32_t kS2, int kR2, uint32_t kP2, bool kRec12 = false,
-          uint32_t kF2 = kS2>
+          uint32_t kF2 = kS2, typename Out>
 hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t chunk_rows,
-                            uint32_t* rep, bool init_rep, void* ws, hipStream_t s, KTimer* timer,
-                            uint32_t rank_base = 0) {
+                            uint32_t* rep, bool init_rep, Out out, void* ws, hipStream_t s,
+                            KTimer* timer, uint32_t rank_base = 0) {
   using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(w + L.tiles);
@@ -1702,12 +1868,12 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
     }
     KScope k(timer, "bucket_group", s);
     if constexpr (kRec12)
-      k_bucket_group12_pk<<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
-                                                          rank_base, fbase, bits,
-                                                          ChunkOf::make(chunk_rows), gkey, gmin, rep);
+      k_bucket_group12_pk<Out><<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
+                                                               rank_base, fbase, bits,
+                                                               ChunkOf::make(chunk_rows), gkey, gmin, out);
     else
-      k_bucket_group_pk<<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits, ChunkOf::make(chunk_rows),
-                                                        gkey, gmin, rep);
+      k_bucket_group_pk<Out><<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits,
+                                                             ChunkOf::make(chunk_rows), gkey, gmin, out);
     return hipGetLastError();
   }
   // pass 1: coarse partition on the top cbits digit bits (rep initialised
@@ -1753,18 +1919,18 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
   }
   KScope k(timer, "bucket_group", s);
   if constexpr (kRec12)
-    k_bucket_group12_pk<<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
-                                                        rank_base, fbase, bits,
-                                                        ChunkOf::make(chunk_rows), gkey, gmin, rep);
+    k_bucket_group12_pk<Out><<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
+                                                             rank_base, fbase, bits,
+                                                             ChunkOf::make(chunk_rows), gkey, gmin, out);
   else
-    k_bucket_group_pk<<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits, ChunkOf::make(chunk_rows),
-                                                      gkey, gmin, rep);
+    k_bucket_group_pk<Out><<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits,
+                                                           ChunkOf::make(chunk_rows), gkey, gmin, out);
   return hipGetLastError();
 }
 
-template <typename In>
+template <typename In, typename Out>
 hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, bool init_rep,
-                        void* ws, hipStream_t s, KTimer* timer) {
+                        Out out, void* ws, hipStream_t s, KTimer* timer) {
   const GroupLayout L = group_layout(n);
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(w + L.hist);
@@ -1779,11 +1945,12 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   if (L.cbits) {
     if constexpr (std::is_same<In, RowsIn>::value) {
       if (!in.rank)  // rank = rank_base + row: 12-byte records
-        return two_level_launch<In, kStage2Bits, kStage2Slots, kStage2Rows, kStage2Blocks, true>(
-            in, n, L, chunk_rows, rep, init_rep, ws, s, timer, in.rank_base);
+        return two_level_launch<In, kStage2Bits, kStage2Slots, kStage2Rows, kStage2Blocks, true,
+                                kStage2Slots>(in, n, L, chunk_rows, rep, init_rep, out, ws, s,
+                                              timer, in.rank_base);
     }
-    return two_level_launch<In, kStage2Bits, kStage2Slots, kStage2Rows, kStage2Blocks>(
-        in, n, L, chunk_rows, rep, init_rep, ws, s, timer);
+    return two_level_launch<In, kStage2Bits, kStage2Slots, kStage2Rows, kStage2Blocks, false,
+                            kStage2Slots>(in, n, L, chunk_rows, rep, init_rep, out, ws, s, timer);
   }
   if (bits == kStageBits) {
     // 12-bit digits: block-major counts, k_fine_scan for every block's start
@@ -1814,9 +1981,10 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
                                                                 rep, fbase);
         }
         KScope k(timer, "bucket_group", s);
-        k_bucket_group12_pk<<<nb, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
-                                                         in.rank_base, fbase, kStageBits,
-                                                         ChunkOf::make(chunk_rows), gkey, gmin, rep);
+        k_bucket_group12_pk<Out><<<nb, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
+                                                              in.rank_base, fbase, kStageBits,
+                                                              ChunkOf::make(chunk_rows), gkey, gmin,
+                                                              out);
         return hipGetLastError();
       }
     }
@@ -1830,8 +1998,8 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
             in, n, kShardBits, fE, rec, rep, nullptr, 0, ftot, fbase);
     }
     KScope k(timer, "bucket_group", s);
-    k_bucket_group_pk<<<nb, kGroupThreads, 0, s>>>(rec, fbase, 1, kStageBits,
-                                                   ChunkOf::make(chunk_rows), gkey, gmin, rep);
+    k_bucket_group_pk<Out><<<nb, kGroupThreads, 0, s>>>(rec, fbase, 1, kStageBits,
+                                                        ChunkOf::make(chunk_rows), gkey, gmin, out);
     return hipGetLastError();
   }
   {
@@ -1853,8 +2021,8 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
     }
   }
   KScope k(timer, "bucket_group", s);
-  k_bucket_group<<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, ChunkOf::make(chunk_rows),
-                                                      gkey, gmin, rep);
+  k_bucket_group<Out><<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, ChunkOf::make(chunk_rows),
+                                                           gkey, gmin, out);
   return hipGetLastError();
 }
 
@@ -1897,9 +2065,21 @@ hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_
   if (in.n == 0) return hipSuccess;
   if (in.rec12)
     return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
-                        chunk_rows, rep, init_rep, ws, s, timer);
+                        chunk_rows, rep, init_rep, RepOut{rep}, ws, s, timer);
   return group_launch(RowsIn{in.key, in.valid, in.rank, in.rank_base}, in.n, chunk_rows, rep,
-                      init_rep, ws, s, timer);
+                      init_rep, RepOut{rep}, ws, s, timer);
+}
+
+hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* who,
+                             uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
+                             KTimer* timer) {
+  if (in.n == 0) return hipSuccess;
+  const ListOut out{who, obj, counts};
+  if (in.rec12)
+    return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
+                        chunk_rows, nullptr, false, out, ws, s, timer);
+  return group_launch(RowsIn{in.key, in.valid, in.rank, in.rank_base}, in.n, chunk_rows, nullptr,
+                      false, out, ws, s, timer);
 }
 
 size_t shard_workspace_bytes(uint32_t shard_bits) {

@@ -155,6 +155,18 @@ size_t dedup_workspace_bytes(uint64_t n);
 // get rep = their rank when init_rep, and are left untouched otherwise).
 hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* rep,
                               bool init_rep, void* ws, hipStream_t s, KTimer* timer = nullptr);
+// The grouping as the Object write set (ListOut in dedup.hip): per bucket, in
+// its record range, creators from the front (who = rank) and linked rows from
+// the back (who = rank | SDGPU_LINKED, obj = creator rank); no rep array.
+// counts[0..2] (zeroed by the caller) += creators, linked; counts[2] = keyed
+// entries.  keyless_list_launch then appends the valid keyless rows.
+hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* who,
+                             uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
+                             KTimer* timer = nullptr);
+size_t keyless_workspace_bytes(uint64_t n);
+hipError_t keyless_list_launch(const uint8_t* has, const uint8_t* valid, const uint32_t* rank,
+                               uint32_t first_rank, uint64_t n, uint32_t* who, uint32_t* counts,
+                               void* ws, hipStream_t s, KTimer* timer = nullptr);
 size_t shard_workspace_bytes(uint32_t shard_bits);
 // Shard of a key = top shard_bits bits of mix64(key) (rows_device.hpp row_hash).
 hipError_t shard_count_launch(const uint64_t* key, const uint8_t* has_key, uint64_t n,

@@ -173,7 +173,110 @@ __global__ __launch_bounds__(kThreads) void k_link_write(
 
 inline uint32_t link_tiles(uint64_t n) { return static_cast<uint32_t>((n + kTile - 1) / kTile); }
 
+// Keyless creators of the fused grouping (sdgpu_group_link_device): rows with
+// no cas_id that are valid (empty files: their own Object, mod.rs:238-239) are
+// not in the bucket records, so they are listed here, in row order, after the
+// keyed entries: who[K + t] = rank of the t-th such row, K = counts[2] (the
+// keyed total the group kernel stored).  A thread takes 16 consecutive rows
+// (one 16-B load of has_key and of valid); 4096-row tiles, counted, scanned,
+// written.
+constexpr int kKlRows = 16;
+constexpr uint32_t kKlTile = kThreads * kKlRows;
+
+__device__ __forceinline__ uint32_t keyless_mask(const uint8_t* __restrict__ has,
+                                                 const uint8_t* __restrict__ valid, uint64_t n,
+                                                 uint64_t i0) {
+  uint32_t m = 0;
+  const bool aligned = (reinterpret_cast<uintptr_t>(has) & 15u) == 0 &&
+                       (reinterpret_cast<uintptr_t>(valid) & 15u) == 0;
+  if (aligned && i0 + kKlRows <= n) {
+    const uint4 h = *reinterpret_cast<const uint4*>(has + i0);
+    const uint4 v = valid ? *reinterpret_cast<const uint4*>(valid + i0) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < kKlRows; ++k) {
+      const uint32_t hb = (hw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+      const uint32_t vb = (vw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+      m |= static_cast<uint32_t>(hb == 0 && vb != 0) << k;
+    }
+  } else {
+    for (int k = 0; k < kKlRows && i0 + k < n; ++k)
+      m |= static_cast<uint32_t>(has[i0 + k] == 0 && (!valid || valid[i0 + k] != 0)) << k;
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(kThreads) void k_keyless_count(const uint8_t* __restrict__ has,
+                                                            const uint8_t* __restrict__ valid,
+                                                            uint64_t n, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t sc[kWaves];
+  const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kKlTile + threadIdx.x * kKlRows;
+  uint32_t c = __popc(keyless_mask(has, valid, n, i0));
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+  if (__lane_id() == 0) sc[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kWaves; ++w) t += sc[w];
+    cnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_keyless_write(
+    const uint8_t* __restrict__ has, const uint8_t* __restrict__ valid, const uint32_t* __restrict__ rank,
+    uint32_t first_rank, uint64_t n, uint32_t nb, const uint32_t* __restrict__ cnt,
+    uint32_t* __restrict__ who, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t sw[kWaves];
+  const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kKlTile + threadIdx.x * kKlRows;
+  const uint32_t K = counts[2];
+  uint32_t m = keyless_mask(has, valid, n, i0);
+  const uint32_t c = __popc(m);
+  uint32_t inc = c;
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d);
+    if (lane >= static_cast<uint32_t>(d)) inc += o;
+  }
+  if (lane == 63) sw[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t pos = K + cnt[blockIdx.x] + inc - c;
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) pos += sw[w];
+  while (m) {
+    const int k = __ffs(m) - 1;
+    m &= m - 1;
+    const uint64_t i = i0 + k;
+    who[pos++] = rank ? rank[i] : first_rank + static_cast<uint32_t>(i);
+  }
+  if (blockIdx.x == nb - 1 && threadIdx.x == 0) {
+    const uint32_t total = cnt[nb];
+    counts[0] += total;
+    counts[2] = K + total;
+  }
+}
+
 }  // namespace
+
+size_t keyless_workspace_bytes(uint64_t n) {
+  const uint64_t m = (n + kKlTile - 1) / kKlTile;
+  return ((m + 1) * 4 + 255) / 256 * 256 + ((scan::tiles_for(m) + 1) * 4 + 255) / 256 * 256;
+}
+
+hipError_t keyless_list_launch(const uint8_t* has, const uint8_t* valid, const uint32_t* rank,
+                               uint32_t first_rank, uint64_t n, uint32_t* who, uint32_t* counts,
+                               void* ws, hipStream_t s, KTimer* timer) {
+  if (n == 0 || !has) return hipSuccess;  // every row keyed: nothing to add
+  const uint32_t nb = static_cast<uint32_t>((n + kKlTile - 1) / kKlTile);
+  uint8_t* b = static_cast<uint8_t*>(ws);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(b);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(b + ((nb + 1) * 4ull + 255) / 256 * 256);
+  KScope k(timer, "keyless_list", s);
+  k_keyless_count<<<nb, kThreads, 0, s>>>(has, valid, n, cnt);
+  scan::exclusive(cnt, nb, cnt, tiles, nullptr, s);
+  k_keyless_write<<<nb, kThreads, 0, s>>>(has, valid, rank, first_rank, n, nb, cnt, who, counts);
+  return hipGetLastError();
+}
 
 size_t link_workspace_bytes(uint64_t n) {
   const uint64_t m = 2ull * link_tiles(n);

@@ -450,6 +450,53 @@ def link_batch_device(rep, rank=None, valid=None, first_rank: int = 0, ctx=None,
     return create[:c], lrow[:l], lobj[:l]
 
 
+LINKED = 0x80000000  # SDGPU_LINKED: the entry's row connects to an Object
+
+
+def group_link_device(key, has_key=None, valid=None, rank=None, first_rank: int = 0,
+                      chunk_rows: int = 100, ctx=None, trim: bool = True):
+    """Fused grouping + Object write set (sdgpu_group_link_device, ABI 4):
+    what group_rows + link_batch_device compute, without a rep array.
+
+    key int64 (u64 cas keys), has_key / valid uint8 or None, rank int32 or None
+    (= first_rank + i).  Returns device tensors (who, obj) trimmed to the
+    entry count and the host counts (creators, linked): who[e] = rank (a new
+    Object, file_identifier/mod.rs:243-297) or rank | LINKED (connects to the
+    Object of creator rank obj[e], mod.rs:189-225); bucket order, not row
+    order (a set).  trim=False: full-length tensors + the device counts [3],
+    no synchronisation."""
+    import torch
+    dev = key.device
+    ctx = ctx or default_context(dev.index)
+    n = key.numel()
+    who = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    obj = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    counts = torch.empty(3, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    check(ctx.lib.sdgpu_group_link_device(ctx.h, key.data_ptr(), ptr(has_key), ptr(valid),
+                                          ptr(rank), first_rank, n, chunk_rows, who.data_ptr(),
+                                          obj.data_ptr(), counts.data_ptr(), s),
+          "sdgpu_group_link_device")
+    if not trim:
+        return who, obj, counts
+    c, l, e = (int(x) for x in counts.cpu().tolist())
+    return who[:e], obj[:e], (c, l)
+
+
+def split_link_lists(who: np.ndarray, obj: np.ndarray):
+    """(create, link_row, link_obj) of a fused write set, each sorted by row
+    rank: the same lists link_batch_device returns (row order), for comparing
+    the two as sets."""
+    w = np.asarray(who).view(np.uint32)
+    o = np.asarray(obj).view(np.uint32)
+    lk = (w & np.uint32(LINKED)) != 0
+    create = np.sort(w[~lk])
+    lr = w[lk] & np.uint32(LINKED - 1)
+    order = np.argsort(lr, kind="stable")
+    return create, lr[order], o[lk][order]
+
+
 def object_stats(rep: np.ndarray, has_key: np.ndarray, ok: np.ndarray | None = None):
     """(created, linked) Object counts the reference's job would report
     (identifier_job_step returns (total_created, updated_file_paths.len()),

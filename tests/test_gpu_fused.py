@@ -1,0 +1,150 @@
+"""GPU parity of the fused grouping + Object write set (sdgpu_group_link_device,
+ABI 4): the create / connect lists the reference's identifier step writes
+(file_identifier/mod.rs:189-333), produced by the group kernel itself without
+a rep array, equal -- as sets -- the oracle's link batch over the oracle's
+grouping (O.link_batch(O.group_reps(...))), on every partition path: the
+small-table path (< 2^12 buckets), the one-level 12-bit path, the two-level
+path, 12- and 16-byte records (implicit / explicit ranks), buckets past the
+LDS table (global table), the hash-sentinel key, keyless and invalid rows."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+M64 = (1 << 64) - 1
+
+
+def inv_mix64(h: int) -> int:
+    """The key whose mix64 (splitmix64 finalizer, csrc/rows_device.hpp) is h."""
+    c1, c2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
+    z = h
+    z ^= (z >> 31) ^ (z >> 62)
+    z = (z * pow(c2, -1, 1 << 64)) & M64
+    z ^= (z >> 27) ^ (z >> 54)
+    z = (z * pow(c1, -1, 1 << 64)) & M64
+    z ^= (z >> 30) ^ (z >> 60)
+    return z
+
+
+SENTINEL_KEY = np.uint64(inv_mix64(M64))  # its hash is the LDS table's empty value
+
+
+def _ref_lists(key, has, valid, rank, first_rank, chunk):
+    """The oracle's write set in rank space: rows ordered by rank, grouped,
+    then link_batch; lists sorted like split_link_lists."""
+    n = key.size
+    r = (np.arange(n, dtype=np.uint64) + first_rank).astype(np.uint32) if rank is None else rank
+    order = np.argsort(r, kind="stable")
+    rep = O.group_reps(key[order], has[order], chunk)  # ranks relative to the sorted rows
+    rs = r[order]
+    rep_r = rs[rep]                                   # as ranks
+    v = None if valid is None else valid[order]
+    c, lr, lo = O.link_batch(rep_r, rs, v, 0)
+    o = np.argsort(lr, kind="stable")
+    return np.sort(c), lr[o], lo[o]
+
+
+def _fused(ctx, key, has, valid, rank, first_rank, chunk):
+    import torch
+    from spacedrive_amd import dedup
+    dk = torch.from_numpy(key.view(np.int64)).cuda()
+    dh = torch.from_numpy(has).cuda() if has is not None else None
+    dv = torch.from_numpy(valid).cuda() if valid is not None else None
+    dr = torch.from_numpy(rank.view(np.int32)).cuda() if rank is not None else None
+    who, obj, (c, l) = dedup.group_link_device(dk, dh, dv, dr, first_rank, chunk, ctx=ctx)
+    w = who.cpu().numpy().view(np.uint32)
+    o = obj.cpu().numpy().view(np.uint32)
+    assert w.size == c + l
+    return dedup.split_link_lists(w, o), (c, l)
+
+
+def _check(ctx, key, has, valid=None, rank=None, first_rank=0, chunk=100):
+    (c, lr, lo), (nc, nl) = _fused(ctx, key, has, valid, rank, first_rank, chunk)
+    rc, rlr, rlo = _ref_lists(key, has if has is not None else np.ones(key.size, np.uint8), valid,
+                              rank, first_rank, chunk)
+    assert (nc, nl) == (rc.size, rlr.size)
+    np.testing.assert_array_equal(c, rc)
+    np.testing.assert_array_equal(lr, rlr)
+    np.testing.assert_array_equal(lo, rlo)
+
+
+@pytest.mark.parametrize("n,pool", [(0, 1), (1, 1), (2, 1), (1000, 10), (100_000, 70_000),
+                                    (300_000, 1), (500_000, 7), (1_000_000, 800_000)])
+def test_fused_small_table_path_vs_oracle(ctx, n, pool):
+    """< 2^12 buckets (hist + scan + 16-B records, the 6144-slot table), one
+    key 300 k times (global table), the hash-sentinel key, keyless rows."""
+    rng = np.random.default_rng(n + 3 * pool)
+    keys = rng.integers(0, 2**64 - 1, max(pool, 1), dtype=np.uint64, endpoint=True)
+    keys[0] = SENTINEL_KEY
+    key = keys[rng.integers(0, keys.size, n)] if n else np.zeros(0, np.uint64)
+    has = (rng.random(n) > 0.01).astype(np.uint8)
+    for chunk in (100, 1, 7):
+        _check(ctx, key, has, chunk=chunk)
+    _check(ctx, key, has, first_rank=12345)
+
+
+@pytest.mark.parametrize("n,chunk", [(7_000_001, 100), (12_500_000, 7), (13_000_000, 100)])
+def test_fused_packed_paths_vs_oracle(ctx, n, chunk):
+    """The one-level 12-bit path (7 M, 12.5 M rows) and the two-level path
+    (13 M rows), implicit ranks (12-byte records) and explicit ranks (16-byte
+    records), a key repeated 60 k times (a bucket past the LDS table)."""
+    rng = np.random.default_rng(n)
+    pool = rng.integers(0, 2**64 - 1, int(n * 0.8), dtype=np.uint64, endpoint=True)
+    pool[1] = SENTINEL_KEY
+    key = pool[rng.integers(0, pool.size, n)]
+    key[rng.choice(n, 60_000, replace=False)] = pool[5]
+    has = (rng.random(n) > 0.001).astype(np.uint8)
+    _check(ctx, key, has, chunk=chunk)
+    _check(ctx, key, has, rank=np.arange(n, dtype=np.uint32), chunk=chunk)
+
+
+def test_fused_permuted_ranks_and_invalid_rows(ctx):
+    """Explicit permuted ranks (rows not in id order) and rows whose metadata
+    failed (valid == 0, has_key == 0: in neither list, mod.rs:113,127), next to
+    valid keyless rows (own Objects, mod.rs:238-239)."""
+    n = 400_000
+    rng = np.random.default_rng(11)
+    pool = rng.integers(0, 2**64 - 1, 250_000, dtype=np.uint64, endpoint=True)
+    key = pool[rng.integers(0, pool.size, n)]
+    valid = (rng.random(n) > 0.02).astype(np.uint8)
+    has = ((rng.random(n) > 0.01) & (valid != 0)).astype(np.uint8)
+    rank = rng.permutation(n).astype(np.uint32)
+    for chunk in (100, 3):
+        _check(ctx, key, has, valid=valid, rank=rank, chunk=chunk)
+    _check(ctx, key, has, valid=valid, chunk=100)
+    _check(ctx, key, None, chunk=100)  # every row keyed: no keyless pass
+
+
+@pytest.mark.parametrize("n", [4095, 4096, 4607, 4608, 4609, 9000])
+def test_fused_one_bucket_at_table_capacity(ctx, n):
+    """Every row in ONE bucket: just under, at and over the packed table's
+    4095 records and the 6144-slot table's 4608 (LDS vs global-table path)."""
+    from tests.test_gpu_dedup import _one_bucket_keys
+    rng = np.random.default_rng(n)
+    keys = _one_bucket_keys(rng, n, int(n * 0.7))
+    key = keys[rng.integers(0, keys.size, n)]
+    has = np.ones(n, np.uint8)
+    for chunk in (100, 1):
+        _check(ctx, key, has, chunk=chunk)
+
+
+def test_fused_equals_group_then_link_batch(ctx):
+    """Same write set as the two-call path it replaces (sdgpu_group_rows_device
+    -> sdgpu_link_batch_device) on the config-4 shape, 12.5 M rows."""
+    import torch
+    from spacedrive_amd import corpus, dedup
+    n = 12_500_000
+    key, has, rank = corpus.synth_dedup_rows_device(4, n, int(n * 0.8), 0, n, ctx=ctx)
+    ops = dedup.HipOps(ctx)
+    rep = ops.group_rows(key, has, None, 100, 0)
+    c, lr, lo = (x.cpu().numpy().view(np.uint32)
+                 for x in dedup.link_batch_device(rep, None, has, 0, ctx=ctx))
+    # the two-call path's valid = has: keyless rows are in neither list there
+    who, obj, _ = dedup.group_link_device(key, has, has, None, 0, 100, ctx=ctx)
+    fc, flr, flo = dedup.split_link_lists(who.cpu().numpy(), obj.cpu().numpy())
+    np.testing.assert_array_equal(fc, np.sort(c))
+    np.testing.assert_array_equal(flr, lr)
+    np.testing.assert_array_equal(flo, lo)
+    torch.cuda.synchronize()

@@ -177,6 +177,17 @@ def test_config4_100m_rows_one_gpu_and_8_ranks(ctx, ctxs):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(rep0.cpu().numpy().view(np.uint32), ref)
     del rep0
+    # the fused write set at full size (sdgpu_group_link_device, no rep array):
+    # the oracle's link batch over the same grouping, as sets
+    who, obj, (nc, nl) = dedup.group_link_device(key, has, None, None, 0, 100, ctx=ctx)
+    fc, flr, flo = dedup.split_link_lists(who.cpu().numpy(), obj.cpu().numpy())
+    del who, obj
+    rc, rlr, rlo = O.link_batch(ref, None, None, 0)
+    assert (nc, nl) == (rc.size, rlr.size)
+    np.testing.assert_array_equal(fc, rc)  # rc is in row order: already sorted
+    np.testing.assert_array_equal(flr, rlr)
+    np.testing.assert_array_equal(flo, rlo)
+    del fc, flr, flo, rc, rlr, rlo
     comms = dedup.Comm.init_all(ctxs)
     per = total // 8
     reps = dedup.group_sharded_all([key[r * per:(r + 1) * per] for r in range(8)],
