@@ -13,6 +13,9 @@
 //       256 MB Infinity Cache), the others appended to a per-bucket pair list
 //       ({row, f}, coalesced) and scattered by a second kernel
 //   GP  every linked row as a pair, then the scatter kernel
+//   GW  the pairs counting-sorted by row window (128 windows, ~3 MB of rep
+//       each) + per-bucket window boundaries; then AW: each window's pairs
+//       applied by the workgroups of ONE XCD, so its rep lines merge in L2
 // and the partition's coarse pass with / without its rep = rank stores.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/exp/exp_repwrite.hip -o build/exp_repwrite
 #include "../../spacedrive_amd/csrc/dedup.hip"
@@ -35,7 +38,8 @@ __global__ void k_rows(uint64_t* key, uint8_t* has, uint64_t n, uint64_t distinc
   }
 }
 
-enum Mode { kG0 = 0, kGN = 1, kGF = 2, kGH = 3 };
+enum Mode { kG0 = 0, kGN = 1, kGF = 2, kGH = 3, kGW = 4 };
+constexpr uint32_t kNW = 128;  // row windows of the GW / AW pair lists
 
 // group_bucket_packed with the output as a policy (buckets <= kPkCap only)
 template <int kMode>
@@ -43,10 +47,12 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_x(
     const uint3* __restrict__ rec, uint32_t rank_base, const uint32_t* __restrict__ offs,
     uint32_t bits, ChunkOf chunk_of, uint32_t* __restrict__ rep, uint32_t* __restrict__ who,
     uint32_t* __restrict__ obj, uint32_t* __restrict__ split_out, uint2* __restrict__ pairs,
-    uint32_t* __restrict__ npairs, uint32_t split_row, uint32_t never) {
+    uint32_t* __restrict__ npairs, uint32_t split_row, uint32_t never,
+    uint32_t* __restrict__ bnd = nullptr, uint32_t win_rows = 1) {
   __shared__ uint64_t tab[kPkSlots];
   __shared__ uint32_t lmin[kPkCap + 1];
   __shared__ uint32_t oc[4][16], ol[4][16];
+  __shared__ uint32_t wc[kNW], wp[kNW + 1];
   constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
   const uint32_t b = blockIdx.x;
   const uint32_t start = offs[b], end = offs[b + 1];
@@ -60,6 +66,7 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_x(
     if (start + threadIdx.x + j * kGroupThreads >= end || m == 0) q[j] = make_uint4(0, 0, kPadRow, kPadRow);
   for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
   for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
+  if (kMode == kGW && threadIdx.x < kNW) wc[threadIdx.x] = 0;
   __syncthreads();
   uint32_t slot[kP], step[kP], owner[kP];
   uint64_t mine[kP];
@@ -116,6 +123,34 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_group_x(
 #pragma unroll
     for (int j = 0; j < kP; ++j)
       if (lk[j]) rep[q[j].w] = f[j];
+  } else if constexpr (kMode == kGW) {
+    // linked pairs counting-sorted by row window (LDS counters), the
+    // bucket's window boundaries written beside: bnd[b][0..kNW]
+    uint32_t rk[kP], wn[kP];
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      wn[j] = lk[j] ? q[j].w / win_rows : 0u;
+      rk[j] = lk[j] ? atomicAdd(&wc[wn[j]], 1u) : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const uint32_t lane = threadIdx.x;
+      const uint32_t a0 = wc[2 * lane], a1 = wc[2 * lane + 1], v = a0 + a1;
+      uint32_t inc = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d);
+        if (lane >= static_cast<uint32_t>(d)) inc += o;
+      }
+      wp[2 * lane] = inc - v;
+      wp[2 * lane + 1] = inc - v + a0;
+      if (lane == 63) wp[kNW] = inc;
+    }
+    __syncthreads();
+    if (threadIdx.x <= kNW) bnd[static_cast<uint64_t>(b) * (kNW + 1) + threadIdx.x] = wp[threadIdx.x];
+#pragma unroll
+    for (int j = 0; j < kP; ++j)
+      if (lk[j]) pairs[start + wp[wn[j]] + rk[j]] = make_uint2(q[j].w, f[j]);
   } else if constexpr (kMode == kGN) {
 #pragma unroll
     for (int j = 0; j < kP; ++j)
@@ -200,6 +235,37 @@ __global__ __launch_bounds__(256) void k_pair_scatter(const uint2* __restrict__ 
   }
 }
 
+// AW: the pairs of row window j from every bucket, scattered into rep while
+// the window's 3 MB of rep stay in one XCD's L2.  Workgroup b runs on XCD
+// b % 8 (round-robin dispatch); the XCD's workgroups take its windows one at
+// a time (32 workgroups per window, each a range of buckets: one per thread).
+__global__ __launch_bounds__(1024) void k_window_apply(const uint2* __restrict__ pairs,
+                                                       const uint32_t* __restrict__ offs,
+                                                       const uint32_t* __restrict__ bnd,
+                                                       uint32_t nb, uint32_t* __restrict__ rep,
+                                                       bool xcd) {
+  const uint32_t b = blockIdx.x;
+  uint32_t j, part;
+  if (xcd) {
+    const uint32_t x = b & 7u, t = b >> 3;
+    j = x + 8u * (t >> 5);
+    part = t & 31u;
+  } else {
+    j = b >> 5;
+    part = b & 31u;
+  }
+  const uint32_t per = (nb + 31) / 32;
+  for (uint32_t bk = part * per + threadIdx.x; bk < min(nb, (part + 1) * per); bk += 1024) {
+    const uint64_t e = static_cast<uint64_t>(bk) * (kNW + 1) + j;
+    const uint32_t base = offs[bk];
+    const uint32_t s = base + bnd[e], t = base + bnd[e + 1];
+    for (uint32_t p = s; p < t; ++p) {
+      const uint2 pr = pairs[p];
+      rep[pr.x] = pr.y;
+    }
+  }
+}
+
 template <typename F>
 float time_ms(F f, int reps) {
   hipEvent_t a, b;
@@ -241,6 +307,9 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&pairs, 8 * n);
   (void)hipMalloc(&split, 4 * (nb + 1));
   (void)hipMalloc(&npairs, 4 * (nb + 1));
+  uint32_t* bnd;
+  (void)hipMalloc(&bnd, 4ull * nb * (kNW + 1));
+  const uint32_t win_rows = static_cast<uint32_t>((n + kNW - 1) / kNW);
   k_rows<<<4096, 256>>>(key, has, n, n * 4 / 5);
   void* ws;
   (void)hipMalloc(&ws, L.total);
@@ -306,6 +375,23 @@ int main(int argc, char** argv) {
       {"GH split n/3 + pair scatter", [&] { G(kGH, n32 / 3); }, true},
       {"GH split n/4 + pair scatter", [&] { G(kGH, n32 / 4); }, true},
       {"GP all pairs + pair scatter", [&] { G(kGH, 0); }, true},
+      {"GW window pairs + L2 window apply",
+       [&] {
+         k_group_x<kGW><<<nb, kGroupThreads>>>(rec, 0, fbase, bits, c, rep1, who, obj, split, pairs,
+                                               npairs, 0, 0xFFFFFFFEu, bnd, win_rows);
+         k_window_apply<<<kNW * 32, 1024>>>(pairs, fbase, bnd, nb, rep1, true);
+       },
+       true},
+      {"  GW group only",
+       [&] {
+         k_group_x<kGW><<<nb, kGroupThreads>>>(rec, 0, fbase, bits, c, rep1, who, obj, split, pairs,
+                                               npairs, 0, 0xFFFFFFFEu, bnd, win_rows);
+       },
+       false},
+      {"  AW apply alone (XCD windows)",
+       [&] { k_window_apply<<<kNW * 32, 1024>>>(pairs, fbase, bnd, nb, rep1, true); }, false},
+      {"  AW apply alone (no XCD mapping)",
+       [&] { k_window_apply<<<kNW * 32, 1024>>>(pairs, fbase, bnd, nb, rep1, false); }, false},
       {"  pairs only (GP without scatter)",
        [&] {
          k_group_x<kGH><<<nb, kGroupThreads>>>(rec, 0, fbase, bits, c, rep1, who, obj, split, pairs,
@@ -356,14 +442,14 @@ int main(int argc, char** argv) {
            (unsigned long long)nc, (unsigned long long)nl, (unsigned long long)bad);
   }
   // the coarse pass with and without its rep = rank stores (two-level only)
+  uint32_t* run_s = reinterpret_cast<uint32_t*>(w + L.run_s);
+  uint32_t* run_l = reinterpret_cast<uint32_t*>(w + L.run_l);
+  uint32_t* segtot = reinterpret_cast<uint32_t*>(w + L.segtot);
+  uint32_t* fine = reinterpret_cast<uint32_t*>(w + L.fine);
+  uint32_t* ovf = reinterpret_cast<uint32_t*>(w + L.ovf);
+  uint4* rec1 = reinterpret_cast<uint4*>(w + L.rec1);
+  const RowsIn in{key, has, nullptr, 0};
   if (L.cbits) {
-    uint32_t* run_s = reinterpret_cast<uint32_t*>(w + L.run_s);
-    uint32_t* run_l = reinterpret_cast<uint32_t*>(w + L.run_l);
-    uint32_t* segtot = reinterpret_cast<uint32_t*>(w + L.segtot);
-    uint32_t* fine = reinterpret_cast<uint32_t*>(w + L.fine);
-    uint32_t* ovf = reinterpret_cast<uint32_t*>(w + L.ovf);
-    uint4* rec1 = reinterpret_cast<uint4*>(w + L.rec1);
-    const RowsIn in{key, has, nullptr, 0};
     vs.push_back({"P1 coarse pass with rep = rank",
                   [&] {
                     k_zero_runs<<<1, 64>>>(segtot, ovf);

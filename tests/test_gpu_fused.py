@@ -35,6 +35,16 @@ def _ref_lists(key, has, valid, rank, first_rank, chunk):
     """The oracle's write set in rank space: rows ordered by rank, grouped,
     then link_batch; lists sorted like split_link_lists."""
     n = key.size
+    if rank is None and first_rank:
+        # the chunk rule runs on GLOBAL ranks (chunk = rank // chunk_rows):
+        # the oracle sees first_rank keyless rows in front, then drops them
+        pad = np.zeros(first_rank, np.uint64)
+        c, lr, lo = _ref_lists(np.concatenate([pad, key]),
+                               np.concatenate([np.zeros(first_rank, np.uint8), has]),
+                               None if valid is None else
+                               np.concatenate([np.zeros(first_rank, np.uint8), valid]),
+                               None, 0, chunk)
+        return c[c >= first_rank], lr, lo
     r = (np.arange(n, dtype=np.uint64) + first_rank).astype(np.uint32) if rank is None else rank
     order = np.argsort(r, kind="stable")
     rep = O.group_reps(key[order], has[order], chunk)  # ranks relative to the sorted rows
