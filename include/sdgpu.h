@@ -299,11 +299,23 @@ int sdgpu_comm_wait(sdgpu_comm *comm, void *stream);
 typedef struct sdgpu_comm_stats_t {
   uint64_t calls;
   uint64_t rows_sent, rows_received;      /* keyed rows to / from every rank incl. self */
-  uint64_t bytes_sent, bytes_received;    /* payload incl. the self share */
+  uint64_t bytes_sent, bytes_received;    /* payload incl. the self share: 12-B records,
+                                             plus the reps this rank returned as an owner
+                                             (sent) / got back as a source (received) */
   uint64_t bytes_remote;                  /* payload that crossed to / from other ranks */
   double count_wait_ms;                   /* host ms until the counts were known */
   double host_ms;                         /* host ms inside the exchange calls */
+  uint64_t rows_returned;                 /* (ABI 4) received rows whose rep went back */
 } sdgpu_comm_stats_t;
+/* Return leg of the exchange (ABI 4).  COMPACT (the default): an owner sends
+ * back only the received rows whose rep is not their own rank, as 8-B {index,
+ * rep} pairs after a second count exchange (a second host synchronisation);
+ * ~1.6 B per row instead of 4 at config 4's 20 % duplicates.  FULL: every
+ * received row's 4-B rep, one synchronisation per call.  All ranks of a
+ * communicator must use the same mode. */
+#define SDGPU_RETURN_FULL 0
+#define SDGPU_RETURN_COMPACT 1
+int sdgpu_comm_set_return(sdgpu_comm *comm, int mode);
 int sdgpu_comm_stats(sdgpu_comm *comm, sdgpu_comm_stats_t *out);
 /* Collective, one process per GPU (RCCL): every rank calls it with its own
  * rows (global ranks in d_rank, required, each < 2^31); rep for each of its

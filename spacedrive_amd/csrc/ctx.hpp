@@ -162,7 +162,7 @@ struct sdgpu_ctx {
   hipEvent_t handover = nullptr;
   // sharded grouping (shard.cpp): send records / positions / counts, received
   // records, their reps, the returned reps; host copies of the counts
-  DevBuf xs_send, xs_recv, xs_back;
+  DevBuf xs_send, xs_recv, xs_back, xs_ret, xs_rback;
   PinBuf xs_counts;
   bool timing = false;
   bool io_uring = false;  // sdgpu_identify_files reads through io_uring (uring.hpp)

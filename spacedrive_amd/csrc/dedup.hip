@@ -1723,7 +1723,8 @@ __global__ void k_dest_counts(const uint32_t* __restrict__ offs, uint32_t world,
 }
 
 // rep[i] of the sender's rows from the reps returned in send order: row i was
-// sent at position pos[i] (~0: no key, it keeps its own rank).
+// sent at position pos[i] (~0: no key, it keeps its own rank); back[p] == ~0
+// (compact return: no pair came back for it) also keeps the rank.
 __global__ __launch_bounds__(256) void k_gather_rep(const uint32_t* __restrict__ back,
                                                     const uint32_t* __restrict__ pos,
                                                     const uint32_t* __restrict__ rank, uint64_t n,
@@ -1731,7 +1732,111 @@ __global__ __launch_bounds__(256) void k_gather_rep(const uint32_t* __restrict__
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) {
     const uint32_t p = pos[i];
-    rep[i] = p == 0xFFFFFFFFu ? rank[i] : back[p];
+    const uint32_t b = back[p == 0xFFFFFFFFu ? 0u : p];
+    rep[i] = (p == 0xFFFFFFFFu || b == 0xFFFFFFFFu) ? rank[i] : b;
+  }
+}
+
+// Compact return leg of the exchange (round 4): an owner sends back only the
+// received rows whose rep is not their own rank, as {index of the row inside
+// its (source -> owner) message, rep} -- 8 B per linked row instead of 4 B
+// per row.  Tiles of kRetTile received rows never straddle a source's
+// segment (the host lays them out per segment, RetTiles), so the pairs come
+// out grouped by source in row order: tile counts, one scan, ranked writes.
+constexpr int kRetThreads = 256;
+constexpr int kRetRows = 16;
+constexpr uint32_t kRetTile = kRetThreads * kRetRows;
+
+__device__ __forceinline__ uint32_t ret_segment(const RetTiles& st, uint32_t blk) {
+  uint32_t p = 0;
+  while (p + 1 < st.world && st.tstart[p + 1] <= blk) ++p;
+  return p;
+}
+
+__global__ __launch_bounds__(kRetThreads) void k_ret_count(RetTiles st, const uint3* __restrict__ rrec,
+                                                           const uint32_t* __restrict__ rrep,
+                                                           uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t sc[kRetThreads / 64];
+  const uint32_t blk = blockIdx.x;
+  uint32_t c = 0;
+  if (blk < st.tstart[st.world]) {
+    const uint32_t p = ret_segment(st, blk);
+    const uint32_t k0 = st.roff[p] + (blk - st.tstart[p]) * kRetTile, k1 = st.roff[p + 1];
+#pragma unroll
+    for (int u = 0; u < kRetRows; ++u) {
+      const uint32_t k = k0 + u * kRetThreads + threadIdx.x;
+      if (k < k1) c += rrep[k] != rrec[k].z;
+    }
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+  if (__lane_id() == 0) sc[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blk] = sc[0] + sc[1] + sc[2] + sc[3];
+}
+
+// cnt: exclusive scan of the tile counts (cnt[tiles] = total).  retcnt[p] =
+// pairs for source p (int64, the count exchange's unit).
+__global__ __launch_bounds__(kRetThreads) void k_ret_write(RetTiles st, const uint3* __restrict__ rrec,
+                                                           const uint32_t* __restrict__ rrep,
+                                                           const uint32_t* __restrict__ cnt,
+                                                           uint2* __restrict__ ret,
+                                                           int64_t* __restrict__ retcnt) {
+  __shared__ uint32_t oc[kRetRows][kRetThreads / 64];
+  const uint32_t blk = blockIdx.x, lane = __lane_id(), w = threadIdx.x >> 6;
+  if (blk == 0 && threadIdx.x < st.world)
+    retcnt[threadIdx.x] = static_cast<int64_t>(cnt[st.tstart[threadIdx.x + 1]]) -
+                          static_cast<int64_t>(cnt[st.tstart[threadIdx.x]]);
+  if (blk >= st.tstart[st.world]) return;  // the one block of an empty receive
+  const uint32_t p = ret_segment(st, blk);
+  const uint32_t k0 = st.roff[p] + (blk - st.tstart[p]) * kRetTile, k1 = st.roff[p + 1];
+  const uint64_t lt = (1ull << lane) - 1ull;
+  bool f[kRetRows];
+  uint32_t v[kRetRows], pr[kRetRows];
+#pragma unroll
+  for (int u = 0; u < kRetRows; ++u) {
+    const uint32_t k = k0 + u * kRetThreads + threadIdx.x;
+    const uint32_t kk = k < k1 ? k : k1 - 1;
+    v[u] = rrep[kk];
+    f[u] = k < k1 && v[u] != rrec[kk].z;
+    const uint64_t b = __ballot(f[u]);
+    pr[u] = __popcll(b & lt);
+    if (lane == 0) oc[u][w] = __popcll(b);
+  }
+  __syncthreads();
+  static_assert(kRetRows * (kRetThreads / 64) == 64, "one wave scans the (row step, wave) counts");
+  if (threadIdx.x < 64) {
+    uint32_t* e = &oc[0][0];
+    const uint32_t a = e[lane];
+    uint32_t inc = a;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
+    }
+    e[lane] = cnt[blk] - cnt[st.tstart[p]] + inc - a;  // index inside the segment's pairs
+  }
+  __syncthreads();
+  const uint32_t seg0 = cnt[st.tstart[p]];
+#pragma unroll
+  for (int u = 0; u < kRetRows; ++u)
+    if (f[u]) {
+      const uint32_t k = k0 + u * kRetThreads + threadIdx.x;
+      ret[seg0 + oc[u][w] + pr[u]] = make_uint2(k - st.roff[p], v[u]);
+    }
+}
+
+// Source side: back[soff[d] + idx] = rep for every pair received from owner d
+// (pairs of d at [poff[d], poff[d + 1]) of rback); back was set to ~0.
+__global__ __launch_bounds__(256) void k_ret_apply(RetApply ap, const uint2* __restrict__ rback,
+                                                   uint32_t* __restrict__ back) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+  const uint64_t total = ap.poff[ap.world];
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < total; i += stride) {
+    uint32_t d = 0;
+    while (d + 1 < ap.world && ap.poff[d + 1] <= i) ++d;
+    const uint2 q = rback[i];
+    back[ap.soff[d] + q.x] = q.y;
   }
 }
 
@@ -2124,6 +2229,46 @@ hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
                                  s, timer);
   if (e != hipSuccess) return e;
   k_dest_counts<<<1, 64, 0, s>>>(hist, world, d_dest_counts);
+  return hipGetLastError();
+}
+
+uint32_t ret_tiles(const RetTiles& st) { return st.tstart[st.world]; }
+
+size_t ret_workspace_bytes(uint32_t tiles) {
+  return align_up(4ull * (tiles + 2), 256) + align_up(4ull * (scan::tiles_for(tiles + 1) + 1), 256);
+}
+
+hipError_t ret_compact_launch(const RetTiles& st, const uint32_t* rrec, const uint32_t* rrep,
+                              uint2* ret, int64_t* retcnt, void* ws, hipStream_t s, KTimer* timer) {
+  const uint32_t nt = st.tstart[st.world];
+  uint8_t* b = static_cast<uint8_t*>(ws);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(b);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(b + align_up(4ull * (nt + 2), 256));
+  KScope k(timer, "ret_compact", s);
+  const uint32_t g = nt ? nt : 1;  // one block writes the (zero) counts of an empty receive
+  const uint3* rr = reinterpret_cast<const uint3*>(rrec);
+  if (nt) {
+    k_ret_count<<<nt, kRetThreads, 0, s>>>(st, rr, rrep, cnt);
+    scan::exclusive(cnt, nt, cnt, tiles, nullptr, s);
+  } else {
+    const hipError_t e = hipMemsetAsync(cnt, 0, 4, s);
+    if (e != hipSuccess) return e;
+  }
+  k_ret_write<<<g, kRetThreads, 0, s>>>(st, rr, rrep, cnt, ret, retcnt);
+  return hipGetLastError();
+}
+
+hipError_t ret_apply_launch(const RetApply& ap, const uint2* rback, uint32_t* back,
+                            uint64_t n_back, hipStream_t s) {
+  if (n_back) {
+    const hipError_t e = hipMemsetAsync(back, 0xFF, 4 * n_back, s);
+    if (e != hipSuccess) return e;
+  }
+  const uint64_t total = ap.poff[ap.world];
+  if (total) {
+    const uint64_t g = std::min<uint64_t>((total + 255) / 256, 16384);
+    k_ret_apply<<<static_cast<uint32_t>(g), 256, 0, s>>>(ap, rback, back);
+  }
   return hipGetLastError();
 }
 

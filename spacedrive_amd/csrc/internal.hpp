@@ -167,6 +167,34 @@ size_t keyless_workspace_bytes(uint64_t n);
 hipError_t keyless_list_launch(const uint8_t* has, const uint8_t* valid, const uint32_t* rank,
                                uint32_t first_rank, uint64_t n, uint32_t* who, uint32_t* counts,
                                void* ws, hipStream_t s, KTimer* timer = nullptr);
+// Compact return leg of the exchange (dedup.hip): the received rows are cut
+// into tiles of 4096 that never straddle a source's segment [roff[p],
+// roff[p + 1]); tstart[p] = first tile of segment p, tstart[world] = tiles.
+constexpr uint32_t kMaxWorld = 64;
+struct RetTiles {
+  uint32_t world;
+  uint32_t tstart[kMaxWorld + 1];
+  uint32_t roff[kMaxWorld + 1];
+};
+// Source side: pairs from owner d at [poff[d], poff[d + 1]) of the received
+// pairs; its rows were sent at [soff[d], ...) of the send order.
+struct RetApply {
+  uint32_t world;
+  uint64_t poff[kMaxWorld + 1];
+  uint32_t soff[kMaxWorld + 1];
+};
+constexpr uint32_t kRetTileRows = 4096;
+uint32_t ret_tiles(const RetTiles& st);
+size_t ret_workspace_bytes(uint32_t tiles);
+// pairs {index in the source's message, rep} of the received rows whose rep
+// is not their rank (rrec: 12-B records {key, rank}), grouped by source;
+// retcnt[p] (int64, device) = pairs for source p.  No synchronisation.
+hipError_t ret_compact_launch(const RetTiles& st, const uint32_t* rrec, const uint32_t* rrep,
+                              uint2* ret, int64_t* retcnt, void* ws, hipStream_t s,
+                              KTimer* timer = nullptr);
+// back[0..n_back) = ~0, then back[soff[d] + idx] = rep for every received pair
+hipError_t ret_apply_launch(const RetApply& ap, const uint2* rback, uint32_t* back,
+                            uint64_t n_back, hipStream_t s);
 size_t shard_workspace_bytes(uint32_t shard_bits);
 // Shard of a key = top shard_bits bits of mix64(key) (rows_device.hpp row_hash).
 hipError_t shard_count_launch(const uint64_t* key, const uint8_t* has_key, uint64_t n,

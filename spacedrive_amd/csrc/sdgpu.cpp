@@ -336,7 +336,7 @@ int sdgpu_close(sdgpu_ctx* c) {
   }
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->plan_pin.p) (void)hipHostFree(c->plan_pin.p);
-  for (DevBuf* b : {&c->xs_send, &c->xs_recv, &c->xs_back})
+  for (DevBuf* b : {&c->xs_send, &c->xs_recv, &c->xs_back, &c->xs_ret, &c->xs_rback})
     if (b->p) (void)hipFree(b->p);
   if (c->xs_counts.p) (void)hipHostFree(c->xs_counts.p);
   if (c->handover) (void)hipEventDestroy(c->handover);

@@ -48,6 +48,10 @@ struct sdgpu_comm {
   int timeout_ms = 0;
   bool aborted = false;
   hipStream_t last_stream = nullptr;  // stream of the last exchange (sdgpu_comm_wait)
+  // return leg: SDGPU_RETURN_COMPACT (only the linked rows' reps travel back,
+  // after a second count exchange) or SDGPU_RETURN_FULL (4 B per row, no
+  // second synchronisation).  Every rank of a communicator must agree.
+  int return_mode = SDGPU_RETURN_COMPACT;
   sdgpu_comm_stats_t stats{};
 };
 
@@ -229,9 +233,15 @@ struct RankJob {
   uint32_t* rrep = nullptr;   // [m]
   uint8_t* rvalid = nullptr;  // [m]
   uint32_t* back = nullptr;   // [total] reps of the sent rows, in send order
-  int64_t* h = nullptr;       // pinned [2W]: send counts, receive counts
+  int64_t* h = nullptr;       // pinned [4W]: send, receive counts; pairs out, pairs in
   std::vector<uint64_t> scnt, rcnt, soff, roff;
   uint64_t total = 0, m = 0;
+  // compact return leg
+  uint2* ret = nullptr;       // [m] pairs this owner returns, grouped by source
+  uint2* rback = nullptr;     // pairs returned to this source
+  int64_t* retcnt = nullptr;  // [W] pairs to each source (device)
+  int64_t* rretcnt = nullptr; // [W] pairs from each owner (device)
+  std::vector<uint64_t> pcnt, pin, poff, pioff;
 };
 
 // One all-to-all round: rank j sends bytes(j, p) from sendp(j, p) to every p
@@ -332,14 +342,18 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
     const size_t o_pos = align_up(12 * n, 256);
     const size_t o_dcnt = align_up(o_pos + 4 * n, 256);
     const size_t o_rcnt = align_up(o_dcnt + 8ull * W, 256);
-    SD_TRY_RC(ensure_dev(j.c, j.c->xs_send, o_rcnt + 8ull * W));
+    const size_t o_pcnt = align_up(o_rcnt + 8ull * W, 256);
+    const size_t o_rpcnt = align_up(o_pcnt + 8ull * W, 256);
+    SD_TRY_RC(ensure_dev(j.c, j.c->xs_send, o_rpcnt + 8ull * W));
     SD_TRY_RC(ensure_dev(j.c, j.c->shard_ws, shard_workspace_bytes(kXShardBits)));
-    SD_TRY_RC(ensure_pin(j.c->xs_counts, 16ull * W));
+    SD_TRY_RC(ensure_pin(j.c->xs_counts, 32ull * W));
     uint8_t* b = static_cast<uint8_t*>(j.c->xs_send.p);
     j.srec = reinterpret_cast<uint32_t*>(b);
     j.spos = reinterpret_cast<uint32_t*>(b + o_pos);
     j.dcnt = reinterpret_cast<int64_t*>(b + o_dcnt);
     j.rcnt_d = reinterpret_cast<int64_t*>(b + o_rcnt);
+    j.retcnt = reinterpret_cast<int64_t*>(b + o_pcnt);
+    j.rretcnt = reinterpret_cast<int64_t*>(b + o_rpcnt);
     j.h = static_cast<int64_t*>(j.c->xs_counts.p);
     SD_TRY(shard_exchange_launch(j.key, j.has, j.rank, n, kXShardBits, W, nullptr, nullptr,
                                  j.srec, j.spos, j.dcnt, j.c->shard_ws.p, j.s, j.c->kt()));
@@ -402,11 +416,84 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
     SD_TRY_RC(group_with_index(j.c, j.idx, in, chunk_rows, j.rrep, j.rvalid, j.s));
   }
   // 5. reps back to their sources, gathered to row order
-  SD_TRY_RC(alltoallv(
-      J, W, deadline, [](RankJob& j, int p) -> void* { return j.rrep + j.roff[p]; },
-      [](RankJob& j, int p) -> void* { return j.back + j.soff[p]; },
-      [](RankJob& j, int p) -> size_t { return 4 * j.rcnt[p]; },
-      [](RankJob& j, int p) -> size_t { return 4 * j.scnt[p]; }));
+  const bool compact = J[0].comm->return_mode == SDGPU_RETURN_COMPACT;
+  if (!compact) {
+    SD_TRY_RC(alltoallv(
+        J, W, deadline, [](RankJob& j, int p) -> void* { return j.rrep + j.roff[p]; },
+        [](RankJob& j, int p) -> void* { return j.back + j.soff[p]; },
+        [](RankJob& j, int p) -> size_t { return 4 * j.rcnt[p]; },
+        [](RankJob& j, int p) -> size_t { return 4 * j.scnt[p]; }));
+  } else {
+    // only the rows whose rep is not their own rank go back, as {index in
+    // the source's message, rep}: the owners compact them per source, the
+    // pair counts cross (the step's second host synchronisation), the pairs
+    // follow, and each source spreads them over its send-order array
+    for (auto& j : J) {
+      SD_TRY(hipSetDevice(j.c->device));
+      RetTiles st{};
+      st.world = static_cast<uint32_t>(W);
+      for (int p = 0; p < W; ++p) {
+        st.roff[p] = static_cast<uint32_t>(j.roff[p]);
+        st.tstart[p + 1] = st.tstart[p] +
+                           static_cast<uint32_t>((j.rcnt[p] + kRetTileRows - 1) / kRetTileRows);
+      }
+      st.roff[W] = static_cast<uint32_t>(j.roff[W]);
+      const size_t o_ws = align_up(8 * j.m + 8, 256);
+      SD_TRY_RC(ensure_dev(j.c, j.c->xs_ret, o_ws + ret_workspace_bytes(ret_tiles(st))));
+      j.ret = static_cast<uint2*>(j.c->xs_ret.p);
+      SD_TRY(ret_compact_launch(st, j.rrec, j.rrep, j.ret,
+                                j.retcnt, static_cast<uint8_t*>(j.c->xs_ret.p) + o_ws, j.s,
+                                j.c->kt()));
+    }
+    SD_TRY_RC(alltoallv(
+        J, W, deadline, [](RankJob& j, int p) -> void* { return j.retcnt + p; },
+        [](RankJob& j, int p) -> void* { return j.rretcnt + p; },
+        [](RankJob&, int) -> size_t { return 8; }, [](RankJob&, int) -> size_t { return 8; }));
+    for (auto& j : J) {
+      SD_TRY(hipSetDevice(j.c->device));
+      SD_TRY(hipMemcpyAsync(j.h + 2 * W, j.retcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
+      SD_TRY(hipMemcpyAsync(j.h + 3 * W, j.rretcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
+    }
+    for (auto& j : J) {
+      SD_TRY(hipSetDevice(j.c->device));
+      if (j.comm->transport == SDGPU_TRANSPORT_RCCL) {
+        SD_TRY_RC(stream_wait(j.comm, j.s, deadline));
+      } else {
+        SD_TRY(hipStreamSynchronize(j.s));
+      }
+      j.pcnt.assign(W, 0);
+      j.pin.assign(W, 0);
+      j.poff.assign(W + 1, 0);
+      j.pioff.assign(W + 1, 0);
+      for (int p = 0; p < W; ++p) {
+        const int64_t a = j.h[2 * W + p], b = j.h[3 * W + p];
+        if (a < 0 || b < 0 || static_cast<uint64_t>(a) > j.rcnt[p] ||
+            static_cast<uint64_t>(b) > j.scnt[p])
+          return -EPROTO;
+        j.pcnt[p] = static_cast<uint64_t>(a);
+        j.pin[p] = static_cast<uint64_t>(b);
+        j.poff[p + 1] = j.poff[p] + j.pcnt[p];
+        j.pioff[p + 1] = j.pioff[p] + j.pin[p];
+      }
+      SD_TRY_RC(ensure_dev(j.c, j.c->xs_rback, 8 * j.pioff[W] + 256));
+      j.rback = static_cast<uint2*>(j.c->xs_rback.p);
+    }
+    SD_TRY_RC(alltoallv(
+        J, W, deadline, [](RankJob& j, int p) -> void* { return j.ret + j.poff[p]; },
+        [](RankJob& j, int p) -> void* { return j.rback + j.pioff[p]; },
+        [](RankJob& j, int p) -> size_t { return 8 * j.pcnt[p]; },
+        [](RankJob& j, int p) -> size_t { return 8 * j.pin[p]; }));
+    for (auto& j : J) {
+      SD_TRY(hipSetDevice(j.c->device));
+      RetApply ap{};
+      ap.world = static_cast<uint32_t>(W);
+      for (int p = 0; p <= W; ++p) {
+        ap.poff[p] = j.pioff[p];
+        ap.soff[p] = static_cast<uint32_t>(j.soff[p]);
+      }
+      SD_TRY(ret_apply_launch(ap, j.rback, j.back, j.total, j.s));
+    }
+  }
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
     SD_TRY(gather_rep_launch(j.back, j.spos, j.rank, j.n, j.rep, j.s));
@@ -414,15 +501,29 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
   const double call_ms =
       std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
   for (auto& j : J) {
-    // payload of this rank: records out + reps back, and what it received
-    const uint64_t self_rows = j.scnt[j.comm->rank];
+    // payload of this rank: the 12-B records it sent, the reps it returned
+    // as an owner (4 B per received row, or 8-B pairs for the linked ones),
+    // and the same for what it received
+    const int me = j.comm->rank;
+    const uint64_t self_rows = j.scnt[me];
     sdgpu_comm_stats_t& st = j.comm->stats;
     st.calls += 1;
     st.rows_sent += j.total;
     st.rows_received += j.m;
-    st.bytes_sent += 16 * j.total;      // 12-B records out, 4-B reps back
-    st.bytes_received += 16 * j.m;
-    st.bytes_remote += 16 * (j.total - self_rows) + 16 * (j.m - j.rcnt[j.comm->rank]);
+    if (compact) {
+      const uint64_t out_p = j.poff[W], in_p = j.pioff[W];
+      st.rows_returned += out_p;
+      st.bytes_sent += 12 * j.total + 8 * out_p;
+      st.bytes_received += 12 * j.m + 8 * in_p;
+      st.bytes_remote += 12 * (j.total - self_rows) + 8 * (out_p - j.pcnt[me]) +
+                         12 * (j.m - j.rcnt[me]) + 8 * (in_p - j.pin[me]);
+    } else {
+      st.rows_returned += j.m;
+      st.bytes_sent += 12 * j.total + 4 * j.m;
+      st.bytes_received += 12 * j.m + 4 * j.total;
+      st.bytes_remote += 12 * (j.total - self_rows) + 4 * (j.m - j.rcnt[me]) +
+                         12 * (j.m - j.rcnt[me]) + 4 * (j.total - self_rows);
+    }
     st.count_wait_ms += count_ms;
     st.host_ms += call_ms;
     j.comm->last_stream = j.s;
@@ -509,6 +610,12 @@ int sdgpu_comm_wait(sdgpu_comm* m, void* stream) {
   if (m->transport != SDGPU_TRANSPORT_RCCL || !m->nccl)
     return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
   return stream_wait(m, s, deadline_of(m->timeout_ms));
+}
+
+int sdgpu_comm_set_return(sdgpu_comm* m, int mode) {
+  if (!m || (mode != SDGPU_RETURN_FULL && mode != SDGPU_RETURN_COMPACT)) return -EINVAL;
+  m->return_mode = mode;
+  return 0;
 }
 
 int sdgpu_comm_stats(sdgpu_comm* m, sdgpu_comm_stats_t* out) {

@@ -274,12 +274,16 @@ def dedup_batch(key, has_key, first_rank: int, index: ObjectIndex | None = None,
 TRANSPORT_AUTO, TRANSPORT_RCCL, TRANSPORT_PEER = 0, 1, 2
 
 
+RETURN_FULL, RETURN_COMPACT = 0, 1  # SDGPU_RETURN_*
+
+
 class CommStats(ctypes.Structure):
     """sdgpu_comm_stats_t (include/sdgpu.h)."""
     _fields_ = [("calls", ctypes.c_uint64), ("rows_sent", ctypes.c_uint64),
                 ("rows_received", ctypes.c_uint64), ("bytes_sent", ctypes.c_uint64),
                 ("bytes_received", ctypes.c_uint64), ("bytes_remote", ctypes.c_uint64),
-                ("count_wait_ms", ctypes.c_double), ("host_ms", ctypes.c_double)]
+                ("count_wait_ms", ctypes.c_double), ("host_ms", ctypes.c_double),
+                ("rows_returned", ctypes.c_uint64)]
 
 
 class Comm:
@@ -321,6 +325,11 @@ class Comm:
     def wait(self, stream=None):
         """Bounded wait for the last exchange's stream (sdgpu_comm_wait)."""
         check(self.ctx.lib.sdgpu_comm_wait(self.h, stream), "sdgpu_comm_wait")
+
+    def set_return(self, mode: int):
+        """SDGPU_RETURN_COMPACT (default: only the linked rows' reps travel
+        back, one more count exchange) or SDGPU_RETURN_FULL (4 B per row)."""
+        check(self.ctx.lib.sdgpu_comm_set_return(self.h, mode), "sdgpu_comm_set_return")
 
     def stats(self) -> dict:
         """Cumulative exchange volume / host time of this rank (sdgpu_comm_stats)."""

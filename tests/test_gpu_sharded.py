@@ -44,8 +44,8 @@ def test_dedup_sharded_two_level_per_rank(ctxs):
     np.testing.assert_array_equal(rep, O.group_reps(k, h, 100))
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_sharded_all_device_with_index_batches(ctxs, world):
+@pytest.mark.parametrize("world,mode", [(2, 1), (3, 1), (8, 1), (3, 0)])
+def test_sharded_all_device_with_index_batches(ctxs, world, mode):
     """Device API over `world` ranks, two batches through per-rank Object
     indexes (each rank holds its shards' keys), plus pre-existing Objects
     registered on every rank: equals the oracle over the union."""
@@ -58,6 +58,8 @@ def test_sharded_all_device_with_index_batches(ctxs, world):
     eh = np.arange(ek.size, dtype=np.uint32) + 5
     comms = dedup.Comm.init_all(ctxs[:world])
     assert comms[0].info() == (world, 0, dedup.TRANSPORT_PEER)
+    for c in comms:
+        c.set_return(mode)  # compact (1) / full (0) return leg
     idxs = [dedup.ObjectIndex(c, 1000) for c in ctxs[:world]]
     for r, ix in enumerate(idxs):  # every rank gets the full list, keeps its share
         ix.add_objects(torch.from_numpy(ek.view(np.int64)).cuda(),
@@ -112,8 +114,20 @@ def test_rccl_transport_one_rank(ctx):
     keyed = int(h.sum())
     assert st["calls"] == 5
     assert st["rows_sent"] == st["rows_received"] == 4 * keyed   # 3 whole + 2 halves
-    assert st["bytes_sent"] == 16 * st["rows_sent"]
+    # compact return leg (the default): 12-B records out,
+    # 8-B {index, rep} pairs back for the linked rows only
+    linked = int(np.count_nonzero(ref != np.arange(ref.size)))
+    assert st["rows_returned"] == 4 * linked
+    assert st["bytes_sent"] == 12 * st["rows_sent"] + 8 * st["rows_returned"]
+    assert st["bytes_sent"] / st["rows_sent"] <= 14.0
     assert st["bytes_remote"] == 0    # one rank: every record is a self-send
+    # the full return leg (4 B per row, one synchronisation): same reps
+    comm.set_return(dedup.RETURN_FULL)
+    rep = dedup.group_sharded(dk, dh, dr, comm, None, 100)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(rep.cpu().numpy().view(np.uint32), ref)
+    st2 = comm.stats()
+    assert st2["bytes_sent"] - st["bytes_sent"] == 16 * keyed
     comm.close()
 
 
