@@ -115,6 +115,8 @@ def k1_split(lens: np.ndarray):
 
 # single-file latency sizes (the GPU / CPU crossover for the watcher callers,
 # include/sdgpu.h): one chunk chain, 16 / 32 / 64 KiB messages, a sampled file
+BURST_FILES = 64
+BURST_SIZES = (("4KiB", 4096), ("64KiB", 65536), ("1MiB", 1 << 20))
 SINGLE_SIZES = (("4KiB", 4096), ("16KiB", 16384), ("32KiB", 32768), ("64KiB", 65536),
                 ("1MiB", 1 << 20))
 
@@ -582,9 +584,56 @@ class Runner:
             res["service_breakdown_4KiB_cas"] = self.ctx.latency_service_diag()
             self.ctx.latency_service(False)
             self._single_sample = [(os.path.join(root, n), s) for n, s in SINGLE_SIZES]
+            res["burst"] = self.run_burst(root, rng)
         finally:
             self._single_root = root
         return res
+
+    def run_burst(self, root, rng, reps=40):
+        """Bursts of single-file calls: BURST_FILES files
+        that arrive together -- a folder copied into a watched location
+        (watcher/utils.rs:236,411,467) or a non-indexed listing
+        (non_indexed.rs:161) -- as ONE sdgpu_identify_files batch (what a
+        coalescing host does, crates/sd-core-gpu/src/burst.rs) against the
+        resident service one call at a time.  Median wall microseconds per
+        burst; the CPU port's figures for the same files are in
+        cpu_baseline.single_file_burst (merged here after that leg)."""
+        from spacedrive_amd import cas
+        from spacedrive_amd import file_identifier as FI
+        out, self._burst_sample = {}, []
+        for name, size in BURST_SIZES:
+            paths = []
+            for i in range(BURST_FILES):
+                p = os.path.join(root, f"burst_{name}_{i}")
+                rng.integers(0, 256, size, dtype=np.uint8).tofile(p)
+                paths.append(p)
+            pl = FI.PathList(paths)
+            sizes = np.full(BURST_FILES, size, np.uint64)
+            for _ in range(5):
+                r = FI.identify(pl, sizes, ctx=self.ctx)
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                r = FI.identify(pl, sizes, ctx=self.ctx)
+                ts.append(time.perf_counter() - t0)
+            assert int(np.count_nonzero(r.status)) == 0
+            batch = float(np.median(ts) * 1e6)
+            self.ctx.latency_service(True)
+            for p in paths[:8]:
+                cas.generate_cas_id(p, size, self.ctx)
+            ts = []
+            for _ in range(max(3, reps // 4)):
+                t0 = time.perf_counter()
+                for p in paths:
+                    cas.generate_cas_id(p, size, self.ctx)
+                ts.append(time.perf_counter() - t0)
+            self.ctx.latency_service(False)
+            seq = float(np.median(ts) * 1e6)
+            out[name] = {"files": BURST_FILES, "file_bytes": size,
+                         "gpu_batch_burst_us": batch, "gpu_batch_per_file_us": batch / BURST_FILES,
+                         "gpu_service_sequential_burst_us": seq}
+            self._burst_sample.append((name, pl, sizes, r.cas8.copy()))
+        return out
 
     # ---------------------------------------------------------------- config 4
     def run_dedup(self, steps, warmup):
@@ -1043,11 +1092,32 @@ class Runner:
                         fn()
                         ts.append(time.perf_counter() - t0)
                     single[f"{fn_name}_{name}_us"] = float(np.median(ts) * 1e6)
+        burst = None
+        if getattr(self, "_burst_sample", None):
+            # the same bursts through the CPU port behind the reference's reads:
+            # one thread (a runtime thread taking the calls one by one) and all
+            # threads (the blocking pool taking them concurrently)
+            burst = {}
+            for name, pl, sizes, gpu8 in self._burst_sample:
+                cpu8, bst = O.cas_paths_simd(pl, sizes, 1)
+                assert np.all(bst == 0)
+                mism = int(np.count_nonzero(np.any(cpu8 != gpu8, axis=1)))
+                assert mism == 0, f"burst {name}: {mism} GPU cas ids differ from the CPU port"
+                row = {"gpu_cas_id_mismatches": mism, "threads": threads}
+                for key_, th in (("cpu_1thread_burst_us", 1), ("cpu_threads_burst_us", threads)):
+                    ts = []
+                    for _ in range(30):
+                        t0 = time.perf_counter()
+                        O.cas_paths_simd(pl, sizes, th)
+                        ts.append(time.perf_counter() - t0)
+                    row[key_] = float(np.median(ts) * 1e6)
+                burst[name] = row
+            self._burst_sample = None
         return {"value": reps * m / dt, "unit": "files/s", "cores": threads, "kind": "port",
                 "cores_note": cores_note, "gpu_cas_id_mismatches": sample_mism,
                 "value_1thread": one, "scalar_value": scalar,
                 "config1_dir": dir_res, "config3_checksum": ck,
-                "single_file_1thread": single,
+                "single_file_1thread": single, "single_file_burst": burst,
                 "sample": f"first {m} files of config 2 (their {int(h_len.sum())} window bytes "
                           f"in host RAM) hashed {reps}x, AVX2 8-way BLAKE3 port "
                           f"(oracle/sd_oracle.c orc_cas_batch_simd), {threads} threads, "
@@ -1280,6 +1350,15 @@ def main(argv=None, runner_cls=None, out=None):
         cpu = leg("cpu_baseline", R.cpu_baseline)
         if cpu:
             log("cpu:", json.dumps(cpu))
+            # bursts: the CPU port's times beside the GPU's, per burst size
+            gb = (comp.get("single_file_latency") or {}).get("burst") or {}
+            for name, row in (cpu.get("single_file_burst") or {}).items():
+                if name in gb:
+                    gb[name].update(row)
+                    gb[name]["gpu_batch_vs_cpu_1thread"] = (row["cpu_1thread_burst_us"] /
+                                                            gb[name]["gpu_batch_burst_us"])
+                    gb[name]["gpu_batch_vs_cpu_threads"] = (row["cpu_threads_burst_us"] /
+                                                            gb[name]["gpu_batch_burst_us"])
     line["cpu_baseline"] = cpu
     leg("cleanup", R.drop_samples)
     if "dedup" in comps:

@@ -14,6 +14,7 @@
 //! Not compiled in this repository (the image has no Rust toolchain); the
 //! symbols it calls are checked against include/sdgpu.h by tests/test_abi.py.
 
+pub mod burst;
 pub mod cas;
 pub mod hash;
 pub mod identifier;
@@ -36,6 +37,7 @@ unsafe impl Send for Gpu {}
 unsafe impl Sync for Gpu {}
 
 static GLOBAL: OnceLock<Arc<Gpu>> = OnceLock::new();
+static COALESCER: OnceLock<burst::Coalescer> = OnceLock::new();
 
 /// Opened once at `Node::new` (core/src/lib.rs:77); the drop-ins use it.
 pub fn init_global(device: i32) -> io::Result<()> {
@@ -46,6 +48,12 @@ pub fn init_global(device: i32) -> io::Result<()> {
 
 pub fn global() -> Arc<Gpu> {
     GLOBAL.get().expect("sd_core_gpu::init_global not called").clone()
+}
+
+/// The single-file callers' front door (burst.rs): per-call CPU / GPU policy
+/// and coalescing of concurrent calls into one batch.
+pub fn coalescer() -> &'static burst::Coalescer {
+    COALESCER.get_or_init(|| burst::Coalescer::new(global()))
 }
 
 pub(crate) fn check(rc: i32) -> io::Result<()> {
