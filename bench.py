@@ -757,16 +757,86 @@ class Runner:
                              "two_call = group_rows + link_batch_device above",
                      "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
                                  for k, v in fz_kt.items()}}
+        xmodel = None
+        if self.world == 1 and self.comm is None and not self.args.no_exchange_model:
+            try:
+                xmodel = self.exchange_model(key, has, rank, steps, warmup, 1e3 * t / steps)
+            except Exception as e:  # noqa: BLE001 -- reported, the leg goes on
+                log(f"bench: exchange model failed: {e!r}")
+                xmodel = {"error": repr(e)[:300]}
         full = None
         if self.world == 1 and self.args.dedup_full_rows:
             full = self.run_dedup_full(steps, warmup)
         return {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * t / steps,
                 "rank": "implicit (row order, 12-byte records)" if implicit else "explicit array",
                 "explicit_rank_ms_per_step": explicit_ms, "exchange": xchg, "roofline": roof, "config4_full_one_gpu": full,
-                "link_batch": link, "fused_job": fused,
+                "link_batch": link, "fused_job": fused, "predicted_scaling": xmodel,
                 "config": {"workload": "config4: 80% distinct u64 keys + 20% dups, 0.1% keyless",
                            "rows_per_gpu": per, "rows_total": total},
                 "kernels": kernels}
+
+    # per-direction rate of one xGMI link under RCCL's all-to-all: 153 GB/s per
+    # link (SURVEY §2.3 / BASELINE.md) at ~65 % protocol efficiency -- an
+    # ASSUMPTION of the model below, not a measurement (no 8-GPU node here)
+    XGMI_LINK_GBPS = 100.0
+
+    def exchange_model(self, key, has, rank, steps, warmup, local_ms):
+        """Predicted per-GPU config-4 step at N = 2 / 4 / 8 (DESIGN.md §6;
+        VERDICT r3 item 4).  The whole exchange path runs on this GPU through
+        a ONE-rank RCCL communicator -- partition by owner, count exchange +
+        host synchronisation, the records' all-to-all (a self send), the local
+        grouping of as many received rows as one GPU gets at any N (weak
+        scaling: every GPU sends its rows and receives ~as many), the compact
+        return (second count exchange + pairs) and the gather -- timed with
+        its kernels; only the xGMI time of the remote share is modelled:
+        every GPU sends rows/N of its rows to each peer over that peer's own
+        link (fully connected node), 12 B per record plus 8 B per returned
+        pair in the same direction."""
+        from spacedrive_amd import dedup
+        per = int(key.numel())
+        comm = dedup.Comm.init_rank(self.ctx, 1, 0, dedup.Comm.unique_id(),
+                                    timeout_ms=self.comm_timeout_ms)
+        try:
+            fn = lambda: dedup.group_sharded(key, has, rank, comm, None, 100)  # noqa: E731
+            fn()
+            comm.wait()
+            s0 = comm.stats()
+            t, kt = self.timed_kernels(fn, steps, warmup)
+            comm.wait()
+            s1 = comm.stats()
+            calls = max(1, s1["calls"] - s0["calls"])
+            linked_frac = (s1["rows_returned"] - s0["rows_returned"]) / max(
+                1, s1["rows_received"] - s0["rows_received"])
+            comm.set_return(dedup.RETURN_FULL)
+            fn()
+            comm.wait()
+            t_full = self.timed(fn, steps, warmup)
+            comm.wait()
+        finally:
+            comm.close()
+        reh = 1e3 * t / steps
+        pred = {}
+        for n_ in (2, 4, 8):
+            link_b = per / n_ * (12 + 8 * linked_frac)  # bytes per link direction
+            x_ms = link_b / (self.XGMI_LINK_GBPS * 1e9) * 1e3
+            step = reh + x_ms
+            pred[str(n_)] = {"step_ms": step, "xgmi_ms": x_ms, "bytes_per_link": int(link_b),
+                             "rows_per_s_total": n_ * per / (step * 1e-3),
+                             "weak_scaling_efficiency": local_ms / step}
+        return {"rehearsal_ms_per_step": reh, "rehearsal_full_return_ms_per_step":
+                1e3 * t_full / steps,
+                "count_wait_ms_per_call": (s1["count_wait_ms"] - s0["count_wait_ms"]) / calls,
+                "host_ms_per_call": (s1["host_ms"] - s0["host_ms"]) / calls,
+                "bytes_sent_per_row": (s1["bytes_sent"] - s0["bytes_sent"]) / max(
+                    1, s1["rows_sent"] - s0["rows_sent"]),
+                "linked_fraction": linked_frac, "local_only_ms_per_step": local_ms,
+                "xgmi_link_GBps_assumed": self.XGMI_LINK_GBPS, "per_n": pred,
+                "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
+                            for k, v in kt.items()},
+                "note": "PREDICTION (unmeasured on hardware at N > 1): the exchange path "
+                        "rehearsed on one GPU (one-rank RCCL: partition, count exchange + "
+                        "sync, records, local grouping of the received rows, compact "
+                        "return, gather) + the modelled xGMI time of rows/N per link"}
 
     def staged_oracle(self):
         """Config 5's parity at full size: the reps of the batched 50 M-file run
@@ -1238,6 +1308,8 @@ def parse_args(argv=None):
                     help="seconds after which the line is printed with what was measured "
                          "and the process ends (the driver's limit is 600 s)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-exchange-model", action="store_true",
+                    help="skip the one-rank RCCL rehearsal behind the N = 2/4/8 prediction")
     ap.add_argument("--no-explicit-rank", action="store_true",
                     help="skip the explicit-rank grouping timed beside the implicit one "
                          "(PMC passes: one variant per kernel name)")
