@@ -281,8 +281,9 @@ class FileIdentifierJob:
         self.index = _dedup.ObjectIndex(self.ctx, max(1024, 2 * (len(self.table) + ek.size)))
         if ek.size:
             dev = torch.device("cuda", self.ctx.device)
-            self.index.add_objects(torch.from_numpy(ek.view(np.int64)).to(dev),
-                                   torch.from_numpy(eh.view(np.int32)).to(dev))
+            # copies: the views may be read-only (torch.from_numpy warns on them)
+            self.index.add_objects(torch.from_numpy(ek.view(np.int64).copy()).to(dev),
+                                   torch.from_numpy(eh.view(np.int32).copy()).to(dev))
 
     def done(self) -> bool:
         return self.step_number >= self.task_count
