@@ -17,15 +17,21 @@ import re
 import sys
 
 
+def kernel_key(name: str) -> str:
+    """k_<name>, plus ':ListOut' for the group kernels' list-output variant
+    (round 4: the RepOut / ListOut instantiations are separate kernels)."""
+    m = re.search(r"(k_\w+)", name)
+    k = m.group(1) if m else name[:80]
+    return k + ":ListOut" if "ListOut" in name else k
+
+
 def load(path, counter):
     agg = collections.defaultdict(list)
     with open(path) as f:
         for r in csv.DictReader(f):
             if r["Counter_Name"] != counter:
                 continue
-            name = r["Kernel_Name"]
-            m = re.search(r"(k_\w+)", name)
-            agg[m.group(1) if m else name[:80]].append(float(r["Counter_Value"]))
+            agg[kernel_key(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return agg
 
 
@@ -54,8 +60,7 @@ def main():
             for r in csv.DictReader(f):
                 if r["Counter_Name"] != "GRBM_GUI_ACTIVE":
                     continue
-                m = re.search(r"(k_\w+)", r["Kernel_Name"])
-                k = m.group(1) if m else r["Kernel_Name"][:80]
+                k = kernel_key(r["Kernel_Name"])
                 dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
                 if dur > 0:
                     acc[k].append(float(r["Counter_Value"]) / 8 / dur / 1e9)

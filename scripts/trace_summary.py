@@ -18,8 +18,9 @@ KERNELS = ["k_leaves3", "k_fold3", "k_tree_level<true>", "k_tree_level<false>",
            "k_part_hist", "k_part_scatter_runs", "k_part_scatter_rec_staged", "k_part_scatter_rec",
            "k_part_scatter_ws", "k_part_private", "k_part2_runs", "k_fine_recount_runs",
            "k_fine_scan", "k_bucket_group12_pk", "k_bucket_group_pk",
-           "k_bucket_group12", "k_bucket_group", "k_link_count", "k_link_write", "k_small_host",
-           "k_small_split", "k_service"]
+           "k_bucket_group12", "k_bucket_group", "k_window_apply", "k_link_count", "k_link_write",
+           "k_keyless_count", "k_keyless_write", "k_ret_count", "k_ret_write", "k_ret_apply",
+           "k_gather_rep", "k_small_host", "k_small_split", "k_service"]
 LONG_MS = 5.0  # K1 launches over a whole 1 M-file step take ~13 ms; every other K1 launch < 2 ms
 
 
@@ -30,6 +31,8 @@ def main(path, out=None):
         short = next((k for k in KERNELS if k in name), None)
         if short is None:
             continue
+        if "ListOut" in name:  # the group kernels' list-output instantiation (round 4)
+            short += ":ListOut"
         ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         key = (short, int(r["Grid_Size_X"]))
         if short in ("k_leaves3", "k_fold3"):
