@@ -324,3 +324,29 @@ def test_histogram_alignment_paths(ctx, key_off, has_off):
     dk, dh = kbuf[key_off:key_off + n], hbuf[has_off:has_off + n]
     rep = dedup.HipOps(ctx).group_rows(dk, dh, None, 100, 0).cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(rep, O.group_reps(key, has, 100))
+
+
+@pytest.mark.parametrize("chunk", [100, 3])
+def test_two_level_window_rep_output(ctx, chunk):
+    """From 2^25 rows the two-level grouping writes its reps through row
+    windows (WinOut pairs + k_window_apply, round 4): 34 M rows, a key
+    repeated 60 k times (its bucket takes the global table and writes rep
+    directly, listing no pairs), keyless rows, implicit (12-B records) and
+    explicit (16-B records) ranks; bit-exact with the oracle."""
+    import torch
+    from spacedrive_amd import dedup
+    n = 34_000_000
+    rng = np.random.default_rng(34 + chunk)
+    pool = rng.integers(0, 2**64 - 1, int(n * 0.8), dtype=np.uint64, endpoint=True)
+    key = pool[rng.integers(0, pool.size, n)]
+    key[rng.choice(n, 60_000, replace=False)] = pool[9]
+    has = (rng.random(n) > 0.001).astype(np.uint8)
+    ref = O.group_reps(key, has, chunk)
+    ops = dedup.HipOps(ctx)
+    dk = torch.from_numpy(key.view(np.int64)).cuda()
+    dh = torch.from_numpy(has).cuda()
+    implicit = ops.group_rows(dk, dh, None, chunk, 0).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(implicit, ref)
+    dr = torch.arange(n, dtype=torch.int32, device="cuda")
+    explicit = ops.group_rows(dk, dh, dr, chunk, 0).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(explicit, ref)
