@@ -399,9 +399,15 @@ int sdgpu_link_batch_device(sdgpu_ctx *ctx, const uint32_t *d_rep, const uint32_
  * part of the contract (the reference's writes are a set; compare as sets).
  * d_counts[0] = creators, [1] = linked rows, [2] = entries (= [0] + [1]). */
 #define SDGPU_LINKED 0x80000000u
-int sdgpu_group_link_device(sdgpu_ctx *ctx, const uint64_t *d_key, const uint8_t *d_has_key,
-                            const uint8_t *d_valid, const uint32_t *d_rank, uint32_t first_rank,
-                            uint64_t n, uint32_t chunk_rows, uint32_t *d_who, uint32_t *d_obj,
+/* idx (may be NULL): the Object index, as in sdgpu_group_rows_indexed_device:
+ * a row whose cas_id already has an Object (registered, or created by an
+ * earlier batch) links to it -- obj = SDGPU_REP_EXISTING | handle, or the
+ * creator's rank -- and the creators of this batch are added to the index.
+ * May synchronise `stream` when the index grows. */
+int sdgpu_group_link_device(sdgpu_ctx *ctx, sdgpu_index *idx, const uint64_t *d_key,
+                            const uint8_t *d_has_key, const uint8_t *d_valid,
+                            const uint32_t *d_rank, uint32_t first_rank, uint64_t n,
+                            uint32_t chunk_rows, uint32_t *d_who, uint32_t *d_obj,
                             uint32_t *d_counts, void *stream);
 
 /* ---- downstream consumers of the grouping ---------------

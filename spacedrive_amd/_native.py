@@ -50,8 +50,8 @@ def _proto(L):
         "sdgpu_cas_stage_pinned": (i32, [ctx, c_vp, c_vp, c_vp, u32, c_vp, c_vp, c_vp]),
         "sdgpu_link_batch_device": (i32, [ctx, c_vp, c_vp, c_vp, u32, u64, c_vp, c_vp, c_vp, c_vp,
                                           c_vp]),
-        "sdgpu_group_link_device": (i32, [ctx, c_vp, c_vp, c_vp, c_vp, u32, u64, u32, c_vp, c_vp,
-                                          c_vp, c_vp]),
+        "sdgpu_group_link_device": (i32, [ctx, c_vp, c_vp, c_vp, c_vp, c_vp, u32, u64, u32, c_vp,
+                                          c_vp, c_vp, c_vp]),
         "sdgpu_generate_cas_id": (i32, [ctx, ctypes.c_char_p, u64, ctypes.c_char_p]),
         "sdgpu_identify_files": (i32, [ctx, c_vp, c_vp, u32, c_vp, c_vp, c_vp]),
         "sdgpu_checksum": (i32, [ctx, c_vp, u64, c_vp]),

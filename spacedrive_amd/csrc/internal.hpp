@@ -159,14 +159,18 @@ hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_
 // its record range, creators from the front (who = rank) and linked rows from
 // the back (who = rank | SDGPU_LINKED, obj = creator rank); no rep array.
 // counts[0..2] (zeroed by the caller) += creators, linked; counts[2] = keyed
-// entries.  keyless_list_launch then appends the valid keyless rows.
+// entries.
 hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* who,
                              uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
                              KTimer* timer = nullptr);
-size_t keyless_workspace_bytes(uint64_t n);
-hipError_t keyless_list_launch(const uint8_t* has, const uint8_t* valid, const uint32_t* rank,
-                               uint32_t first_rank, uint64_t n, uint32_t* who, uint32_t* counts,
-                               void* ws, hipStream_t s, KTimer* timer = nullptr);
+// extra_list_launch then appends, in row order, the valid keyless rows and
+// (with an index: grouped = the probe's mask, hitrep = its reps) the keyed
+// rows the probe decided.
+size_t extra_workspace_bytes(uint64_t n);
+hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uint8_t* grouped,
+                             const uint32_t* hitrep, const uint32_t* rank, uint32_t first_rank,
+                             uint64_t n, uint32_t* who, uint32_t* obj, uint32_t* counts, void* ws,
+                             hipStream_t s, KTimer* timer = nullptr);
 // Compact return leg of the exchange (dedup.hip): the received rows are cut
 // into tiles of 4096 that never straddle a source's segment [roff[p],
 // roff[p + 1]); tstart[p] = first tile of segment p, tstart[world] = tiles.

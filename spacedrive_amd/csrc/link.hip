@@ -173,45 +173,60 @@ __global__ __launch_bounds__(kThreads) void k_link_write(
 
 inline uint32_t link_tiles(uint64_t n) { return static_cast<uint32_t>((n + kTile - 1) / kTile); }
 
-// Keyless creators of the fused grouping (sdgpu_group_link_device): rows with
-// no cas_id that are valid (empty files: their own Object, mod.rs:238-239) are
-// not in the bucket records, so they are listed here, in row order, after the
-// keyed entries: who[K + t] = rank of the t-th such row, K = counts[2] (the
-// keyed total the group kernel stored).  A thread takes 16 consecutive rows
-// (one 16-B load of has_key and of valid); 4096-row tiles, counted, scanned,
-// written.
+// Entries of the fused write set that are not in the bucket records
+// (sdgpu_group_link_device), appended in row order after the keyed entries
+// (who[K + t], K = counts[2], the keyed total the group kernel stored):
+//   * valid rows without a cas_id (empty files: their own Objects,
+//     mod.rs:238-239): who = rank;
+//   * with an Object index, the keyed rows the probe decided (grouped[i] == 0:
+//     their cas_id belongs to an Object that existed before the batch,
+//     mod.rs:189-225): who = rank | SDGPU_LINKED, obj = the probe's rep -- or
+//     who = rank when the probe kept the row's own Object (same chunk).
+// A thread takes 16 consecutive rows (16-B loads of has_key / valid /
+// grouped); 4096-row tiles, counted, scanned, written; one atomic per block
+// adds its creators and linked rows to counts[0] / counts[1].
 constexpr int kKlRows = 16;
 constexpr uint32_t kKlTile = kThreads * kKlRows;
+constexpr uint32_t kLinkedBit = 0x80000000u;  // SDGPU_LINKED
 
-__device__ __forceinline__ uint32_t keyless_mask(const uint8_t* __restrict__ has,
-                                                 const uint8_t* __restrict__ valid, uint64_t n,
-                                                 uint64_t i0) {
+__device__ __forceinline__ uint32_t bytes16_mask(const uint8_t* __restrict__ p, uint64_t n,
+                                                 uint64_t i0, bool aligned, uint32_t absent) {
+  if (!p) return absent;
   uint32_t m = 0;
-  const bool aligned = (reinterpret_cast<uintptr_t>(has) & 15u) == 0 &&
-                       (reinterpret_cast<uintptr_t>(valid) & 15u) == 0;
   if (aligned && i0 + kKlRows <= n) {
-    const uint4 h = *reinterpret_cast<const uint4*>(has + i0);
-    const uint4 v = valid ? *reinterpret_cast<const uint4*>(valid + i0) : make_uint4(~0u, ~0u, ~0u, ~0u);
-    const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, vw[4] = {v.x, v.y, v.z, v.w};
+    const uint4 h = *reinterpret_cast<const uint4*>(p + i0);
+    const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
-    for (int k = 0; k < kKlRows; ++k) {
-      const uint32_t hb = (hw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-      const uint32_t vb = (vw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-      m |= static_cast<uint32_t>(hb == 0 && vb != 0) << k;
-    }
+    for (int k = 0; k < kKlRows; ++k)
+      m |= static_cast<uint32_t>(((hw[k >> 2] >> (8 * (k & 3))) & 0xFFu) != 0) << k;
   } else {
-    for (int k = 0; k < kKlRows && i0 + k < n; ++k)
-      m |= static_cast<uint32_t>(has[i0 + k] == 0 && (!valid || valid[i0 + k] != 0)) << k;
+    for (int k = 0; k < kKlRows && i0 + k < n; ++k) m |= static_cast<uint32_t>(p[i0 + k] != 0) << k;
   }
   return m;
 }
 
-__global__ __launch_bounds__(kThreads) void k_keyless_count(const uint8_t* __restrict__ has,
-                                                            const uint8_t* __restrict__ valid,
-                                                            uint64_t n, uint32_t* __restrict__ cnt) {
+// bit k: row i0 + k is an extra entry
+__device__ __forceinline__ uint32_t extra_mask(const uint8_t* __restrict__ has,
+                                               const uint8_t* __restrict__ valid,
+                                               const uint8_t* __restrict__ grouped, uint64_t n,
+                                               uint64_t i0) {
+  const bool aligned = ((reinterpret_cast<uintptr_t>(has) | reinterpret_cast<uintptr_t>(valid) |
+                         reinterpret_cast<uintptr_t>(grouped)) & 15u) == 0;
+  const uint32_t in_range = i0 >= n ? 0u : (i0 + kKlRows <= n ? 0xFFFFu : (1u << (n - i0)) - 1u);
+  const uint32_t h = bytes16_mask(has, n, i0, aligned, 0xFFFFu);
+  const uint32_t v = bytes16_mask(valid, n, i0, aligned, 0xFFFFu);
+  const uint32_t g = bytes16_mask(grouped, n, i0, aligned, 0xFFFFu);
+  // keyless and valid, or keyed and decided by the probe
+  return in_range & ((~h & v) | (grouped ? (h & ~g) : 0u));
+}
+
+__global__ __launch_bounds__(kThreads) void k_extra_count(const uint8_t* __restrict__ has,
+                                                          const uint8_t* __restrict__ valid,
+                                                          const uint8_t* __restrict__ grouped,
+                                                          uint64_t n, uint32_t* __restrict__ cnt) {
   __shared__ uint32_t sc[kWaves];
   const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kKlTile + threadIdx.x * kKlRows;
-  uint32_t c = __popc(keyless_mask(has, valid, n, i0));
+  uint32_t c = __popc(extra_mask(has, valid, grouped, n, i0));
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
   if (__lane_id() == 0) sc[threadIdx.x >> 6] = c;
@@ -223,58 +238,89 @@ __global__ __launch_bounds__(kThreads) void k_keyless_count(const uint8_t* __res
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_keyless_write(
-    const uint8_t* __restrict__ has, const uint8_t* __restrict__ valid, const uint32_t* __restrict__ rank,
-    uint32_t first_rank, uint64_t n, uint32_t nb, const uint32_t* __restrict__ cnt,
-    uint32_t* __restrict__ who, uint32_t* __restrict__ counts) {
-  __shared__ uint32_t sw[kWaves];
+__global__ __launch_bounds__(kThreads) void k_extra_write(
+    const uint8_t* __restrict__ has, const uint8_t* __restrict__ valid,
+    const uint8_t* __restrict__ grouped, const uint32_t* __restrict__ hitrep,
+    const uint32_t* __restrict__ rank, uint32_t first_rank, uint64_t n,
+    const uint32_t* __restrict__ cnt, uint32_t* __restrict__ who, uint32_t* __restrict__ obj,
+    uint32_t* __restrict__ counts) {
+  __shared__ uint32_t sw[kWaves], sl[kWaves];
   const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kKlTile + threadIdx.x * kKlRows;
-  const uint32_t K = counts[2];
-  uint32_t m = keyless_mask(has, valid, n, i0);
+  const uint32_t K = counts[2];  // the keyed entries (the group kernel); updated only after this kernel
+  uint32_t m = extra_mask(has, valid, grouped, n, i0);
+  const uint32_t hm = has ? bytes16_mask(has, n, i0, false, 0u) : 0xFFFFu;
   const uint32_t c = __popc(m);
   uint32_t inc = c;
-  const uint32_t lane = __lane_id();
+  const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t o = __shfl_up(inc, d);
     if (lane >= static_cast<uint32_t>(d)) inc += o;
   }
-  if (lane == 63) sw[threadIdx.x >> 6] = inc;
+  if (lane == 63) sw[wv] = inc;
   __syncthreads();
   uint32_t pos = K + cnt[blockIdx.x] + inc - c;
-  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) pos += sw[w];
+  for (uint32_t w = 0; w < wv; ++w) pos += sw[w];
+  uint32_t linked = 0;
   while (m) {
     const int k = __ffs(m) - 1;
     m &= m - 1;
     const uint64_t i = i0 + k;
-    who[pos++] = rank ? rank[i] : first_rank + static_cast<uint32_t>(i);
+    const uint32_t r = rank ? rank[i] : first_rank + static_cast<uint32_t>(i);
+    uint32_t w = r;
+    if ((hm >> k) & 1u) {  // keyed: decided by the probe
+      const uint32_t out = hitrep[i];
+      if (out != r) {
+        w = r | kLinkedBit;
+        obj[pos] = out;
+        ++linked;
+      }
+    }
+    who[pos++] = w;
   }
-  if (blockIdx.x == nb - 1 && threadIdx.x == 0) {
-    const uint32_t total = cnt[nb];
-    counts[0] += total;
-    counts[2] = K + total;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) linked += __shfl_xor(linked, d);
+  if (lane == 0) sl[wv] = linked;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tl = 0, tt = 0;
+    for (int w = 0; w < kWaves; ++w) {
+      tl += sl[w];
+      tt += sw[w];
+    }
+    if (tt - tl) atomicAdd(&counts[0], tt - tl);
+    if (tl) atomicAdd(&counts[1], tl);
   }
+}
+
+// counts[2] = keyed entries + extra entries (after every block read K)
+__global__ void k_extra_finish(const uint32_t* __restrict__ cnt, uint32_t nb,
+                               uint32_t* __restrict__ counts) {
+  if (threadIdx.x == 0) counts[2] += cnt[nb];
 }
 
 }  // namespace
 
-size_t keyless_workspace_bytes(uint64_t n) {
+size_t extra_workspace_bytes(uint64_t n) {
   const uint64_t m = (n + kKlTile - 1) / kKlTile;
   return ((m + 1) * 4 + 255) / 256 * 256 + ((scan::tiles_for(m) + 1) * 4 + 255) / 256 * 256;
 }
 
-hipError_t keyless_list_launch(const uint8_t* has, const uint8_t* valid, const uint32_t* rank,
-                               uint32_t first_rank, uint64_t n, uint32_t* who, uint32_t* counts,
-                               void* ws, hipStream_t s, KTimer* timer) {
-  if (n == 0 || !has) return hipSuccess;  // every row keyed: nothing to add
+hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uint8_t* grouped,
+                             const uint32_t* hitrep, const uint32_t* rank, uint32_t first_rank,
+                             uint64_t n, uint32_t* who, uint32_t* obj, uint32_t* counts, void* ws,
+                             hipStream_t s, KTimer* timer) {
+  if (n == 0 || (!has && !grouped)) return hipSuccess;  // every row keyed, no probe: nothing extra
   const uint32_t nb = static_cast<uint32_t>((n + kKlTile - 1) / kKlTile);
   uint8_t* b = static_cast<uint8_t*>(ws);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(b);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(b + ((nb + 1) * 4ull + 255) / 256 * 256);
-  KScope k(timer, "keyless_list", s);
-  k_keyless_count<<<nb, kThreads, 0, s>>>(has, valid, n, cnt);
+  KScope k(timer, "extra_list", s);
+  k_extra_count<<<nb, kThreads, 0, s>>>(has, valid, grouped, n, cnt);
   scan::exclusive(cnt, nb, cnt, tiles, nullptr, s);
-  k_keyless_write<<<nb, kThreads, 0, s>>>(has, valid, rank, first_rank, n, nb, cnt, who, counts);
+  k_extra_write<<<nb, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, cnt,
+                                        who, obj, counts);
+  k_extra_finish<<<1, 64, 0, s>>>(cnt, nb, counts);
   return hipGetLastError();
 }
 

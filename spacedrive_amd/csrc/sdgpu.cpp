@@ -1205,32 +1205,6 @@ int sdgpu_group_rows_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8_t* 
   return 0;
 }
 
-int sdgpu_group_link_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8_t* d_has_key,
-                            const uint8_t* d_valid, const uint32_t* d_rank, uint32_t first_rank,
-                            uint64_t n, uint32_t chunk_rows, uint32_t* d_who, uint32_t* d_obj,
-                            uint32_t* d_counts, void* stream) {
-  if (!c || chunk_rows == 0 || !d_counts || (n && (!d_key || !d_who || !d_obj))) return -EINVAL;
-  // ranks must stay below the SDGPU_LINKED bit
-  if (n >= (1ull << 31) || (!d_rank && first_rank + n > (1ull << 31))) return -EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  SD_TRY(hipSetDevice(c->device));
-  hipStream_t s = pick(c, stream);
-  SD_TRY(hipMemsetAsync(d_counts, 0, 3 * sizeof(uint32_t), s));
-  if (n == 0) return 0;
-  SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(n)));
-  SD_TRY_RC(ensure_dev(c, c->link_ws, keyless_workspace_bytes(n)));
-  GroupInput in;
-  in.key = d_key;
-  in.valid = d_has_key;
-  in.rank = d_rank;
-  in.rank_base = first_rank;
-  in.n = n;
-  SD_TRY(dedup_list_launch(in, chunk_rows, d_who, d_obj, d_counts, c->dedup_ws.p, s, c->kt()));
-  SD_TRY(keyless_list_launch(d_has_key, d_valid, d_rank, first_rank, n, d_who, d_counts,
-                             c->link_ws.p, s, c->kt()));
-  return 0;
-}
-
 int sdgpu_shard_count_device(sdgpu_ctx* c, const uint64_t* d_key, const uint8_t* d_has_key,
                              uint64_t n, uint32_t shard_bits, uint64_t* h_counts, void* stream) {
   if (!c || !h_counts || shard_bits > 8 || (n && !d_key) || n >= (1ull << 32)) return -EINVAL;

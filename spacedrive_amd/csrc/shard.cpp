@@ -795,6 +795,58 @@ int sdgpu_group_rows_indexed_device(sdgpu_ctx* c, sdgpu_index* x, const uint64_t
   return group_with_index(c, x, in, chunk_rows, d_rep, static_cast<uint8_t*>(c->xs_recv.p), s);
 }
 
+// Fused grouping + Object write set (ABI 4).  With an index: the probe
+// decides the rows whose cas_id already has an Object (reps into a scratch
+// array, its mask as the grouping's valid), the group kernel lists the other
+// keyed rows, the extra pass lists the probe's rows and the valid keyless
+// rows, and every grouped row is offered to the index with its rank -- the
+// index keeps the minimum, i.e. the creator (a linked row's rank is never
+// below its creator's), so this inserts exactly the creators' values.
+int sdgpu_group_link_device(sdgpu_ctx* c, sdgpu_index* x, const uint64_t* d_key,
+                            const uint8_t* d_has_key, const uint8_t* d_valid,
+                            const uint32_t* d_rank, uint32_t first_rank, uint64_t n,
+                            uint32_t chunk_rows, uint32_t* d_who, uint32_t* d_obj,
+                            uint32_t* d_counts, void* stream) {
+  if (!c || chunk_rows == 0 || !d_counts || (n && (!d_key || !d_who || !d_obj))) return -EINVAL;
+  if (x && x->ctx->device != c->device) return -EINVAL;
+  // ranks stay below the SDGPU_LINKED / SDGPU_REP_EXISTING bit
+  if (n >= (1ull << 31) || (!d_rank && first_rank + n > (1ull << 31))) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  SD_TRY(hipMemsetAsync(d_counts, 0, 3 * sizeof(uint32_t), s));
+  if (n == 0) return 0;
+  SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(n)));
+  SD_TRY_RC(ensure_dev(c, c->link_ws, extra_workspace_bytes(n)));
+  GroupInput in;
+  in.key = d_key;
+  in.valid = d_has_key;
+  in.rank = d_rank;
+  in.rank_base = first_rank;
+  in.n = n;
+  if (!x) {
+    SD_TRY(dedup_list_launch(in, chunk_rows, d_who, d_obj, d_counts, c->dedup_ws.p, s, c->kt()));
+    SD_TRY(extra_list_launch(d_has_key, d_valid, nullptr, nullptr, d_rank, first_rank, n, d_who,
+                             d_obj, d_counts, c->link_ws.p, s, c->kt()));
+    return 0;
+  }
+  // probe scratch: reps [n] + mask [n]
+  const size_t o_mask = align_up(4 * n, 256);
+  SD_TRY_RC(ensure_dev(c, c->xs_recv, o_mask + n + 256));
+  uint32_t* hitrep = static_cast<uint32_t*>(c->xs_recv.p);
+  uint8_t* mask = static_cast<uint8_t*>(c->xs_recv.p) + o_mask;
+  SD_TRY_RC(index_reserve(x, n, s));
+  SD_TRY(index_probe_launch(x->ref, in, chunk_rows, hitrep, mask, s, c->kt()));
+  GroupInput gi = in;
+  gi.valid = mask;
+  SD_TRY(dedup_list_launch(gi, chunk_rows, d_who, d_obj, d_counts, c->dedup_ws.p, s, c->kt()));
+  SD_TRY(extra_list_launch(d_has_key, d_valid, mask, hitrep, d_rank, first_rank, n, d_who, d_obj,
+                           d_counts, c->link_ws.p, s, c->kt()));
+  // hitrep[i] == rank for every grouped row: all of them are offered
+  SD_TRY(index_creators_launch(x->ref, in, hitrep, mask, s, c->kt()));
+  return 0;
+}
+
 int sdgpu_dedup_batch(sdgpu_ctx* c, sdgpu_index* x, const uint64_t* key, const uint8_t* has_key,
                       uint32_t first_rank, uint32_t n, uint32_t chunk_rows, uint32_t* rep) {
   if (!c || chunk_rows == 0 || (n && (!key || !has_key || !rep))) return -EINVAL;

@@ -473,7 +473,9 @@ def group_link_device(key, has_key=None, valid=None, rank=None, first_rank: int 
     Object, file_identifier/mod.rs:243-297) or rank | LINKED (connects to the
     Object of creator rank obj[e], mod.rs:189-225); bucket order, not row
     order (a set).  trim=False: full-length tensors + the device counts [3],
-    no synchronisation."""
+    no synchronisation.  index: an ObjectIndex (rows whose cas_id already
+    has an Object link to it: obj = REP_EXISTING | handle or the creator's
+    rank from an earlier batch; this batch's creators are added)."""
     import torch
     dev = key.device
     ctx = ctx or default_context(dev.index)
@@ -483,8 +485,9 @@ def group_link_device(key, has_key=None, valid=None, rank=None, first_rank: int 
     counts = torch.empty(3, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream(dev).cuda_stream
     ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
-    check(ctx.lib.sdgpu_group_link_device(ctx.h, key.data_ptr(), ptr(has_key), ptr(valid),
-                                          ptr(rank), first_rank, n, chunk_rows, who.data_ptr(),
+    check(ctx.lib.sdgpu_group_link_device(ctx.h, index.h if index is not None else None,
+                                          key.data_ptr(), ptr(has_key), ptr(valid), ptr(rank),
+                                          first_rank, n, chunk_rows, who.data_ptr(),
                                           obj.data_ptr(), counts.data_ptr(), s),
           "sdgpu_group_link_device")
     if not trim:
