@@ -158,3 +158,46 @@ def test_fused_equals_group_then_link_batch(ctx):
     np.testing.assert_array_equal(flr, lr)
     np.testing.assert_array_equal(flo, lo)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("chunk,bounds", [(100, [0, 100_000, 200_000]),
+                                          (100, [0, 150, 1000, 50_037, 200_000]),
+                                          (7, [0, 3, 70_000, 200_000])])
+def test_fused_batches_through_the_object_index(ctx, chunk, bounds):
+    """Batches in id order through one Object index, with Objects registered
+    before the run (existing handles), via the fused call: the union of the
+    batches' write sets equals the oracle's link batch over the whole run's
+    grouping against those Objects (O.group_reps_existing, mod.rs:168-241)
+    -- rows of a later batch link to Objects of an earlier one or to the
+    registered ones (obj = REP_EXISTING | handle); batch bounds split chunks."""
+    import torch
+    from spacedrive_amd import dedup
+    total = bounds[-1]
+    rng = np.random.default_rng(chunk + len(bounds))
+    pool = rng.integers(0, 2**64 - 1, 120_000, dtype=np.uint64, endpoint=True)
+    pool[0] = SENTINEL_KEY
+    key = pool[rng.integers(0, pool.size, total)]
+    has = (rng.random(total) > 0.01).astype(np.uint8)
+    ek = rng.choice(pool, 3000)
+    eh = (np.arange(ek.size, dtype=np.uint32) * 7 + 11)
+    idx = dedup.ObjectIndex(ctx, 1000)  # small: grows and rehashes on the way
+    idx.add_objects(torch.from_numpy(ek.view(np.int64)).cuda(),
+                    torch.from_numpy(eh.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    ws, os_ = [], []
+    nc = nl = 0
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        dk = torch.from_numpy(key[a:b].view(np.int64)).cuda()
+        dh = torch.from_numpy(has[a:b]).cuda()
+        who, obj, (c, l) = dedup.group_link_device(dk, dh, None, None, a, chunk, ctx=ctx,
+                                                   index=idx)
+        ws.append(who.cpu().numpy())
+        os_.append(obj.cpu().numpy())
+        nc, nl = nc + c, nl + l
+    fc, flr, flo = dedup.split_link_lists(np.concatenate(ws), np.concatenate(os_))
+    ref = O.group_reps_existing(key, has, chunk, ek, eh)
+    rc, rlr, rlo = O.link_batch(ref, None, None, 0)
+    assert (nc, nl) == (rc.size, rlr.size)
+    np.testing.assert_array_equal(fc, rc)
+    np.testing.assert_array_equal(flr, rlr)
+    np.testing.assert_array_equal(flo, rlo)
