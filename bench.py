@@ -444,14 +444,18 @@ class Runner:
             cas.cas_stage_pinned(h_arena, off, ln, out, st, ctx=self.ctx)
             key = out.view(torch.int64).view(-1)
             corpus.vary_keys_device(key, vary, s, ctx=self.ctx)
+            if self.comm is None and W == 1:
+                # one GPU: grouping against the index + the write set in one
+                # pass (sdgpu_group_link_device); every row is an entry
+                who, obj, cnt = dedup.group_link_device(key, has, None, None, s * n, 100,
+                                                        ctx=self.ctx, trim=False, index=index)
+                return ("lists", who, obj, cnt)
             if self.comm is not None:
                 rep = dedup.group_sharded(key, has, ranks[s], self.comm, index, 100)
-            elif W == 1:
-                rep = dedup.group_rows_indexed(key, has, ranks[s], index, 100)
             else:  # gloo rehearsal: the exchange has no index
                 rep = self.group(key, has, ranks[s])
             dedup.link_batch_device(rep, ranks[s], None, 0, ctx=self.ctx, trim=False)
-            return rep
+            return ("rep", rep)
 
         step(nsteps)  # warm-up on a step outside the run's key space
         torch.cuda.synchronize()
@@ -466,29 +470,42 @@ class Runner:
         if verify:
             keys_all = torch.empty(nsteps * n, dtype=torch.int64, device=self.dev)
             reps_all = torch.empty(nsteps * n, dtype=torch.int32, device=self.dev)
+            obj_all = torch.empty(nsteps * n, dtype=torch.int32, device=self.dev)
 
         def run():
             for s in range(nsteps):
-                rep = step(s)
-                if verify:
+                res = step(s)
+                if verify:  # device copies only; decoded after the timing
                     keys_all[s * n:(s + 1) * n].copy_(out.view(torch.int64).view(-1))
-                    reps_all[s * n:(s + 1) * n].copy_(rep)
-            self._staged_last = rep
+                    reps_all[s * n:(s + 1) * n].copy_(res[1][:n])
+                    if res[0] == "lists":
+                        obj_all[s * n:(s + 1) * n].copy_(res[2][:n])
+            self._staged_last = res
 
         t = self.timed(run, 1, 0)
         whole = None
+        last = self._staged_last
+        if last[0] == "lists":
+            linked_last = int(last[3].cpu()[1])
+        else:
+            linked_last = int((last[1] != ranks[nsteps - 1]).sum())
         if verify:
             # checked after the timing against the ORACLE's grouping of all the
             # run's rows (staged_oracle leg, rank 0 at N = 1): batching through
-            # the Object index must equal the whole-run rule
+            # the Object index must equal the whole-run rule.  The fused steps'
+            # write sets (every row one entry) are turned back into reps here.
+            reps = reps_all.cpu().numpy().view(np.uint32)
+            if last[0] == "lists":
+                who = reps
+                obj = obj_all.cpu().numpy().view(np.uint32)
+                r = who & np.uint32(0x7FFFFFFF)
+                reps = np.empty(nsteps * n, np.uint32)
+                reps[r] = np.where((who & np.uint32(0x80000000)) != 0, obj, r)
             self._staged_verify = (keys_all.cpu().numpy().view(np.uint64),
-                                   np.tile(has.cpu().numpy(), nsteps),
-                                   reps_all.cpu().numpy().view(np.uint32))
+                                   np.tile(has.cpu().numpy(), nsteps), reps)
             whole = {"rows": nsteps * n, "checked_by": "staged_oracle leg (O.group_reps)"}
-            del keys_all, reps_all
+            del keys_all, reps_all, obj_all
         assert int(st.abs().sum()) == 0
-        last = self._staged_last
-        linked_last = int((last != ranks[nsteps - 1]).sum())
         distinct = index.count() if index is not None else None
         files = W * n * nsteps
         per_gpu_Bps = window_bytes * nsteps / t
@@ -506,9 +523,10 @@ class Runner:
                                        f"({nsteps} steps x {n} files/GPU x {W} GPU), windows in "
                                        "pinned host memory, staged H2D (3-slab ring) + K1 + "
                                        "grouping against the run's Object index "
-                                       + ("(sharded, RCCL)" if self.comm is not None else
-                                          "(one GPU)" if W == 1 else "(no index: rehearsal)")
-                                       + " + Object link batch",
+                                       + ("(sharded, RCCL) + Object link batch"
+                                          if self.comm is not None else
+                                          "+ Object write set in one pass (one GPU)" if W == 1
+                                          else "(no index: rehearsal) + Object link batch"),
                            "files_per_gpu_per_step": n, "window_bytes_per_gpu_per_step": window_bytes}}
 
     # ---------------------------------------------------------------- config 1
