@@ -54,35 +54,76 @@ impl Drop for ObjectIndex {
     }
 }
 
-/// One job step over `paths` (rows in id order; `sizes` from fs::metadata,
-/// mod.rs:65) whose first row has rank `first_rank`.
-pub fn identify_step(gpu: &Gpu, idx: &ObjectIndex, paths: &[PathBuf], sizes: &[u64],
-                     first_rank: u32) -> io::Result<Vec<IdentifiedRow>> {
+impl ObjectIndex {
+    /// Objects that exist before the job (mod.rs:168-185): key -> object id.
+    pub fn add_objects(&self, gpu: &Gpu, keys: &[u64], ids: &[u32]) -> io::Result<()> {
+        if keys.is_empty() {
+            return Ok(());
+        }
+        let ctx = gpu.ctx();
+        let n = keys.len();
+        let mut dk = ptr::null_mut();
+        let mut dh = ptr::null_mut();
+        check(unsafe { sys::sdgpu_alloc_device(*ctx, 8 * n, &mut dk) })?;
+        check(unsafe { sys::sdgpu_alloc_device(*ctx, 4 * n, &mut dh) })?;
+        let stream = unsafe { sys::sdgpu_stream(*ctx) };
+        let rc = unsafe {
+            check(sys::sdgpu_memcpy_async(*ctx, dk, keys.as_ptr().cast(), 8 * n, stream))
+                .and_then(|_| check(sys::sdgpu_memcpy_async(*ctx, dh, ids.as_ptr().cast(), 4 * n, stream)))
+                .and_then(|_| check(sys::sdgpu_index_add_objects_device(self.0, dk.cast(), dh.cast(),
+                                                                       n as u64, 1, 0, stream)))
+                .and_then(|_| check(sys::sdgpu_sync(*ctx)))
+        };
+        unsafe {
+            sys::sdgpu_free_device(*ctx, dk);
+            sys::sdgpu_free_device(*ctx, dh);
+        }
+        rc
+    }
+}
+
+/// What one batched read + hash of the candidates gives (FileMetadata::new of
+/// every row, mod.rs:107-134): cas bytes, has_key, -errno per row.
+pub struct Identified {
+    pub cas8: Vec<[u8; 8]>,
+    pub has_key: Vec<u8>,
+    pub status: Vec<i32>,
+}
+
+pub fn identify(gpu: &Gpu, paths: &[PathBuf], sizes: &[u64]) -> io::Result<Identified> {
     let n = paths.len();
     let c: Vec<_> = paths.iter().map(|p| cpath(p)).collect();
     let ptrs: Vec<*const c_char> = c.iter().map(|s| s.as_ptr()).collect();
-    let mut cas8 = vec![[0u8; 8]; n];
-    let mut has_key = vec![0u8; n];
-    let mut status = vec![0i32; n];
-    let mut rep = vec![0u32; n];
+    let mut out = Identified { cas8: vec![[0u8; 8]; n], has_key: vec![0u8; n], status: vec![0i32; n] };
     let ctx = gpu.ctx();
     check(unsafe {
-        sys::sdgpu_identify_files(*ctx, ptrs.as_ptr(), sizes.as_ptr(), n as u32, cas8.as_mut_ptr(),
-                                  has_key.as_mut_ptr(), status.as_mut_ptr())
+        sys::sdgpu_identify_files(*ctx, ptrs.as_ptr(), sizes.as_ptr(), n as u32, out.cas8.as_mut_ptr(),
+                                  out.has_key.as_mut_ptr(), out.status.as_mut_ptr())
     })?;
-    // rows whose read failed take no part in the grouping (they stay orphans)
-    let grouped: Vec<u8> = has_key.iter().zip(&status).map(|(&h, &s)| (h != 0 && s == 0) as u8).collect();
-    let keys: Vec<u64> = cas8.iter().map(|b| u64::from_le_bytes(*b)).collect();
-    check(unsafe {
-        sys::sdgpu_dedup_batch(*ctx, idx.0, keys.as_ptr(), grouped.as_ptr(), first_rank, n as u32,
-                               sys::SDGPU_IDENTIFIER_CHUNK_SIZE, rep.as_mut_ptr())
-    })?;
+    Ok(out)
+}
+
+/// The grouping of one batch of identified rows against the index (rows in
+/// id order, ranks first_rank + i); rows whose read failed take no part.
+pub fn group(gpu: &Gpu, idx: &ObjectIndex, rows: &Identified, first_rank: u32) -> io::Result<Vec<IdentifiedRow>> {
+    let n = rows.cas8.len();
+    let mut rep = vec![0u32; n];
+    let grouped: Vec<u8> =
+        rows.has_key.iter().zip(&rows.status).map(|(&h, &s)| (h != 0 && s == 0) as u8).collect();
+    let keys: Vec<u64> = rows.cas8.iter().map(|b| u64::from_le_bytes(*b)).collect();
+    {
+        let ctx = gpu.ctx();
+        check(unsafe {
+            sys::sdgpu_dedup_batch(*ctx, idx.0, keys.as_ptr(), grouped.as_ptr(), first_rank, n as u32,
+                                   sys::SDGPU_IDENTIFIER_CHUNK_SIZE, rep.as_mut_ptr())
+        })?;
+    }
     Ok((0..n)
         .map(|i| {
-            if status[i] != 0 {
-                return IdentifiedRow { cas_id: None, link: Link::Failed(check(status[i]).unwrap_err()) };
+            if rows.status[i] != 0 {
+                return IdentifiedRow { cas_id: None, link: Link::Failed(check(rows.status[i]).unwrap_err()) };
             }
-            let cas_id = (has_key[i] != 0).then(|| hex::encode(cas8[i]));
+            let cas_id = (rows.has_key[i] != 0).then(|| hex::encode(rows.cas8[i]));
             let r = first_rank + i as u32;
             let link = if rep[i] == r {
                 Link::Create
@@ -94,4 +135,12 @@ pub fn identify_step(gpu: &Gpu, idx: &ObjectIndex, paths: &[PathBuf], sizes: &[u
             IdentifiedRow { cas_id, link }
         })
         .collect())
+}
+
+/// One job step over `paths` (rows in id order; `sizes` from fs::metadata,
+/// mod.rs:65) whose first row has rank `first_rank`.
+pub fn identify_step(gpu: &Gpu, idx: &ObjectIndex, paths: &[PathBuf], sizes: &[u64],
+                     first_rank: u32) -> io::Result<Vec<IdentifiedRow>> {
+    let rows = identify(gpu, paths, sizes)?;
+    group(gpu, idx, &rows, first_rank)
 }

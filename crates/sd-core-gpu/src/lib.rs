@@ -18,6 +18,7 @@ pub mod burst;
 pub mod cas;
 pub mod hash;
 pub mod identifier;
+pub mod job;
 
 use std::{
     ffi::{CStr, CString},
