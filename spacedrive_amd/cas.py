@@ -121,3 +121,86 @@ def hex_ids(out8: np.ndarray) -> list[str]:
 def keys_of(out8) -> np.ndarray:
     """8 digest bytes as little-endian u64 grouping keys."""
     return np.ascontiguousarray(out8, np.uint8).reshape(-1, 8).view("<u8").reshape(-1)
+
+
+class Coalescer:
+    """Concurrent single-file ``generate_cas_id`` calls coalesced into batches
+    (host mirror of crates/sd-core-gpu/src/burst.rs).
+
+    The watcher (location/manager/watcher/utils.rs:236,411,467) and the
+    non-indexed listing (location/non_indexed.rs:161) call generate_cas_id
+    once per file; when many arrive together (a folder copied into a watched
+    location) the calls queued while the worker is busy leave as ONE
+    ``sdgpu_identify_files`` batch (the library's read pool + one K1 launch).
+    A lone call goes through the resident latency service (the Rust host
+    hashes a lone small file on the CPU with the reference's own blake3 crate
+    instead; there is no CPU hasher in this package).  No timer: the worker
+    drains what is queued when it looks, so a lone call never waits."""
+
+    def __init__(self, ctx=None, batch_from: int = 4, batch_max: int = 1024):
+        import queue
+        import threading
+        self.ctx = ctx or default_context()
+        self.batch_from, self.batch_max = batch_from, batch_max
+        self.q = queue.Queue()
+        self.stats = {"calls": 0, "batches": 0, "batched_calls": 0, "single": 0}
+        self._t = threading.Thread(target=self._worker, name="sd-gpu-cas", daemon=True)
+        self._t.start()
+
+    def cas_id(self, path, size: int) -> str:
+        """generate_cas_id(path, size) (cas.rs:23) through the worker; blocks."""
+        import concurrent.futures as cf
+        fut = cf.Future()
+        self.q.put((os.fspath(path), int(size), fut))
+        return fut.result()
+
+    def close(self):
+        self.q.put(None)
+        self._t.join(timeout=10)
+
+    def _worker(self):
+        import queue
+        from .file_identifier import identify
+        while True:
+            first = self.q.get()
+            if first is None:
+                return
+            group = [first]
+            while len(group) < self.batch_max:
+                try:
+                    r = self.q.get_nowait()
+                except queue.Empty:
+                    break
+                if r is None:
+                    self.q.put(None)
+                    break
+                group.append(r)
+            self.stats["calls"] += len(group)
+            if len(group) >= self.batch_from:
+                self.stats["batches"] += 1
+                self.stats["batched_calls"] += len(group)
+                try:
+                    res = identify([p for p, _, _ in group],
+                                   np.array([s for _, s, _ in group], np.uint64), ctx=self.ctx)
+                except Exception as e:  # noqa: BLE001 -- every caller sees it
+                    for _, _, fut in group:
+                        fut.set_exception(e)
+                    continue
+                for i, (p, s, fut) in enumerate(group):
+                    if res.status[i] != 0:
+                        fut.set_exception(SdgpuError(int(res.status[i]), p))
+                    elif s == 0:  # identify treats size 0 as "no cas_id"; the drop-in hashes 8 zeros
+                        self._single(p, s, fut)
+                    else:
+                        fut.set_result(bytes(res.cas8[i]).hex())
+                continue
+            for p, s, fut in group:
+                self.stats["single"] += 1
+                self._single(p, s, fut)
+
+    def _single(self, p, s, fut):
+        try:
+            self.ctx.latency_service(True)
+            fut.set_result(generate_cas_id(p, s, self.ctx))
+        except Exception as e:  # noqa: BLE001
+            fut.set_exception(e)
