@@ -968,18 +968,12 @@ class Runner:
         nfine = 1 << 15
         tile = -(-total // 256)  # rows per coarse block (ceil)
         rounds = -(-tile // 4096)
-        # from 2^25 rows the group kernel writes its linked rows as {row, rep}
-        # pairs sorted by row window (+ 129 u16 window bounds per bucket) and
-        # k_window_apply writes them into rep window by window
-        windowed = total >= (1 << 25)
         alg = {"bucket_scatter1": 13 * total + 12 * nk + 8 * 256 * rounds * 64 + 4 * nfine * 256,
                "bucket_fine_scan": 4 * nfine * 256 + 4 * nfine * 128 + 4 * nfine,
                "bucket_scatter": 24 * nk,
-               "bucket_group": 12 * nk + (8 * linked + 258 * nfine if windowed else 4 * linked)}
-        if windowed:
-            alg["bucket_apply"] = 12 * linked + 258 * nfine
+               "bucket_group": 12 * nk + 4 * linked}
         pmc_names = {"bucket_scatter1": "k_part_private", "bucket_scatter": "k_part2_runs",
-                     "bucket_group": "k_bucket_group12_pk", "bucket_apply": "k_window_apply"}
+                     "bucket_group": "k_bucket_group12_pk"}
         step_s = t / steps
         roof = {"bound": "hbm", "peak": HBM_PEAK / 1e9, "unit": "GB/s", "linked_rows": linked,
                 "kernels": {}, "note": "algorithmic bytes of the two-level partition + group-by "

@@ -1313,85 +1313,10 @@ struct ListOut {
     }
   }
 };
-// WinOut (round 4): the rep API's scattered writes for large tables.  At
-// 100 M rows the group kernel's 20 M rep[row] = f stores land anywhere in a
-// 400 MB array (beyond the 256 MB Infinity Cache): 0.64 GB of 32-B partial
-// writes, ~0.3 ms of the kernel (scripts/exp/exp_repwrite.hip).  Instead each
-// bucket writes its linked rows as {row, f} pairs, counting-sorted by ROW
-// WINDOW (kWinCount windows of ceil(n / kWinCount) rows, ~3 MB of rep each),
-// into its own record range of a pair array, with the window boundaries
-// (u16: a bucket holds < 4096 records) beside; k_window_apply then hands
-// every window to the workgroups of ONE XCD, so its rep lines are written
-// while they sit in that XCD's 4 MB L2.  Oversized buckets (global table)
-// write rep directly and list no pairs.
-constexpr uint32_t kWinCount = 128;
-struct WinOut {
-  static constexpr int kScratch = kListScratch;  // window counts [0, 128) + starts [128, 257)
-  uint32_t* rep;
-  uint2* pairs;
-  uint16_t* bnd;  // [bucket][kWinCount + 1]
-  uint32_t win_rows;
-  template <int kSteps>
-  __device__ __forceinline__ void emit(const bool (&live)[kSteps], const bool (&lk)[kSteps],
-                                       const uint32_t (&r)[kSteps], const uint32_t (&w)[kSteps],
-                                       const uint32_t (&f)[kSteps], uint32_t start, uint32_t,
-                                       uint32_t&, uint32_t&, uint32_t* scr, bool reuse) const {
-    if (reuse) {  // the global-table path (chunks): direct writes
-#pragma unroll
-      for (int j = 0; j < kSteps; ++j)
-        if (lk[j]) rep[w[j]] = f[j];
-      return;
-    }
-    uint32_t wn[kSteps], rk[kSteps];
-#pragma unroll
-    for (int j = 0; j < kSteps; ++j) {
-      wn[j] = lk[j] ? w[j] / win_rows : 0u;
-      rk[j] = lk[j] ? atomicAdd(&scr[wn[j]], 1u) : 0u;
-    }
-    __syncthreads();
-    static_assert(kWinCount == 128 && 2 * kWinCount + 1 <= kListScratch, "two windows per lane");
-    if (threadIdx.x < 64) {
-      const uint32_t lane = threadIdx.x;
-      const uint32_t a0 = scr[2 * lane], a1 = scr[2 * lane + 1], v = a0 + a1;
-      uint32_t inc = v;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(inc, d);
-        if (lane >= static_cast<uint32_t>(d)) inc += o;
-      }
-      scr[kWinCount + 2 * lane] = inc - v;
-      scr[kWinCount + 2 * lane + 1] = inc - v + a0;
-      if (lane == 63) scr[2 * kWinCount] = inc;
-    }
-    __syncthreads();
-    if (threadIdx.x <= kWinCount)
-      bnd[static_cast<uint64_t>(blockIdx.x) * (kWinCount + 1) + threadIdx.x] =
-          static_cast<uint16_t>(scr[kWinCount + threadIdx.x]);
-#pragma unroll
-    for (int j = 0; j < kSteps; ++j)
-      if (lk[j]) pairs[start + scr[kWinCount + wn[j]] + rk[j]] = make_uint2(w[j], f[j]);
-    (void)live;
-    (void)r;
-  }
-};
 __device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t) {}
-__device__ __forceinline__ void out_done(const WinOut&, uint32_t, uint32_t, uint32_t) {}
 __device__ __forceinline__ void out_done(const ListOut& o, uint32_t c_run, uint32_t l_run,
                                          uint32_t end) {
   o.done(c_run, l_run, end);
-}
-// before the bucket's first barrier (scratch the output uses)
-__device__ __forceinline__ void out_init(const RepOut&, uint32_t*) {}
-__device__ __forceinline__ void out_init(const ListOut&, uint32_t*) {}
-__device__ __forceinline__ void out_init(const WinOut&, uint32_t* scr) {
-  if (threadIdx.x < kWinCount) scr[threadIdx.x] = 0;
-}
-// a bucket that lists nothing in its window table (empty, or the global path)
-__device__ __forceinline__ void out_skip(const RepOut&) {}
-__device__ __forceinline__ void out_skip(const ListOut&) {}
-__device__ __forceinline__ void out_skip(const WinOut& o) {
-  if (threadIdx.x <= kWinCount)
-    o.bnd[static_cast<uint64_t>(blockIdx.x) * (kWinCount + 1) + threadIdx.x] = 0;
 }
 
 // Bucket records as {hash lo, hash hi, rank, row}: 16-byte records as stored,
@@ -1612,16 +1537,13 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
   constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
   const uint32_t m = end - start;
   if (m == 0) {
-    out_skip(out);
     out_done(out, 0u, 0u, end);
     return;
   }
   if (m > kPkCap) {
-    out_skip(out);
     group_bucket_global(rec, start, end, chunk_of, gkey, gmin, out, special_min, scr);
     return;
   }
-  out_init(out, scr);
   // every load issued unconditionally (past the end: the bucket's last record)
   // and the pad selected after: a guarded `i < end ? rec(i) : pad` made the
   // compiler branch around each load and wait out its latency before the
@@ -1759,32 +1681,6 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12_pk(
   const uint32_t b = blockIdx.x;
   group_bucket_packed(Rec12Src{rec, rank_base}, offs[b], offs[b + 1], bits, chunk_of, gkey, gmin,
                       out, tab, lmin, special_min, scr);
-}
-
-// The pairs of row window j from every bucket, scattered into rep while the
-// window's ~3 MB of rep stay in one XCD's L2: workgroup b runs on XCD b % 8
-// (round-robin dispatch), and the XCD's workgroups take its windows in turn,
-// kWinParts per window, each a range of buckets (one bucket per thread).
-constexpr uint32_t kWinParts = 32;
-constexpr uint32_t kWinThreads = 1024;
-__global__ __launch_bounds__(kWinThreads) void k_window_apply(const uint2* __restrict__ pairs,
-                                                              const uint32_t* __restrict__ offs,
-                                                              const uint16_t* __restrict__ bnd,
-                                                              uint32_t nb, uint32_t* __restrict__ rep) {
-  static_assert(kWinCount % 8 == 0, "windows spread evenly over the 8 XCDs");
-  const uint32_t b = blockIdx.x, x = b & 7u, t = b >> 3;
-  const uint32_t j = x + 8u * (t / kWinParts), part = t % kWinParts;
-  const uint32_t per = (nb + kWinParts - 1) / kWinParts;
-  const uint32_t b1 = min(nb, (part + 1) * per);
-  for (uint32_t bk = part * per + threadIdx.x; bk < b1; bk += kWinThreads) {
-    const uint64_t e = static_cast<uint64_t>(bk) * (kWinCount + 1) + j;
-    const uint32_t base = offs[bk];
-    const uint32_t s0 = base + bnd[e], s1 = base + bnd[e + 1];
-    for (uint32_t p = s0; p < s1; ++p) {
-      const uint2 pr = pairs[p];
-      rep[pr.x] = pr.y;
-    }
-  }
 }
 
 // the segment sizes k_part_private adds to, and the fine-count overflow flag
@@ -1974,14 +1870,9 @@ struct GroupLayout {
   // run table [block][round][digit] (starts, lengths) and the segment sizes
   uint32_t max_rounds;
   size_t run_s, run_l, segtot;
-  size_t bnd;  // two-level rep output for large n: per-bucket row-window bounds (WinOut)
   size_t total;
 };
 
-// The rep array outgrows the Infinity Cache (256 MB) past ~64 M rows; from
-// 2^25 rows (a 128 MB rep array, with the records streaming beside it) the
-// two-level grouping writes its reps through row windows (WinOut).
-constexpr uint64_t kWindowRepRows = 1ull << 25;
 
 GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
   GroupLayout L;
@@ -2010,7 +1901,6 @@ GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
   L.run_s = o; o = align_up(o + 4 * nrun, 256);
   L.run_l = o; o = align_up(o + 4 * nrun, 256);
   L.segtot = o; o = align_up(o + 4 * kRunMaxBins, 256);
-  L.bnd = o; o = align_up(o + (L.cbits ? 2 * (kWinCount + 1) * nf : 0), 256);
   L.total = o;
   return L;
 }
@@ -2081,30 +1971,6 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
       KScope k(timer, "bucket_scatter", s);
       k_part2_runs<kRec12, kB2, kS2, kR2, kF2><<<dim3(kP2, nseg), kPartThreads, 0, s>>>(
           rec1, skip2, fE, rec, run_s, run_l, L.max_rounds, P, kPartBlocks / kP2, segtot, ftot, fbase);
-    }
-    if constexpr (std::is_same<Out, RepOut>::value) {
-      if (n >= kWindowRepRows) {
-        // the reps through row windows: pairs in the (now free) coarse-record
-        // region, window bounds beside, then the XCD-local apply
-        uint2* pairs = reinterpret_cast<uint2*>(rec1);
-        uint16_t* bnd = reinterpret_cast<uint16_t*>(w + L.bnd);
-        const WinOut wo{out.rep, pairs, bnd,
-                        static_cast<uint32_t>((n + kWinCount - 1) / kWinCount)};
-        {
-          KScope k(timer, "bucket_group", s);
-          if constexpr (kRec12)
-            k_bucket_group12_pk<WinOut><<<nfine, kGroupThreads, 0, s>>>(
-                reinterpret_cast<const uint3*>(rec), rank_base, fbase, bits,
-                ChunkOf::make(chunk_rows), gkey, gmin, wo);
-          else
-            k_bucket_group_pk<WinOut><<<nfine, kGroupThreads, 0, s>>>(
-                rec, fbase, 1, bits, ChunkOf::make(chunk_rows), gkey, gmin, wo);
-        }
-        KScope k(timer, "bucket_apply", s);
-        k_window_apply<<<kWinCount * kWinParts, kWinThreads, 0, s>>>(pairs, fbase, bnd, nfine,
-                                                                     out.rep);
-        return hipGetLastError();
-      }
     }
     KScope k(timer, "bucket_group", s);
     if constexpr (kRec12)

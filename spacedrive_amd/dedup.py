@@ -463,7 +463,7 @@ LINKED = 0x80000000  # SDGPU_LINKED: the entry's row connects to an Object
 
 
 def group_link_device(key, has_key=None, valid=None, rank=None, first_rank: int = 0,
-                      chunk_rows: int = 100, ctx=None, trim: bool = True):
+                      chunk_rows: int = 100, ctx=None, trim: bool = True, index=None):
     """Fused grouping + Object write set (sdgpu_group_link_device, ABI 4):
     what group_rows + link_batch_device compute, without a rep array.
 

@@ -327,12 +327,11 @@ def test_histogram_alignment_paths(ctx, key_off, has_off):
 
 
 @pytest.mark.parametrize("chunk", [100, 3])
-def test_two_level_window_rep_output(ctx, chunk):
-    """From 2^25 rows the two-level grouping writes its reps through row
-    windows (WinOut pairs + k_window_apply, round 4): 34 M rows, a key
-    repeated 60 k times (its bucket takes the global table and writes rep
-    directly, listing no pairs), keyless rows, implicit (12-B records) and
-    explicit (16-B records) ranks; bit-exact with the oracle."""
+def test_two_level_34m_rows_both_record_sizes(ctx, chunk):
+    """The two-level grouping at 34 M rows (32 segments, 2^14 buckets): a key
+    repeated 60 k times (its bucket takes the global table), keyless rows,
+    implicit (12-B records) and explicit (16-B records) ranks; bit-exact with
+    the oracle."""
     import torch
     from spacedrive_amd import dedup
     n = 34_000_000
