@@ -88,10 +88,13 @@ inline int64_t read_cas_message(const char* path, uint64_t size, uint8_t* dst, s
     rc = -ENOBUFS;
   } else {
     const uint64_t hf = SDGPU_CAS_HEADER_OR_FOOTER_SIZE, ss = SDGPU_CAS_SAMPLE_SIZE;
-    rc = pread_exact(fd, dst + len, hf, 0);  // header (cas.rs:35-38)
-    len += hf;
+    // header (cas.rs:35-38) and the first sample, which starts where the
+    // header ends (current_pos = 8192, cas.rs:41-51): file[0, 18432) is one
+    // contiguous range of the message, so one pread instead of two
+    rc = pread_exact(fd, dst + len, hf + ss, 0);
+    len += hf + ss;
     const uint64_t jump = (size - 2 * hf) / SDGPU_CAS_SAMPLE_COUNT;  // cas.rs:41
-    for (uint32_t k = 0; k < SDGPU_CAS_SAMPLE_COUNT && rc == 0; ++k) {  // cas.rs:42-51
+    for (uint32_t k = 1; k < SDGPU_CAS_SAMPLE_COUNT && rc == 0; ++k) {  // cas.rs:42-51
       rc = pread_exact(fd, dst + len, ss, static_cast<off_t>(hf + k * jump));
       len += ss;
     }

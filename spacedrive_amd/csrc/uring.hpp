@@ -34,7 +34,7 @@
 namespace sdgpu {
 namespace uring {
 
-// Files per submission batch (one ring per thread; 10 SQEs per sampled file).
+// Files per submission batch (one ring per thread; 9 SQEs per sampled file).
 constexpr uint32_t kBatchFiles = 32;
 constexpr uint32_t kSqeMax = kBatchFiles * 10;
 
@@ -292,9 +292,10 @@ inline bool read_cas_batch(Ring& ring, FileJob* f, uint32_t n, int fail_after = 
         rd(0, j.dst + 8, static_cast<uint32_t>(std::min<size_t>(j.cap - 8, 1u << 30)), 0, true);
       } else {
         const uint64_t jump = (j.size - 2 * hf) / SDGPU_CAS_SAMPLE_COUNT;
-        rd(0, j.dst + 8, hf, 0, true);
-        for (uint32_t k = 0; k < SDGPU_CAS_SAMPLE_COUNT; ++k)
-          rd(1 + k, j.dst + 8 + hf + k * ss, ss, hf + k * jump, true);
+        // header + the first sample (contiguous: file[0, 18432)) in one READ
+        rd(0, j.dst + 8, hf + ss, 0, true);
+        for (uint32_t k = 1; k < SDGPU_CAS_SAMPLE_COUNT; ++k)
+          rd(k, j.dst + 8 + hf + k * ss, ss, hf + k * jump, true);
         rd(5, j.dst + 8 + hf + 4 * ss, hf, j.size - hf, true);  // footer at the STAT size
       }
       if (!ok) break;
@@ -356,10 +357,10 @@ inline bool read_cas_batch(Ring& ring, FileJob* f, uint32_t n, int fail_after = 
                static_cast<uint64_t>(got) == sl.sx.stx_size;
         if (fast) j.result = 8 + got;
       } else if (fast) {
-        fast = sl.res[kOpRead0] == static_cast<int32_t>(hf) && sl.res[kOpRead0 + 5] == static_cast<int32_t>(hf) &&
-               sl.sx.stx_size == j.size;
-        for (uint32_t k = 0; k < SDGPU_CAS_SAMPLE_COUNT && fast; ++k)
-          fast = sl.res[kOpRead0 + 1 + k] == static_cast<int32_t>(ss);
+        fast = sl.res[kOpRead0] == static_cast<int32_t>(hf + ss) &&
+               sl.res[kOpRead0 + 5] == static_cast<int32_t>(hf) && sl.sx.stx_size == j.size;
+        for (uint32_t k = 1; k < SDGPU_CAS_SAMPLE_COUNT && fast; ++k)
+          fast = sl.res[kOpRead0 + k] == static_cast<int32_t>(ss);
         if (fast) j.result = SDGPU_CAS_SAMPLED_MSG_LEN;
       }
       if (!fast) j.result = hostio::read_cas_message(j.path, j.size, j.dst, j.cap);
