@@ -1251,9 +1251,11 @@ __device__ __forceinline__ void wg_list_ranks(const bool (&c)[kSteps], const boo
 //            keyed row, so the positions need no global coordination:
 //            creators from the front in record order, who = rank; linked rows
 //            from the back, who = rank | SDGPU_LINKED, obj = f.  Coalesced;
-//            no rep array.  counts[0] / [1] += the bucket's creators / linked
-//            (one atomic each per workgroup); the last bucket stores the
-//            keyed total in counts[2].
+//            no rep array.  lcnt[bucket] = its linked rows; the last bucket
+//            stores the keyed total in counts[2]; k_list_finish then sets
+//            counts[0] / [1] (no same-address atomics: 32 k workgroups adding
+//            to one word serialised at ~4 ns each, +0.29 ms at 100 M rows in
+//            r4e's fused_job leg).
 struct RepOut {
   static constexpr int kScratch = 1;
   uint32_t* rep;
@@ -1275,6 +1277,7 @@ struct ListOut {
   uint32_t* who;
   uint32_t* obj;
   uint32_t* counts;
+  uint32_t* lcnt;
   // c_run / l_run: creators / linked already written for this bucket (the
   // global-table path emits a bucket in several chunks)
   template <int kSteps>
@@ -1307,12 +1310,35 @@ struct ListOut {
   // once per bucket, after its last emit
   __device__ __forceinline__ void done(uint32_t c_run, uint32_t l_run, uint32_t end) const {
     if (threadIdx.x == 0) {
-      if (c_run) atomicAdd(&counts[0], c_run);
-      if (l_run) atomicAdd(&counts[1], l_run);
+      lcnt[blockIdx.x] = l_run;
       if (blockIdx.x == gridDim.x - 1) counts[2] = end;
     }
+    (void)c_run;
   }
 };
+
+// counts[1] = the buckets' linked rows, counts[0] = keyed - linked (one block)
+__global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict__ lcnt,
+                                                      uint32_t nb, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t sw[16];
+  uint32_t t = 0;
+  for (uint32_t i = threadIdx.x; i < nb; i += 1024) t += lcnt[i];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d);
+  if (__lane_id() == 0) sw[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t l = 0;
+    for (int w = 0; w < 16; ++w) l += sw[w];
+    counts[1] = l;
+    counts[0] = counts[2] - l;
+  }
+}
+hipError_t out_finish(const RepOut&, uint32_t, hipStream_t) { return hipSuccess; }
+hipError_t out_finish(const ListOut& o, uint32_t nb, hipStream_t s) {
+  k_list_finish<<<1, 1024, 0, s>>>(o.lcnt, nb, o.counts);
+  return hipGetLastError();
+}
 __device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t) {}
 __device__ __forceinline__ void out_done(const ListOut& o, uint32_t c_run, uint32_t l_run,
                                          uint32_t end) {
@@ -1870,6 +1896,7 @@ struct GroupLayout {
   // run table [block][round][digit] (starts, lengths) and the segment sizes
   uint32_t max_rounds;
   size_t run_s, run_l, segtot;
+  size_t lcnt;
   size_t total;
 };
 
@@ -1901,6 +1928,7 @@ GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
   L.run_s = o; o = align_up(o + 4 * nrun, 256);
   L.run_l = o; o = align_up(o + 4 * nrun, 256);
   L.segtot = o; o = align_up(o + 4 * kRunMaxBins, 256);
+  L.lcnt = o; o = align_up(o + 4 * nf, 256);  // ListOut: linked rows per bucket
   L.total = o;
   return L;
 }
@@ -1980,7 +2008,7 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
     else
       k_bucket_group_pk<Out><<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits,
                                                              ChunkOf::make(chunk_rows), gkey, gmin, out);
-    return hipGetLastError();
+    return out_finish(out, nfine, s);
   }
   // pass 1: coarse partition on the top cbits digit bits (rep initialised
   // here), counting every row's final bucket on the way
@@ -2031,7 +2059,7 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
   else
     k_bucket_group_pk<Out><<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits,
                                                            ChunkOf::make(chunk_rows), gkey, gmin, out);
-  return hipGetLastError();
+  return out_finish(out, nfine, s);
 }
 
 template <typename In, typename Out>
@@ -2091,7 +2119,7 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
                                                               in.rank_base, fbase, kStageBits,
                                                               ChunkOf::make(chunk_rows), gkey, gmin,
                                                               out);
-        return hipGetLastError();
+        return out_finish(out, nb, s);
       }
     }
     {
@@ -2106,7 +2134,7 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
     KScope k(timer, "bucket_group", s);
     k_bucket_group_pk<Out><<<nb, kGroupThreads, 0, s>>>(rec, fbase, 1, kStageBits,
                                                         ChunkOf::make(chunk_rows), gkey, gmin, out);
-    return hipGetLastError();
+    return out_finish(out, nb, s);
   }
   {
     KScope k(timer, "bucket_hist", s);
@@ -2129,7 +2157,7 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   KScope k(timer, "bucket_group", s);
   k_bucket_group<Out><<<1u << bits, kGroupThreads, 0, s>>>(rec, hist, P, ChunkOf::make(chunk_rows),
                                                            gkey, gmin, out);
-  return hipGetLastError();
+  return out_finish(out, 1u << bits, s);
 }
 
 size_t shard_hist_bytes(uint32_t shard_bits) {
@@ -2180,7 +2208,8 @@ hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t
                              uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
                              KTimer* timer) {
   if (in.n == 0) return hipSuccess;
-  const ListOut out{who, obj, counts};
+  const ListOut out{who, obj, counts,
+                    reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ws) + group_layout(in.n).lcnt)};
   if (in.rec12)
     return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
                         chunk_rows, nullptr, false, out, ws, s, timer);

@@ -48,13 +48,15 @@ __device__ __forceinline__ uint64_t slot_key(const uint4& q) {
 __device__ __forceinline__ uint32_t enc_value(uint32_t v) { return v ^ kRepExisting; }
 
 // Insert (k, v): keeps the minimum enc_value over inserts (existing Objects
-// first).  Returns nothing; counts new keys.
-__device__ __forceinline__ void index_insert(const IndexRef& t, uint64_t k, uint32_t v) {
+// first).  Returns 1 when k took a new slot (the caller adds those up per wave:
+// one atomic per wave on t.count instead of one per key -- same-address
+// device atomics serialise at a few ns each).
+__device__ __forceinline__ uint32_t index_insert(const IndexRef& t, uint64_t k, uint32_t v) {
   const uint32_t e = enc_value(v);
   if (k == kEmptyKey) {
     atomicMax(&t.special[0], 1u);
     atomicMin(&t.special[1], e);
-    return;
+    return 0;
   }
   uint64_t h = row_hash(k) & (t.cap - 1);
   for (;;) {
@@ -62,12 +64,18 @@ __device__ __forceinline__ void index_insert(const IndexRef& t, uint64_t k, uint
     const unsigned long long prev =
         atomicCAS(kp, static_cast<unsigned long long>(kEmptyKey), static_cast<unsigned long long>(k));
     if (prev == kEmptyKey || prev == k) {
-      if (prev == kEmptyKey) atomicAdd(t.count, 1ull);
       atomicMin(&t.slots[h].z, e);
-      return;
+      return prev == kEmptyKey ? 1u : 0u;
     }
     h = (h + 1) & (t.cap - 1);
   }
+}
+
+// after a grid-stride loop (every lane of the wave arrives): the wave's new keys
+__device__ __forceinline__ void count_added(const IndexRef& t, uint32_t added) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) added += __shfl_xor(added, d);
+  if (__lane_id() == 0 && added) atomicAdd(t.count, static_cast<unsigned long long>(added));
 }
 
 // Value of k, or false.
@@ -104,11 +112,13 @@ __global__ __launch_bounds__(kThreads) void k_index_clear(IndexRef t) {
 // Re-insert every entry of `from` into the (cleared, larger) `to`.
 __global__ __launch_bounds__(kThreads) void k_index_rehash(IndexRef from, IndexRef to) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+  uint32_t added = 0;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < from.cap;
        i += stride) {
     const uint4 q = from.slots[i];
-    if (slot_key(q) != kEmptyKey) index_insert(to, slot_key(q), enc_value(q.z));
+    if (slot_key(q) != kEmptyKey) added += index_insert(to, slot_key(q), enc_value(q.z));
   }
+  count_added(to, added);
   if (blockIdx.x == 0 && threadIdx.x == 0 && from.special[0]) {
     to.special[0] = 1;
     to.special[1] = from.special[1];
@@ -122,12 +132,14 @@ __global__ __launch_bounds__(kThreads) void k_index_objects(IndexRef t, const ui
                                                             uint64_t n, uint32_t world,
                                                             uint32_t rank) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+  uint32_t added = 0;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n;
        i += stride) {
     const uint64_t k = key[i];
     if (world > 1 && ((row_hash(k) >> 56) * world) >> 8 != rank) continue;
-    index_insert(t, k, kRepExisting | (handle[i] & ~kRepExisting));
+    added += index_insert(t, k, kRepExisting | (handle[i] & ~kRepExisting));
   }
+  count_added(t, added);
 }
 
 template <typename In>
@@ -160,6 +172,7 @@ __global__ __launch_bounds__(kThreads) void k_index_creators(IndexRef t, In in, 
                                                              const uint32_t* __restrict__ rep,
                                                              const uint8_t* __restrict__ grouped) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+  uint32_t added = 0;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n;
        i += stride) {
     if (!grouped[i]) continue;
@@ -167,8 +180,9 @@ __global__ __launch_bounds__(kThreads) void k_index_creators(IndexRef t, In in, 
     uint32_t r;
     bool v;
     in.get(i, k, r, v);
-    if (rep[i] == r) index_insert(t, k, r);
+    if (rep[i] == r) added += index_insert(t, k, r);
   }
+  count_added(t, added);
 }
 
 uint32_t grid_for(uint64_t n) {

@@ -183,8 +183,9 @@ inline uint32_t link_tiles(uint64_t n) { return static_cast<uint32_t>((n + kTile
 //     mod.rs:189-225): who = rank | SDGPU_LINKED, obj = the probe's rep -- or
 //     who = rank when the probe kept the row's own Object (same chunk).
 // A thread takes 16 consecutive rows (16-B loads of has_key / valid /
-// grouped); 4096-row tiles, counted, scanned, written; one atomic per block
-// adds its creators and linked rows to counts[0] / counts[1].
+// grouped); 4096-row tiles, counted, scanned, written; each block stores its
+// linked rows in xl[block] and k_extra_finish adds the totals to counts[]
+// (per-block same-address atomics serialised: 24 k blocks at 100 M rows).
 constexpr int kKlRows = 16;
 constexpr uint32_t kKlTile = kThreads * kKlRows;
 constexpr uint32_t kLinkedBit = 0x80000000u;  // SDGPU_LINKED
@@ -205,15 +206,15 @@ __device__ __forceinline__ uint32_t bytes16_mask(const uint8_t* __restrict__ p, 
   return m;
 }
 
-// bit k: row i0 + k is an extra entry
+// bit k: row i0 + k is an extra entry; h: bit k = row i0 + k is keyed
 __device__ __forceinline__ uint32_t extra_mask(const uint8_t* __restrict__ has,
                                                const uint8_t* __restrict__ valid,
                                                const uint8_t* __restrict__ grouped, uint64_t n,
-                                               uint64_t i0) {
+                                               uint64_t i0, uint32_t& h) {
   const bool aligned = ((reinterpret_cast<uintptr_t>(has) | reinterpret_cast<uintptr_t>(valid) |
                          reinterpret_cast<uintptr_t>(grouped)) & 15u) == 0;
   const uint32_t in_range = i0 >= n ? 0u : (i0 + kKlRows <= n ? 0xFFFFu : (1u << (n - i0)) - 1u);
-  const uint32_t h = bytes16_mask(has, n, i0, aligned, 0xFFFFu);
+  h = bytes16_mask(has, n, i0, aligned, 0xFFFFu);
   const uint32_t v = bytes16_mask(valid, n, i0, aligned, 0xFFFFu);
   const uint32_t g = bytes16_mask(grouped, n, i0, aligned, 0xFFFFu);
   // keyless and valid, or keyed and decided by the probe
@@ -226,7 +227,8 @@ __global__ __launch_bounds__(kThreads) void k_extra_count(const uint8_t* __restr
                                                           uint64_t n, uint32_t* __restrict__ cnt) {
   __shared__ uint32_t sc[kWaves];
   const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kKlTile + threadIdx.x * kKlRows;
-  uint32_t c = __popc(extra_mask(has, valid, grouped, n, i0));
+  uint32_t h;
+  uint32_t c = __popc(extra_mask(has, valid, grouped, n, i0, h));
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
   if (__lane_id() == 0) sc[threadIdx.x >> 6] = c;
@@ -243,12 +245,12 @@ __global__ __launch_bounds__(kThreads) void k_extra_write(
     const uint8_t* __restrict__ grouped, const uint32_t* __restrict__ hitrep,
     const uint32_t* __restrict__ rank, uint32_t first_rank, uint64_t n,
     const uint32_t* __restrict__ cnt, uint32_t* __restrict__ who, uint32_t* __restrict__ obj,
-    uint32_t* __restrict__ counts) {
+    const uint32_t* __restrict__ counts, uint32_t* __restrict__ xl) {
   __shared__ uint32_t sw[kWaves], sl[kWaves];
   const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kKlTile + threadIdx.x * kKlRows;
   const uint32_t K = counts[2];  // the keyed entries (the group kernel); updated only after this kernel
-  uint32_t m = extra_mask(has, valid, grouped, n, i0);
-  const uint32_t hm = has ? bytes16_mask(has, n, i0, false, 0u) : 0xFFFFu;
+  uint32_t hm;
+  uint32_t m = extra_mask(has, valid, grouped, n, i0, hm);
   const uint32_t c = __popc(m);
   uint32_t inc = c;
   const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
@@ -283,27 +285,39 @@ __global__ __launch_bounds__(kThreads) void k_extra_write(
   if (lane == 0) sl[wv] = linked;
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t tl = 0, tt = 0;
-    for (int w = 0; w < kWaves; ++w) {
-      tl += sl[w];
-      tt += sw[w];
-    }
-    if (tt - tl) atomicAdd(&counts[0], tt - tl);
-    if (tl) atomicAdd(&counts[1], tl);
+    uint32_t tl = 0;
+    for (int w = 0; w < kWaves; ++w) tl += sl[w];
+    xl[blockIdx.x] = tl;
   }
 }
 
-// counts[2] = keyed entries + extra entries (after every block read K)
-__global__ void k_extra_finish(const uint32_t* __restrict__ cnt, uint32_t nb,
-                               uint32_t* __restrict__ counts) {
-  if (threadIdx.x == 0) counts[2] += cnt[nb];
+// after every block read K: counts[0] / [1] += the extra creators / linked,
+// counts[2] += the extra entries (cnt[nb]: the scan's total)
+__global__ __launch_bounds__(1024) void k_extra_finish(const uint32_t* __restrict__ cnt,
+                                                       const uint32_t* __restrict__ xl, uint32_t nb,
+                                                       uint32_t* __restrict__ counts) {
+  __shared__ uint32_t sw[16];
+  uint32_t t = 0;
+  for (uint32_t i = threadIdx.x; i < nb; i += 1024) t += xl[i];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d);
+  if (__lane_id() == 0) sw[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t l = 0;
+    for (int w = 0; w < 16; ++w) l += sw[w];
+    const uint32_t e = cnt[nb];
+    counts[0] += e - l;
+    counts[1] += l;
+    counts[2] += e;
+  }
 }
 
 }  // namespace
 
 size_t extra_workspace_bytes(uint64_t n) {
   const uint64_t m = (n + kKlTile - 1) / kKlTile;
-  return ((m + 1) * 4 + 255) / 256 * 256 + ((scan::tiles_for(m) + 1) * 4 + 255) / 256 * 256;
+  return 2 * (((m + 1) * 4 + 255) / 256 * 256) + ((scan::tiles_for(m) + 1) * 4 + 255) / 256 * 256;
 }
 
 hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uint8_t* grouped,
@@ -313,14 +327,16 @@ hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uin
   if (n == 0 || (!has && !grouped)) return hipSuccess;  // every row keyed, no probe: nothing extra
   const uint32_t nb = static_cast<uint32_t>((n + kKlTile - 1) / kKlTile);
   uint8_t* b = static_cast<uint8_t*>(ws);
+  const size_t cb = ((nb + 1) * 4ull + 255) / 256 * 256;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(b);
-  uint32_t* tiles = reinterpret_cast<uint32_t*>(b + ((nb + 1) * 4ull + 255) / 256 * 256);
+  uint32_t* xl = reinterpret_cast<uint32_t*>(b + cb);
+  uint32_t* tiles = reinterpret_cast<uint32_t*>(b + 2 * cb);
   KScope k(timer, "extra_list", s);
   k_extra_count<<<nb, kThreads, 0, s>>>(has, valid, grouped, n, cnt);
   scan::exclusive(cnt, nb, cnt, tiles, nullptr, s);
   k_extra_write<<<nb, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, cnt,
-                                        who, obj, counts);
-  k_extra_finish<<<1, 64, 0, s>>>(cnt, nb, counts);
+                                        who, obj, counts, xl);
+  k_extra_finish<<<1, 1024, 0, s>>>(cnt, xl, nb, counts);
   return hipGetLastError();
 }
 
