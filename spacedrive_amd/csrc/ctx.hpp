@@ -87,13 +87,17 @@ struct EventTimer final : KTimer {
     (void)hipEventCreate(&e);
     return e;
   }
+  std::vector<size_t> open;  // pending entries whose scope has not ended (scopes nest)
   void begin(const char* name, hipStream_t s) override {
     Pending p{name, get(), get()};
     (void)hipEventRecord(p.a, s);
+    open.push_back(pending.size());
     pending.push_back(p);
   }
   void end(hipStream_t s) override {
-    if (!pending.empty()) (void)hipEventRecord(pending.back().b, s);
+    if (open.empty()) return;
+    (void)hipEventRecord(pending[open.back()].b, s);
+    open.pop_back();
   }
   void resolve() {
     for (auto& p : pending) {
@@ -113,6 +117,7 @@ struct EventTimer final : KTimer {
       pool.push_back(p.b);
     }
     pending.clear();
+    open.clear();
   }
   // a host-side phase (ms of wall time), reported beside the kernels
   void host(const char* name, double ms) {
