@@ -998,6 +998,18 @@ class Runner:
                          "no rep array (sdgpu_group_link_device, valid = all rows)",
                  "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
                              for k, v in fz_kt.items()}}
+        # the list-writing group kernel: reads every keyed record, writes the
+        # write set itself (who for every keyed row, obj for the linked ones)
+        # -- no scattered rep stores
+        gms = fused["kernels"].get("bucket_group", {}).get("avg_ms")
+        if gms:
+            gb = 12 * nk + 4 * nk + 4 * linked
+            pt, _ = pmc_traffic("k_bucket_group12_pk:ListOut", "dedup_full")
+            fused["roofline"] = {"bucket_group": {
+                "algorithmic_bytes": gb, "achieved": gb / (gms * 1e-3) / 1e9,
+                "frac": gb / (gms * 1e-3) / HBM_PEAK, "pmc_traffic": pt,
+                "note": "reads 12 B per keyed record; writes who (4 B per keyed row) and obj "
+                        "(4 B per linked row)"}}
         if parity is not None:
             fused["list_mismatches_vs_oracle"] = fz_bad
         out = {"value": total * steps / t, "unit": "rows/s", "ms_per_step": 1e3 * step_s,

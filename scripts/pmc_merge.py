@@ -14,7 +14,7 @@ import sys
 
 def main():
     prof, out, tag = sys.argv[1], sys.argv[2], sys.argv[3]
-    doc = {"source": f"rocprofv3 --pmc passes of scripts/gpu_r3_profile.sh (TAG={tag}): "
+    doc = {"source": f"rocprofv3 --pmc passes of scripts/gpu_r4_profile.sh (TAG={tag}): "
                      "'kernels' = bench.py --components cas (config-2 1M-file step), "
                      "'dedup' = bench.py --components dedup --dedup-full-rows 0 (12.5M-row "
                      "grouping), 'dedup_full' = --dedup-rows 100000000 --dedup-full-rows 0 "
