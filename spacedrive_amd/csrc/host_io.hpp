@@ -183,11 +183,19 @@ class Pool {
   const pid_t pid = getpid();  // a fork()ed child has the object but not the threads
 
  private:
+  // guided self-scheduling: a grab takes 1/(4 x threads) of what is left, at
+  // most `grain` and at least 1, so the threads finish within about one file
+  // of each other (fixed grains left up to a grain of files on one thread at
+  // the end of every slab fill)
   void work(const std::function<void(uint32_t)>* f, uint32_t n, uint32_t grain) {
+    const uint32_t share = 4 * (static_cast<uint32_t>(th_.size()) + 1);
     for (;;) {
-      const uint32_t i0 = next_.fetch_add(grain);
-      if (i0 >= n) break;
-      const uint32_t i1 = std::min(n, i0 + grain);
+      uint32_t i0 = next_.load(std::memory_order_relaxed), g;
+      do {
+        if (i0 >= n) return;
+        g = std::max(1u, std::min(grain, (n - i0) / share));
+      } while (!next_.compare_exchange_weak(i0, i0 + g, std::memory_order_relaxed));
+      const uint32_t i1 = std::min(n, i0 + g);
       for (uint32_t i = i0; i < i1; ++i) (*f)(i);
     }
   }
@@ -233,7 +241,7 @@ inline void parallel_for(uint32_t n, F&& f) {
     for (uint32_t i = 0; i < n; ++i) f(i);
     return;
   }
-  const uint32_t grain = std::max(1u, std::min(64u, n / (8 * nt)));
+  const uint32_t grain = std::max(1u, std::min(64u, n / (4 * nt)));
   Pool& p = pool();
   if (p.pid == getpid() && p.busy.try_lock()) {
     const std::function<void(uint32_t)> fn = [&](uint32_t i) { f(i); };

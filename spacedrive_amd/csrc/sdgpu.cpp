@@ -166,10 +166,19 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
            reinterpret_cast<const int32_t*>(sl.h + L.status));
     return 0;
   };
+  // The device work left after the last read is the last slab's copy + hash:
+  // the final slabs shrink geometrically (half of what is left, down to
+  // kTailBytes) so that tail is a few MiB, not a sixth of the call.
+  constexpr uint64_t kTailBytes = 4ull << 20;
+  uint64_t left = want;
   uint32_t i = 0, k = 0;
   while (rc == 0 && i < n) {
     Slab& sl = slabs[k % S];
     if ((rc = drain(sl)) != 0) break;
+    const uint64_t cap_now =
+        left >= 2 * L.arena_cap
+            ? L.arena_cap
+            : std::min<uint64_t>(L.arena_cap, std::max<uint64_t>(left / 2, kTailBytes));
     // assign files to this slab
     uint8_t* hb = sl.h;
     uint64_t* off = reinterpret_cast<uint64_t*>(hb + L.off);
@@ -180,9 +189,10 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     uint32_t cnt = 0;
     while (i + cnt < n && cnt < L.files_cap) {
       const uint64_t need = align_up(est(i + cnt), 16);
-      if (pos + need > L.arena_cap && cnt > 0) break;
+      if (pos + need > cap_now && cnt > 0) break;
       off[cnt] = pos;
       pos += std::min<uint64_t>(need, L.arena_cap);
+      left -= std::min<uint64_t>(need, left);
       ++cnt;
     }
     sl.count = cnt;
