@@ -160,7 +160,9 @@ __global__ __launch_bounds__(kThreads) void k_orphan_write(const int32_t* __rest
 
 // ---- thumbnail shards -----------------------------------------------------------
 constexpr uint32_t kShardBins = 256;
-constexpr uint32_t kShardBlocks = 256;
+// 1024 tiles (4 per CU): 256 left one workgroup per CU walking 16 serial
+// rounds of its tile (0.11 ms for 1 M rows, r4x trace)
+constexpr uint32_t kShardBlocks = 1024;
 
 __device__ __forceinline__ void tile(uint64_t n, uint64_t& t0, uint64_t& t1) {
   const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
