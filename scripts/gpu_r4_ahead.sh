@@ -1,4 +1,5 @@
 # A/B of the packed group kernel's L2 touch-ahead (SDGPU_GROUP_AHEAD=0 / 1):
+# (Negative: the touch-ahead was removed after this A/B; logs in profiles/r4/ahead_ab/.)
 # GPU tests of the grouping paths, then the dedup leg (12.5 M + 100 M rows,
 # two-call and fused) with the touch off and on.
 #   TAG=r4g bash scripts/gpu_r4_ahead.sh

@@ -1307,12 +1307,11 @@ struct ListOut {
     l_run += tl;
     (void)w;
   }
-  // once per bucket b, after its last emit (last: the final bucket)
-  __device__ __forceinline__ void done(uint32_t c_run, uint32_t l_run, uint32_t end, uint32_t b,
-                                       bool last) const {
+  // once per bucket, after its last emit
+  __device__ __forceinline__ void done(uint32_t c_run, uint32_t l_run, uint32_t end) const {
     if (threadIdx.x == 0) {
-      lcnt[b] = l_run;
-      if (last) counts[2] = end;
+      lcnt[blockIdx.x] = l_run;
+      if (blockIdx.x == gridDim.x - 1) counts[2] = end;
     }
     (void)c_run;
   }
@@ -1340,30 +1339,21 @@ hipError_t out_finish(const ListOut& o, uint32_t nb, hipStream_t s) {
   k_list_finish<<<1, 1024, 0, s>>>(o.lcnt, nb, o.counts);
   return hipGetLastError();
 }
-__device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t, uint32_t,
-                                         bool) {}
+__device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t) {}
 __device__ __forceinline__ void out_done(const ListOut& o, uint32_t c_run, uint32_t l_run,
-                                         uint32_t end, uint32_t b, bool last) {
-  o.done(c_run, l_run, end, b, last);
+                                         uint32_t end) {
+  o.done(c_run, l_run, end);
 }
 
 // Bucket records as {hash lo, hash hi, rank, row}: 16-byte records as stored,
 // or 12-byte ones {hash lo, hash hi, row} with rank = rank_base + row.
 struct Rec16Src {
-  static constexpr uint32_t kBytes = 16;
   const uint4* __restrict__ p;
   __device__ __forceinline__ uint4 operator()(uint32_t i) const { return p[i]; }
-  __device__ __forceinline__ const uint8_t* bytes() const {
-    return reinterpret_cast<const uint8_t*>(p);
-  }
 };
 struct Rec12Src {
-  static constexpr uint32_t kBytes = 12;
   const uint3* __restrict__ p;
   uint32_t rank_base;
-  __device__ __forceinline__ const uint8_t* bytes() const {
-    return reinterpret_cast<const uint8_t*>(p);
-  }
   __device__ __forceinline__ uint4 operator()(uint32_t i) const {
     const uint3 v = p[i];
     return make_uint4(v.x, v.y, rank_base + v.z, v.z);
@@ -1392,8 +1382,7 @@ template <typename Src, typename Out>
 __device__ __forceinline__ void group_bucket_global(Src rec, uint32_t start, uint32_t end,
                                                     ChunkOf chunk_of, uint64_t* __restrict__ gkey,
                                                     uint32_t* __restrict__ gmin, const Out& out,
-                                                    uint32_t& special_min, uint32_t* scr,
-                                                    uint32_t b, bool last) {
+                                                    uint32_t& special_min, uint32_t* scr) {
   const uint32_t m = end - start;
   uint64_t tsize = 1;
   while (tsize * 2 <= 4ull * m) tsize *= 2;  // 2m < tsize <= 4m (64-bit: no wrap)
@@ -1455,7 +1444,7 @@ __device__ __forceinline__ void group_bucket_global(Src rec, uint32_t start, uin
     }
     out.template emit<1>(live, lk, r, w, f, start, end, c_run, l_run, scr, true);
   }
-  out_done(out, c_run, l_run, end, b, last);
+  out_done(out, c_run, l_run, end);
 }
 
 // Group-by of one bucket, rows [start, end) of rec (q_reg preloaded by
@@ -1466,14 +1455,14 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
                                              ChunkOf chunk_of, uint64_t* __restrict__ gkey,
                                              uint32_t* __restrict__ gmin, const Out& out,
                                              uint64_t* lkey, uint32_t* lmin, uint32_t& special_min,
-                                             uint32_t* scr, uint32_t b, bool last) {
+                                             uint32_t* scr) {
   const uint32_t m = end - start;
   if (m == 0) {
-    out_done(out, 0u, 0u, end, b, last);
+    out_done(out, 0u, 0u, end);
     return;
   }
   if (m > kLdsCap) {
-    group_bucket_global(rec, start, end, chunk_of, gkey, gmin, out, special_min, scr, b, last);
+    group_bucket_global(rec, start, end, chunk_of, gkey, gmin, out, special_min, scr);
     return;
   }
   // (the LDS code names lkey / lmin directly: through generic pointers shared
@@ -1542,7 +1531,7 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
   }
   uint32_t c_run = 0, l_run = 0;
   out.template emit<kPer>(lv, lk, r, w, f, start, end, c_run, l_run, scr, false);
-  out_done(out, c_run, l_run, end, b, last);
+  out_done(out, c_run, l_run, end);
 }
 
 // K5 with a PACKED 8-byte LDS table, for buckets of >= 12 digit bits (the
@@ -1564,44 +1553,33 @@ __device__ __forceinline__ uint64_t key_rest(uint64_t h, uint32_t bits) {
   return (h & ((1ull << lo) - 1)) | ((h >> (64 - kShardBits)) << lo);
 }
 
-constexpr int kPkPer = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
-
-// A packed bucket's records into registers (pads past the end).  Every load is
-// issued unconditionally (past the end: the bucket's last record) and the pad
-// selected after: a guarded `i < end ? rec(i) : pad` made the compiler branch
-// around each load and wait out its latency before the next one (four serial
-// memory latencies per workgroup).  Buckets the LDS table does not take
-// (empty, or above kPkCap records) load nothing.
-template <typename Src>
-__device__ __forceinline__ void load_packed(Src rec, uint32_t start, uint32_t end,
-                                            uint4 (&q)[kPkPer]) {
-  if (end == start || end - start > kPkCap) return;
-#pragma unroll
-  for (int j = 0; j < kPkPer; ++j) q[j] = rec(min(start + threadIdx.x + j * kGroupThreads, end - 1));
-#pragma unroll
-  for (int j = 0; j < kPkPer; ++j)
-    if (start + threadIdx.x + j * kGroupThreads >= end) q[j] = make_uint4(0, 0, kPadRow, kPadRow);
-}
-
-// Group-by of packed bucket b, its records already in q (load_packed).
 template <typename Src, typename Out>
-__device__ __forceinline__ void group_bucket_packed_q(Src rec, uint32_t start, uint32_t end,
-                                                      const uint4 (&q)[kPkPer], uint32_t bits,
-                                                      ChunkOf chunk_of, uint64_t* __restrict__ gkey,
-                                                      uint32_t* __restrict__ gmin, const Out& out,
-                                                      uint64_t* tab, uint32_t* lmin,
-                                                      uint32_t& special_min, uint32_t* scr,
-                                                      uint32_t b, bool last) {
-  constexpr int kP = kPkPer;
+__device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uint32_t end,
+                                                    uint32_t bits, ChunkOf chunk_of,
+                                                    uint64_t* __restrict__ gkey,
+                                                    uint32_t* __restrict__ gmin, const Out& out,
+                                                    uint64_t* tab, uint32_t* lmin,
+                                                    uint32_t& special_min, uint32_t* scr) {
+  constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
   const uint32_t m = end - start;
   if (m == 0) {
-    out_done(out, 0u, 0u, end, b, last);
+    out_done(out, 0u, 0u, end);
     return;
   }
   if (m > kPkCap) {
-    group_bucket_global(rec, start, end, chunk_of, gkey, gmin, out, special_min, scr, b, last);
+    group_bucket_global(rec, start, end, chunk_of, gkey, gmin, out, special_min, scr);
     return;
   }
+  // every load issued unconditionally (past the end: the bucket's last record)
+  // and the pad selected after: a guarded `i < end ? rec(i) : pad` made the
+  // compiler branch around each load and wait out its latency before the
+  // next one (four serial memory latencies per workgroup)
+  uint4 q[kP];
+#pragma unroll
+  for (int j = 0; j < kP; ++j) q[j] = rec(min(start + threadIdx.x + j * kGroupThreads, end - 1));
+#pragma unroll
+  for (int j = 0; j < kP; ++j)
+    if (start + threadIdx.x + j * kGroupThreads >= end) q[j] = make_uint4(0, 0, kPadRow, kPadRow);
   for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
   for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
   __syncthreads();
@@ -1663,45 +1641,9 @@ __device__ __forceinline__ void group_bucket_packed_q(Src rec, uint32_t start, u
   }
   uint32_t c_run = 0, l_run = 0;
   out.template emit<kP>(lv, lk, r, w, f, start, end, c_run, l_run, scr, false);
-  out_done(out, c_run, l_run, end, b, last);
+  out_done(out, c_run, l_run, end);
 }
 
-template <typename Src, typename Out>
-__device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uint32_t end,
-                                                    uint32_t bits, ChunkOf chunk_of,
-                                                    uint64_t* __restrict__ gkey,
-                                                    uint32_t* __restrict__ gmin, const Out& out,
-                                                    uint64_t* tab, uint32_t* lmin,
-                                                    uint32_t& special_min, uint32_t* scr,
-                                                    uint32_t b, bool last) {
-  uint4 q[kPkPer];
-  load_packed(rec, start, end, q);
-  group_bucket_packed_q(rec, start, end, q, bits, chunk_of, gkey, gmin, out, tab, lmin,
-                        special_min, scr, b, last);
-}
-
-// L2 touch-ahead for the packed K5 (one workgroup per bucket): workgroup b
-// touches every 128-B line of bucket b + ahead (one dword per thread,
-// consumed only at the end of the kernel).  ahead = the resident grid, a
-// multiple of 8: that bucket is dispatched about when this one retires, to
-// the same XCD (workgroups go round-robin over the 8 XCDs), so its loads hit
-// that XCD's L2 instead of waiting out HBM latency behind a cold start.  The
-// barriers inside wait only for LDS (lgkmcnt), so the touch stays in flight.
-struct OffsAt {
-  const uint32_t* __restrict__ p;
-  __device__ __forceinline__ uint32_t operator()(uint32_t b) const { return p[b]; }
-};
-
-template <typename Src, typename Offs>
-__device__ __forceinline__ uint32_t touch_bucket(Src rec, Offs offs, uint32_t b, uint32_t nb,
-                                                 uint32_t ahead) {
-  const uint32_t bn = b + ahead;
-  if (ahead == 0 || bn >= nb) return 0;
-  const uint64_t b0 = static_cast<uint64_t>(offs(bn)) * Src::kBytes,
-                 b1 = static_cast<uint64_t>(offs(bn + 1)) * Src::kBytes;
-  const uint64_t a = (b0 & ~127ull) + 128ull * threadIdx.x;  // rec is 256-B aligned
-  return a < b1 ? *reinterpret_cast<const uint32_t*>(rec.bytes() + a) : 0u;
-}
 
 // One workgroup per bucket.  Rows of bucket b: [offs[b*P], offs[(b+1)*P]).
 template <typename Out>
@@ -1718,7 +1660,7 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group(
   uint4 q_reg[kPer];
   load_bucket(Rec16Src{rec}, start, end, q_reg);
   group_bucket(Rec16Src{rec}, start, end, q_reg, chunk_of, gkey, gmin, out, lkey, lmin,
-               special_min, scr, b, b == gridDim.x - 1);
+               special_min, scr);
 }
 
 // k_bucket_group over 12-byte records (rank = rank_base + row).
@@ -1735,42 +1677,36 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12(
   const Rec12Src src{rec, rank_base};
   uint4 q_reg[kPer];
   load_bucket(src, start, end, q_reg);
-  group_bucket(src, start, end, q_reg, chunk_of, gkey, gmin, out, lkey, lmin, special_min, scr, b,
-               b == gridDim.x - 1);
+  group_bucket(src, start, end, q_reg, chunk_of, gkey, gmin, out, lkey, lmin, special_min, scr);
 }
 
 // Packed-table K5 (>= 12 digit bits): rows of bucket b in [offs[b*P], offs[(b+1)*P]).
 template <typename Out>
 __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group_pk(
-    const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t bits,
-    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin, Out out,
-    uint32_t ahead) {
+    const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P, uint32_t bits,
+    ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin, Out out) {
   __shared__ uint64_t tab[kPkSlots];
   __shared__ uint32_t lmin[kPkCap + 1];
   __shared__ uint32_t special_min;
   __shared__ uint32_t scr[Out::kScratch];
   const uint32_t b = blockIdx.x;
-  const uint32_t touch = touch_bucket(Rec16Src{rec}, OffsAt{offs}, b, gridDim.x, ahead);
-  group_bucket_packed(Rec16Src{rec}, offs[b], offs[b + 1], bits, chunk_of, gkey, gmin, out, tab,
-                      lmin, special_min, scr, b, b == gridDim.x - 1);
-  asm volatile("" ::"v"(touch));
+  group_bucket_packed(Rec16Src{rec}, offs[static_cast<uint64_t>(b) * P],
+                      offs[static_cast<uint64_t>(b + 1) * P], bits, chunk_of, gkey, gmin, out, tab,
+                      lmin, special_min, scr);
 }
 
 template <typename Out>
 __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12_pk(
     const uint3* __restrict__ rec, uint32_t rank_base, const uint32_t* __restrict__ offs,
     uint32_t bits, ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
-    Out out, uint32_t ahead) {
+    Out out) {
   __shared__ uint64_t tab[kPkSlots];
   __shared__ uint32_t lmin[kPkCap + 1];
   __shared__ uint32_t special_min;
   __shared__ uint32_t scr[Out::kScratch];
   const uint32_t b = blockIdx.x;
-  const Rec12Src src{rec, rank_base};
-  const uint32_t touch = touch_bucket(src, OffsAt{offs}, b, gridDim.x, ahead);
-  group_bucket_packed(src, offs[b], offs[b + 1], bits, chunk_of, gkey, gmin, out, tab, lmin,
-                      special_min, scr, b, b == gridDim.x - 1);
-  asm volatile("" ::"v"(touch));
+  group_bucket_packed(Rec12Src{rec, rank_base}, offs[b], offs[b + 1], bits, chunk_of, gkey, gmin,
+                      out, tab, lmin, special_min, scr);
 }
 
 // the segment sizes k_part_private adds to, and the fine-count overflow flag
@@ -1952,51 +1888,6 @@ uint32_t bucket_bits_for(uint64_t n) {
 // blocks per segment).  A single 2^15-way scatter keeps 32 k partially written
 // lines open per block and ran 3.7 ms for 100 M rows
 // (profiles/r2/bench_r2b.json); the two passes move 2 x 32 B per row instead.
-// Packed K5 launches: one workgroup per bucket with the L2 touch-ahead
-// (touch_bucket) of the bucket one resident grid later; SDGPU_GROUP_AHEAD=0
-// turns it off (A/B).
-template <typename Out, bool kRec12>
-uint32_t pk_ahead() {
-  static const bool on = [] {
-    const char* e = getenv("SDGPU_GROUP_AHEAD");
-    return !(e && e[0] == '0');
-  }();
-  static int cached_dev = -1;
-  static uint32_t cached = 0;
-  if (!on) return 0;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (dev != cached_dev) {
-    int cus = 0, per = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if constexpr (kRec12)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bucket_group12_pk<Out>,
-                                                         kGroupThreads, 0);
-    else
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bucket_group_pk<Out>,
-                                                         kGroupThreads, 0);
-    // a multiple of the 8 XCDs: the touched bucket runs on this one's XCD
-    cached = (static_cast<uint32_t>(std::max(1, cus) * std::max(1, per)) + 7u) & ~7u;
-    cached_dev = dev;
-  }
-  return cached;
-}
-
-// rows of bucket b in [fbase[b], fbase[b + 1]), nb buckets
-template <typename Out>
-void launch_group12_pk(const uint3* rec, uint32_t rank_base, const uint32_t* fbase, uint32_t nb,
-                       uint32_t bits, ChunkOf chunk_of, uint64_t* gkey, uint32_t* gmin, Out out,
-                       hipStream_t s) {
-  k_bucket_group12_pk<Out><<<nb, kGroupThreads, 0, s>>>(rec, rank_base, fbase, bits, chunk_of, gkey,
-                                                        gmin, out, pk_ahead<Out, true>());
-}
-template <typename Out>
-void launch_group_pk(const uint4* rec, const uint32_t* fbase, uint32_t nb, uint32_t bits,
-                     ChunkOf chunk_of, uint64_t* gkey, uint32_t* gmin, Out out, hipStream_t s) {
-  k_bucket_group_pk<Out><<<nb, kGroupThreads, 0, s>>>(rec, fbase, bits, chunk_of, gkey, gmin, out,
-                                                      pk_ahead<Out, false>());
-}
-
 struct GroupLayout {
   uint32_t bits, cbits;
   size_t hist, tiles, rec, hist1, rec1, gkey, gmin;
@@ -2111,10 +2002,12 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
     }
     KScope k(timer, "bucket_group", s);
     if constexpr (kRec12)
-      launch_group12_pk(reinterpret_cast<const uint3*>(rec), rank_base, fbase, nfine, bits,
-                        ChunkOf::make(chunk_rows), gkey, gmin, out, s);
+      k_bucket_group12_pk<Out><<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
+                                                               rank_base, fbase, bits,
+                                                               ChunkOf::make(chunk_rows), gkey, gmin, out);
     else
-      launch_group_pk(rec, fbase, nfine, bits, ChunkOf::make(chunk_rows), gkey, gmin, out, s);
+      k_bucket_group_pk<Out><<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits,
+                                                             ChunkOf::make(chunk_rows), gkey, gmin, out);
     return out_finish(out, nfine, s);
   }
   // pass 1: coarse partition on the top cbits digit bits (rep initialised
@@ -2160,10 +2053,12 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
   }
   KScope k(timer, "bucket_group", s);
   if constexpr (kRec12)
-    launch_group12_pk(reinterpret_cast<const uint3*>(rec), rank_base, fbase, nfine, bits,
-                      ChunkOf::make(chunk_rows), gkey, gmin, out, s);
+    k_bucket_group12_pk<Out><<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
+                                                             rank_base, fbase, bits,
+                                                             ChunkOf::make(chunk_rows), gkey, gmin, out);
   else
-    launch_group_pk(rec, fbase, nfine, bits, ChunkOf::make(chunk_rows), gkey, gmin, out, s);
+    k_bucket_group_pk<Out><<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits,
+                                                           ChunkOf::make(chunk_rows), gkey, gmin, out);
   return out_finish(out, nfine, s);
 }
 
@@ -2220,8 +2115,10 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
                                                                 rep, fbase);
         }
         KScope k(timer, "bucket_group", s);
-        launch_group12_pk(reinterpret_cast<const uint3*>(rec), in.rank_base, fbase, nb, kStageBits,
-                          ChunkOf::make(chunk_rows), gkey, gmin, out, s);
+        k_bucket_group12_pk<Out><<<nb, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
+                                                              in.rank_base, fbase, kStageBits,
+                                                              ChunkOf::make(chunk_rows), gkey, gmin,
+                                                              out);
         return out_finish(out, nb, s);
       }
     }
@@ -2235,7 +2132,8 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
             in, n, kShardBits, fE, rec, rep, nullptr, 0, ftot, fbase);
     }
     KScope k(timer, "bucket_group", s);
-    launch_group_pk(rec, fbase, nb, kStageBits, ChunkOf::make(chunk_rows), gkey, gmin, out, s);
+    k_bucket_group_pk<Out><<<nb, kGroupThreads, 0, s>>>(rec, fbase, 1, kStageBits,
+                                                        ChunkOf::make(chunk_rows), gkey, gmin, out);
     return out_finish(out, nb, s);
   }
   {
