@@ -183,9 +183,10 @@ inline uint32_t link_tiles(uint64_t n) { return static_cast<uint32_t>((n + kTile
 //     mod.rs:189-225): who = rank | SDGPU_LINKED, obj = the probe's rep -- or
 //     who = rank when the probe kept the row's own Object (same chunk).
 // A thread takes 16 consecutive rows (16-B loads of has_key / valid /
-// grouped); 4096-row tiles, counted, scanned, written; each block stores its
-// linked rows in xl[block] and k_extra_finish adds the totals to counts[]
-// (per-block same-address atomics serialised: 24 k blocks at 100 M rows).
+// grouped); 4096-row tiles.  Three launches: k_extra_count (entries and
+// linked entries per tile), k_extra_scan (ONE block: the tiles' offsets, and
+// counts[] settled from the totals -- no same-address atomics, which
+// serialised at ~5 ns each over 24 k tiles at 100 M rows), k_extra_write.
 constexpr int kKlRows = 16;
 constexpr uint32_t kKlTile = kThreads * kKlRows;
 constexpr uint32_t kLinkedBit = 0x80000000u;  // SDGPU_LINKED
@@ -221,22 +222,107 @@ __device__ __forceinline__ uint32_t extra_mask(const uint8_t* __restrict__ has,
   return in_range & ((~h & v) | (grouped ? (h & ~g) : 0u));
 }
 
-__global__ __launch_bounds__(kThreads) void k_extra_count(const uint8_t* __restrict__ has,
-                                                          const uint8_t* __restrict__ valid,
-                                                          const uint8_t* __restrict__ grouped,
-                                                          uint64_t n, uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t sc[kWaves];
+// the entry of extra row i: who (rank, | LINKED when the probe's rep is
+// another row's), obj (the probe's rep when linked)
+__device__ __forceinline__ bool extra_linked(bool keyed, const uint32_t* __restrict__ hitrep,
+                                             uint64_t i, uint32_t r, uint32_t& o) {
+  if (!keyed) return false;
+  o = hitrep[i];
+  return o != r;
+}
+
+__device__ __forceinline__ uint32_t rank_of(const uint32_t* __restrict__ rank, uint32_t first_rank,
+                                            uint64_t i) {
+  return rank ? rank[i] : first_rank + static_cast<uint32_t>(i);
+}
+
+// per tile: cnt[b] = extra entries, lk[b] = the linked ones among them
+__global__ __launch_bounds__(kThreads) void k_extra_count(
+    const uint8_t* __restrict__ has, const uint8_t* __restrict__ valid,
+    const uint8_t* __restrict__ grouped, const uint32_t* __restrict__ hitrep,
+    const uint32_t* __restrict__ rank, uint32_t first_rank, uint64_t n, uint32_t* __restrict__ cnt,
+    uint32_t* __restrict__ lk) {
+  __shared__ uint32_t sc[kWaves], sl[kWaves];
   const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kKlTile + threadIdx.x * kKlRows;
   uint32_t h;
-  uint32_t c = __popc(extra_mask(has, valid, grouped, n, i0, h));
+  uint32_t m = extra_mask(has, valid, grouped, n, i0, h);
+  uint32_t c = __popc(m), l = 0;
+  // linked entries exist only among probe-decided keyed rows (an index)
+  uint32_t d = grouped ? (m & h) : 0u;
+  while (d) {
+    const int k = __ffs(d) - 1;
+    d &= d - 1;
+    uint32_t o;
+    l += extra_linked(true, hitrep, i0 + k, rank_of(rank, first_rank, i0 + k), o) ? 1u : 0u;
+  }
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
-  if (__lane_id() == 0) sc[threadIdx.x >> 6] = c;
+  for (int s = 32; s > 0; s >>= 1) {
+    c += __shfl_xor(c, s);
+    l += __shfl_xor(l, s);
+  }
+  if (__lane_id() == 0) {
+    sc[threadIdx.x >> 6] = c;
+    sl[threadIdx.x >> 6] = l;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < kWaves; ++w) t += sc[w];
-    cnt[blockIdx.x] = t;
+    uint32_t tc = 0, tl = 0;
+    for (int w = 0; w < kWaves; ++w) {
+      tc += sc[w];
+      tl += sl[w];
+    }
+    cnt[blockIdx.x] = tc;
+    lk[blockIdx.x] = tl;
+  }
+}
+
+// ONE block: cnt[] -> exclusive tile offsets; kx[0] = K (the keyed entries,
+// counts[2] as the group kernel left it, for k_extra_write); counts[0..2] +=
+// the extra creators / linked / entries
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void k_extra_scan(uint32_t* __restrict__ cnt,
+                                                             const uint32_t* __restrict__ lk,
+                                                             uint32_t nb, uint32_t* __restrict__ kx,
+                                                             uint32_t* __restrict__ counts) {
+  __shared__ uint32_t sw[kScanThreads / 64], slk[kScanThreads / 64];
+  const uint32_t per = (nb + kScanThreads - 1) / kScanThreads;
+  const uint32_t b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+  uint32_t t = 0, l = 0;
+  for (uint32_t b = b0; b < b1; ++b) {
+    t += cnt[b];
+    l += lk[b];
+  }
+  // block-wide exclusive scan of t (wave scan + wave totals)
+  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+  uint32_t inc = t;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d);
+    if (lane >= static_cast<uint32_t>(d)) inc += o;
+  }
+  uint32_t lw = l;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) lw += __shfl_xor(lw, d);
+  if (lane == 63) sw[w] = inc;
+  if (lane == 0) slk[w] = lw;
+  __syncthreads();
+  uint32_t base = inc - t, tot = 0, ltot = 0;
+  for (uint32_t v = 0; v < kScanThreads / 64; ++v) {
+    if (v < w) base += sw[v];
+    tot += sw[v];
+    ltot += slk[v];
+  }
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t c = cnt[b];
+    cnt[b] = base;
+    base += c;
+  }
+  if (threadIdx.x == 0) {
+    const uint32_t K = counts[2];
+    kx[0] = K;
+    counts[0] += tot - ltot;
+    counts[1] += ltot;
+    counts[2] = K + tot;
   }
 }
 
@@ -244,11 +330,10 @@ __global__ __launch_bounds__(kThreads) void k_extra_write(
     const uint8_t* __restrict__ has, const uint8_t* __restrict__ valid,
     const uint8_t* __restrict__ grouped, const uint32_t* __restrict__ hitrep,
     const uint32_t* __restrict__ rank, uint32_t first_rank, uint64_t n,
-    const uint32_t* __restrict__ cnt, uint32_t* __restrict__ who, uint32_t* __restrict__ obj,
-    const uint32_t* __restrict__ counts, uint32_t* __restrict__ xl) {
-  __shared__ uint32_t sw[kWaves], sl[kWaves];
+    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ kx, uint32_t* __restrict__ who,
+    uint32_t* __restrict__ obj) {
+  __shared__ uint32_t sw[kWaves];
   const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kKlTile + threadIdx.x * kKlRows;
-  const uint32_t K = counts[2];  // the keyed entries (the group kernel); updated only after this kernel
   uint32_t hm;
   uint32_t m = extra_mask(has, valid, grouped, n, i0, hm);
   const uint32_t c = __popc(m);
@@ -261,55 +346,20 @@ __global__ __launch_bounds__(kThreads) void k_extra_write(
   }
   if (lane == 63) sw[wv] = inc;
   __syncthreads();
-  uint32_t pos = K + cnt[blockIdx.x] + inc - c;
+  if (__syncthreads_or(m != 0) == 0) return;  // a tile without extras (uniform)
+  uint32_t pos = kx[0] + cnt[blockIdx.x] + inc - c;
   for (uint32_t w = 0; w < wv; ++w) pos += sw[w];
-  uint32_t linked = 0;
   while (m) {
     const int k = __ffs(m) - 1;
     m &= m - 1;
     const uint64_t i = i0 + k;
-    const uint32_t r = rank ? rank[i] : first_rank + static_cast<uint32_t>(i);
-    uint32_t w = r;
-    if ((hm >> k) & 1u) {  // keyed: decided by the probe
-      const uint32_t out = hitrep[i];
-      if (out != r) {
-        w = r | kLinkedBit;
-        obj[pos] = out;
-        ++linked;
-      }
+    const uint32_t r = rank_of(rank, first_rank, i);
+    uint32_t o, w = r;
+    if (extra_linked((hm >> k) & 1u, hitrep, i, r, o)) {  // keyed: decided by the probe
+      w = r | kLinkedBit;
+      obj[pos] = o;
     }
     who[pos++] = w;
-  }
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) linked += __shfl_xor(linked, d);
-  if (lane == 0) sl[wv] = linked;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t tl = 0;
-    for (int w = 0; w < kWaves; ++w) tl += sl[w];
-    xl[blockIdx.x] = tl;
-  }
-}
-
-// after every block read K: counts[0] / [1] += the extra creators / linked,
-// counts[2] += the extra entries (cnt[nb]: the scan's total)
-__global__ __launch_bounds__(1024) void k_extra_finish(const uint32_t* __restrict__ cnt,
-                                                       const uint32_t* __restrict__ xl, uint32_t nb,
-                                                       uint32_t* __restrict__ counts) {
-  __shared__ uint32_t sw[16];
-  uint32_t t = 0;
-  for (uint32_t i = threadIdx.x; i < nb; i += 1024) t += xl[i];
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d);
-  if (__lane_id() == 0) sw[threadIdx.x >> 6] = t;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t l = 0;
-    for (int w = 0; w < 16; ++w) l += sw[w];
-    const uint32_t e = cnt[nb];
-    counts[0] += e - l;
-    counts[1] += l;
-    counts[2] += e;
   }
 }
 
@@ -317,7 +367,7 @@ __global__ __launch_bounds__(1024) void k_extra_finish(const uint32_t* __restric
 
 size_t extra_workspace_bytes(uint64_t n) {
   const uint64_t m = (n + kKlTile - 1) / kKlTile;
-  return 2 * (((m + 1) * 4 + 255) / 256 * 256) + ((scan::tiles_for(m) + 1) * 4 + 255) / 256 * 256;
+  return 2 * (((m + 1) * 4 + 255) / 256 * 256) + 256;
 }
 
 hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uint8_t* grouped,
@@ -329,14 +379,13 @@ hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uin
   uint8_t* b = static_cast<uint8_t*>(ws);
   const size_t cb = ((nb + 1) * 4ull + 255) / 256 * 256;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(b);
-  uint32_t* xl = reinterpret_cast<uint32_t*>(b + cb);
-  uint32_t* tiles = reinterpret_cast<uint32_t*>(b + 2 * cb);
+  uint32_t* lk = reinterpret_cast<uint32_t*>(b + cb);
+  uint32_t* kx = reinterpret_cast<uint32_t*>(b + 2 * cb);
   KScope k(timer, "extra_list", s);
-  k_extra_count<<<nb, kThreads, 0, s>>>(has, valid, grouped, n, cnt);
-  scan::exclusive(cnt, nb, cnt, tiles, nullptr, s);
-  k_extra_write<<<nb, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, cnt,
-                                        who, obj, counts, xl);
-  k_extra_finish<<<1, 1024, 0, s>>>(cnt, xl, nb, counts);
+  k_extra_count<<<nb, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, cnt, lk);
+  k_extra_scan<<<1, kScanThreads, 0, s>>>(cnt, lk, nb, kx, counts);
+  k_extra_write<<<nb, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, cnt, kx,
+                                        who, obj);
   return hipGetLastError();
 }
 
