@@ -201,3 +201,50 @@ def test_fused_batches_through_the_object_index(ctx, chunk, bounds):
     np.testing.assert_array_equal(fc, rc)
     np.testing.assert_array_equal(flr, rlr)
     np.testing.assert_array_equal(flo, rlo)
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4097, 65_537, 5_000_003])
+def test_fused_extras_only_and_ragged_tiles(ctx, n):
+    """The extra-entry pass alone and at tile edges: every row keyless (the
+    group kernels see no record, every valid row is its own Object), then a
+    ragged row count with 30 % keyless rows and 5 % invalid ones, so the
+    one-block scan runs over more tiles than it has threads (5 M rows: 1221
+    tiles) and the last tile is partial."""
+    rng = np.random.default_rng(n + 77)
+    key = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    _check(ctx, key, np.zeros(n, np.uint8))
+    valid = (rng.random(n) > 0.05).astype(np.uint8)
+    _check(ctx, key, np.zeros(n, np.uint8), valid=valid, first_rank=300)
+    pool = key[: max(1, n // 3)]
+    key2 = pool[rng.integers(0, pool.size, n)]
+    has = ((rng.random(n) > 0.3) & (valid != 0)).astype(np.uint8)
+    _check(ctx, key2, has, valid=valid)
+
+
+def test_fused_every_row_decided_by_the_index(ctx):
+    """A batch whose every cas_id already has an Object (registered before
+    the run): the probe decides every keyed row, the group kernels get no
+    record, and every entry comes from the extra pass (linked to the
+    registered Object); keyless rows stay their own Objects."""
+    import torch
+    from spacedrive_amd import dedup
+    n = 300_000
+    rng = np.random.default_rng(5)
+    pool = rng.integers(0, 2**64 - 1, 50_000, dtype=np.uint64, endpoint=True)
+    key = pool[rng.integers(0, pool.size, n)]
+    has = (rng.random(n) > 0.02).astype(np.uint8)
+    eh = np.arange(pool.size, dtype=np.uint32) * 3 + 1
+    idx = dedup.ObjectIndex(ctx, 1 << 17)
+    idx.add_objects(torch.from_numpy(pool.view(np.int64)).cuda(),
+                    torch.from_numpy(eh.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    dk = torch.from_numpy(key.view(np.int64)).cuda()
+    dh = torch.from_numpy(has).cuda()
+    who, obj, (c, l) = dedup.group_link_device(dk, dh, None, None, 0, 100, ctx=ctx, index=idx)
+    fc, flr, flo = dedup.split_link_lists(who.cpu().numpy(), obj.cpu().numpy())
+    ref = O.group_reps_existing(key, has, 100, pool, eh)
+    rc, rlr, rlo = O.link_batch(ref, None, None, 0)
+    assert (c, l) == (rc.size, rlr.size) and l == int(has.sum())
+    np.testing.assert_array_equal(fc, rc)
+    np.testing.assert_array_equal(flr, rlr)
+    np.testing.assert_array_equal(flo, rlo)
