@@ -99,8 +99,8 @@ int cas_grown_locked(sdgpu_ctx* c, const char* path, uint64_t size, uint8_t out8
 // producer (the file reads, on the pool threads), H2D + K1 + D2H on the
 // context stream, three slabs in rotation so the host fills slab k+1 while the
 // GPU works on slab k.  The reads are the bound, so slabs are sized to about a
-// sixth of the call's bytes (16-256 MiB): the device work left after the last
-// read is one small slab, not half the input.
+// tenth of the call's bytes (16-256 MiB) and the last ones shrink: the device
+// work left after the last read is one small slab, not half the input.
 // ---------------------------------------------------------------------------
 
 struct Slab {
@@ -137,7 +137,10 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     want += e;
     biggest = std::max(biggest, e);
   }
-  const uint64_t target = want <= (kSlabMinBytes << 1) ? want : std::max(want / 6, kSlabMinBytes);
+  // a tenth of the call (r4h: with sixths the slab before the shrinking
+  // tail was still on the device when the ring came back to it -- 2.6 ms of
+  // stage_wait in an 18 ms config-1 call)
+  const uint64_t target = want <= (kSlabMinBytes << 1) ? want : std::max(want / 10, kSlabMinBytes);
   const SlabLayout L = slab_layout(
       static_cast<size_t>(std::clamp<uint64_t>(std::max(target, biggest), 4096, kSlabBytes)),
       std::clamp<uint32_t>(n, 1, kSlabFiles));
