@@ -35,13 +35,14 @@ uint32_t grid_for(uint64_t n, uint64_t per = kThreads) {
 // lines leave whole.  Every file_path id is read once per range (8 times in
 // all, the repeats from the shared last-level cache): one scattered byte store
 // per row into the whole map left each store a partial-line write of its own.
-constexpr uint32_t kMarkRanges = 8;
+// ranges: 8 (one per XCD), or fewer (A/B, SDGPU_MARK_RANGES: XCDs x and
+// x + ranges share a range; fewer re-reads of the file_path ids)
 __global__ __launch_bounds__(kThreads) void k_mark(const int32_t* __restrict__ fp_obj, uint64_t n,
                                                    uint8_t* __restrict__ mark, uint32_t max_id,
-                                                   uint32_t span) {
-  const uint32_t r = blockIdx.x % kMarkRanges, g = blockIdx.x / kMarkRanges;
+                                                   uint32_t span, uint32_t ranges) {
+  const uint32_t r = blockIdx.x % ranges, g = blockIdx.x / ranges;
   const uint32_t lo = r * span;
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x / kMarkRanges) * kThreads * 4;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x / ranges) * kThreads * 4;
   for (uint64_t i0 = static_cast<uint64_t>(g) * kThreads * 4 + threadIdx.x; i0 < n; i0 += stride) {
     int32_t o[4];
     // loads unconditional (clamped), the tail masked after: a guarded load
@@ -257,10 +258,15 @@ hipError_t orphan_objects_launch(const int32_t* obj, uint64_t n_obj, const int32
   uint32_t* tiles = cnt + blocks + 1;
   (void)hipMemsetAsync(bits, 0, map, s);
   if (n_fp) {
-    const uint32_t span = static_cast<uint32_t>((static_cast<uint64_t>(max_id) + kMarkRanges) / kMarkRanges);
+    static const uint32_t ranges = [] {
+      const char* e = getenv("SDGPU_MARK_RANGES");
+      const unsigned long v = e ? strtoul(e, nullptr, 10) : 0;
+      return (v == 1 || v == 2 || v == 4 || v == 8) ? static_cast<uint32_t>(v) : 8u;
+    }();
+    const uint32_t span = static_cast<uint32_t>((static_cast<uint64_t>(max_id) + ranges) / ranges);
     const uint64_t per = (n_fp + 4 * kThreads - 1) / (4 * kThreads);  // 1024-row groups
-    const uint32_t groups = static_cast<uint32_t>(per < 256 ? per : 256);
-    k_mark<<<groups * kMarkRanges, kThreads, 0, s>>>(fp_obj, n_fp, bits, max_id, span);
+    const uint32_t groups = static_cast<uint32_t>(per < 256 ? per : 256) * (8 / ranges);
+    k_mark<<<groups * ranges, kThreads, 0, s>>>(fp_obj, n_fp, bits, max_id, span, ranges);
   }
   if (blocks) {
     k_orphan_count<<<static_cast<uint32_t>(blocks), kThreads, 0, s>>>(obj, n_obj, bits, max_id,
