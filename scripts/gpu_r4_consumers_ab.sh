@@ -17,7 +17,7 @@ d=json.loads(open('gpurun_out/${TAG}_cons_r$R.json').read().strip().splitlines()
 print('ranges $R orphan_remover ms', round(d['orphan_remover']['ms_per_step'],4), 'thumbnail ms', round(d['thumbnail_shards']['ms_per_step'],4))"
 done
 for k in 1 2; do
-  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --components dir \
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --components cas,dir \
     > gpurun_out/${TAG}_dir$k.json 2> gpurun_out/${TAG}_dir$k.err || exit 1
   python3 -c "
 import json
