@@ -184,7 +184,8 @@ inline uint32_t link_tiles(uint64_t n) { return static_cast<uint32_t>((n + kTile
 //     who = rank when the probe kept the row's own Object (same chunk).
 // A thread takes 16 consecutive rows (16-B loads of has_key / valid /
 // grouped); 4096-row tiles.  Three launches: k_extra_count (entries and
-// linked entries per tile), k_extra_scan (ONE block: the tiles' offsets, and
+// linked entries per segment of tiles), k_extra_scan (ONE block: the
+// segments' offsets, and
 // counts[] settled from the totals -- no same-address atomics, which
 // serialised at ~5 ns each over 24 k tiles at 100 M rows), k_extra_write.
 constexpr int kKlRows = 16;
@@ -236,24 +237,42 @@ __device__ __forceinline__ uint32_t rank_of(const uint32_t* __restrict__ rank, u
   return rank ? rank[i] : first_rank + static_cast<uint32_t>(i);
 }
 
-// per tile: cnt[b] = extra entries, lk[b] = the linked ones among them
+// Blocks work on SEGMENTS of whole tiles (at most kExtraSegs of them, so the
+// one-block scan reads a few values per thread: with one tile per block its
+// 24 k-tile loop at 100 M rows was serial load latency, 0.09 ms).
+constexpr uint32_t kExtraSegs = 2048;
+struct ExtraSegs {
+  uint32_t nseg, tps;  // segments, tiles per segment
+  uint64_t tiles;
+};
+__device__ __forceinline__ uint64_t seg_tile0(const ExtraSegs& g, uint32_t seg) {
+  return static_cast<uint64_t>(seg) * g.tps;
+}
+__device__ __forceinline__ uint64_t seg_tile1(const ExtraSegs& g, uint32_t seg) {
+  return min(g.tiles, static_cast<uint64_t>(seg + 1) * g.tps);
+}
+
+// per segment: cnt[s] = extra entries, lk[s] = the linked ones among them
 __global__ __launch_bounds__(kThreads) void k_extra_count(
     const uint8_t* __restrict__ has, const uint8_t* __restrict__ valid,
     const uint8_t* __restrict__ grouped, const uint32_t* __restrict__ hitrep,
-    const uint32_t* __restrict__ rank, uint32_t first_rank, uint64_t n, uint32_t* __restrict__ cnt,
-    uint32_t* __restrict__ lk) {
+    const uint32_t* __restrict__ rank, uint32_t first_rank, uint64_t n, ExtraSegs g,
+    uint32_t* __restrict__ cnt, uint32_t* __restrict__ lk) {
   __shared__ uint32_t sc[kWaves], sl[kWaves];
-  const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kKlTile + threadIdx.x * kKlRows;
-  uint32_t h;
-  uint32_t m = extra_mask(has, valid, grouped, n, i0, h);
-  uint32_t c = __popc(m), l = 0;
-  // linked entries exist only among probe-decided keyed rows (an index)
-  uint32_t d = grouped ? (m & h) : 0u;
-  while (d) {
-    const int k = __ffs(d) - 1;
-    d &= d - 1;
-    uint32_t o;
-    l += extra_linked(true, hitrep, i0 + k, rank_of(rank, first_rank, i0 + k), o) ? 1u : 0u;
+  uint32_t c = 0, l = 0;
+  for (uint64_t t = seg_tile0(g, blockIdx.x); t < seg_tile1(g, blockIdx.x); ++t) {
+    const uint64_t i0 = t * kKlTile + threadIdx.x * kKlRows;
+    uint32_t h;
+    const uint32_t m = extra_mask(has, valid, grouped, n, i0, h);
+    c += __popc(m);
+    // linked entries exist only among probe-decided keyed rows (an index)
+    uint32_t d = grouped ? (m & h) : 0u;
+    while (d) {
+      const int k = __ffs(d) - 1;
+      d &= d - 1;
+      uint32_t o;
+      l += extra_linked(true, hitrep, i0 + k, rank_of(rank, first_rank, i0 + k), o) ? 1u : 0u;
+    }
   }
 #pragma unroll
   for (int s = 32; s > 0; s >>= 1) {
@@ -329,45 +348,62 @@ __global__ __launch_bounds__(kScanThreads) void k_extra_scan(uint32_t* __restric
 __global__ __launch_bounds__(kThreads) void k_extra_write(
     const uint8_t* __restrict__ has, const uint8_t* __restrict__ valid,
     const uint8_t* __restrict__ grouped, const uint32_t* __restrict__ hitrep,
-    const uint32_t* __restrict__ rank, uint32_t first_rank, uint64_t n,
+    const uint32_t* __restrict__ rank, uint32_t first_rank, uint64_t n, ExtraSegs g,
     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ kx, uint32_t* __restrict__ who,
     uint32_t* __restrict__ obj) {
   __shared__ uint32_t sw[kWaves];
-  const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kKlTile + threadIdx.x * kKlRows;
-  uint32_t hm;
-  uint32_t m = extra_mask(has, valid, grouped, n, i0, hm);
-  const uint32_t c = __popc(m);
-  uint32_t inc = c;
   const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+  uint32_t base = kx[0] + cnt[blockIdx.x];  // this segment's first entry
+  for (uint64_t t = seg_tile0(g, blockIdx.x); t < seg_tile1(g, blockIdx.x); ++t) {
+    const uint64_t i0 = t * kKlTile + threadIdx.x * kKlRows;
+    uint32_t hm;
+    uint32_t m = extra_mask(has, valid, grouped, n, i0, hm);
+    const uint32_t c = __popc(m);
+    uint32_t inc = c;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(inc, d);
-    if (lane >= static_cast<uint32_t>(d)) inc += o;
-  }
-  if (lane == 63) sw[wv] = inc;
-  __syncthreads();
-  if (__syncthreads_or(m != 0) == 0) return;  // a tile without extras (uniform)
-  uint32_t pos = kx[0] + cnt[blockIdx.x] + inc - c;
-  for (uint32_t w = 0; w < wv; ++w) pos += sw[w];
-  while (m) {
-    const int k = __ffs(m) - 1;
-    m &= m - 1;
-    const uint64_t i = i0 + k;
-    const uint32_t r = rank_of(rank, first_rank, i);
-    uint32_t o, w = r;
-    if (extra_linked((hm >> k) & 1u, hitrep, i, r, o)) {  // keyed: decided by the probe
-      w = r | kLinkedBit;
-      obj[pos] = o;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
     }
-    who[pos++] = w;
+    if (lane == 63) sw[wv] = inc;
+    __syncthreads();
+    uint32_t pos = base + inc - c, tile_total = 0;
+    for (uint32_t w = 0; w < kWaves; ++w) {
+      if (w < wv) pos += sw[w];
+      tile_total += sw[w];
+    }
+    __syncthreads();  // sw is rewritten by the next tile
+    base += tile_total;
+    while (m) {
+      const int k = __ffs(m) - 1;
+      m &= m - 1;
+      const uint64_t i = i0 + k;
+      const uint32_t r = rank_of(rank, first_rank, i);
+      uint32_t o, w = r;
+      if (extra_linked((hm >> k) & 1u, hitrep, i, r, o)) {  // keyed: decided by the probe
+        w = r | kLinkedBit;
+        obj[pos] = o;
+      }
+      who[pos++] = w;
+    }
   }
 }
 
 }  // namespace
 
-size_t extra_workspace_bytes(uint64_t n) {
-  const uint64_t m = (n + kKlTile - 1) / kKlTile;
-  return 2 * (((m + 1) * 4 + 255) / 256 * 256) + 256;
+namespace {
+ExtraSegs extra_segs(uint64_t n) {
+  ExtraSegs g;
+  g.tiles = (n + kKlTile - 1) / kKlTile;
+  g.nseg = static_cast<uint32_t>(std::min<uint64_t>(g.tiles, kExtraSegs));
+  g.tps = static_cast<uint32_t>((g.tiles + g.nseg - 1) / g.nseg);
+  g.nseg = static_cast<uint32_t>((g.tiles + g.tps - 1) / g.tps);  // no empty segment
+  return g;
+}
+}  // namespace
+
+size_t extra_workspace_bytes(uint64_t) {
+  return 2 * (((kExtraSegs + 1) * 4 + 255) / 256 * 256) + 256;
 }
 
 hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uint8_t* grouped,
@@ -375,17 +411,18 @@ hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uin
                              uint64_t n, uint32_t* who, uint32_t* obj, uint32_t* counts, void* ws,
                              hipStream_t s, KTimer* timer) {
   if (n == 0 || (!has && !grouped)) return hipSuccess;  // every row keyed, no probe: nothing extra
-  const uint32_t nb = static_cast<uint32_t>((n + kKlTile - 1) / kKlTile);
+  const ExtraSegs g = extra_segs(n);
   uint8_t* b = static_cast<uint8_t*>(ws);
-  const size_t cb = ((nb + 1) * 4ull + 255) / 256 * 256;
+  const size_t cb = ((kExtraSegs + 1) * 4ull + 255) / 256 * 256;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(b);
   uint32_t* lk = reinterpret_cast<uint32_t*>(b + cb);
   uint32_t* kx = reinterpret_cast<uint32_t*>(b + 2 * cb);
   KScope k(timer, "extra_list", s);
-  k_extra_count<<<nb, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, cnt, lk);
-  k_extra_scan<<<1, kScanThreads, 0, s>>>(cnt, lk, nb, kx, counts);
-  k_extra_write<<<nb, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, cnt, kx,
-                                        who, obj);
+  k_extra_count<<<g.nseg, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, g,
+                                            cnt, lk);
+  k_extra_scan<<<1, kScanThreads, 0, s>>>(cnt, lk, g.nseg, kx, counts);
+  k_extra_write<<<g.nseg, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, g,
+                                            cnt, kx, who, obj);
   return hipGetLastError();
 }
 
