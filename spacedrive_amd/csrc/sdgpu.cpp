@@ -99,8 +99,8 @@ int cas_grown_locked(sdgpu_ctx* c, const char* path, uint64_t size, uint8_t out8
 // producer (the file reads, on the pool threads), H2D + K1 + D2H on the
 // context stream, three slabs in rotation so the host fills slab k+1 while the
 // GPU works on slab k.  The reads are the bound, so slabs are sized to about a
-// tenth of the call's bytes (16-256 MiB) and the last ones shrink: the device
-// work left after the last read is one small slab, not half the input.
+// sixth of the call's bytes (16-256 MiB): the device work left after the last
+// read is one small slab, not half the input.
 // ---------------------------------------------------------------------------
 
 struct Slab {
@@ -137,10 +137,19 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     want += e;
     biggest = std::max(biggest, e);
   }
-  // a tenth of the call (r4h: with sixths the slab before the shrinking
-  // tail was still on the device when the ring came back to it -- 2.6 ms of
-  // stage_wait in an 18 ms config-1 call)
-  const uint64_t target = want <= (kSlabMinBytes << 1) ? want : std::max(want / 10, kSlabMinBytes);
+  // slab = a sixth of the call; SDGPU_SLAB_DIV / SDGPU_SLAB_TAPER (A/B of
+  // config-1 staging, scripts/gpu_r4_slab_ab.sh) override the division and
+  // switch the tail taper below on
+  static const uint64_t div = [] {
+    const char* e = getenv("SDGPU_SLAB_DIV");
+    const unsigned long v = e ? strtoul(e, nullptr, 10) : 0;
+    return v >= 2 && v <= 64 ? static_cast<uint64_t>(v) : uint64_t(6);
+  }();
+  static const bool taper = [] {
+    const char* e = getenv("SDGPU_SLAB_TAPER");
+    return e && e[0] == '1';
+  }();
+  const uint64_t target = want <= (kSlabMinBytes << 1) ? want : std::max(want / div, kSlabMinBytes);
   const SlabLayout L = slab_layout(
       static_cast<size_t>(std::clamp<uint64_t>(std::max(target, biggest), 4096, kSlabBytes)),
       std::clamp<uint32_t>(n, 1, kSlabFiles));
@@ -169,9 +178,11 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
            reinterpret_cast<const int32_t*>(sl.h + L.status));
     return 0;
   };
-  // The device work left after the last read is the last slab's copy + hash:
-  // the final slabs shrink geometrically (half of what is left, down to
-  // kTailBytes) so that tail is a few MiB, not a sixth of the call.
+  // Taper (off by default): the device work left after the last read is the
+  // last slab's copy + hash, so the final slabs may shrink geometrically (half
+  // of what is left, down to kTailBytes).  Round 3 measured a taper as a loss
+  // (651 k -> 516 k files/s: per-slab planning and pool barriers); round 4's
+  // guided pool grains reopened the question (A/B: DESIGN.md §8).
   constexpr uint64_t kTailBytes = 4ull << 20;
   uint64_t left = want;
   uint32_t i = 0, k = 0;
@@ -179,7 +190,7 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
     Slab& sl = slabs[k % S];
     if ((rc = drain(sl)) != 0) break;
     const uint64_t cap_now =
-        left >= 2 * L.arena_cap
+        !taper || left >= 2 * L.arena_cap
             ? L.arena_cap
             : std::min<uint64_t>(L.arena_cap, std::max<uint64_t>(left / 2, kTailBytes));
     // assign files to this slab
