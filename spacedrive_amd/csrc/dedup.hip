@@ -1339,9 +1339,66 @@ hipError_t out_finish(const ListOut& o, uint32_t nb, hipStream_t s) {
   k_list_finish<<<1, 1024, 0, s>>>(o.lcnt, nb, o.counts);
   return hipGetLastError();
 }
-__device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t) {}
+// ListOutA: the same write set, each wave's entries placed by ONE LDS atomic
+// per (step, list) on the bucket's creator / linked counters (scr[0..1],
+// zeroed with the table) instead of workgroup ranks: no barriers in emit, one
+// at the end for the linked total.  The entries' order inside a bucket then
+// depends on wave timing (not part of the contract).  A/B: SDGPU_LIST_RANKS.
+struct ListOutA {
+  static constexpr int kScratch = 2;
+  uint32_t* who;
+  uint32_t* obj;
+  uint32_t* counts;
+  uint32_t* lcnt;
+  template <int kSteps>
+  __device__ __forceinline__ void emit(const bool (&live)[kSteps], const bool (&lk)[kSteps],
+                                       const uint32_t (&r)[kSteps], const uint32_t (&w)[kSteps],
+                                       const uint32_t (&f)[kSteps], uint32_t start, uint32_t end,
+                                       uint32_t&, uint32_t&, uint32_t* scr, bool) const {
+    const uint32_t lane = __lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int j = 0; j < kSteps; ++j) {
+      const bool c = live[j] && !lk[j], l = lk[j];
+      const uint64_t bc = __ballot(c), bl = __ballot(l);
+      uint32_t cb = 0, lb = 0;
+      if (lane == 0) {
+        if (bc) cb = atomicAdd(&scr[0], static_cast<uint32_t>(__popcll(bc)));
+        if (bl) lb = atomicAdd(&scr[1], static_cast<uint32_t>(__popcll(bl)));
+      }
+      cb = __shfl(cb, 0);
+      lb = __shfl(lb, 0);
+      if (c) who[start + cb + __popcll(bc & lt)] = r[j];
+      if (l) {
+        const uint32_t p = end - 1 - (lb + __popcll(bl & lt));
+        who[p] = r[j] | kLinkedBit;
+        obj[p] = f[j];
+      }
+    }
+    (void)w;
+  }
+};
+__device__ __forceinline__ void out_init(const RepOut&, uint32_t*) {}
+__device__ __forceinline__ void out_init(const ListOut&, uint32_t*) {}
+__device__ __forceinline__ void out_init(const ListOutA&, uint32_t* scr) {
+  if (threadIdx.x < 2) scr[threadIdx.x] = 0;  // before the bucket's first barrier
+}
+__device__ __forceinline__ void out_done(const ListOutA& o, uint32_t, uint32_t, uint32_t end,
+                                         const uint32_t* scr) {
+  __syncthreads();  // every wave's atomics on the counters are done
+  if (threadIdx.x == 0) {
+    o.lcnt[blockIdx.x] = scr[1];
+    if (blockIdx.x == gridDim.x - 1) o.counts[2] = end;
+  }
+}
+__device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t,
+                                         const uint32_t*) {}
+hipError_t out_finish(const ListOutA& o, uint32_t nb, hipStream_t s) {
+  k_list_finish<<<1, 1024, 0, s>>>(o.lcnt, nb, o.counts);
+  return hipGetLastError();
+}
 __device__ __forceinline__ void out_done(const ListOut& o, uint32_t c_run, uint32_t l_run,
-                                         uint32_t end) {
+                                         uint32_t end, const uint32_t*) {
   o.done(c_run, l_run, end);
 }
 
@@ -1393,6 +1450,7 @@ __device__ __forceinline__ void group_bucket_global(Src rec, uint32_t start, uin
     tm[s] = 0xFFFFFFFFu;
   }
   if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
+  out_init(out, scr);
   __syncthreads();
   for (uint32_t i = start + threadIdx.x; i < end; i += kGroupThreads) {
     const uint4 q = rec(i);
@@ -1444,7 +1502,7 @@ __device__ __forceinline__ void group_bucket_global(Src rec, uint32_t start, uin
     }
     out.template emit<1>(live, lk, r, w, f, start, end, c_run, l_run, scr, true);
   }
-  out_done(out, c_run, l_run, end);
+  out_done(out, c_run, l_run, end, scr);
 }
 
 // Group-by of one bucket, rows [start, end) of rec (q_reg preloaded by
@@ -1458,7 +1516,7 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
                                              uint32_t* scr) {
   const uint32_t m = end - start;
   if (m == 0) {
-    out_done(out, 0u, 0u, end);
+    out_done(out, 0u, 0u, end, scr);
     return;
   }
   if (m > kLdsCap) {
@@ -1472,6 +1530,7 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
     lmin[s] = 0xFFFFFFFFu;
   }
   if (threadIdx.x == 0) special_min = 0xFFFFFFFFu;
+  out_init(out, scr);
   __syncthreads();
   // A thread's records probe in lock step: every pass issues the LDS
   // round trips of all its pending records back to back and only then
@@ -1531,7 +1590,7 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
   }
   uint32_t c_run = 0, l_run = 0;
   out.template emit<kPer>(lv, lk, r, w, f, start, end, c_run, l_run, scr, false);
-  out_done(out, c_run, l_run, end);
+  out_done(out, c_run, l_run, end, scr);
 }
 
 // K5 with a PACKED 8-byte LDS table, for buckets of >= 12 digit bits (the
@@ -1563,7 +1622,7 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
   constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
   const uint32_t m = end - start;
   if (m == 0) {
-    out_done(out, 0u, 0u, end);
+    out_done(out, 0u, 0u, end, scr);
     return;
   }
   if (m > kPkCap) {
@@ -1582,6 +1641,7 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
     if (start + threadIdx.x + j * kGroupThreads >= end) q[j] = make_uint4(0, 0, kPadRow, kPadRow);
   for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
   for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
+  out_init(out, scr);
   __syncthreads();
   uint32_t slot[kP], step[kP], owner[kP];
   uint64_t mine[kP];
@@ -1641,7 +1701,7 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
   }
   uint32_t c_run = 0, l_run = 0;
   out.template emit<kP>(lv, lk, r, w, f, start, end, c_run, l_run, scr, false);
-  out_done(out, c_run, l_run, end);
+  out_done(out, c_run, l_run, end, scr);
 }
 
 
@@ -2208,8 +2268,21 @@ hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t
                              uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
                              KTimer* timer) {
   if (in.n == 0) return hipSuccess;
-  const ListOut out{who, obj, counts,
-                    reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ws) + group_layout(in.n).lcnt)};
+  uint32_t* lcnt =
+      reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ws) + group_layout(in.n).lcnt);
+  static const bool atomic_ranks = [] {
+    const char* e = getenv("SDGPU_LIST_RANKS");
+    return e && e[0] == 'a';
+  }();
+  if (atomic_ranks) {
+    const ListOutA out{who, obj, counts, lcnt};
+    if (in.rec12)
+      return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
+                          chunk_rows, nullptr, false, out, ws, s, timer);
+    return group_launch(RowsIn{in.key, in.valid, in.rank, in.rank_base}, in.n, chunk_rows,
+                        nullptr, false, out, ws, s, timer);
+  }
+  const ListOut out{who, obj, counts, lcnt};
   if (in.rec12)
     return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
                         chunk_rows, nullptr, false, out, ws, s, timer);
