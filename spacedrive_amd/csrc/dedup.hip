@@ -1516,6 +1516,7 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
                                              uint32_t* scr) {
   const uint32_t m = end - start;
   if (m == 0) {
+    out_init(out, scr);  // an empty bucket: counters zeroed for done
     out_done(out, 0u, 0u, end, scr);
     return;
   }
@@ -1622,6 +1623,7 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
   constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
   const uint32_t m = end - start;
   if (m == 0) {
+    out_init(out, scr);  // an empty bucket: counters zeroed for done
     out_done(out, 0u, 0u, end, scr);
     return;
   }
