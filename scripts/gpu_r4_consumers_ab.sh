@@ -1,4 +1,5 @@
 # A/B: the orphan remover's mark ranges (SDGPU_MARK_RANGES 8/4/2/1: fewer
+# (Done: 8 ranges kept, the knob removed; logs in profiles/r4/consumers_ab/.)
 # re-reads of the file_path ids vs L2-local marking), with the consumer tests
 # under each; then the config-1 directory leg (staging slabs of a tenth).
 #   TAG=r4i bash scripts/gpu_r4_consumers_ab.sh

@@ -1,4 +1,5 @@
 # A/B: the list-writing group kernel's in-bucket ranks -- workgroup ranks
+# (Done: atomic ranks adopted as the only ListOut, the knob removed; profiles/r4/listranks_ab/.)
 # (ListOut, two barriers + a one-wave scan) vs one LDS atomic per wave
 # (ListOutA, SDGPU_LIST_RANKS=atomic); the fused-path tests under the atomic
 # variant, then the dedup leg alternating.

@@ -35,8 +35,10 @@ uint32_t grid_for(uint64_t n, uint64_t per = kThreads) {
 // lines leave whole.  Every file_path id is read once per range (8 times in
 // all, the repeats from the shared last-level cache): one scattered byte store
 // per row into the whole map left each store a partial-line write of its own.
-// ranges: 8 (one per XCD), or fewer (A/B, SDGPU_MARK_RANGES: XCDs x and
-// x + ranges share a range; fewer re-reads of the file_path ids)
+// Fewer ranges (XCDs sharing a range, fewer re-reads of the file_path ids)
+// measured slower: 4 / 2 / 1 ranges 0.198 / 0.230 / 0.230 ms per call against
+// 0.170 ms with 8 (profiles/r4/consumers_ab/).
+constexpr uint32_t kMarkRanges = 8;
 __global__ __launch_bounds__(kThreads) void k_mark(const int32_t* __restrict__ fp_obj, uint64_t n,
                                                    uint8_t* __restrict__ mark, uint32_t max_id,
                                                    uint32_t span, uint32_t ranges) {
@@ -258,11 +260,7 @@ hipError_t orphan_objects_launch(const int32_t* obj, uint64_t n_obj, const int32
   uint32_t* tiles = cnt + blocks + 1;
   (void)hipMemsetAsync(bits, 0, map, s);
   if (n_fp) {
-    static const uint32_t ranges = [] {
-      const char* e = getenv("SDGPU_MARK_RANGES");
-      const unsigned long v = e ? strtoul(e, nullptr, 10) : 0;
-      return (v == 1 || v == 2 || v == 4 || v == 8) ? static_cast<uint32_t>(v) : 8u;
-    }();
+    constexpr uint32_t ranges = kMarkRanges;
     const uint32_t span = static_cast<uint32_t>((static_cast<uint64_t>(max_id) + ranges) / ranges);
     const uint64_t per = (n_fp + 4 * kThreads - 1) / (4 * kThreads);  // 1024-row groups
     const uint32_t groups = static_cast<uint32_t>(per < 256 ? per : 256) * (8 / ranges);

@@ -1185,63 +1185,6 @@ __device__ __forceinline__ uint64_t global_slot(uint64_t h, uint64_t tsize) {
 
 constexpr int kPer = (kLdsCap + kGroupThreads - 1) / kGroupThreads;
 
-// Ranks of flagged items across a workgroup in record order (record index =
-// thread + step * kGroupThreads, i.e. step-major): pc[j] / pl[j] = creators /
-// linked items of the workgroup before the thread's item of step j, tc / tl
-// = the workgroup's totals.  Per-(step, wave) ballots, then ONE wave scans the
-// 2 x kSteps x 16 wave counts (two per lane).  scr: kListScratch words.  With
-// `reuse`, a leading barrier protects scr from the previous call's readers.
-constexpr int kGroupWaves = kGroupThreads / 64;
-constexpr int kListScratch = 2 * 8 * kGroupWaves + 2;
-template <int kSteps>
-__device__ __forceinline__ void wg_list_ranks(const bool (&c)[kSteps], const bool (&l)[kSteps],
-                                              uint32_t (&pc)[kSteps], uint32_t (&pl)[kSteps],
-                                              uint32_t& tc, uint32_t& tl, uint32_t* scr,
-                                              bool reuse) {
-  constexpr int kE = kSteps * kGroupWaves;  // entries per list
-  static_assert(2 * kE + 2 <= kListScratch && kE <= 128, "two entries per lane of one wave");
-  const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  if (reuse) __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kSteps; ++j) {
-    const uint64_t bc = __ballot(c[j]), bl = __ballot(l[j]);
-    pc[j] = __popcll(bc & lt);
-    pl[j] = __popcll(bl & lt);
-    if (lane == 0) {
-      scr[j * kGroupWaves + w] = __popcll(bc);
-      scr[kE + j * kGroupWaves + w] = __popcll(bl);
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {
-#pragma unroll
-    for (int list = 0; list < 2; ++list) {
-      uint32_t* e = scr + list * kE;
-      const uint32_t i0 = 2 * lane;
-      const uint32_t a0 = i0 < kE ? e[i0] : 0u, a1 = i0 + 1 < kE ? e[i0 + 1] : 0u;
-      const uint32_t v = a0 + a1;
-      uint32_t inc = v;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(inc, d);
-        if (lane >= static_cast<uint32_t>(d)) inc += o;
-      }
-      if (i0 < kE) e[i0] = inc - v;
-      if (i0 + 1 < kE) e[i0 + 1] = inc - v + a0;
-      if (lane == 63) scr[2 * kE + list] = inc;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kSteps; ++j) {
-    pc[j] += scr[j * kGroupWaves + w];
-    pl[j] += scr[kE + j * kGroupWaves + w];
-  }
-  tc = scr[2 * kE];
-  tl = scr[2 * kE + 1];
-}
-
 // Where K5 puts a bucket's result.  Per record: live (a keyed row of the
 // bucket), r (its rank), w (its row), f (the lowest rank of its key).
 //   RepOut:  rep[w] = f for the rows that link to an earlier chunk (the
@@ -1249,8 +1192,8 @@ __device__ __forceinline__ void wg_list_ranks(const bool (&c)[kSteps], const boo
 //   ListOut: the Object write set itself (round 4; sdgpu_group_link_device),
 //            in the bucket's own record range [start, end) -- one entry per
 //            keyed row, so the positions need no global coordination:
-//            creators from the front in record order, who = rank; linked rows
-//            from the back, who = rank | SDGPU_LINKED, obj = f.  Coalesced;
+//            creators from the front, who = rank; linked rows from the back,
+//            who = rank | SDGPU_LINKED, obj = f.  Coalesced;
 //            no rep array.  lcnt[bucket] = its linked rows; the last bucket
 //            stores the keyed total in counts[2]; k_list_finish then sets
 //            counts[0] / [1] (no same-address atomics: 32 k workgroups adding
@@ -1271,52 +1214,6 @@ struct RepOut {
     (void)r;
   }
 };
-constexpr uint32_t kLinkedBit = 0x80000000u;
-struct ListOut {
-  static constexpr int kScratch = kListScratch;
-  uint32_t* who;
-  uint32_t* obj;
-  uint32_t* counts;
-  uint32_t* lcnt;
-  // c_run / l_run: creators / linked already written for this bucket (the
-  // global-table path emits a bucket in several chunks)
-  template <int kSteps>
-  __device__ __forceinline__ void emit(const bool (&live)[kSteps], const bool (&lk)[kSteps],
-                                       const uint32_t (&r)[kSteps], const uint32_t (&w)[kSteps],
-                                       const uint32_t (&f)[kSteps], uint32_t start, uint32_t end,
-                                       uint32_t& c_run, uint32_t& l_run, uint32_t* scr,
-                                       bool reuse) const {
-    bool c[kSteps], l[kSteps];
-    uint32_t pc[kSteps], pl[kSteps], tc, tl;
-#pragma unroll
-    for (int j = 0; j < kSteps; ++j) {
-      c[j] = live[j] && !lk[j];
-      l[j] = lk[j];
-    }
-    wg_list_ranks<kSteps>(c, l, pc, pl, tc, tl, scr, reuse);
-#pragma unroll
-    for (int j = 0; j < kSteps; ++j) {
-      if (c[j]) who[start + c_run + pc[j]] = r[j];
-      if (l[j]) {
-        const uint32_t p = end - 1 - (l_run + pl[j]);
-        who[p] = r[j] | kLinkedBit;
-        obj[p] = f[j];
-      }
-    }
-    c_run += tc;
-    l_run += tl;
-    (void)w;
-  }
-  // once per bucket, after its last emit
-  __device__ __forceinline__ void done(uint32_t c_run, uint32_t l_run, uint32_t end) const {
-    if (threadIdx.x == 0) {
-      lcnt[blockIdx.x] = l_run;
-      if (blockIdx.x == gridDim.x - 1) counts[2] = end;
-    }
-    (void)c_run;
-  }
-};
-
 // counts[1] = the buckets' linked rows, counts[0] = keyed - linked (one block)
 __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict__ lcnt,
                                                       uint32_t nb, uint32_t* __restrict__ counts) {
@@ -1335,16 +1232,15 @@ __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict
   }
 }
 hipError_t out_finish(const RepOut&, uint32_t, hipStream_t) { return hipSuccess; }
-hipError_t out_finish(const ListOut& o, uint32_t nb, hipStream_t s) {
-  k_list_finish<<<1, 1024, 0, s>>>(o.lcnt, nb, o.counts);
-  return hipGetLastError();
-}
-// ListOutA: the same write set, each wave's entries placed by ONE LDS atomic
-// per (step, list) on the bucket's creator / linked counters (scr[0..1],
-// zeroed with the table) instead of workgroup ranks: no barriers in emit, one
-// at the end for the linked total.  The entries' order inside a bucket then
-// depends on wave timing (not part of the contract).  A/B: SDGPU_LIST_RANKS.
-struct ListOutA {
+// ListOut: each wave's entries are placed by ONE LDS atomic per (step, list)
+// on the bucket's creator / linked counters (scr[0..1], zeroed with the
+// table): no barrier in emit, one at the end for the linked total.  The
+// entries' order inside a bucket depends on wave timing (not part of the
+// contract).  Workgroup-wide ranks in record order (two barriers + a one-wave
+// scan per emit) measured slower: 100 M rows 1.870 -> 1.850 ms, 12.5 M rows
+// 0.246 -> 0.244 ms (profiles/r4/listranks_ab/).
+constexpr uint32_t kLinkedBit = 0x80000000u;
+struct ListOut {
   static constexpr int kScratch = 2;
   uint32_t* who;
   uint32_t* obj;
@@ -1379,11 +1275,10 @@ struct ListOutA {
   }
 };
 __device__ __forceinline__ void out_init(const RepOut&, uint32_t*) {}
-__device__ __forceinline__ void out_init(const ListOut&, uint32_t*) {}
-__device__ __forceinline__ void out_init(const ListOutA&, uint32_t* scr) {
+__device__ __forceinline__ void out_init(const ListOut&, uint32_t* scr) {
   if (threadIdx.x < 2) scr[threadIdx.x] = 0;  // before the bucket's first barrier
 }
-__device__ __forceinline__ void out_done(const ListOutA& o, uint32_t, uint32_t, uint32_t end,
+__device__ __forceinline__ void out_done(const ListOut& o, uint32_t, uint32_t, uint32_t end,
                                          const uint32_t* scr) {
   __syncthreads();  // every wave's atomics on the counters are done
   if (threadIdx.x == 0) {
@@ -1393,13 +1288,9 @@ __device__ __forceinline__ void out_done(const ListOutA& o, uint32_t, uint32_t, 
 }
 __device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t,
                                          const uint32_t*) {}
-hipError_t out_finish(const ListOutA& o, uint32_t nb, hipStream_t s) {
+hipError_t out_finish(const ListOut& o, uint32_t nb, hipStream_t s) {
   k_list_finish<<<1, 1024, 0, s>>>(o.lcnt, nb, o.counts);
   return hipGetLastError();
-}
-__device__ __forceinline__ void out_done(const ListOut& o, uint32_t c_run, uint32_t l_run,
-                                         uint32_t end, const uint32_t*) {
-  o.done(c_run, l_run, end);
 }
 
 // Bucket records as {hash lo, hash hi, rank, row}: 16-byte records as stored,
@@ -2272,18 +2163,6 @@ hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t
   if (in.n == 0) return hipSuccess;
   uint32_t* lcnt =
       reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ws) + group_layout(in.n).lcnt);
-  static const bool atomic_ranks = [] {
-    const char* e = getenv("SDGPU_LIST_RANKS");
-    return e && e[0] == 'a';
-  }();
-  if (atomic_ranks) {
-    const ListOutA out{who, obj, counts, lcnt};
-    if (in.rec12)
-      return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
-                          chunk_rows, nullptr, false, out, ws, s, timer);
-    return group_launch(RowsIn{in.key, in.valid, in.rank, in.rank_base}, in.n, chunk_rows,
-                        nullptr, false, out, ws, s, timer);
-  }
   const ListOut out{who, obj, counts, lcnt};
   if (in.rec12)
     return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
