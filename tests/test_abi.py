@@ -106,3 +106,23 @@ def test_rust_wrappers_call_only_declared_symbols():
             "Result<String, io::Error>") in text            # core/src/object/cas.rs:23
     assert ("pub async fn file_checksum(path: impl AsRef<Path>) -> "
             "Result<String, io::Error>") in text            # validation/hash.rs:10
+
+
+def test_rust_job_step_mirrors_the_reference_job():
+    """crates/sd-core-gpu/src/job.rs: the identifier job's
+    stateful loop -- init / resume / execute_step over the split identify /
+    group calls, with the reference's run metadata and cursor
+    (file_identifier_job.rs:52-70, 174-309) in a serialisable state."""
+    import os
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    job = open(os.path.join(root, "crates", "sd-core-gpu", "src", "job.rs")).read()
+    lib = open(os.path.join(root, "crates", "sd-core-gpu", "src", "lib.rs")).read()
+    assert re.search(r"\bpub mod job\b|\bmod job\b", lib)
+    for item in ("pub fn init(", "pub fn resume(", "pub fn execute_step(", "pub trait OrphanTable",
+                 "#[derive(Clone, Debug, Default, Serialize, Deserialize)]"):
+        assert item in job, item
+    for field in ("cursor: Option<i32>", "total_orphan_paths", "total_objects_created",
+                  "total_objects_linked", "total_objects_ignored", "chunks_per_step"):
+        assert field in job, field
+    assert "identify(self.gpu" in job and "group(self.gpu" in job
