@@ -824,6 +824,7 @@ class Runner:
         comm = dedup.Comm.init_rank(self.ctx, 1, 0, dedup.Comm.unique_id(),
                                     timeout_ms=self.comm_timeout_ms)
         try:
+            comm.set_return(dedup.RETURN_COMPACT)
             fn = lambda: dedup.group_sharded(key, has, rank, comm, None, 100)  # noqa: E731
             fn()
             comm.wait()
@@ -842,16 +843,20 @@ class Runner:
         finally:
             comm.close()
         reh = 1e3 * t / steps
+        reh_full = 1e3 * t_full / steps
         pred = {}
         for n_ in (2, 4, 8):
-            link_b = per / n_ * (12 + 8 * linked_frac)  # bytes per link direction
+            # the library's default (SDGPU_RETURN_AUTO): compact iff rows / N >= 4 Mi
+            compact = per // n_ >= (4 << 20)
+            ret_b = 8 * linked_frac if compact else 4.0
+            link_b = per / n_ * (12 + ret_b)  # bytes per link direction
             x_ms = link_b / (self.XGMI_LINK_GBPS * 1e9) * 1e3
-            step = reh + x_ms
-            pred[str(n_)] = {"step_ms": step, "xgmi_ms": x_ms, "bytes_per_link": int(link_b),
+            step = (reh if compact else reh_full) + x_ms
+            pred[str(n_)] = {"return_leg": "compact" if compact else "full",
+                             "step_ms": step, "xgmi_ms": x_ms, "bytes_per_link": int(link_b),
                              "rows_per_s_total": n_ * per / (step * 1e-3),
                              "weak_scaling_efficiency": local_ms / step}
-        return {"rehearsal_ms_per_step": reh, "rehearsal_full_return_ms_per_step":
-                1e3 * t_full / steps,
+        return {"rehearsal_ms_per_step": reh, "rehearsal_full_return_ms_per_step": reh_full,
                 "count_wait_ms_per_call": (s1["count_wait_ms"] - s0["count_wait_ms"]) / calls,
                 "host_ms_per_call": (s1["host_ms"] - s0["host_ms"]) / calls,
                 "bytes_sent_per_row": (s1["bytes_sent"] - s0["bytes_sent"]) / max(
@@ -862,8 +867,9 @@ class Runner:
                             for k, v in kt.items()},
                 "note": "PREDICTION (unmeasured on hardware at N > 1): the exchange path "
                         "rehearsed on one GPU (one-rank RCCL: partition, count exchange + "
-                        "sync, records, local grouping of the received rows, compact "
-                        "return, gather) + the modelled xGMI time of rows/N per link"}
+                        "sync, records, local grouping of the received rows, the return "
+                        "leg SDGPU_RETURN_AUTO picks at that N, gather) + the modelled "
+                        "xGMI time of rows/N per link"}
 
     def staged_oracle(self):
         """Config 5's parity at full size: the reps of the batched 50 M-file run

@@ -307,14 +307,18 @@ typedef struct sdgpu_comm_stats_t {
   double host_ms;                         /* host ms inside the exchange calls */
   uint64_t rows_returned;                 /* (ABI 4) received rows whose rep went back */
 } sdgpu_comm_stats_t;
-/* Return leg of the exchange (ABI 4).  COMPACT (the default): an owner sends
- * back only the received rows whose rep is not their own rank, as 8-B {index,
- * rep} pairs after a second count exchange (a second host synchronisation);
- * ~1.6 B per row instead of 4 at config 4's 20 % duplicates.  FULL: every
- * received row's 4-B rep, one synchronisation per call.  All ranks of a
- * communicator must use the same mode. */
+/* Return leg of the exchange (ABI 4).  COMPACT: an owner sends back only the
+ * received rows whose rep is not their own rank, as 8-B {index, rep} pairs
+ * after a second count exchange (a second host synchronisation); ~1.6 B per
+ * row instead of 4 at config 4's 20 % duplicates.  FULL: every received row's
+ * 4-B rep, one synchronisation per call.  AUTO (the default): COMPACT when the
+ * largest rank's rows / nranks >= 4 Mi (the bytes it saves per link outweigh
+ * the second synchronisation), else FULL -- decided per call from every
+ * rank's n, which travels with the counts, so all ranks agree.  All ranks of
+ * a communicator must set the same mode. */
 #define SDGPU_RETURN_FULL 0
 #define SDGPU_RETURN_COMPACT 1
+#define SDGPU_RETURN_AUTO 2
 int sdgpu_comm_set_return(sdgpu_comm *comm, int mode);
 int sdgpu_comm_stats(sdgpu_comm *comm, sdgpu_comm_stats_t *out);
 /* Collective, one process per GPU (RCCL): every rank calls it with its own

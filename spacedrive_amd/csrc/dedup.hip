@@ -1693,12 +1693,21 @@ __global__ void k_copy_counts(const uint32_t* __restrict__ offs, uint32_t nbins,
 
 // Rows per destination rank of the exchange, from the scanned offsets of the
 // destination-digit partition.
+// msgs (may be NULL): the count messages of the exchange, {rows for d, n}
+// per destination d (every rank learns every rank's n with the counts).
 __global__ void k_dest_counts(const uint32_t* __restrict__ offs, uint32_t world,
-                              int64_t* __restrict__ counts) {
+                              int64_t* __restrict__ counts, int64_t* __restrict__ msgs,
+                              int64_t n) {
   const uint32_t d = threadIdx.x;
-  if (d < world)
-    counts[d] = static_cast<int64_t>(offs[static_cast<uint64_t>(d + 1) * kPartBlocks]) -
-                offs[static_cast<uint64_t>(d) * kPartBlocks];
+  if (d < world) {
+    const int64_t c = static_cast<int64_t>(offs[static_cast<uint64_t>(d + 1) * kPartBlocks]) -
+                      offs[static_cast<uint64_t>(d) * kPartBlocks];
+    counts[d] = c;
+    if (msgs) {
+      msgs[2 * d] = c;
+      msgs[2 * d + 1] = n;
+    }
+  }
 }
 
 // rep[i] of the sender's rows from the reps returned in send order: row i was
@@ -2204,7 +2213,7 @@ hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
                                  const uint32_t* rank, uint64_t n, uint32_t shard_bits,
                                  uint32_t world, uint64_t* out_key, uint32_t* out_rank,
                                  uint32_t* out_rec12, uint32_t* out_pos, int64_t* d_dest_counts,
-                                 void* ws, hipStream_t s, KTimer* timer) {
+                                 void* ws, hipStream_t s, KTimer* timer, int64_t* d_count_msgs) {
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(w);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(w + shard_hist_bytes(shard_bits));
@@ -2212,7 +2221,8 @@ hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
                                  out_key, out_rank, reinterpret_cast<uint3*>(out_rec12), out_pos,
                                  s, timer);
   if (e != hipSuccess) return e;
-  k_dest_counts<<<1, 64, 0, s>>>(hist, world, d_dest_counts);
+  k_dest_counts<<<1, 64, 0, s>>>(hist, world, d_dest_counts, d_count_msgs,
+                                 static_cast<int64_t>(n));
   return hipGetLastError();
 }
 

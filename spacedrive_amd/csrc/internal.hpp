@@ -217,7 +217,8 @@ hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
                                  const uint32_t* rank, uint64_t n, uint32_t shard_bits,
                                  uint32_t world, uint64_t* out_key, uint32_t* out_rank,
                                  uint32_t* out_rec12, uint32_t* out_pos, int64_t* d_dest_counts,
-                                 void* ws, hipStream_t s, KTimer* timer = nullptr);
+                                 void* ws, hipStream_t s, KTimer* timer = nullptr,
+                                 int64_t* d_count_msgs = nullptr);
 // rep[i] = pos[i] == ~0 ? rank[i] : back[pos[i]] (the exchange's return path)
 hipError_t gather_rep_launch(const uint32_t* back, const uint32_t* pos, const uint32_t* rank,
                              uint64_t n, uint32_t* rep, hipStream_t s);

@@ -49,9 +49,10 @@ struct sdgpu_comm {
   bool aborted = false;
   hipStream_t last_stream = nullptr;  // stream of the last exchange (sdgpu_comm_wait)
   // return leg: SDGPU_RETURN_COMPACT (only the linked rows' reps travel back,
-  // after a second count exchange) or SDGPU_RETURN_FULL (4 B per row, no
-  // second synchronisation).  Every rank of a communicator must agree.
-  int return_mode = SDGPU_RETURN_COMPACT;
+  // after a second count exchange), SDGPU_RETURN_FULL (4 B per row, no
+  // second synchronisation) or SDGPU_RETURN_AUTO (per call, see
+  // compact_pays).  Every rank of a communicator must agree.
+  int return_mode = SDGPU_RETURN_AUTO;
   sdgpu_comm_stats_t stats{};
 };
 
@@ -65,6 +66,19 @@ struct sdgpu_index {
 namespace {
 
 constexpr uint32_t kXShardBits = 8;  // 256 shards; rank d owns shards s with s*W>>8 == d
+
+// SDGPU_RETURN_AUTO: the compact return leg saves 2.4 B per returned row on
+// every link (8-B pairs for the ~20 % linked rows instead of 4 B for all) but
+// costs a second count exchange + host synchronisation and three kernels:
+// 0.064 ms in the one-rank rehearsal at 12.5 M rows (r4e
+// predicted_scaling).  At ~100 GB/s per xGMI link that pays once a link
+// carries more than ~2.7 M rows; with margin for the collective's latency
+// at 8 ranks, compact iff the largest rank's rows / W >= 4 M.  The decision
+// uses every rank's n, carried in the count messages, so all ranks agree.
+constexpr uint64_t kCompactRowsPerPeer = 4ull << 20;
+bool compact_pays(uint64_t n_max, int W) {
+  return n_max / static_cast<uint64_t>(W) >= kCompactRowsPerPeer;
+}
 
 int nccl_err(ncclResult_t r) { return r == ncclSuccess ? 0 : -EIO; }
 
@@ -228,7 +242,8 @@ struct RankJob {
   uint32_t* srec = nullptr;   // [n][3]
   uint32_t* spos = nullptr;   // [n] send position of row i (~0: keyless)
   int64_t* dcnt = nullptr;    // [W] rows to each owner
-  int64_t* rcnt_d = nullptr;  // [W] rows from each source
+  int64_t* xmsg = nullptr;    // [W][2] count messages: {rows to the owner, this rank's n}
+  int64_t* rcnt_d = nullptr;  // [W][2] from each source: {rows, its n}
   uint32_t* rrec = nullptr;   // [m][3]
   uint32_t* rrep = nullptr;   // [m]
   uint8_t* rvalid = nullptr;  // [m]
@@ -341,33 +356,38 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
     const uint64_t n = j.n;
     const size_t o_pos = align_up(12 * n, 256);
     const size_t o_dcnt = align_up(o_pos + 4 * n, 256);
-    const size_t o_rcnt = align_up(o_dcnt + 8ull * W, 256);
-    const size_t o_pcnt = align_up(o_rcnt + 8ull * W, 256);
+    const size_t o_xmsg = align_up(o_dcnt + 8ull * W, 256);
+    const size_t o_rcnt = align_up(o_xmsg + 16ull * W, 256);
+    const size_t o_pcnt = align_up(o_rcnt + 16ull * W, 256);
     const size_t o_rpcnt = align_up(o_pcnt + 8ull * W, 256);
     SD_TRY_RC(ensure_dev(j.c, j.c->xs_send, o_rpcnt + 8ull * W));
     SD_TRY_RC(ensure_dev(j.c, j.c->shard_ws, shard_workspace_bytes(kXShardBits)));
-    SD_TRY_RC(ensure_pin(j.c->xs_counts, 32ull * W));
+    SD_TRY_RC(ensure_pin(j.c->xs_counts, 64ull * W));
     uint8_t* b = static_cast<uint8_t*>(j.c->xs_send.p);
     j.srec = reinterpret_cast<uint32_t*>(b);
     j.spos = reinterpret_cast<uint32_t*>(b + o_pos);
     j.dcnt = reinterpret_cast<int64_t*>(b + o_dcnt);
+    j.xmsg = reinterpret_cast<int64_t*>(b + o_xmsg);
     j.rcnt_d = reinterpret_cast<int64_t*>(b + o_rcnt);
     j.retcnt = reinterpret_cast<int64_t*>(b + o_pcnt);
     j.rretcnt = reinterpret_cast<int64_t*>(b + o_rpcnt);
     j.h = static_cast<int64_t*>(j.c->xs_counts.p);
     SD_TRY(shard_exchange_launch(j.key, j.has, j.rank, n, kXShardBits, W, nullptr, nullptr,
-                                 j.srec, j.spos, j.dcnt, j.c->shard_ws.p, j.s, j.c->kt()));
+                                 j.srec, j.spos, j.dcnt, j.c->shard_ws.p, j.s, j.c->kt(),
+                                 j.xmsg));
   }
-  // 2. counts all-to-all, then the one host synchronisation
+  // 2. count messages all-to-all ({rows for the peer, my n}), then the host
+  // synchronisation
   SD_TRY_RC(alltoallv(
-      J, W, deadline, [](RankJob& j, int p) -> void* { return j.dcnt + p; },
-      [](RankJob& j, int p) -> void* { return j.rcnt_d + p; },
-      [](RankJob&, int) -> size_t { return 8; }, [](RankJob&, int) -> size_t { return 8; }));
+      J, W, deadline, [](RankJob& j, int p) -> void* { return j.xmsg + 2 * p; },
+      [](RankJob& j, int p) -> void* { return j.rcnt_d + 2 * p; },
+      [](RankJob&, int) -> size_t { return 16; }, [](RankJob&, int) -> size_t { return 16; }));
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
     SD_TRY(hipMemcpyAsync(j.h, j.dcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
-    SD_TRY(hipMemcpyAsync(j.h + W, j.rcnt_d, 8ull * W, hipMemcpyDeviceToHost, j.s));
+    SD_TRY(hipMemcpyAsync(j.h + W, j.rcnt_d, 16ull * W, hipMemcpyDeviceToHost, j.s));
   }
+  uint64_t n_max = 0;  // every rank's n arrived with the counts: the same on all ranks
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
     if (j.comm->transport == SDGPU_TRANSPORT_RCCL) {
@@ -380,9 +400,11 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
     j.soff.assign(W + 1, 0);
     j.roff.assign(W + 1, 0);
     for (int p = 0; p < W; ++p) {
-      if (j.h[p] < 0 || j.h[W + p] < 0) return -EPROTO;
+      const int64_t rc = j.h[W + 2 * p], np = j.h[W + 2 * p + 1];
+      if (j.h[p] < 0 || rc < 0 || np < 0) return -EPROTO;
+      n_max = std::max(n_max, static_cast<uint64_t>(np));
       j.scnt[p] = static_cast<uint64_t>(j.h[p]);
-      j.rcnt[p] = static_cast<uint64_t>(j.h[W + p]);
+      j.rcnt[p] = static_cast<uint64_t>(rc);
       j.soff[p + 1] = j.soff[p] + j.scnt[p];
       j.roff[p + 1] = j.roff[p] + j.rcnt[p];
     }
@@ -416,7 +438,9 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
     SD_TRY_RC(group_with_index(j.c, j.idx, in, chunk_rows, j.rrep, j.rvalid, j.s));
   }
   // 5. reps back to their sources, gathered to row order
-  const bool compact = J[0].comm->return_mode == SDGPU_RETURN_COMPACT;
+  const int mode = J[0].comm->return_mode;
+  const bool compact =
+      mode == SDGPU_RETURN_COMPACT || (mode == SDGPU_RETURN_AUTO && compact_pays(n_max, W));
   if (!compact) {
     SD_TRY_RC(alltoallv(
         J, W, deadline, [](RankJob& j, int p) -> void* { return j.rrep + j.roff[p]; },
@@ -451,8 +475,8 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
         [](RankJob&, int) -> size_t { return 8; }, [](RankJob&, int) -> size_t { return 8; }));
     for (auto& j : J) {
       SD_TRY(hipSetDevice(j.c->device));
-      SD_TRY(hipMemcpyAsync(j.h + 2 * W, j.retcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
-      SD_TRY(hipMemcpyAsync(j.h + 3 * W, j.rretcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
+      SD_TRY(hipMemcpyAsync(j.h + 3 * W, j.retcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
+      SD_TRY(hipMemcpyAsync(j.h + 4 * W, j.rretcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
     }
     for (auto& j : J) {
       SD_TRY(hipSetDevice(j.c->device));
@@ -466,7 +490,7 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
       j.poff.assign(W + 1, 0);
       j.pioff.assign(W + 1, 0);
       for (int p = 0; p < W; ++p) {
-        const int64_t a = j.h[2 * W + p], b = j.h[3 * W + p];
+        const int64_t a = j.h[3 * W + p], b = j.h[4 * W + p];
         if (a < 0 || b < 0 || static_cast<uint64_t>(a) > j.rcnt[p] ||
             static_cast<uint64_t>(b) > j.scnt[p])
           return -EPROTO;
@@ -613,7 +637,9 @@ int sdgpu_comm_wait(sdgpu_comm* m, void* stream) {
 }
 
 int sdgpu_comm_set_return(sdgpu_comm* m, int mode) {
-  if (!m || (mode != SDGPU_RETURN_FULL && mode != SDGPU_RETURN_COMPACT)) return -EINVAL;
+  if (!m || (mode != SDGPU_RETURN_FULL && mode != SDGPU_RETURN_COMPACT &&
+             mode != SDGPU_RETURN_AUTO))
+    return -EINVAL;
   m->return_mode = mode;
   return 0;
 }

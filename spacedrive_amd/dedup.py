@@ -274,7 +274,7 @@ def dedup_batch(key, has_key, first_rank: int, index: ObjectIndex | None = None,
 TRANSPORT_AUTO, TRANSPORT_RCCL, TRANSPORT_PEER = 0, 1, 2
 
 
-RETURN_FULL, RETURN_COMPACT = 0, 1  # SDGPU_RETURN_*
+RETURN_FULL, RETURN_COMPACT, RETURN_AUTO = 0, 1, 2  # SDGPU_RETURN_*
 
 
 class CommStats(ctypes.Structure):
@@ -327,8 +327,9 @@ class Comm:
         check(self.ctx.lib.sdgpu_comm_wait(self.h, stream), "sdgpu_comm_wait")
 
     def set_return(self, mode: int):
-        """SDGPU_RETURN_COMPACT (default: only the linked rows' reps travel
-        back, one more count exchange) or SDGPU_RETURN_FULL (4 B per row)."""
+        """SDGPU_RETURN_COMPACT (only the linked rows' reps travel back, one
+        more count exchange), SDGPU_RETURN_FULL (4 B per row) or
+        SDGPU_RETURN_AUTO (the default: compact for large calls, sdgpu.h)."""
         check(self.ctx.lib.sdgpu_comm_set_return(self.h, mode), "sdgpu_comm_set_return")
 
     def stats(self) -> dict:

@@ -44,7 +44,7 @@ def test_dedup_sharded_two_level_per_rank(ctxs):
     np.testing.assert_array_equal(rep, O.group_reps(k, h, 100))
 
 
-@pytest.mark.parametrize("world,mode", [(2, 1), (3, 1), (8, 1), (3, 0)])
+@pytest.mark.parametrize("world,mode", [(2, 1), (3, 1), (8, 1), (3, 0), (3, 2)])
 def test_sharded_all_device_with_index_batches(ctxs, world, mode):
     """Device API over `world` ranks, two batches through per-rank Object
     indexes (each rank holds its shards' keys), plus pre-existing Objects
@@ -59,7 +59,7 @@ def test_sharded_all_device_with_index_batches(ctxs, world, mode):
     comms = dedup.Comm.init_all(ctxs[:world])
     assert comms[0].info() == (world, 0, dedup.TRANSPORT_PEER)
     for c in comms:
-        c.set_return(mode)  # compact (1) / full (0) return leg
+        c.set_return(mode)  # compact (1) / full (0) / auto (2) return leg
     idxs = [dedup.ObjectIndex(c, 1000) for c in ctxs[:world]]
     for r, ix in enumerate(idxs):  # every rank gets the full list, keeps its share
         ix.add_objects(torch.from_numpy(ek.view(np.int64)).cuda(),
@@ -95,6 +95,7 @@ def test_rccl_transport_one_rank(ctx):
     uid = dedup.Comm.unique_id()
     comm = dedup.Comm.init_rank(ctx, 1, 0, uid)
     assert comm.info() == (1, 0, dedup.TRANSPORT_RCCL)
+    comm.set_return(dedup.RETURN_COMPACT)  # the default (AUTO) picks FULL at this size
     k, h, rk = O.synth_dedup_rows(29, 500_000, 400_000, 0, 500_000)
     dk = torch.from_numpy(k.view(np.int64)).cuda()
     dh = torch.from_numpy(h).cuda()
@@ -114,7 +115,7 @@ def test_rccl_transport_one_rank(ctx):
     keyed = int(h.sum())
     assert st["calls"] == 5
     assert st["rows_sent"] == st["rows_received"] == 4 * keyed   # 3 whole + 2 halves
-    # compact return leg (the default): 12-B records out,
+    # compact return leg: 12-B records out,
     # 8-B {index, rep} pairs back for the linked rows only
     linked = int(np.count_nonzero(ref != np.arange(ref.size)))
     assert st["rows_returned"] == 4 * linked
@@ -128,6 +129,15 @@ def test_rccl_transport_one_rank(ctx):
     np.testing.assert_array_equal(rep.cpu().numpy().view(np.uint32), ref)
     st2 = comm.stats()
     assert st2["bytes_sent"] - st["bytes_sent"] == 16 * keyed
+    # AUTO (the default): 500 k rows on one rank is below the compact
+    # threshold (4 Mi rows per rank), so the full leg runs
+    comm.set_return(dedup.RETURN_AUTO)
+    rep = dedup.group_sharded(dk, dh, dr, comm, None, 100)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(rep.cpu().numpy().view(np.uint32), ref)
+    st3 = comm.stats()
+    assert st3["bytes_sent"] - st2["bytes_sent"] == 16 * keyed
+    assert st3["rows_returned"] - st2["rows_returned"] == keyed
     comm.close()
 
 
