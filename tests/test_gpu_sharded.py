@@ -85,6 +85,45 @@ def test_sharded_all_device_with_index_batches(ctxs, world, mode):
         c.close()
 
 
+def test_auto_return_takes_the_compact_leg_for_large_calls(ctxs):
+    """SDGPU_RETURN_AUTO (the default): two ranks of 8.5 M rows each exceed
+    4 Mi rows per peer, so every rank takes the compact leg (pairs for the
+    linked rows only), decided from the n in the count messages; a second
+    call with uneven shares (one rank 1 M rows, the other 8.5 M) takes it too
+    -- the larger rank decides for both -- and a small call the full leg."""
+    import torch
+    from spacedrive_amd import dedup
+    per = 8_500_000
+    total = 2 * per
+    k, h, _ = O.synth_dedup_rows(37, total, int(total * 0.8), 0, total)
+    ref = O.group_reps(k, h, 100)
+    comms = dedup.Comm.init_all(ctxs[:2])
+
+    def run(bounds):
+        keys, hass, ranks = [], [], []
+        for a, b in bounds:
+            keys.append(torch.from_numpy(k[a:b].view(np.int64)).cuda())
+            hass.append(torch.from_numpy(h[a:b]).cuda())
+            ranks.append(torch.arange(a, b, dtype=torch.int64).to(torch.int32).cuda())
+        before = [c.stats() for c in comms]
+        reps = dedup.group_sharded_all(keys, hass, ranks, comms, None, 100)
+        torch.cuda.synchronize()
+        for (a, b), rp in zip(bounds, reps):
+            np.testing.assert_array_equal(rp.cpu().numpy().view(np.uint32), ref[a:b])
+        after = [c.stats() for c in comms]
+        return [{x: a_[x] - b_[x] for x in ("rows_received", "rows_returned", "bytes_sent")}
+                for a_, b_ in zip(after, before)]
+
+    for d in run([(0, per), (per, total)]):              # 8.5 M rows per rank: compact
+        assert 0 < d["rows_returned"] < d["rows_received"] // 2
+    for d in run([(0, 1_000_000), (1_000_000, total)]):  # the larger rank decides
+        assert 0 < d["rows_returned"] < d["rows_received"] // 2
+    for d in run([(0, 200_000), (200_000, 400_000)]):    # small: the full leg
+        assert d["rows_returned"] == d["rows_received"]
+    for c in comms:
+        c.close()
+
+
 def test_rccl_transport_one_rank(ctx):
     """The RCCL code path on hardware: a one-rank communicator from
     sdgpu_comm_unique_id + sdgpu_comm_init_rank, the whole exchange through
