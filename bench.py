@@ -325,6 +325,12 @@ class Runner:
                 # (sdgpu_group_link_device; rows in id order, rank = row)
                 dedup.group_link_device(key, has, None, None, 0, 100, ctx=self.ctx, trim=False)
                 return
+            if self.comm is not None:
+                # N GPUs over libsdgpu's RCCL communicator: the records go to
+                # their owners and each owner writes the write set of the rows
+                # it owns (sdgpu_group_link_sharded_device): no return leg
+                dedup.group_link_sharded(key, has, None, grank, self.comm, 100, trim=False)
+                return
             rep = self.group(key, has, grank)
             dedup.link_batch_device(rep, grank, None, 0, ctx=self.ctx, trim=False)
 
@@ -348,7 +354,11 @@ class Runner:
             res["job"] = {"value": self.world * n * steps / t_job,
                           "ms_per_step": 1e3 * t_job / steps,
                           "grouping": ("fused group + write set (sdgpu_group_link_device)"
-                                       if fused else "sharded grouping + link batch")}
+                                       if fused else
+                                       "sharded write set, no return leg "
+                                       "(sdgpu_group_link_sharded_device)"
+                                       if self.comm is not None else
+                                       "sharded grouping + link batch (torch.distributed)")}
         except Exception as e:  # noqa: BLE001 -- reported in the line
             log(f"bench: identifier job step failed: {e!r}")
             res["job"] = {"error": repr(e)[:400]}
@@ -840,6 +850,13 @@ class Runner:
             comm.wait()
             t_full = self.timed(fn, steps, warmup)
             comm.wait()
+            # the write-set form (sdgpu_group_link_sharded_device): no return leg
+            fl = lambda: dedup.group_link_sharded(key, has, None, rank, comm, 100,  # noqa: E731
+                                                  trim=False)
+            fl()
+            comm.wait()
+            t_lists = self.timed(fl, steps, warmup)
+            comm.wait()
         finally:
             comm.close()
         reh = 1e3 * t / steps
@@ -856,7 +873,21 @@ class Runner:
                              "step_ms": step, "xgmi_ms": x_ms, "bytes_per_link": int(link_b),
                              "rows_per_s_total": n_ * per / (step * 1e-3),
                              "weak_scaling_efficiency": local_ms / step}
+        reh_lists = 1e3 * t_lists / steps
+        pred_lists = {}
+        for n_ in (2, 4, 8):
+            link_b = per / n_ * 12
+            x_ms = link_b / (self.XGMI_LINK_GBPS * 1e9) * 1e3
+            step = reh_lists + x_ms
+            pred_lists[str(n_)] = {"step_ms": step, "xgmi_ms": x_ms, "bytes_per_link": int(link_b),
+                                   "rows_per_s_total": n_ * per / (step * 1e-3)}
         return {"rehearsal_ms_per_step": reh, "rehearsal_full_return_ms_per_step": reh_full,
+                "rehearsal_write_set_ms_per_step": reh_lists,
+                "per_n_write_set": pred_lists,
+                "write_set_note": "grouping + Object write set with no return leg "
+                                  "(sdgpu_group_link_sharded_device, the N > 1 identifier "
+                                  "step's path): 12 B per row on the wire; against "
+                                  "fused_job.ms_per_step at N = 1",
                 "count_wait_ms_per_call": (s1["count_wait_ms"] - s0["count_wait_ms"]) / calls,
                 "host_ms_per_call": (s1["host_ms"] - s0["host_ms"]) / calls,
                 "bytes_sent_per_row": (s1["bytes_sent"] - s0["bytes_sent"]) / max(

@@ -336,6 +336,33 @@ int sdgpu_group_sharded_all_device(sdgpu_ctx *const *ctx, sdgpu_comm *const *com
                                    const uint32_t *const *d_rank, const uint64_t *n,
                                    uint32_t chunk_rows, uint32_t *const *d_rep,
                                    void *const *streams);
+/* Sharded grouping + Object write set, with no return leg: each rank writes
+ * the write-set entries (as sdgpu_group_link_device: who = rank, or rank |
+ * SDGPU_LINKED with obj = the creator's rank) of the keyed rows it OWNS --
+ * their cas_id hashes to its shard, whichever rank identified them -- and of
+ * its own valid keyless rows.  The union over the ranks is the write set of
+ * all rows (a set, mod.rs:189-333), so only the 12-B records cross xGMI.
+ * Global ranks in d_rank (required, < 2^31).  d_who / d_obj hold cap
+ * entries: -ENOSPC (after the exchange, before any list is written; the
+ * peers are unaffected) when this rank's owned rows + own keyless rows
+ * exceed cap -- up to nranks x n when every row shares one cas_id.
+ * d_counts (device) = [creators, linked, entries].  No Object index (use
+ * sdgpu_group_sharded_device with one). */
+int sdgpu_group_link_sharded_device(sdgpu_ctx *ctx, sdgpu_comm *comm, const uint64_t *d_key,
+                                    const uint8_t *d_has_key, const uint8_t *d_valid,
+                                    const uint32_t *d_rank, uint64_t n, uint32_t chunk_rows,
+                                    uint32_t *d_who, uint32_t *d_obj, uint64_t cap,
+                                    uint32_t *d_counts, void *stream);
+/* The same from one process for all ngpu ranks (arrays indexed by rank;
+ * d_has_key, d_valid and streams may be NULL). */
+int sdgpu_group_link_sharded_all_device(sdgpu_ctx *const *ctx, sdgpu_comm *const *comm, int ngpu,
+                                        const uint64_t *const *d_key,
+                                        const uint8_t *const *d_has_key,
+                                        const uint8_t *const *d_valid,
+                                        const uint32_t *const *d_rank, const uint64_t *n,
+                                        uint32_t chunk_rows, uint32_t *const *d_who,
+                                        uint32_t *const *d_obj, const uint64_t *cap,
+                                        uint32_t *const *d_counts, void *const *streams);
 /* SURVEY §8(b)'s sdgpu_dedup(ctx[], ngpu, ...): host arrays in rank order,
  * split into ngpu contiguous ranges, grouped across the ngpu contexts
  * (communicators created and destroyed inside). */

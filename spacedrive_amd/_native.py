@@ -93,6 +93,10 @@ def _proto(L):
                                              c_vp]),
         "sdgpu_group_sharded_all_device": (i32, [c_vp, c_vp, c_vp, i32, c_vp, c_vp, c_vp, c_vp,
                                                  u32, c_vp, c_vp]),
+        "sdgpu_group_link_sharded_device": (i32, [ctx, c_vp, c_vp, c_vp, c_vp, c_vp, u64, u32,
+                                                  c_vp, c_vp, u64, c_vp, c_vp]),
+        "sdgpu_group_link_sharded_all_device": (i32, [c_vp, c_vp, i32, c_vp, c_vp, c_vp, c_vp,
+                                                      c_vp, u32, c_vp, c_vp, c_vp, c_vp, c_vp]),
         "sdgpu_dedup_sharded": (i32, [c_vp, i32, c_vp, c_vp, u32, u32, c_vp]),
         "sdgpu_synth_cas_arena_device": (i32, [ctx, c_vp, c_vp, c_vp, u32, c_vp, c_vp]),
         "sdgpu_synth_file_device": (i32, [ctx, u64, u64, u64, c_vp, c_vp]),

@@ -238,6 +238,12 @@ struct RankJob {
   const uint32_t* rank = nullptr;
   uint64_t n = 0;
   uint32_t* rep = nullptr;
+  // write-set form (sdgpu_group_link_sharded_device): lists of the owned rows
+  const uint8_t* valid = nullptr;
+  uint32_t* who = nullptr;
+  uint32_t* obj = nullptr;
+  uint32_t* counts = nullptr;
+  uint64_t cap = 0;
   // device workspace
   uint32_t* srec = nullptr;   // [n][3]
   uint32_t* spos = nullptr;   // [n] send position of row i (~0: keyless)
@@ -347,9 +353,12 @@ int run_sharded(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
   return rc;
 }
 
-int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
-  const auto t_start = Clock::now();
-  const Clock::time_point deadline = deadline_of(J[0].comm->timeout_ms);
+// Steps 1-3 of an exchange, shared by the rep and the write-set forms: every
+// rank's keyed rows partitioned by owner, the count messages (with every
+// rank's n -> n_max, the same on all ranks), the host synchronisation, the
+// records to their owners.  count_ms: host time until the counts were known.
+int exchange_forward(std::vector<RankJob>& J, int W, Clock::time_point t_start,
+                     Clock::time_point deadline, uint64_t& n_max, double& count_ms) {
   // 1. send side: packed records by owner + per-owner counts, on each GPU
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
@@ -387,7 +396,7 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
     SD_TRY(hipMemcpyAsync(j.h, j.dcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
     SD_TRY(hipMemcpyAsync(j.h + W, j.rcnt_d, 16ull * W, hipMemcpyDeviceToHost, j.s));
   }
-  uint64_t n_max = 0;  // every rank's n arrived with the counts: the same on all ranks
+  n_max = 0;  // every rank's n arrived with the counts: the same on all ranks
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
     if (j.comm->transport == SDGPU_TRANSPORT_RCCL) {
@@ -421,14 +430,22 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
     j.rvalid = r + o_val;
     j.back = static_cast<uint32_t*>(j.c->xs_back.p);
   }
-  const double count_ms =
-      std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
+  count_ms = std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
   // 3. the rows, one message per (source, owner) pair
   SD_TRY_RC(alltoallv(
       J, W, deadline, [](RankJob& j, int p) -> void* { return j.srec + 3 * j.soff[p]; },
       [](RankJob& j, int p) -> void* { return j.rrec + 3 * j.roff[p]; },
       [](RankJob& j, int p) -> size_t { return 12 * j.scnt[p]; },
       [](RankJob& j, int p) -> size_t { return 12 * j.rcnt[p]; }));
+  return 0;
+}
+
+int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
+  const auto t_start = Clock::now();
+  const Clock::time_point deadline = deadline_of(J[0].comm->timeout_ms);
+  uint64_t n_max = 0;
+  double count_ms = 0;
+  SD_TRY_RC(exchange_forward(J, W, t_start, deadline, n_max, count_ms));
   // 4. local grouping of the received rows (every key's rows are all here)
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
@@ -553,6 +570,62 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
     j.comm->last_stream = j.s;
   }
   return 0;
+}
+
+// The write-set form: after the forward exchange each owner groups the rows
+// it received and writes their Object write set itself (the list-writing
+// group kernel of sdgpu_group_link_device, ranks from the records), then
+// appends its OWN valid keyless rows.  No return leg, no gather: the union of
+// the ranks' lists is the write set of all rows (a set, mod.rs:189-333).
+int run_lists_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
+  const auto t_start = Clock::now();
+  const Clock::time_point deadline = deadline_of(J[0].comm->timeout_ms);
+  uint64_t n_max = 0;
+  double count_ms = 0;
+  SD_TRY_RC(exchange_forward(J, W, t_start, deadline, n_max, count_ms));
+  // no collective follows: a rank whose lists do not fit fails alone
+  for (auto& j : J) {
+    SD_TRY(hipSetDevice(j.c->device));
+    if (j.m + j.n > j.cap) return -ENOSPC;
+    SD_TRY(hipMemsetAsync(j.counts, 0, 3 * sizeof(uint32_t), j.s));
+    SD_TRY_RC(ensure_dev(j.c, j.c->dedup_ws, dedup_workspace_bytes(std::max<uint64_t>(j.m, 1))));
+    SD_TRY_RC(ensure_dev(j.c, j.c->link_ws, extra_workspace_bytes(j.n)));
+    GroupInput in;
+    in.rec12 = j.rrec;  // {key, global rank}: 16-B bucket records
+    in.n = j.m;
+    SD_TRY(dedup_list_launch(in, chunk_rows, j.who, j.obj, j.counts, j.c->dedup_ws.p, j.s,
+                             j.c->kt()));
+    SD_TRY(extra_list_launch(j.has, j.valid, nullptr, nullptr, j.rank, 0, j.n, j.who, j.obj,
+                             j.counts, j.c->link_ws.p, j.s, j.c->kt()));
+  }
+  const double call_ms =
+      std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
+  for (auto& j : J) {
+    const int me = j.comm->rank;
+    sdgpu_comm_stats_t& st = j.comm->stats;
+    st.calls += 1;
+    st.rows_sent += j.total;
+    st.rows_received += j.m;
+    st.bytes_sent += 12 * j.total;
+    st.bytes_received += 12 * j.m;
+    st.bytes_remote += 12 * (j.total - j.scnt[me]) + 12 * (j.m - j.rcnt[me]);
+    st.count_wait_ms += count_ms;
+    st.host_ms += call_ms;
+    j.comm->last_stream = j.s;
+  }
+  (void)n_max;
+  return 0;
+}
+
+int run_lists(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
+  for (auto& j : J)
+    if (j.comm->aborted || (j.comm->transport == SDGPU_TRANSPORT_RCCL && !j.comm->nccl))
+      return -ECONNABORTED;
+  const int rc = run_lists_impl(J, W, chunk_rows);
+  if (rc != 0 && rc != -ENOSPC)  // -ENOSPC: after the last collective, the peers are fine
+    for (auto& j : J)
+      if (j.comm->transport == SDGPU_TRANSPORT_RCCL) comm_fail(j.comm, rc);
+  return rc;
 }
 
 bool same_devices(sdgpu_ctx* const* ctx, int ngpu) {
@@ -979,6 +1052,79 @@ int sdgpu_group_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* com
     j.rep = d_rep[r];
   }
   return run_sharded(J, ngpu, chunk_rows);
+}
+
+int sdgpu_group_link_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, const uint64_t* d_key,
+                                    const uint8_t* d_has_key, const uint8_t* d_valid,
+                                    const uint32_t* d_rank, uint64_t n, uint32_t chunk_rows,
+                                    uint32_t* d_who, uint32_t* d_obj, uint64_t cap,
+                                    uint32_t* d_counts, void* stream) {
+  if (!c || !comm || chunk_rows == 0 || !d_counts || !d_who || !d_obj ||
+      (n && (!d_key || !d_rank)))
+    return -EINVAL;
+  if (comm->device != c->device) return -EINVAL;
+  if (comm->transport != SDGPU_TRANSPORT_RCCL) return -EINVAL;  // peer: the _all form
+  if (n >= (1ull << 31)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  std::vector<RankJob> J(1);
+  RankJob& j = J[0];
+  j.c = c;
+  j.comm = comm;
+  j.s = pick(c, stream);
+  j.key = d_key;
+  j.has = d_has_key;
+  j.valid = d_valid;
+  j.rank = d_rank;
+  j.n = n;
+  j.who = d_who;
+  j.obj = d_obj;
+  j.counts = d_counts;
+  j.cap = cap;
+  return run_lists(J, comm->nranks, chunk_rows);
+}
+
+int sdgpu_group_link_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* comm, int ngpu,
+                                        const uint64_t* const* d_key,
+                                        const uint8_t* const* d_has_key,
+                                        const uint8_t* const* d_valid,
+                                        const uint32_t* const* d_rank, const uint64_t* n,
+                                        uint32_t chunk_rows, uint32_t* const* d_who,
+                                        uint32_t* const* d_obj, const uint64_t* cap,
+                                        uint32_t* const* d_counts, void* const* streams) {
+  if (!ctx || !comm || ngpu < 1 || ngpu > 64 || !d_key || !d_rank || !n || !d_who || !d_obj ||
+      !cap || !d_counts || chunk_rows == 0)
+    return -EINVAL;
+  for (int r = 0; r < ngpu; ++r) {
+    if (!ctx[r] || !comm[r] || comm[r]->nranks != ngpu || comm[r]->rank != r ||
+        comm[r]->device != ctx[r]->device || comm[r]->transport != comm[0]->transport)
+      return -EINVAL;
+    if (!d_who[r] || !d_obj[r] || !d_counts[r] || (n[r] && (!d_key[r] || !d_rank[r])))
+      return -EINVAL;
+    if (n[r] >= (1ull << 31)) return -EINVAL;
+    for (int q = 0; q < r; ++q)
+      if (ctx[q] == ctx[r]) return -EINVAL;  // one context per rank
+  }
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (int r = 0; r < ngpu; ++r) locks.emplace_back(ctx[r]->mu);
+  std::vector<RankJob> J(ngpu);
+  for (int r = 0; r < ngpu; ++r) {
+    RankJob& j = J[r];
+    j.c = ctx[r];
+    j.comm = comm[r];
+    SD_TRY(hipSetDevice(ctx[r]->device));
+    j.s = pick(ctx[r], streams ? streams[r] : nullptr);
+    j.key = d_key[r];
+    j.has = d_has_key ? d_has_key[r] : nullptr;
+    j.valid = d_valid ? d_valid[r] : nullptr;
+    j.rank = d_rank[r];
+    j.n = n[r];
+    j.who = d_who[r];
+    j.obj = d_obj[r];
+    j.counts = d_counts[r];
+    j.cap = cap[r];
+  }
+  return run_lists(J, ngpu, chunk_rows);
 }
 
 int sdgpu_dedup_sharded(sdgpu_ctx* const* ctx, int ngpu, const uint64_t* key,

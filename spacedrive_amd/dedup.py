@@ -497,6 +497,67 @@ def group_link_device(key, has_key=None, valid=None, rank=None, first_rank: int 
     return who[:e], obj[:e], (c, l)
 
 
+def group_link_sharded(key, has_key, valid, rank, comm, chunk_rows: int = 100,
+                       cap: int | None = None, trim: bool = True):
+    """Sharded grouping + Object write set with no return leg
+    (sdgpu_group_link_sharded_device): this rank's lists hold the entries of
+    the keyed rows it OWNS (hash shard) and of its own valid keyless rows; the
+    union over the ranks is the write set of all rows.  rank: int32 global
+    ranks (required).  cap: list capacity (default nranks x n + n: enough
+    when every row shares one cas_id and the ranks hold equal shares).  Returns (who, obj, (c, l)) trimmed,
+    or full-length tensors + device counts with trim=False."""
+    import torch
+    dev = key.device
+    ctx = comm.ctx
+    n = key.numel()
+    nranks = comm.info()[0]
+    cap = cap if cap is not None else max(1, nranks * n + n)
+    who = torch.empty(cap, dtype=torch.int32, device=dev)
+    obj = torch.empty(cap, dtype=torch.int32, device=dev)
+    counts = torch.empty(3, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    check(ctx.lib.sdgpu_group_link_sharded_device(ctx.h, comm.h, key.data_ptr(), ptr(has_key),
+                                                  ptr(valid), rank.data_ptr(), n, chunk_rows,
+                                                  who.data_ptr(), obj.data_ptr(), cap,
+                                                  counts.data_ptr(), s),
+          "sdgpu_group_link_sharded_device")
+    if not trim:
+        return who, obj, counts
+    c, l, e = (int(x) for x in counts.cpu().tolist())
+    return who[:e], obj[:e], (c, l)
+
+
+def group_link_sharded_all(keys, hass, valids, ranks, comms, chunk_rows: int = 100):
+    """All ranks from one process (sdgpu_group_link_sharded_all_device): lists
+    of device tensors per rank -> [(who, obj, (c, l))] per rank, trimmed."""
+    import ctypes
+    import torch
+    W = len(keys)
+    vp = ctypes.c_void_p
+    arr = lambda xs: (vp * W)(*xs)  # noqa: E731
+    ctxs = [c.ctx for c in comms]
+    n = [k.numel() for k in keys]
+    caps = [max(1, sum(n) + m) for m in n]  # every keyed row may land on one owner
+    whos = [torch.empty(c_, dtype=torch.int32, device=k.device) for c_, k in zip(caps, keys)]
+    objs = [torch.empty(c_, dtype=torch.int32, device=k.device) for c_, k in zip(caps, keys)]
+    cnts = [torch.empty(3, dtype=torch.int32, device=k.device) for k in keys]
+    opt = lambda xs: arr([x.data_ptr() if x is not None else None for x in xs]) if xs else None  # noqa: E731
+    check(ctxs[0].lib.sdgpu_group_link_sharded_all_device(
+        arr([c.h.value for c in ctxs]), arr([c.h.value for c in comms]), W,
+        arr([k.data_ptr() for k in keys]), opt(hass), opt(valids),
+        arr([r.data_ptr() for r in ranks]), (ctypes.c_uint64 * W)(*n), chunk_rows,
+        arr([w.data_ptr() for w in whos]), arr([o.data_ptr() for o in objs]),
+        (ctypes.c_uint64 * W)(*caps), arr([c.data_ptr() for c in cnts]),
+        arr([torch.cuda.current_stream(k.device).cuda_stream for k in keys])),
+        "sdgpu_group_link_sharded_all_device")
+    out = []
+    for w, o, c in zip(whos, objs, cnts):
+        cc, ll, e = (int(x) for x in c.cpu().tolist())
+        out.append((w[:e], o[:e], (cc, ll)))
+    return out
+
+
 def split_link_lists(who: np.ndarray, obj: np.ndarray):
     """(create, link_row, link_obj) of a fused write set, each sorted by row
     rank: the same lists link_batch_device returns (row order), for comparing

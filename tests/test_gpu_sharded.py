@@ -124,6 +124,84 @@ def test_auto_return_takes_the_compact_leg_for_large_calls(ctxs):
         c.close()
 
 
+def _lists_union(parts):
+    from spacedrive_amd import dedup
+    w = np.concatenate([p[0].cpu().numpy() for p in parts])
+    o = np.concatenate([p[1].cpu().numpy() for p in parts])
+    return dedup.split_link_lists(w, o), sum(p[2][0] for p in parts), sum(p[2][1] for p in parts)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_link_sharded_union_is_the_write_set(ctxs, world):
+    """sdgpu_group_link_sharded_all_device (peer transport, all ranks in one
+    process): each rank lists the rows it owns + its own keyless rows; the
+    union over the ranks equals the oracle's link batch over the grouping of
+    all rows, as sets -- uneven shares, keyless and invalid rows, a key
+    repeated 40 k times (one owner gets all its rows)."""
+    import torch
+    from spacedrive_amd import dedup
+    total = 400_000
+    rng = np.random.default_rng(world + 40)
+    pool = rng.integers(0, 2**64 - 1, 250_000, dtype=np.uint64, endpoint=True)
+    k = pool[rng.integers(0, pool.size, total)]
+    k[rng.choice(total, 40_000, replace=False)] = pool[3]
+    valid = (rng.random(total) > 0.02).astype(np.uint8)
+    h = ((rng.random(total) > 0.01) & (valid != 0)).astype(np.uint8)
+    comms = dedup.Comm.init_all(ctxs[:world])
+    keys, hass, vals, ranks = [], [], [], []
+    for r in range(world):
+        a, b = total * r * r // (world * world), total * (r + 1) * (r + 1) // (world * world)
+        keys.append(torch.from_numpy(k[a:b].view(np.int64)).cuda())
+        hass.append(torch.from_numpy(h[a:b]).cuda())
+        vals.append(torch.from_numpy(valid[a:b]).cuda())
+        ranks.append(torch.arange(a, b, dtype=torch.int64).to(torch.int32).cuda())
+    parts = dedup.group_link_sharded_all(keys, hass, vals, ranks, comms, 100)
+    (c, lr, lo), nc, nl = _lists_union(parts)
+    rc, rlr, rlo = O.link_batch(O.group_reps(k, h, 100), None, valid, 0)
+    assert (nc, nl) == (rc.size, rlr.size)
+    np.testing.assert_array_equal(c, rc)
+    np.testing.assert_array_equal(lr, rlr)
+    np.testing.assert_array_equal(lo, rlo)
+    for cm in comms:
+        st = cm.stats()
+        assert st["rows_returned"] == 0 and st["bytes_sent"] == 12 * st["rows_sent"]
+        cm.close()
+
+
+def test_link_sharded_one_rank_rccl(ctx):
+    """The write-set form through a one-rank RCCL communicator (the N > 1
+    headline step's code path): equal to the oracle, 12 B per row on the
+    wire, and -ENOSPC for lists that do not fit leaves the communicator
+    usable."""
+    import errno
+    import torch
+    from spacedrive_amd import dedup
+    from spacedrive_amd._native import SdgpuError
+    comm = dedup.Comm.init_rank(ctx, 1, 0, dedup.Comm.unique_id())
+    n = 1_000_000
+    k, h, rk = O.synth_dedup_rows(41, n, 800_000, 0, n)
+    dk = torch.from_numpy(k.view(np.int64)).cuda()
+    dh = torch.from_numpy(h).cuda()
+    dr = torch.from_numpy(rk.view(np.int32)).cuda()
+    rc, rlr, rlo = O.link_batch(O.group_reps(k, h, 100), None, None, 0)
+    for _ in range(2):
+        who, obj, (c, l) = dedup.group_link_sharded(dk, dh, None, dr, comm, 100)
+        torch.cuda.synchronize()
+        fc, flr, flo = dedup.split_link_lists(who.cpu().numpy(), obj.cpu().numpy())
+        assert (c, l) == (rc.size, rlr.size)
+        np.testing.assert_array_equal(fc, rc)
+        np.testing.assert_array_equal(flr, rlr)
+        np.testing.assert_array_equal(flo, rlo)
+    with pytest.raises(SdgpuError) as e:
+        dedup.group_link_sharded(dk, dh, None, dr, comm, 100, cap=1000)
+    assert e.value.rc == -errno.ENOSPC
+    who, obj, (c, l) = dedup.group_link_sharded(dk, dh, None, dr, comm, 100)
+    assert (c, l) == (rc.size, rlr.size)
+    st = comm.stats()
+    assert st["rows_returned"] == 0 and st["bytes_sent"] == 12 * st["rows_sent"]
+    comm.close()
+
+
 def test_rccl_transport_one_rank(ctx):
     """The RCCL code path on hardware: a one-rank communicator from
     sdgpu_comm_unique_id + sdgpu_comm_init_rank, the whole exchange through
