@@ -23,8 +23,9 @@ warm-up, barrier + synchronize on both sides, max over ranks):
   dir      config 1: a real 10 k-file directory (sparse files, warm cache)
            through sdgpu_identify_files (pread -> pinned -> K1)         files/s
 `roofline` is for the dominant kernel (K1 "cas_leaves"), timed live with HIP
-events on its launch stream; `cpu_baseline` times an AVX2 8-way C port of
-generate_cas_id's hashing (the crate's multi-chunk SIMD idea) on this host's
+events on its launch stream; `cpu_baseline` times a SIMD C port of
+generate_cas_id's hashing (the crate's multi-chunk SIMD idea: AVX-512 16-way
+where the host has it, as the crate's hash_many does, else AVX2 8-way) on this host's
 cores over a bounded sample, with the scalar oracle and 1-thread figures beside.
 """
 from __future__ import annotations
@@ -1201,7 +1202,7 @@ class Runner:
                        "gpu_cas_id_mismatches": mism,
                        "sample": f"config 1: {len(paths)} real files, warm cache, the "
                                  f"reference's reads per file (open, header / 4 samples / "
-                                 f"footer, cas.rs:23-62) + AVX2 8-way BLAKE3 "
+                                 f"footer, cas.rs:23-62) + {O.simd_isa()} BLAKE3 "
                                  f"(oracle orc_cas_paths_simd), {threads} threads; "
                                  f"scalar_value = scalar oracle cas_id_path, same threads"}
             shutil.rmtree(root, ignore_errors=True)
@@ -1220,7 +1221,7 @@ class Runner:
         ckt = time.perf_counter() - t0
         ck = {"value": threads * ck_reps * buf.size / ckt / 1e9, "unit": "GB/s",
               "threads": threads, "value_1thread": ck1 / 1e9,
-              "sample": f"{threads} threads x {ck_reps} x 256 MiB in host RAM, AVX2 8-way "
+              "sample": f"{threads} threads x {ck_reps} x 256 MiB in host RAM, {O.simd_isa()} "
                         f"BLAKE3 over 1024-chunk subtrees (oracle orc_checksum_simd_mt)"}
         del buf
         single = None
@@ -1265,7 +1266,7 @@ class Runner:
                 "config1_dir": dir_res, "config3_checksum": ck,
                 "single_file_1thread": single, "single_file_burst": burst,
                 "sample": f"first {m} files of config 2 (their {int(h_len.sum())} window bytes "
-                          f"in host RAM) hashed {reps}x, AVX2 8-way BLAKE3 port "
+                          f"in host RAM) hashed {reps}x, {O.simd_isa()} BLAKE3 port "
                           f"(oracle/sd_oracle.c orc_cas_batch_simd), {threads} threads, "
                           f"{dt:.1f} s wall; scalar_value = scalar oracle, same threads; "
                           f"value_1thread = one thread (the reference hashes a 100-file "

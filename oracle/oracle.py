@@ -204,10 +204,17 @@ def cas_batch(arena: np.ndarray, off: np.ndarray, length: np.ndarray, threads: i
     return out
 
 
+def simd_isa() -> str:
+    """The SIMD hashers' width on this host: "AVX-512 16-way" or "AVX2 8-way"
+    (ORC_SIMD_WIDTH=8 forces the latter)."""
+    return "AVX-512 16-way" if lib().orc_simd_width() == 16 else "AVX2 8-way"
+
+
 def cas_batch_simd(arena: np.ndarray, off: np.ndarray, length: np.ndarray,
                    threads: int = 1) -> np.ndarray:
-    """cas bytes (n x 8) with the AVX2 8-way chunk/parent hashing (CPU baseline:
-    the reference crate's multi-chunk SIMD idea, restated)."""
+    """cas bytes (n x 8) with the SIMD chunk/parent hashing -- AVX-512 16-way
+    on hosts that have it, else AVX2 8-way, as the reference crate's
+    hash_many picks (CPU baseline: the multi-chunk SIMD idea, restated)."""
     arena = np.ascontiguousarray(arena, np.uint8)
     off = np.ascontiguousarray(off, np.uint64)
     length = np.ascontiguousarray(length, np.uint32)
@@ -217,7 +224,7 @@ def cas_batch_simd(arena: np.ndarray, off: np.ndarray, length: np.ndarray,
 
 
 def blake3_simd(data: np.ndarray) -> bytes:
-    """BLAKE3 of a buffer with the AVX2 subtree hasher (CPU baseline of
+    """BLAKE3 of a buffer with the SIMD subtree hasher (CPU baseline of
     file_checksum, hash.rs:10-24)."""
     data = np.ascontiguousarray(data, np.uint8)
     out = np.zeros(32, np.uint8)
@@ -226,7 +233,7 @@ def blake3_simd(data: np.ndarray) -> bytes:
 
 
 def checksum_simd_mt(data: np.ndarray, threads: int, reps: int) -> bytes:
-    """`threads` threads each hash `data` `reps` times with the AVX2 hasher
+    """`threads` threads each hash `data` `reps` times with the SIMD hasher
     (one file per thread); returns thread 0's digest."""
     data = np.ascontiguousarray(data, np.uint8)
     out = np.zeros(32, np.uint8)
@@ -236,7 +243,7 @@ def checksum_simd_mt(data: np.ndarray, threads: int, reps: int) -> bytes:
 
 def cas_paths_simd(paths, sizes, threads: int = 1):
     """(cas bytes [n, 8], status [n]) of real files: the reference's reads per
-    file (cas.rs:23-62) + the AVX2 8-way hasher, `threads` C threads (CPU
+    file (cas.rs:23-62) + the SIMD hasher, `threads` C threads (CPU
     baseline of the config-1 directory)."""
     n = len(paths)
     arr = getattr(paths, "c_paths", None)  # pre-encoded (file_identifier.PathList)

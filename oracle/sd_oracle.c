@@ -1132,6 +1132,197 @@ static void s_parent_cv(const uint32_t l[8], const uint32_t r[8], uint32_t flags
   memcpy(cv, w, 32);
 }
 
+/* ------------------------------------------------------------------------- */
+/* AVX-512 16-way (CPU BASELINE ONLY), used when the host has AVX-512F/VL:    */
+/* the blake3 crate's hash_many takes 16 inputs at a time there, so an AVX2   */
+/* baseline would understate the reference on such a host.  Same scheme as   */
+/* above with 16 lanes: native 32-bit rotates (vprord), a 16 x 16 word        */
+/* transpose per 64-byte block.                                               */
+/* ------------------------------------------------------------------------- */
+#define T512 __attribute__((target("avx512f,avx512vl")))
+typedef __m512i v16u;
+
+#define WG(a, b, c, d, x, y)                          \
+  do {                                                \
+    a = _mm512_add_epi32(_mm512_add_epi32(a, b), x);  \
+    d = _mm512_ror_epi32(_mm512_xor_si512(d, a), 16); \
+    c = _mm512_add_epi32(c, d);                       \
+    b = _mm512_ror_epi32(_mm512_xor_si512(b, c), 12); \
+    a = _mm512_add_epi32(_mm512_add_epi32(a, b), y);  \
+    d = _mm512_ror_epi32(_mm512_xor_si512(d, a), 8);  \
+    c = _mm512_add_epi32(c, d);                       \
+    b = _mm512_ror_epi32(_mm512_xor_si512(b, c), 7);  \
+  } while (0)
+
+T512 static inline void w_compress(v16u h[8], const v16u m[16], v16u ctr_lo, v16u ctr_hi,
+                                   uint32_t blen, uint32_t flags) {
+  static const uint8_t S[7][16] = {
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8},
+      {3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1},
+      {10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6},
+      {12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4},
+      {9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7},
+      {11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13}};
+  v16u v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3], v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
+  v16u v8 = _mm512_set1_epi32((int)B3_IV[0]), v9 = _mm512_set1_epi32((int)B3_IV[1]),
+       v10 = _mm512_set1_epi32((int)B3_IV[2]), v11 = _mm512_set1_epi32((int)B3_IV[3]);
+  v16u v12 = ctr_lo, v13 = ctr_hi, v14 = _mm512_set1_epi32((int)blen),
+       v15 = _mm512_set1_epi32((int)flags);
+  for (int r = 0; r < 7; ++r) {
+    const uint8_t *sg = S[r];
+    WG(v0, v4, v8, v12, m[sg[0]], m[sg[1]]);
+    WG(v1, v5, v9, v13, m[sg[2]], m[sg[3]]);
+    WG(v2, v6, v10, v14, m[sg[4]], m[sg[5]]);
+    WG(v3, v7, v11, v15, m[sg[6]], m[sg[7]]);
+    WG(v0, v5, v10, v15, m[sg[8]], m[sg[9]]);
+    WG(v1, v6, v11, v12, m[sg[10]], m[sg[11]]);
+    WG(v2, v7, v8, v13, m[sg[12]], m[sg[13]]);
+    WG(v3, v4, v9, v14, m[sg[14]], m[sg[15]]);
+  }
+  h[0] = _mm512_xor_si512(v0, v8);
+  h[1] = _mm512_xor_si512(v1, v9);
+  h[2] = _mm512_xor_si512(v2, v10);
+  h[3] = _mm512_xor_si512(v3, v11);
+  h[4] = _mm512_xor_si512(v4, v12);
+  h[5] = _mm512_xor_si512(v5, v13);
+  h[6] = _mm512_xor_si512(v6, v14);
+  h[7] = _mm512_xor_si512(v7, v15);
+}
+
+/* r[j] = the 16 words of lane j -> m[w] = word w of every lane.  32-bit then
+ * 64-bit unpacks inside 128-bit lanes, then two 128-bit lane shuffles. */
+T512 static inline void w_transpose16(const v16u r[16], v16u m[16]) {
+  v16u t[16], u[16];
+  for (int i = 0; i < 8; ++i) {
+    t[2 * i] = _mm512_unpacklo_epi32(r[2 * i], r[2 * i + 1]);
+    t[2 * i + 1] = _mm512_unpackhi_epi32(r[2 * i], r[2 * i + 1]);
+  }
+  for (int i = 0; i < 4; ++i) {  /* u[4i + k], 128-bit lane L: rows 4i..4i+3 of word 4L + k */
+    u[4 * i + 0] = _mm512_unpacklo_epi64(t[4 * i + 0], t[4 * i + 2]);
+    u[4 * i + 1] = _mm512_unpackhi_epi64(t[4 * i + 0], t[4 * i + 2]);
+    u[4 * i + 2] = _mm512_unpacklo_epi64(t[4 * i + 1], t[4 * i + 3]);
+    u[4 * i + 3] = _mm512_unpackhi_epi64(t[4 * i + 1], t[4 * i + 3]);
+  }
+  for (int k = 0; k < 4; ++k) {
+    const v16u x0 = _mm512_shuffle_i32x4(u[k], u[4 + k], 0x44);
+    const v16u x1 = _mm512_shuffle_i32x4(u[8 + k], u[12 + k], 0x44);
+    const v16u x2 = _mm512_shuffle_i32x4(u[k], u[4 + k], 0xEE);
+    const v16u x3 = _mm512_shuffle_i32x4(u[8 + k], u[12 + k], 0xEE);
+    m[k] = _mm512_shuffle_i32x4(x0, x1, 0x88);
+    m[4 + k] = _mm512_shuffle_i32x4(x0, x1, 0xDD);
+    m[8 + k] = _mm512_shuffle_i32x4(x2, x3, 0x88);
+    m[12 + k] = _mm512_shuffle_i32x4(x2, x3, 0xDD);
+  }
+}
+
+T512 static inline void w_store_cvs(const v16u h[8], uint32_t *out[16]) {
+  uint32_t t[8][16] __attribute__((aligned(64)));
+  for (int w = 0; w < 8; ++w) _mm512_store_si512((void *)t[w], h[w]);
+  for (int j = 0; j < 16; ++j)
+    for (int w = 0; w < 8; ++w) out[j][w] = t[w][j];
+}
+
+/* CVs of 16 FULL non-root chunks p[j] with chunk counters ctr0 + j. */
+T512 static void w_chunks16(const uint8_t *const p[16], uint64_t ctr0, uint32_t *out[16]) {
+  v16u h[8], m[16], r[16];
+  for (int w = 0; w < 8; ++w) h[w] = _mm512_set1_epi32((int)B3_IV[w]);
+  uint32_t lo[16], hi[16];
+  for (int j = 0; j < 16; ++j) {
+    lo[j] = (uint32_t)(ctr0 + j);
+    hi[j] = (uint32_t)((ctr0 + j) >> 32);
+  }
+  const v16u clo = _mm512_loadu_si512(lo), chi = _mm512_loadu_si512(hi);
+  for (int b = 0; b < 16; ++b) {
+    for (int j = 0; j < 16; ++j) r[j] = _mm512_loadu_si512(p[j] + 64 * b);
+    w_transpose16(r, m);
+    w_compress(h, m, clo, chi, 64, (b == 0 ? B3_CHUNK_START : 0) | (b == 15 ? B3_CHUNK_END : 0));
+  }
+  w_store_cvs(h, out);
+}
+
+/* 16 parents: out[j] = P(pairs[j][0..8), pairs[j][8..16)). */
+T512 static void w_parents16(const uint32_t *pairs[16], uint32_t *out[16]) {
+  v16u h[8], m[16], r[16];
+  for (int w = 0; w < 8; ++w) h[w] = _mm512_set1_epi32((int)B3_IV[w]);
+  for (int j = 0; j < 16; ++j) r[j] = _mm512_loadu_si512(pairs[j]);
+  w_transpose16(r, m);
+  const v16u z = _mm512_setzero_si512();
+  w_compress(h, m, z, z, 64, B3_PARENT);
+  w_store_cvs(h, out);
+}
+
+/* 16 when the host has AVX-512F/VL (the crate's hash_many width there), else 8. */
+int orc_simd_width(void) {
+  static int w = 0;
+  if (!w) {
+    __builtin_cpu_init();
+    w = (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl")) ? 16 : 8;
+    const char *e = getenv("ORC_SIMD_WIDTH"); /* "8": the AVX2 path on any host (A/B) */
+    if (e && e[0] == '8') w = 8;
+  }
+  return w;
+}
+
+/* CVs of `count` consecutive FULL non-root chunks at p (counters ctr0..),
+ * 16 / 8 at a time, the rest one by one. */
+static void chunks_batch(const uint8_t *p, size_t count, uint64_t ctr0, uint32_t (*out)[8]) {
+  size_t c = 0;
+  if (orc_simd_width() == 16)
+    for (; c + 16 <= count; c += 16) {
+      const uint8_t *pp[16];
+      uint32_t *o[16];
+      for (int j = 0; j < 16; ++j) {
+        pp[j] = p + (c + j) * B3_CHUNK;
+        o[j] = out[c + j];
+      }
+      w_chunks16(pp, ctr0 + c, o);
+    }
+  for (; c + 8 <= count; c += 8) {
+    const uint8_t *pp[8];
+    uint32_t *o[8];
+    for (int j = 0; j < 8; ++j) {
+      pp[j] = p + (c + j) * B3_CHUNK;
+      o[j] = out[c + j];
+    }
+    v_chunks8(pp, ctr0 + c, o);
+  }
+  for (; c < count; ++c) s_chunk_cv(p + c * B3_CHUNK, B3_CHUNK, ctr0 + c, out[c]);
+}
+
+/* One tree level in place: cvs[k] = P(cvs[2k], cvs[2k+1]) for k < half. */
+static void parents_batch(uint32_t (*cvs)[8], size_t half) {
+  size_t k = 0;
+  if (orc_simd_width() == 16)
+    for (; k + 16 <= half; k += 16) {
+      const uint32_t *pr[16];
+      uint32_t *o[16];
+      uint32_t tmp[16][8];
+      for (int j = 0; j < 16; ++j) {
+        pr[j] = cvs[2 * (k + j)];
+        o[j] = tmp[j];
+      }
+      w_parents16(pr, o);
+      for (int j = 0; j < 16; ++j) memcpy(cvs[k + j], tmp[j], 32);
+    }
+  for (; k + 8 <= half; k += 8) {
+    const uint32_t *pr[8];
+    uint32_t *o[8];
+    uint32_t tmp[8][8] __attribute__((aligned(32)));
+    for (int j = 0; j < 8; ++j) {
+      pr[j] = cvs[2 * (k + j)];
+      o[j] = tmp[j];
+    }
+    v_parents8(pr, o);
+    for (int j = 0; j < 8; ++j) memcpy(cvs[k + j], tmp[j], 32);
+  }
+  for (; k < half; ++k) {
+    uint32_t t[8];
+    s_parent_cv(cvs[2 * k], cvs[2 * k + 1], 0, t);
+    memcpy(cvs[k], t, 32);
+  }
+}
+
 /* BLAKE3 (hash mode, first 8 digest bytes) of one message <= 128 chunks. */
 static void simd_hash8(const uint8_t *msg, size_t len, uint8_t out8[8]) {
   const size_t nch = len <= B3_CHUNK ? 1 : (len + B3_CHUNK - 1) / B3_CHUNK;
@@ -1142,42 +1333,17 @@ static void simd_hash8(const uint8_t *msg, size_t len, uint8_t out8[8]) {
     return;
   }
   uint32_t cvs[128][8] __attribute__((aligned(32)));
-  size_t c = 0;
-  /* full chunks 8 at a time (the last chunk is never ROOT here: nch >= 2) */
+  /* full chunks 16 / 8 at a time (the last chunk is never ROOT here: nch >= 2) */
   const size_t full = len / B3_CHUNK;
-  for (; c + 8 <= full; c += 8) {
-    const uint8_t *p[8];
-    uint32_t *o[8];
-    for (int j = 0; j < 8; ++j) {
-      p[j] = msg + (c + j) * B3_CHUNK;
-      o[j] = cvs[c + j];
-    }
-    v_chunks8(p, c, o);
-  }
-  for (; c < nch; ++c) {
+  chunks_batch(msg, full, 0, cvs);
+  for (size_t c = full; c < nch; ++c) {
     const size_t clen = len - c * B3_CHUNK < B3_CHUNK ? len - c * B3_CHUNK : B3_CHUNK;
     s_chunk_cv(msg + c * B3_CHUNK, clen, c, cvs[c]);
   }
   size_t cnt = nch;
   while (cnt > 2) {
     const size_t half = cnt / 2;
-    size_t k = 0;
-    for (; k + 8 <= half; k += 8) {
-      const uint32_t *pr[8];
-      uint32_t *o[8];
-      uint32_t tmp[8][8] __attribute__((aligned(32)));
-      for (int j = 0; j < 8; ++j) {
-        pr[j] = cvs[2 * (k + j)];
-        o[j] = tmp[j];
-      }
-      v_parents8(pr, o);
-      for (int j = 0; j < 8; ++j) memcpy(cvs[k + j], tmp[j], 32);
-    }
-    for (; k < half; ++k) {
-      uint32_t t[8];
-      s_parent_cv(cvs[2 * k], cvs[2 * k + 1], 0, t);
-      memcpy(cvs[k], t, 32);
-    }
+    parents_batch(cvs, half);
     if (cnt & 1) memcpy(cvs[half], cvs[cnt - 1], 32);
     cnt = half + (cnt & 1);
   }
@@ -1227,35 +1393,8 @@ void orc_cas_batch_simd(const uint8_t *arena, const uint64_t *off, const uint32_
 /* CV (non-root) of the aligned subtree of 1024 full chunks at chunk ctr0. */
 static void simd_subtree1024(const uint8_t *p, uint64_t ctr0, uint32_t cv[8]) {
   uint32_t cvs[1024][8] __attribute__((aligned(32)));
-  for (size_t c = 0; c < 1024; c += 8) {
-    const uint8_t *pp[8];
-    uint32_t *o[8];
-    for (int j = 0; j < 8; ++j) {
-      pp[j] = p + (c + j) * B3_CHUNK;
-      o[j] = cvs[c + j];
-    }
-    v_chunks8(pp, ctr0 + c, o);
-  }
-  for (size_t cnt = 1024; cnt > 2; cnt /= 2) {
-    const size_t half = cnt / 2;
-    size_t k = 0;
-    for (; k + 8 <= half; k += 8) {
-      const uint32_t *pr[8];
-      uint32_t *o[8];
-      uint32_t tmp[8][8] __attribute__((aligned(32)));
-      for (int j = 0; j < 8; ++j) {
-        pr[j] = cvs[2 * (k + j)];
-        o[j] = tmp[j];
-      }
-      v_parents8(pr, o);
-      for (int j = 0; j < 8; ++j) memcpy(cvs[k + j], tmp[j], 32);
-    }
-    for (; k < half; ++k) {
-      uint32_t t[8];
-      s_parent_cv(cvs[2 * k], cvs[2 * k + 1], 0, t);
-      memcpy(cvs[k], t, 32);
-    }
-  }
+  chunks_batch(p, 1024, ctr0, cvs);
+  for (size_t cnt = 1024; cnt > 2; cnt /= 2) parents_batch(cvs, cnt / 2);
   s_parent_cv(cvs[0], cvs[1], 0, cv);
 }
 

@@ -274,3 +274,34 @@ def test_simd_file_hasher_matches_oracle():
               4 * S + 1024, 5 * S + 3000):
         assert O.blake3_simd(data[:n]) == O.blake3(data[:n].tobytes()), n
     assert O.checksum_simd_mt(data[:3 * S + 5], 3, 2) == O.blake3(data[:3 * S + 5].tobytes())
+
+
+def test_simd_widths_agree_with_the_scalar_oracle():
+    """The CPU baseline's SIMD hashers at both widths (AVX-512 16-way where the
+    host has it, AVX2 8-way forced by ORC_SIMD_WIDTH=8, in a subprocess since
+    the width is chosen once per process) against the scalar oracle."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as O
+rng = np.random.default_rng(3)
+lens = [1025, 8 * 1024, 16 * 1024, 16 * 1024 + 5, 24 * 1024 + 1, 57352, 102408]
+buf = [rng.integers(0, 256, n, dtype=np.uint8) for n in lens]
+arena = np.concatenate(buf)
+off = np.cumsum([0] + lens[:-1]).astype(np.uint64)
+ln = np.array(lens, np.uint32)
+assert np.array_equal(O.cas_batch(arena, off, ln), O.cas_batch_simd(arena, off, ln))
+d = rng.integers(0, 256, (3 << 20) + 77, dtype=np.uint8)
+assert O.blake3(d) == O.blake3_simd(d)
+print(O.simd_isa())
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for env in ({}, {"ORC_SIMD_WIDTH": "8"}):
+        r = subprocess.run([sys.executable, "-c", code, root], capture_output=True, text=True,
+                           env={**os.environ, **env}, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        if env:
+            assert r.stdout.strip() == "AVX2 8-way"
