@@ -7,6 +7,9 @@
 //   private  one 110 KiB buffer per thread (cache-hot, like the CPU port)
 //   nodata   open + close only (the syscall floor of a file)
 //   ntcopy   private buffer, then non-temporal 32-B stores into the arena
+//   ring     per thread a ring of small staging buffers (RING_KB each, 4 of
+//            them) filled file after file and reused: stands in for small
+//            pinned buffers copied H2D into a device arena as they fill
 // Build: g++ -O2 -std=c++17 -pthread scripts/exp/exp_reads.cpp -o /tmp/exp_reads
 // Run:   SDGPU_IO_THREADS=16 /tmp/exp_reads listing.tsv 5
 #include <immintrin.h>
@@ -56,9 +59,17 @@ int main(int argc, char** argv) {
       const auto t0 = std::chrono::steady_clock::now();
       parallel_for(n, [&](uint32_t i) {
         thread_local std::vector<uint8_t> priv(SDGPU_CAS_SAMPLED_MSG_LEN + 8 + (100 << 10) + 4096);
+        static const size_t ring_kb = getenv("RING_KB") ? strtoul(getenv("RING_KB"), nullptr, 10) : 1024;
+        thread_local std::vector<uint8_t> ring(4 * ring_kb * 1024 + (200 << 10));
+        thread_local size_t ring_pos = 0;
         const char* p = paths[i].c_str();
         int64_t got = 0;
-        if (mode == 4) {
+        if (mode == 6) {
+          const size_t cap = off[i + 1] - off[i];
+          if (ring_pos + cap > 4 * ring_kb * 1024) ring_pos = 0;
+          got = read_cas_message(p, sizes[i], ring.data() + ring_pos, cap);
+          ring_pos += cap;
+        } else if (mode == 4) {
           got = read_cas_message(p, sizes[i], priv.data(), off[i + 1] - off[i]);
           if (got > 0) {
             const size_t m = align_up(static_cast<size_t>(got), 32);
@@ -94,5 +105,8 @@ int main(int argc, char** argv) {
   run("ntcopy", 4);
   run("arena", 0);
   run("ntcopy", 4);
+  run("ring", 6);
+  run("arena", 0);
+  run("ring", 6);
   return 0;
 }
