@@ -1,4 +1,5 @@
 # A/B: ring staging of sdgpu_identify_files (SDGPU_STAGE=ring: small hot
+# (Negative: ring staging removed after this A/B; logs in profiles/r4/ring_ab/.)
 # pinned buffers copied H2D into a device arena, K1 per segment) against the
 # slab pipeline; the path tests under ring staging first, then the config-1
 # directory leg alternating (one box), then the small-copy H2D experiment.

@@ -6,7 +6,6 @@
 #include <errno.h>
 
 #include <algorithm>
-#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -161,21 +160,6 @@ struct sdgpu_ctx {
   hipEvent_t pipe_evt[kPipeSlabs] = {};
   hipStream_t copy_stream = nullptr;  // H2D of staged slabs (SDMA), created on first use
   hipEvent_t stage_copied[3] = {}, stage_freed[3] = {};
-  // ring staging of sdgpu_identify_files (SDGPU_STAGE=ring): small pinned
-  // buffers, reused while their lines are still in the host's caches, each
-  // copied H2D into the call's device arena as it fills
-  static constexpr int kRingBufs = 32, kRingStreams = 8;
-  static constexpr size_t kRingBytes = size_t(1) << 20;
-  PinBuf ring_h;
-  hipEvent_t ring_evt[kRingBufs] = {};
-  bool ring_used[kRingBufs] = {};
-  hipStream_t ring_stream[kRingStreams] = {};
-  hipEvent_t ring_done[kRingStreams] = {};
-  std::vector<int> ring_free;
-  std::mutex ring_mu;
-  std::condition_variable ring_cv;
-  DevBuf ring_arena, ring_dmeta;
-  PinBuf ring_meta;
   PinBuf plan_pin;
   hipEvent_t plan_evt = nullptr;
   bool plan_pending = false;

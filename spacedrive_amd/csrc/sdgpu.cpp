@@ -282,141 +282,6 @@ int run_pipeline(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&
   return rc;
 }
 
-// Ring staging (SDGPU_STAGE=ring; DESIGN.md §8 config-1 reads): the call's
-// files in consecutive BATCHES of at most kRingBytes of messages; a pool
-// thread takes a batch, reads its files into a free ring buffer (small and
-// reused, so its lines are still in the host caches: no write-allocate from
-// DRAM as in a fresh staging slab), copies it H2D into the call's device
-// arena at the batch's offset on one of the ring streams and returns the
-// buffer (reused once that copy's event has completed).  The batches run in
-// kSeg segments; K1 hashes a segment on the context stream once its copies
-// are in while the next segment is read.
-bool ring_staging() {
-  static const bool on = [] {
-    const char* e = getenv("SDGPU_STAGE");
-    return e && e[0] == 'r';
-  }();
-  return on;
-}
-
-int ring_init(sdgpu_ctx* c) {
-  if (c->ring_h.p) return 0;
-  SD_TRY_RC(ensure_pin(c->ring_h, sdgpu_ctx::kRingBytes * sdgpu_ctx::kRingBufs));
-  for (int k = 0; k < sdgpu_ctx::kRingBufs; ++k) {
-    SD_TRY(hipEventCreateWithFlags(&c->ring_evt[k], hipEventDisableTiming));
-    c->ring_free.push_back(k);
-  }
-  for (int k = 0; k < sdgpu_ctx::kRingStreams; ++k) {
-    SD_TRY(hipStreamCreateWithFlags(&c->ring_stream[k], hipStreamNonBlocking));
-    SD_TRY(hipEventCreateWithFlags(&c->ring_done[k], hipEventDisableTiming));
-  }
-  return 0;
-}
-
-template <typename Est, typename Produce, typename Finish>
-int run_ring(sdgpu_ctx* c, uint32_t n, Est&& est, Produce&& produce, Finish&& finish) {
-  (void)pick(c, nullptr);
-  SD_TRY_RC(ring_init(c));
-  constexpr uint64_t RB = sdgpu_ctx::kRingBytes;
-  // layout: every file's message at a 16-B aligned offset of the arena
-  const size_t o_len = align_up(8ull * (n + 1), 256), o_pst = align_up(o_len + 4ull * n, 256),
-               o_out = align_up(o_pst + 4ull * n, 256), meta = align_up(o_out + 8ull * n, 256);
-  SD_TRY_RC(ensure_pin(c->ring_meta, meta));
-  uint8_t* hm = static_cast<uint8_t*>(c->ring_meta.p);
-  uint64_t* off = reinterpret_cast<uint64_t*>(hm);
-  uint32_t* len = reinterpret_cast<uint32_t*>(hm + o_len);
-  int32_t* pst = reinterpret_cast<int32_t*>(hm + o_pst);
-  uint8_t(*out8)[8] = reinterpret_cast<uint8_t(*)[8]>(hm + o_out);
-  std::vector<uint32_t> bstart;  // batch b = files [bstart[b], bstart[b + 1])
-  uint64_t pos = 0, bpos = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint64_t e = std::min<uint64_t>(align_up(est(i), 16), RB);
-    if (i == 0 || pos + e - bpos > RB) {
-      bstart.push_back(i);
-      bpos = pos;
-    }
-    off[i] = pos;
-    pos += e;
-  }
-  off[n] = pos;
-  bstart.push_back(n);
-  const uint32_t nb = static_cast<uint32_t>(bstart.size() - 1);
-  SD_TRY_RC(ensure_dev(c, c->ring_arena, std::max<uint64_t>(pos, 16)));
-  SD_TRY_RC(ensure_dev(c, c->ring_dmeta, meta));
-  uint8_t* D = static_cast<uint8_t*>(c->ring_arena.p);
-  uint8_t* dm = static_cast<uint8_t*>(c->ring_dmeta.p);
-  BatchWork w;
-  // K1's workspace: one segment at a time
-  constexpr uint32_t kSeg = 4;
-  SD_TRY_RC(batch_work(c, n, pos / kChunkLen + n + 4ull * kSeg, w));
-  EventTimer* ht = c->timing ? &c->timer : nullptr;
-  std::atomic<int> err{0};
-  uint8_t* ring = static_cast<uint8_t*>(c->ring_h.p);
-  for (uint32_t sg = 0; sg < kSeg; ++sg) {
-    const uint32_t b0 = static_cast<uint32_t>(static_cast<uint64_t>(nb) * sg / kSeg),
-                   b1 = static_cast<uint32_t>(static_cast<uint64_t>(nb) * (sg + 1) / kSeg);
-    if (b0 == b1) continue;
-    const auto t_fill = std::chrono::steady_clock::now();
-    parallel_for(b1 - b0, [&](uint32_t bi) {
-      const uint32_t b = b0 + bi, f0 = bstart[b], f1 = bstart[b + 1];
-      int k;
-      {
-        std::unique_lock<std::mutex> lk(c->ring_mu);
-        c->ring_cv.wait(lk, [&] { return !c->ring_free.empty(); });
-        k = c->ring_free.back();
-        c->ring_free.pop_back();
-      }
-      if (c->ring_used[k] && hipEventSynchronize(c->ring_evt[k]) != hipSuccess) err = -EIO;
-      uint8_t* buf = ring + static_cast<size_t>(k) * RB;
-      for (uint32_t i = f0; i < f1; ++i) {
-        const int64_t r = produce(i, buf + (off[i] - off[f0]), static_cast<size_t>(off[i + 1] - off[i]));
-        if (r >= 0 && r != 0x7fffffff) {
-          len[i] = static_cast<uint32_t>(r);
-          pst[i] = 0;
-        } else {
-          len[i] = 0;
-          pst[i] = r == 0x7fffffff ? 1 : static_cast<int32_t>(r);
-        }
-      }
-      hipStream_t st = c->ring_stream[b % sdgpu_ctx::kRingStreams];
-      if (hipMemcpyAsync(D + off[f0], buf, off[f1] - off[f0], hipMemcpyHostToDevice, st) !=
-              hipSuccess ||
-          hipEventRecord(c->ring_evt[k], st) != hipSuccess)
-        err = -EIO;
-      {
-        std::lock_guard<std::mutex> lk(c->ring_mu);
-        c->ring_used[k] = true;
-        c->ring_free.push_back(k);
-      }
-      c->ring_cv.notify_one();
-    });
-    if (ht)
-      ht->host("stage_fill", std::chrono::duration<double, std::milli>(
-                                 std::chrono::steady_clock::now() - t_fill).count());
-    if (err.load()) return err.load();
-    // the segment's copies, then its lengths, then K1 on the context stream
-    hipStream_t s = c->stream;
-    for (int q = 0; q < sdgpu_ctx::kRingStreams; ++q) {
-      SD_TRY(hipEventRecord(c->ring_done[q], c->ring_stream[q]));
-      SD_TRY(hipStreamWaitEvent(s, c->ring_done[q], 0));
-    }
-    const uint32_t f0 = bstart[b0], f1 = bstart[b1], cnt = f1 - f0;
-    if (sg == 0) SD_TRY(hipMemcpyAsync(dm, off, 8ull * (n + 1), hipMemcpyHostToDevice, s));
-    SD_TRY(hipMemcpyAsync(dm + o_len + 4ull * f0, len + f0, 4ull * cnt, hipMemcpyHostToDevice, s));
-    SD_TRY(batch_hash_launch(D, pos, reinterpret_cast<const uint64_t*>(dm) + f0,
-                             reinterpret_cast<const uint32_t*>(dm + o_len) + f0, cnt, kStageMaxMsg,
-                             2, dm + o_out + 8ull * f0, nullptr, w, s, c->kt()));
-    SD_TRY(hipMemcpyAsync(out8 + f0, dm + o_out + 8ull * f0, 8ull * cnt, hipMemcpyDeviceToHost, s));
-  }
-  const auto t_wait = std::chrono::steady_clock::now();
-  SD_TRY(hipStreamSynchronize(c->stream));
-  if (ht)
-    ht->host("stage_wait", std::chrono::duration<double, std::milli>(
-                               std::chrono::steady_clock::now() - t_wait).count());
-  finish(0u, n, const_cast<const uint8_t(*)[8]>(out8), const_cast<const int32_t*>(pst));
-  return 0;
-}
-
 }  // namespace
 
 // ===========================================================================
@@ -494,19 +359,6 @@ int sdgpu_close(sdgpu_ctx* c) {
     if (c->stage_freed[k]) (void)hipEventDestroy(c->stage_freed[k]);
   }
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-  for (int k = 0; k < sdgpu_ctx::kRingStreams; ++k) {
-    if (c->ring_stream[k]) {
-      (void)hipStreamSynchronize(c->ring_stream[k]);
-      (void)hipStreamDestroy(c->ring_stream[k]);
-    }
-    if (c->ring_done[k]) (void)hipEventDestroy(c->ring_done[k]);
-  }
-  for (int k = 0; k < sdgpu_ctx::kRingBufs; ++k)
-    if (c->ring_evt[k]) (void)hipEventDestroy(c->ring_evt[k]);
-  for (DevBuf* b : {&c->ring_arena, &c->ring_dmeta})
-    if (b->p) (void)hipFree(b->p);
-  for (PinBuf* b : {&c->ring_h, &c->ring_meta})
-    if (b->p) (void)hipHostFree(b->p);
   if (c->plan_pin.p) (void)hipHostFree(c->plan_pin.p);
   for (DevBuf* b : {&c->xs_send, &c->xs_recv, &c->xs_back, &c->xs_ret, &c->xs_rback})
     if (b->p) (void)hipFree(b->p);
@@ -713,30 +565,28 @@ int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t*
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
   std::vector<uint32_t> grown;  // <= 100 KiB at stat, longer than its room at read
-  auto est_f = [&](uint32_t i) -> uint64_t {
-    if (size[i] == 0) return 16;
-    return size[i] <= SDGPU_CAS_MINIMUM_FILE_SIZE ? 8 + size[i] + 4096  // room to grow
-                                                  : SDGPU_CAS_SAMPLED_MSG_LEN;
-  };
-  auto produce_f = [&](uint32_t i, uint8_t* dst, size_t cap) -> int64_t {
-    if (size[i] == 0) return 0x7fffffff;  // cas_id None (file_identifier/mod.rs:80-88)
-    return read_cas_message(paths[i], size[i], dst, cap);
-  };
-  auto finish_f = [&](uint32_t first, uint32_t cnt, const uint8_t (*o)[8], const int32_t* st) {
-    for (uint32_t j = 0; j < cnt; ++j) {
-      const int32_t sj = st[j];
-      const bool ok = sj == 0;
-      if (sj == -EFBIG) grown.push_back(first + j);
-      if (ok) memcpy(out8[first + j], o[j], 8);
-      else memset(out8[first + j], 0, 8);
-      if (has_key) has_key[first + j] = ok ? 1 : 0;
-      if (status) status[first + j] = sj == 1 ? 0 : sj;
-    }
-  };
-  const int rc = (ring_staging() && !c->io_uring && n > kSmallBatch)
-                     ? run_ring(c, n, est_f, produce_f, finish_f) :
-                 run_pipeline(
-      c, n, est_f, produce_f, finish_f,
+  const int rc = run_pipeline(
+      c, n,
+      [&](uint32_t i) -> uint64_t {
+        if (size[i] == 0) return 16;
+        return size[i] <= SDGPU_CAS_MINIMUM_FILE_SIZE ? 8 + size[i] + 4096  // room to grow
+                                                      : SDGPU_CAS_SAMPLED_MSG_LEN;
+      },
+      [&](uint32_t i, uint8_t* dst, size_t cap) -> int64_t {
+        if (size[i] == 0) return 0x7fffffff;  // cas_id None (file_identifier/mod.rs:80-88)
+        return read_cas_message(paths[i], size[i], dst, cap);
+      },
+      [&](uint32_t first, uint32_t cnt, const uint8_t (*o)[8], const int32_t* st) {
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const int32_t sj = st[j];
+          const bool ok = sj == 0;
+          if (sj == -EFBIG) grown.push_back(first + j);
+          if (ok) memcpy(out8[first + j], o[j], 8);
+          else memset(out8[first + j], 0, 8);
+          if (has_key) has_key[first + j] = ok ? 1 : 0;
+          if (status) status[first + j] = sj == 1 ? 0 : sj;
+        }
+      },
       [&](uint32_t first, uint32_t cnt, const uint64_t* off, uint64_t end, uint8_t* hb,
           auto&& settle) -> bool {
         // batched io_uring chains (csrc/uring.hpp), one ring per pool thread:
