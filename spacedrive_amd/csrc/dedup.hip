@@ -137,17 +137,56 @@ __device__ __forceinline__ uint32_t wave_add(uint32_t* cnt, uint32_t d, bool v) 
   return slot;
 }
 
-template <typename In>
+// The valid keyless rows of a fused grouping call (ListOut without an Object
+// index; mod.rs:238-239: each is its own Object), collected by the FIRST
+// partition pass that already reads every row's has_key: block j appends the
+// ranks of its tile's keyless rows with valid[i] != 0 (valid null: all) to
+// st[j * cap, ...) and stores how many in cnt[j]; k_list_finish moves them
+// behind the keyed entries.  This replaced a separate pass over has_key /
+// valid (three launches, 0.062 ms at 100 M rows, 0.017 ms at 12.5 M).
+struct XSink {
+  const uint8_t* valid = nullptr;
+  uint32_t* st = nullptr;  // null: no sink
+  uint32_t* cnt = nullptr;
+  uint32_t cap = 0;        // rows per first-pass tile
+};
+
+// Called by a wave's active lanes; `keyless`: row i is in range with has_key
+// == 0.  One LDS atomic per wave that has such rows (rare: no cost otherwise).
+__device__ __forceinline__ void sink_keyless(const XSink& x, const RowsIn& in, bool keyless,
+                                             uint64_t i, uint32_t* xn) {
+  const bool e = keyless && (!x.valid || x.valid[i] != 0);
+  const uint64_t b = __ballot(e);
+  if (!b) return;
+  const uint32_t lane = __lane_id();
+  const int leader = __ffsll(static_cast<unsigned long long>(b)) - 1;
+  uint32_t base = 0;
+  if (lane == static_cast<uint32_t>(leader)) base = atomicAdd(xn, static_cast<uint32_t>(__popcll(b)));
+  base = __shfl(base, leader);
+  if (e)
+    x.st[static_cast<uint64_t>(part_block()) * x.cap + base + __popcll(b & ((1ull << lane) - 1ull))] =
+        in.rank ? in.rank[i] : in.rank_base + static_cast<uint32_t>(i);
+}
+
+template <typename In, bool kX = false>
 __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, uint32_t skip,
                                                             uint32_t bits, uint32_t world,
                                                             uint32_t* __restrict__ hist,
                                                             uint32_t* __restrict__ zero = nullptr,
-                                                            bool blk_major = false) {
+                                                            bool blk_major = false,
+                                                            XSink xs = XSink{}) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
+  __shared__ uint32_t xn;
   const uint32_t nbins = world ? world : 1u << bits;
   if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;  // a flag of the next kernels
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) cnt[b] = 0;
+  if (kX && threadIdx.x == 0) xn = 0;
   __syncthreads();
+  // the sink's count, after the block's last append (its final barrier)
+  auto sink_done = [&]() {
+    if constexpr (kX)
+      if (threadIdx.x == 0) xs.cnt[part_block()] = xn;
+  };
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
   if constexpr (std::is_same<In, RowsIn>::value) {
@@ -160,9 +199,16 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
         if (v) atomicAdd(&cnt[part_digit(row_hash(k), skip, bits, 0)], 1u);
       };
       const uint64_t p0 = (t0 + 1) / 2, p1 = t1 / 2;  // whole pairs: rows [2 p0, 2 p1)
-      if (threadIdx.x == 0 && (t0 & 1u) && t0 < t1) count(in.key[t0], !in.valid || in.valid[t0]);
-      if (threadIdx.x == 1 && (t1 & 1u) && t1 - 1 >= 2 * p0)
-        count(in.key[t1 - 1], !in.valid || in.valid[t1 - 1]);
+      if (threadIdx.x == 0 && (t0 & 1u) && t0 < t1) {
+        const bool v = !in.valid || in.valid[t0];
+        count(in.key[t0], v);
+        if constexpr (kX) sink_keyless(xs, in, !v, t0, &xn);
+      }
+      if (threadIdx.x == 1 && (t1 & 1u) && t1 - 1 >= 2 * p0) {
+        const bool v = !in.valid || in.valid[t1 - 1];
+        count(in.key[t1 - 1], v);
+        if constexpr (kX) sink_keyless(xs, in, !v, t1 - 1, &xn);
+      }
       const uint4* __restrict__ k4 = reinterpret_cast<const uint4*>(in.key);
       const uint16_t* __restrict__ v2 = reinterpret_cast<const uint16_t*>(in.valid);
       constexpr int kP = kUnroll / 2;
@@ -177,15 +223,21 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
         }
 #pragma unroll
         for (int u = 0; u < kP; ++u) {
-          if (q0 + static_cast<uint64_t>(u) * kPartThreads >= p1) continue;
+          const uint64_t q = q0 + static_cast<uint64_t>(u) * kPartThreads;
+          if (q >= p1) continue;
           count((static_cast<uint64_t>(kk[u].y) << 32) | kk[u].x, (vv[u] & 0xFFu) != 0);
           count((static_cast<uint64_t>(kk[u].w) << 32) | kk[u].z, (vv[u] >> 8) != 0);
+          if constexpr (kX) {
+            sink_keyless(xs, in, (vv[u] & 0xFFu) == 0, 2 * q, &xn);
+            sink_keyless(xs, in, (vv[u] >> 8) == 0, 2 * q + 1, &xn);
+          }
         }
       }
       __syncthreads();
       for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
         hist[blk_major ? static_cast<uint64_t>(part_block()) * nbins + b
                        : static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
+      sink_done();
       return;
     }
   }
@@ -196,6 +248,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
     for (int u = 0; u < kUnroll; ++u) {
       const bool v = in.valid_of(q, u);
       const uint64_t k = in.key_of(q, u);
+      if constexpr (kX) sink_keyless(xs, in, q.in[u] && !v, q.row[u], &xn);
       if (world) {
         (void)wave_add(cnt, v ? part_digit(in_hash<In>(k), skip, bits, world) : 0u, v);
       } else if (v) {
@@ -209,6 +262,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
     hist[blk_major ? static_cast<uint64_t>(part_block()) * nbins + b
                    : static_cast<uint64_t>(b) * gridDim.x + part_block()] = cnt[b];
+  sink_done();
 }
 
 // Shard partition of the multi-GPU exchange: keyed rows packed by digit (the
@@ -409,12 +463,12 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
 // pass (k_part2_runs) reads a segment's records as those runs, so no global
 // offsets -- and no k_part_hist pass over all rows -- are needed.  Fine
 // counts per final bucket as in k_part_scatter_runs.
-template <typename In, bool kInitRep, bool kRec12 = false>
+template <typename In, bool kInitRep, bool kRec12 = false, bool kX = false>
 __global__ __launch_bounds__(kPartThreads) void k_part_private(
     In in, uint64_t n, uint32_t skip, uint32_t bits, uint4* __restrict__ rec,
     uint32_t* __restrict__ rep, uint32_t fbits, uint32_t* __restrict__ fine,
     uint32_t* __restrict__ ovf, uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_len,
-    uint32_t max_rounds, uint32_t* __restrict__ segtot) {
+    uint32_t max_rounds, uint32_t* __restrict__ segtot, XSink xs = XSink{}) {
   constexpr int U = 4;
   constexpr uint32_t R = U * kPartThreads;
   using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
@@ -424,7 +478,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
   __shared__ uint32_t fc[1u << (kMaxBucketBits - 1)];  // 2 x 16-bit counters per word
   const uint32_t nbins = 1u << bits, nfine = 1u << fbits;
   const uint32_t blk = part_block();
+  __shared__ uint32_t xn;
   for (uint32_t b = threadIdx.x; b < nfine / 2; b += kPartThreads) fc[b] = 0;
+  if (kX && threadIdx.x == 0) xn = 0;  // ordered before use by the round's first barrier
   bool over = false;
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
@@ -441,6 +497,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
       if (!q.in[u]) continue;
       const uint32_t rk = in.rank_of(q, u);
       if (kInitRep) rep[i] = rk;
+      if constexpr (kX) sink_keyless(xs, in, !in.valid_of(q, u), i, &xn);
       if (!in.valid_of(q, u)) continue;
       const uint64_t h = in_hash<In>(in.key_of(q, u));
       dg[u] = digit_of(h, skip, bits);
@@ -502,6 +559,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
   }
   if (over) *ovf = 1u;
   __syncthreads();
+  if (kX && threadIdx.x == 0) xs.cnt[blk] = xn;
   uint32_t* f = fine + static_cast<uint64_t>(blk) * nfine;
   for (uint32_t b = threadIdx.x; b < nfine; b += kPartThreads)
     f[b] = (fc[b >> 1] >> ((b & 1u) << 4)) & 0xFFFFu;
@@ -1195,8 +1253,8 @@ constexpr int kPer = (kLdsCap + kGroupThreads - 1) / kGroupThreads;
 //            creators from the front, who = rank; linked rows from the back,
 //            who = rank | SDGPU_LINKED, obj = f.  Coalesced;
 //            no rep array.  lcnt[bucket] = its linked rows; the last bucket
-//            stores the keyed total in counts[2]; k_list_finish then sets
-//            counts[0] / [1] (no same-address atomics: 32 k workgroups adding
+//            stores the keyed total in lcnt[buckets]; k_list_finish then sets
+//            counts[0..2] (no same-address atomics: 32 k workgroups adding
 //            to one word serialised at ~4 ns each, +0.29 ms at 100 M rows in
 //            r4e's fused_job leg).
 struct RepOut {
@@ -1214,22 +1272,50 @@ struct RepOut {
     (void)r;
   }
 };
-// counts[1] = the buckets' linked rows, counts[0] = keyed - linked (one block)
+// counts[1] = the buckets' linked rows, counts[0] = keyed - linked (block 0);
+// K = the keyed entries, lcnt[nb] (the last bucket's end).  With a keyless
+// sink (XSink) every block j also moves first-pass block j's valid keyless
+// rows (who = rank, own Objects) to who[K + (rows of blocks < j) ...], and
+// block 0 adds them to counts[0] / [2].
 __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict__ lcnt,
-                                                      uint32_t nb, uint32_t* __restrict__ counts) {
+                                                      uint32_t nb, uint32_t* __restrict__ counts,
+                                                      uint32_t* __restrict__ who, XSink xs) {
   __shared__ uint32_t sw[16];
-  uint32_t t = 0;
-  for (uint32_t i = threadIdx.x; i < nb; i += 1024) t += lcnt[i];
+  const uint32_t lane = __lane_id(), K = lcnt[nb];
+  uint32_t before = 0, E = 0;  // the sink's rows of blocks < j, all of them
+  if (xs.st && threadIdx.x < 64) {
+    for (uint32_t b = lane; b < kPartBlocks; b += 64) {
+      const uint32_t c = xs.cnt[b];
+      E += c;
+      if (b < blockIdx.x) before += c;
+    }
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d);
-  if (__lane_id() == 0) sw[threadIdx.x >> 6] = t;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t l = 0;
-    for (int w = 0; w < 16; ++w) l += sw[w];
-    counts[1] = l;
-    counts[0] = counts[2] - l;
+    for (int d = 32; d > 0; d >>= 1) {
+      E += __shfl_xor(E, d);
+      before += __shfl_xor(before, d);
+    }
   }
+  if (blockIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t i = threadIdx.x; i < nb; i += 1024) t += lcnt[i];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d);
+    if (lane == 0) sw[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t l = 0;
+      for (int w = 0; w < 16; ++w) l += sw[w];
+      counts[1] = l;
+      counts[0] = K - l + E;
+      counts[2] = K + E;
+    }
+  }
+  if (!xs.st) return;
+  if (threadIdx.x == 0) sw[0] = before;
+  __syncthreads();
+  const uint32_t c = xs.cnt[blockIdx.x], o = K + sw[0];
+  const uint32_t* src = xs.st + static_cast<uint64_t>(blockIdx.x) * xs.cap;
+  for (uint32_t k = threadIdx.x; k < c; k += 1024) who[o + k] = src[k];
 }
 hipError_t out_finish(const RepOut&, uint32_t, hipStream_t) { return hipSuccess; }
 // ListOut: each wave's entries are placed by ONE LDS atomic per (step, list)
@@ -1245,7 +1331,8 @@ struct ListOut {
   uint32_t* who;
   uint32_t* obj;
   uint32_t* counts;
-  uint32_t* lcnt;
+  uint32_t* lcnt;  // [bucket]: linked rows; [buckets]: the keyed total
+  XSink x;         // the valid keyless rows, when the partition collects them
   template <int kSteps>
   __device__ __forceinline__ void emit(const bool (&live)[kSteps], const bool (&lk)[kSteps],
                                        const uint32_t (&r)[kSteps], const uint32_t (&w)[kSteps],
@@ -1283,13 +1370,13 @@ __device__ __forceinline__ void out_done(const ListOut& o, uint32_t, uint32_t, u
   __syncthreads();  // every wave's atomics on the counters are done
   if (threadIdx.x == 0) {
     o.lcnt[blockIdx.x] = scr[1];
-    if (blockIdx.x == gridDim.x - 1) o.counts[2] = end;
+    if (blockIdx.x == gridDim.x - 1) o.lcnt[gridDim.x] = end;
   }
 }
 __device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t,
                                          const uint32_t*) {}
 hipError_t out_finish(const ListOut& o, uint32_t nb, hipStream_t s) {
-  k_list_finish<<<1, 1024, 0, s>>>(o.lcnt, nb, o.counts);
+  k_list_finish<<<o.x.st ? kPartBlocks : 1u, 1024, 0, s>>>(o.lcnt, nb, o.counts, o.who, o.x);
   return hipGetLastError();
 }
 
@@ -1859,6 +1946,7 @@ struct GroupLayout {
   uint32_t max_rounds;
   size_t run_s, run_l, segtot;
   size_t lcnt;
+  size_t xst, xcnt;  // ListOut's keyless sink (XSink)
   size_t total;
 };
 
@@ -1890,7 +1978,9 @@ GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
   L.run_s = o; o = align_up(o + 4 * nrun, 256);
   L.run_l = o; o = align_up(o + 4 * nrun, 256);
   L.segtot = o; o = align_up(o + 4 * kRunMaxBins, 256);
-  L.lcnt = o; o = align_up(o + 4 * nf, 256);  // ListOut: linked rows per bucket
+  L.lcnt = o; o = align_up(o + 4 * (nf + 1), 256);  // ListOut: linked rows per bucket, keyed total
+  L.xst = o; o = align_up(o + 4 * (n + kMaxPartBlocks), 256);
+  L.xcnt = o; o = align_up(o + 4 * kMaxPartBlocks, 256);
   L.total = o;
   return L;
 }
@@ -1901,6 +1991,27 @@ void allow_lds(K kernel, size_t bytes) {
   if (bytes > (size_t(64) << 10))
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+}
+
+XSink sink_of(const RepOut&) { return XSink{}; }
+XSink sink_of(const ListOut& o) { return o.x; }
+
+// A first-pass histogram, with the keyless sink when the output has one
+// (RowsIn only: the rows the caller passed).
+template <typename In>
+void hist_launch(const XSink& xs, size_t lds, hipStream_t s, In in, uint64_t n, uint32_t skip,
+                 uint32_t bits, uint32_t* hist, uint32_t* zero = nullptr, bool blk_major = false) {
+  const uint32_t P = bucket_part_blocks();
+  if constexpr (std::is_same<In, RowsIn>::value) {
+    if (xs.st) {
+      allow_lds(k_part_hist<In, true>, lds);
+      k_part_hist<In, true><<<P, kPartThreads, lds, s>>>(in, n, skip, bits, 0, hist, zero,
+                                                         blk_major, xs);
+      return;
+    }
+  }
+  allow_lds(k_part_hist<In>, lds);
+  k_part_hist<In><<<P, kPartThreads, lds, s>>>(in, n, skip, bits, 0, hist, zero, blk_major);
 }
 
 // Two-level partition (n > 4096 x kBucketRows) + group: see group_layout.
@@ -1943,12 +2054,24 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
     k_zero_runs<<<1, 64, 0, s>>>(segtot, ovf);
     {
       KScope k(timer, "bucket_scatter1", s);
-      if (init_rep)
+      bool sunk = false;
+      if constexpr (std::is_same<In, RowsIn>::value) {
+        const XSink xs = sink_of(out);
+        if (xs.st) {
+          k_part_private<In, false, kRec12, true><<<P, kPartThreads, 0, s>>>(
+              in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, L.max_rounds,
+              segtot, xs);
+          sunk = true;
+        }
+      }
+      if (sunk) {
+      } else if (init_rep) {
         k_part_private<In, true, kRec12><<<P, kPartThreads, 0, s>>>(
             in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, L.max_rounds, segtot);
-      else
+      } else {
         k_part_private<In, false, kRec12><<<P, kPartThreads, 0, s>>>(
             in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, L.max_rounds, segtot);
+      }
     }
     {
       KScope k(timer, "bucket_fine_scan", s);
@@ -1980,7 +2103,7 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
   const size_t lds1 = sizeof(uint32_t) << L.cbits;
   {
     KScope k(timer, "bucket_hist", s);
-    k_part_hist<In><<<P, kPartThreads, lds1, s>>>(in, n, kShardBits, L.cbits, 0, hist1, ovf);
+    hist_launch(sink_of(out), lds1, s, in, n, kShardBits, L.cbits, hist1, ovf);
   }
   scan::exclusive(hist1, static_cast<uint64_t>(nseg) * P, hist1, tiles, nullptr, s);
   {
@@ -2061,7 +2184,7 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
     static_assert(kPartBlocks % 16 == 0, "k_fine_scan: blocks per thread");
     {
       KScope k(timer, "bucket_hist", s);
-      k_part_hist<In><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, 0, fine, nullptr, true);
+      hist_launch(sink_of(out), lds, s, in, n, kShardBits, bits, fine, nullptr, true);
       k_fine_scan<kPartBlocks, 1><<<nb / 64, 1024, 0, s>>>(fine, nb, fE, ftot, ovf);
     }
     if constexpr (std::is_same<In, RowsIn>::value) {
@@ -2100,8 +2223,7 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   }
   {
     KScope k(timer, "bucket_hist", s);
-    allow_lds(k_part_hist<In>, lds);
-    k_part_hist<In><<<P, kPartThreads, lds, s>>>(in, n, kShardBits, bits, 0, hist);
+    hist_launch(sink_of(out), lds, s, in, n, kShardBits, bits, hist);
   }
   scan::exclusive(hist, nh, hist, tiles, nullptr, s);
   {
@@ -2168,11 +2290,17 @@ hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_
 
 hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* who,
                              uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
-                             KTimer* timer) {
+                             KTimer* timer, bool sink_keyless, const uint8_t* keyless_valid) {
   if (in.n == 0) return hipSuccess;
-  uint32_t* lcnt =
-      reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ws) + group_layout(in.n).lcnt);
-  const ListOut out{who, obj, counts, lcnt};
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  const GroupLayout L = group_layout(in.n);
+  ListOut out{who, obj, counts, reinterpret_cast<uint32_t*>(w + L.lcnt), XSink{}};
+  if (sink_keyless && !in.rec12 && in.valid) {
+    out.x.valid = keyless_valid;
+    out.x.st = reinterpret_cast<uint32_t*>(w + L.xst);
+    out.x.cnt = reinterpret_cast<uint32_t*>(w + L.xcnt);
+    out.x.cap = static_cast<uint32_t>((in.n + bucket_part_blocks() - 1) / bucket_part_blocks());
+  }
   if (in.rec12)
     return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
                         chunk_rows, nullptr, false, out, ws, s, timer);

@@ -159,10 +159,14 @@ hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_
 // its record range, creators from the front (who = rank) and linked rows from
 // the back (who = rank | SDGPU_LINKED, obj = creator rank); no rep array.
 // counts[0..2] (zeroed by the caller) += creators, linked; counts[2] = keyed
-// entries.
+// entries.  sink_keyless (caller's rows with a has_key array): the first
+// partition pass also lists the valid keyless rows (keyless_valid[i] != 0,
+// null: all) as creators behind the keyed entries -- what extra_list_launch
+// does without an index, with no pass of its own.
 hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* who,
                              uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
-                             KTimer* timer = nullptr);
+                             KTimer* timer = nullptr, bool sink_keyless = false,
+                             const uint8_t* keyless_valid = nullptr);
 // extra_list_launch then appends, in row order, the valid keyless rows and
 // (with an index: grouped = the probe's mask, hitrep = its reps) the keyed
 // rows the probe decided.

@@ -923,10 +923,9 @@ int sdgpu_group_link_device(sdgpu_ctx* c, sdgpu_index* x, const uint64_t* d_key,
   in.rank = d_rank;
   in.rank_base = first_rank;
   in.n = n;
-  if (!x) {
-    SD_TRY(dedup_list_launch(in, chunk_rows, d_who, d_obj, d_counts, c->dedup_ws.p, s, c->kt()));
-    SD_TRY(extra_list_launch(d_has_key, d_valid, nullptr, nullptr, d_rank, first_rank, n, d_who,
-                             d_obj, d_counts, c->link_ws.p, s, c->kt()));
+  if (!x) {  // the valid keyless rows collected by the partition's first pass
+    SD_TRY(dedup_list_launch(in, chunk_rows, d_who, d_obj, d_counts, c->dedup_ws.p, s, c->kt(),
+                             true, d_valid));
     return 0;
   }
   // probe scratch: reps [n] + mask [n]

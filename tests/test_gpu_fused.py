@@ -248,3 +248,46 @@ def test_fused_every_row_decided_by_the_index(ctx):
     np.testing.assert_array_equal(fc, rc)
     np.testing.assert_array_equal(flr, rlr)
     np.testing.assert_array_equal(flo, rlo)
+
+
+@pytest.mark.parametrize("n", [300_001, 7_000_001])
+def test_fused_keyless_sink_on_unaligned_rows(ctx, n):
+    """The keyless rows are collected by the first partition pass (XSink in
+    dedup.hip).  Key / has_key / valid views that start one row into their
+    buffers miss the histogram's paired 16-B / 2-B loads, so the per-row
+    path collects them (small-table and 12-bit paths); the aligned case runs
+    in the other tests."""
+    import torch
+    from spacedrive_amd import dedup
+    rng = np.random.default_rng(n + 5)
+    pool = rng.integers(0, 2**64 - 1, n // 2, dtype=np.uint64, endpoint=True)
+    key = pool[rng.integers(0, pool.size, n)]
+    valid = (rng.random(n) > 0.03).astype(np.uint8)
+    has = ((rng.random(n) > 0.1) & (valid != 0)).astype(np.uint8)
+    pad = lambda a: np.concatenate([a[:1], a])  # noqa: E731
+    dk = torch.from_numpy(pad(key).view(np.int64)).cuda()[1:]
+    dh = torch.from_numpy(pad(has)).cuda()[1:]
+    dv = torch.from_numpy(pad(valid)).cuda()[1:]
+    assert dk.data_ptr() % 16 == 8 and dh.data_ptr() % 2 == 1
+    who, obj, (c, l) = dedup.group_link_device(dk, dh, dv, None, 40, 100, ctx=ctx)
+    fc, flr, flo = dedup.split_link_lists(who.cpu().numpy(), obj.cpu().numpy())
+    rc, rlr, rlo = _ref_lists(key, has, valid, None, 40, 100)
+    assert (c, l) == (rc.size, rlr.size)
+    np.testing.assert_array_equal(fc, rc)
+    np.testing.assert_array_equal(flr, rlr)
+    np.testing.assert_array_equal(flo, rlo)
+
+
+def test_fused_two_level_path_all_keyless_tiles(ctx):
+    """Two-level path (13 M rows): whole first-pass tiles of keyless rows (a
+    block's sink filled to its tile size) next to tiles of keyed ones."""
+    n = 13_000_000
+    rng = np.random.default_rng(13)
+    pool = rng.integers(0, 2**64 - 1, n // 2, dtype=np.uint64, endpoint=True)
+    key = pool[rng.integers(0, pool.size, n)]
+    has = np.ones(n, np.uint8)
+    has[: n // 4] = 0             # the first quarter of the tiles: keyless
+    has[n // 2: n // 2 + 1000] = 0
+    valid = np.ones(n, np.uint8)
+    valid[n // 8: n // 8 + 5000] = 0
+    _check(ctx, key, has, valid=valid)
