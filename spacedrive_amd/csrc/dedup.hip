@@ -227,9 +227,20 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
           if (q >= p1) continue;
           count((static_cast<uint64_t>(kk[u].y) << 32) | kk[u].x, (vv[u] & 0xFFu) != 0);
           count((static_cast<uint64_t>(kk[u].w) << 32) | kk[u].z, (vv[u] >> 8) != 0);
-          if constexpr (kX) {
-            sink_keyless(xs, in, (vv[u] & 0xFFu) == 0, 2 * q, &xn);
-            sink_keyless(xs, in, (vv[u] >> 8) == 0, 2 * q + 1, &xn);
+        }
+        if constexpr (kX) {  // one wave-uniform test per step: keyless rows are rare
+          bool any = false;
+#pragma unroll
+          for (int u = 0; u < kP; ++u)
+            any |= q0 + static_cast<uint64_t>(u) * kPartThreads < p1 &&
+                   ((vv[u] & 0xFFu) == 0 || (vv[u] & 0xFF00u) == 0);
+          if (__ballot(any)) {
+#pragma unroll
+            for (int u = 0; u < kP; ++u) {
+              const uint64_t q = q0 + static_cast<uint64_t>(u) * kPartThreads;
+              sink_keyless(xs, in, q < p1 && (vv[u] & 0xFFu) == 0, 2 * q, &xn);
+              sink_keyless(xs, in, q < p1 && (vv[u] >> 8) == 0, 2 * q + 1, &xn);
+            }
           }
         }
       }
@@ -488,6 +499,17 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
   auto round = [&](const RowBatch<U>& q, uint64_t i0) {
     if (threadIdx.x < nbins) cnt[threadIdx.x] = 0;
     lds_barrier();
+    if constexpr (kX) {  // one wave-uniform test per round: keyless rows are rare
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < U; ++u) any |= q.in[u] && !in.valid_of(q, u);
+      if (__ballot(any)) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          sink_keyless(xs, in, q.in[u] && !in.valid_of(q, u),
+                       i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads, &xn);
+      }
+    }
     uint32_t dg[U], lr[U];
     RecT rq[U];
 #pragma unroll
@@ -497,7 +519,6 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
       if (!q.in[u]) continue;
       const uint32_t rk = in.rank_of(q, u);
       if (kInitRep) rep[i] = rk;
-      if constexpr (kX) sink_keyless(xs, in, !in.valid_of(q, u), i, &xn);
       if (!in.valid_of(q, u)) continue;
       const uint64_t h = in_hash<In>(in.key_of(q, u));
       dg[u] = digit_of(h, skip, bits);
