@@ -499,17 +499,6 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
   auto round = [&](const RowBatch<U>& q, uint64_t i0) {
     if (threadIdx.x < nbins) cnt[threadIdx.x] = 0;
     lds_barrier();
-    if constexpr (kX) {  // one wave-uniform test per round: keyless rows are rare
-      bool any = false;
-#pragma unroll
-      for (int u = 0; u < U; ++u) any |= q.in[u] && !in.valid_of(q, u);
-      if (__ballot(any)) {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          sink_keyless(xs, in, q.in[u] && !in.valid_of(q, u),
-                       i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads, &xn);
-      }
-    }
     uint32_t dg[U], lr[U];
     RecT rq[U];
 #pragma unroll
@@ -556,6 +545,20 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
     lds_barrier();
     const uint32_t total = base[nbins];
     for (uint32_t k = threadIdx.x; k < total; k += kPartThreads) out[t0 + acc + k] = buf[k];
+    // the keyless rows' sink stores go out with the round's record stores: a
+    // store issued before the next round's wait on its prefetched rows made
+    // that wait cover it (+0.035 ms at 100 M rows, r4x)
+    if constexpr (kX) {  // one wave-uniform test per round: keyless rows are rare
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < U; ++u) any |= q.in[u] && !in.valid_of(q, u);
+      if (__ballot(any)) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          sink_keyless(xs, in, q.in[u] && !in.valid_of(q, u),
+                       i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads, &xn);
+      }
+    }
     acc += total;
     ++r;
     lds_barrier();
