@@ -139,33 +139,40 @@ __device__ __forceinline__ uint32_t wave_add(uint32_t* cnt, uint32_t d, bool v) 
 
 // The valid keyless rows of a fused grouping call (ListOut without an Object
 // index; mod.rs:238-239: each is its own Object), collected by the FIRST
-// partition pass that already reads every row's has_key: block j appends the
-// ranks of its tile's keyless rows with valid[i] != 0 (valid null: all) to
-// st[j * cap, ...) and stores how many in cnt[j]; k_list_finish moves them
-// behind the keyed entries.  This replaced a separate pass over has_key /
-// valid (three launches, 0.062 ms at 100 M rows, 0.017 ms at 12.5 M).
+// partition pass that already reads every row's has_key.  Each WAVE appends the
+// ranks of its keyless rows with valid[i] != 0 (valid null: all) to its own
+// segment st[(block * 16 + wave) * cap, ...), counting them in a register (a
+// ballot per test, no LDS atomic and no barrier), and stores the count in
+// cnt[block * 16 + wave]; k_list_finish moves them behind the keyed entries.
+// This replaced a separate pass over has_key / valid (three launches, 0.062 ms
+// at 100 M rows, 0.017 ms at 12.5 M).
+constexpr uint32_t kSinkWaves = kPartThreads / 64;
 struct XSink {
   const uint8_t* valid = nullptr;
   uint32_t* st = nullptr;  // null: no sink
   uint32_t* cnt = nullptr;
-  uint32_t cap = 0;        // rows per first-pass tile
+  uint32_t cap = 0;        // rows per wave segment (>= the rows a wave reads)
 };
 
-// Called by a wave's active lanes; `keyless`: row i is in range with has_key
-// == 0.  One LDS atomic per wave that has such rows (rare: no cost otherwise).
+// Called by every lane of a wave that is still in the partition's row loop
+// (the lanes that left it never return to it, so the active lanes' `wn`
+// agree, and lane 0 -- the last to leave -- holds the wave's count);
+// `keyless`: row i is in range with has_key == 0.
 __device__ __forceinline__ void sink_keyless(const XSink& x, const RowsIn& in, bool keyless,
-                                             uint64_t i, uint32_t* xn) {
+                                             uint64_t i, uint32_t& wn) {
   const bool e = keyless && (!x.valid || x.valid[i] != 0);
   const uint64_t b = __ballot(e);
   if (!b) return;
-  const uint32_t lane = __lane_id();
-  const int leader = __ffsll(static_cast<unsigned long long>(b)) - 1;
-  uint32_t base = 0;
-  if (lane == static_cast<uint32_t>(leader)) base = atomicAdd(xn, static_cast<uint32_t>(__popcll(b)));
-  base = __shfl(base, leader);
-  if (e)
-    x.st[static_cast<uint64_t>(part_block()) * x.cap + base + __popcll(b & ((1ull << lane) - 1ull))] =
+  if (e) {
+    const uint32_t lane = __lane_id();
+    const uint64_t seg = static_cast<uint64_t>(part_block()) * kSinkWaves + (threadIdx.x >> 6);
+    x.st[seg * x.cap + wn + __popcll(b & ((1ull << lane) - 1ull))] =
         in.rank ? in.rank[i] : in.rank_base + static_cast<uint32_t>(i);
+  }
+  wn += static_cast<uint32_t>(__popcll(b));
+}
+__device__ __forceinline__ void sink_count(const XSink& x, uint32_t wn) {
+  if (__lane_id() == 0) x.cnt[part_block() * kSinkWaves + (threadIdx.x >> 6)] = wn;
 }
 
 template <typename In, bool kX = false>
@@ -176,16 +183,13 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
                                                             bool blk_major = false,
                                                             XSink xs = XSink{}) {
   extern __shared__ __attribute__((aligned(16))) uint32_t cnt[];
-  __shared__ uint32_t xn;
+  uint32_t wn = 0;  // the wave's keyless rows (XSink)
   const uint32_t nbins = world ? world : 1u << bits;
   if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;  // a flag of the next kernels
   for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads) cnt[b] = 0;
-  if (kX && threadIdx.x == 0) xn = 0;
   __syncthreads();
-  // the sink's count, after the block's last append (its final barrier)
   auto sink_done = [&]() {
-    if constexpr (kX)
-      if (threadIdx.x == 0) xs.cnt[part_block()] = xn;
+    if constexpr (kX) sink_count(xs, wn);
   };
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
@@ -199,15 +203,14 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
         if (v) atomicAdd(&cnt[part_digit(row_hash(k), skip, bits, 0)], 1u);
       };
       const uint64_t p0 = (t0 + 1) / 2, p1 = t1 / 2;  // whole pairs: rows [2 p0, 2 p1)
-      if (threadIdx.x == 0 && (t0 & 1u) && t0 < t1) {
-        const bool v = !in.valid || in.valid[t0];
-        count(in.key[t0], v);
-        if constexpr (kX) sink_keyless(xs, in, !v, t0, &xn);
-      }
-      if (threadIdx.x == 1 && (t1 & 1u) && t1 - 1 >= 2 * p0) {
-        const bool v = !in.valid || in.valid[t1 - 1];
-        count(in.key[t1 - 1], v);
-        if constexpr (kX) sink_keyless(xs, in, !v, t1 - 1, &xn);
+      const bool e0 = (t0 & 1u) && t0 < t1, e1 = (t1 & 1u) && t1 - 1 >= 2 * p0;
+      if (threadIdx.x == 0 && e0) count(in.key[t0], !in.valid || in.valid[t0]);
+      if (threadIdx.x == 1 && e1) count(in.key[t1 - 1], !in.valid || in.valid[t1 - 1]);
+      if constexpr (kX) {
+        if (threadIdx.x < 64) {  // the whole wave 0 (its ballots)
+          sink_keyless(xs, in, threadIdx.x == 0 && e0 && !in.valid[t0], t0, wn);
+          sink_keyless(xs, in, threadIdx.x == 1 && e1 && !in.valid[t1 - 1], t1 - 1, wn);
+        }
       }
       const uint4* __restrict__ k4 = reinterpret_cast<const uint4*>(in.key);
       const uint16_t* __restrict__ v2 = reinterpret_cast<const uint16_t*>(in.valid);
@@ -238,8 +241,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
 #pragma unroll
             for (int u = 0; u < kP; ++u) {
               const uint64_t q = q0 + static_cast<uint64_t>(u) * kPartThreads;
-              sink_keyless(xs, in, q < p1 && (vv[u] & 0xFFu) == 0, 2 * q, &xn);
-              sink_keyless(xs, in, q < p1 && (vv[u] >> 8) == 0, 2 * q + 1, &xn);
+              sink_keyless(xs, in, q < p1 && (vv[u] & 0xFFu) == 0, 2 * q, wn);
+              sink_keyless(xs, in, q < p1 && (vv[u] >> 8) == 0, 2 * q + 1, wn);
             }
           }
         }
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
     for (int u = 0; u < kUnroll; ++u) {
       const bool v = in.valid_of(q, u);
       const uint64_t k = in.key_of(q, u);
-      if constexpr (kX) sink_keyless(xs, in, q.in[u] && !v, q.row[u], &xn);
+      if constexpr (kX) sink_keyless(xs, in, q.in[u] && !v, q.row[u], wn);
       if (world) {
         (void)wave_add(cnt, v ? part_digit(in_hash<In>(k), skip, bits, world) : 0u, v);
       } else if (v) {
@@ -489,9 +492,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
   __shared__ uint32_t fc[1u << (kMaxBucketBits - 1)];  // 2 x 16-bit counters per word
   const uint32_t nbins = 1u << bits, nfine = 1u << fbits;
   const uint32_t blk = part_block();
-  __shared__ uint32_t xn;
+  uint32_t wn = 0;  // the wave's keyless rows (XSink)
   for (uint32_t b = threadIdx.x; b < nfine / 2; b += kPartThreads) fc[b] = 0;
-  if (kX && threadIdx.x == 0) xn = 0;  // ordered before use by the round's first barrier
   bool over = false;
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
@@ -545,9 +547,6 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
     lds_barrier();
     const uint32_t total = base[nbins];
     for (uint32_t k = threadIdx.x; k < total; k += kPartThreads) out[t0 + acc + k] = buf[k];
-    // the keyless rows' sink stores go out with the round's record stores: a
-    // store issued before the next round's wait on its prefetched rows made
-    // that wait cover it (+0.035 ms at 100 M rows, r4x)
     if constexpr (kX) {  // one wave-uniform test per round: keyless rows are rare
       bool any = false;
 #pragma unroll
@@ -556,7 +555,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
 #pragma unroll
         for (int u = 0; u < U; ++u)
           sink_keyless(xs, in, q.in[u] && !in.valid_of(q, u),
-                       i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads, &xn);
+                       i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads, wn);
       }
     }
     acc += total;
@@ -583,7 +582,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
   }
   if (over) *ovf = 1u;
   __syncthreads();
-  if (kX && threadIdx.x == 0) xs.cnt[blk] = xn;
+  if constexpr (kX) sink_count(xs, wn);
   uint32_t* f = fine + static_cast<uint64_t>(blk) * nfine;
   for (uint32_t b = threadIdx.x; b < nfine; b += kPartThreads)
     f[b] = (fc[b >> 1] >> ((b & 1u) << 4)) & 0xFFFFu;
@@ -1298,33 +1297,48 @@ struct RepOut {
 };
 // counts[1] = the buckets' linked rows, counts[0] = keyed - linked (block 0);
 // K = the keyed entries, lcnt[nb] (the last bucket's end).  With a keyless
-// sink (XSink) every block j also moves first-pass block j's valid keyless
-// rows (who = rank, own Objects) to who[K + (rows of blocks < j) ...], and
-// block 0 adds them to counts[0] / [2].
+// sink (XSink) block j also moves the 16 wave segments of first-pass block j
+// (valid keyless rows, who = rank: own Objects) to who[K + (rows of the
+// segments before) ...], one wave per segment, and block 0 adds them to
+// counts[0] / [2].
 __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict__ lcnt,
                                                       uint32_t nb, uint32_t* __restrict__ counts,
                                                       uint32_t* __restrict__ who, XSink xs) {
-  __shared__ uint32_t sw[16];
-  const uint32_t lane = __lane_id(), K = lcnt[nb];
-  uint32_t before = 0, E = 0;  // the sink's rows of blocks < j, all of them
-  if (xs.st && threadIdx.x < 64) {
-    for (uint32_t b = lane; b < kPartBlocks; b += 64) {
-      const uint32_t c = xs.cnt[b];
-      E += c;
-      if (b < blockIdx.x) before += c;
+  __shared__ uint32_t sw[16], sb[16], sseg[kSinkWaves];
+  const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6, K = lcnt[nb];
+  uint32_t E = 0, before = 0;  // the sink's rows: all, in the segments before this block's
+  if (xs.st) {
+    constexpr uint32_t nseg = kPartBlocks * kSinkWaves;
+    const uint32_t seg0 = blockIdx.x * kSinkWaves;
+    uint32_t e = 0, bf = 0;
+    for (uint32_t g = threadIdx.x; g < nseg; g += 1024) {
+      const uint32_t c = xs.cnt[g];
+      e += c;
+      if (g < seg0) bf += c;
+      if (g >= seg0 && g < seg0 + kSinkWaves) sseg[g - seg0] = c;
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) {
-      E += __shfl_xor(E, d);
-      before += __shfl_xor(before, d);
+      e += __shfl_xor(e, d);
+      bf += __shfl_xor(bf, d);
     }
+    if (lane == 0) {
+      sw[wv] = e;
+      sb[wv] = bf;
+    }
+    __syncthreads();
+    for (uint32_t w = 0; w < 16; ++w) {
+      E += sw[w];
+      before += sb[w];
+    }
+    __syncthreads();  // sw is reused below
   }
   if (blockIdx.x == 0) {
     uint32_t t = 0;
     for (uint32_t i = threadIdx.x; i < nb; i += 1024) t += lcnt[i];
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d);
-    if (lane == 0) sw[threadIdx.x >> 6] = t;
+    if (lane == 0) sw[wv] = t;
     __syncthreads();
     if (threadIdx.x == 0) {
       uint32_t l = 0;
@@ -1335,11 +1349,11 @@ __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict
     }
   }
   if (!xs.st) return;
-  if (threadIdx.x == 0) sw[0] = before;
-  __syncthreads();
-  const uint32_t c = xs.cnt[blockIdx.x], o = K + sw[0];
-  const uint32_t* src = xs.st + static_cast<uint64_t>(blockIdx.x) * xs.cap;
-  for (uint32_t k = threadIdx.x; k < c; k += 1024) who[o + k] = src[k];
+  uint32_t o = K + before;  // wave wv copies segment wv of this block
+  for (uint32_t w = 0; w < wv; ++w) o += sseg[w];
+  const uint32_t c = sseg[wv];
+  const uint32_t* src = xs.st + (static_cast<uint64_t>(blockIdx.x) * kSinkWaves + wv) * xs.cap;
+  for (uint32_t k = lane; k < c; k += 64) who[o + k] = src[k];
 }
 hipError_t out_finish(const RepOut&, uint32_t, hipStream_t) { return hipSuccess; }
 // ListOut: each wave's entries are placed by ONE LDS atomic per (step, list)
@@ -1975,6 +1989,14 @@ struct GroupLayout {
 };
 
 
+// Rows per XSink wave segment: at least the rows one wave of a first-pass
+// block reads -- a 16th of the block's tile plus one step of rows
+// (k_part_private: 256 per round; k_part_hist: 512 per step, +2 edge rows).
+uint32_t sink_cap(uint64_t n) {
+  const uint64_t tile = (n + kPartBlocks - 1) / kPartBlocks;
+  return static_cast<uint32_t>((tile + kSinkWaves - 1) / kSinkWaves + 520);
+}
+
 GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
   GroupLayout L;
   L.bits = bucket_bits_for(n);
@@ -2003,8 +2025,8 @@ GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
   L.run_l = o; o = align_up(o + 4 * nrun, 256);
   L.segtot = o; o = align_up(o + 4 * kRunMaxBins, 256);
   L.lcnt = o; o = align_up(o + 4 * (nf + 1), 256);  // ListOut: linked rows per bucket, keyed total
-  L.xst = o; o = align_up(o + 4 * (n + kMaxPartBlocks), 256);
-  L.xcnt = o; o = align_up(o + 4 * kMaxPartBlocks, 256);
+  L.xst = o; o = align_up(o + 4 * static_cast<uint64_t>(kPartBlocks) * kSinkWaves * sink_cap(n), 256);
+  L.xcnt = o; o = align_up(o + 4 * kPartBlocks * kSinkWaves, 256);
   L.total = o;
   return L;
 }
@@ -2323,7 +2345,7 @@ hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t
     out.x.valid = keyless_valid;
     out.x.st = reinterpret_cast<uint32_t*>(w + L.xst);
     out.x.cnt = reinterpret_cast<uint32_t*>(w + L.xcnt);
-    out.x.cap = static_cast<uint32_t>((in.n + bucket_part_blocks() - 1) / bucket_part_blocks());
+    out.x.cap = sink_cap(in.n);
   }
   if (in.rec12)
     return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
