@@ -426,7 +426,7 @@ int sdgpu_link_batch_device(sdgpu_ctx *ctx, const uint32_t *d_rep, const uint32_
  *                                    the row of rank d_obj[e]
  * Keyed rows come first, grouped by an internal hash bucket (creators before
  * linked rows inside a bucket); the valid keyless rows (own Objects,
- * mod.rs:238-239) follow in row order.  The ORDER of the entries is not
+ * mod.rs:238-239) follow them.  The ORDER of the entries is not
  * part of the contract (the reference's writes are a set; compare as sets).
  * d_counts[0] = creators, [1] = linked rows, [2] = entries (= [0] + [1]). */
 #define SDGPU_LINKED 0x80000000u

@@ -157,17 +157,20 @@ struct XSink {
 // Called by every lane of a wave that is still in the partition's row loop
 // (the lanes that left it never return to it, so the active lanes' `wn`
 // agree, and lane 0 -- the last to leave -- holds the wave's count);
-// `keyless`: row i is in range with has_key == 0.
+// `keyless`: row i is in range with has_key == 0.  kImplicit: in.rank is
+// null (rank = rank_base + row; no load).  Segment offsets fit 32 bits (n <
+// 2^31, 16 x 256 segments of a 16th of a tile + 520 rows).
+template <bool kImplicit = false>
 __device__ __forceinline__ void sink_keyless(const XSink& x, const RowsIn& in, bool keyless,
                                              uint64_t i, uint32_t& wn) {
   const bool e = keyless && (!x.valid || x.valid[i] != 0);
   const uint64_t b = __ballot(e);
   if (!b) return;
   if (e) {
-    const uint32_t lane = __lane_id();
-    const uint64_t seg = static_cast<uint64_t>(part_block()) * kSinkWaves + (threadIdx.x >> 6);
-    x.st[seg * x.cap + wn + __popcll(b & ((1ull << lane) - 1ull))] =
-        in.rank ? in.rank[i] : in.rank_base + static_cast<uint32_t>(i);
+    const uint32_t seg = part_block() * kSinkWaves + (threadIdx.x >> 6);
+    const uint32_t r = in.rank_base + static_cast<uint32_t>(i);
+    x.st[seg * x.cap + wn + __popcll(b & ((1ull << __lane_id()) - 1ull))] =
+        kImplicit ? r : (in.rank ? in.rank[i] : r);
   }
   wn += static_cast<uint32_t>(__popcll(b));
 }
@@ -554,8 +557,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
       if (__ballot(any)) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          sink_keyless(xs, in, q.in[u] && !in.valid_of(q, u),
-                       i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads, wn);
+          sink_keyless<kRec12>(xs, in, q.in[u] && !in.valid_of(q, u),
+                               i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads, wn);
       }
     }
     acc += total;
