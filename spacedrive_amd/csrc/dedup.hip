@@ -1310,56 +1310,58 @@ struct RepOut {
     (void)r;
   }
 };
-// counts[1] = the buckets' linked rows, counts[0] = keyed - linked (block 0);
-// K = the keyed entries, lcnt[nb] (the last bucket's end).  With a keyless
-// sink (XSink) block j also moves the 16 wave segments of first-pass block j
-// (valid keyless rows, who = rank: own Objects) to who[K + (rows of the
-// segments before) ...], one wave per segment, and block 0 adds them to
-// counts[0] / [2].
+// counts[] (zero on entry) from the buckets' linked counts lcnt[] and K =
+// the keyed entries, lcnt[nb] (the last bucket's end): counts[1] = L, [0] =
+// K - L + E, [2] = K + E.  Every block reduces a slice of lcnt and adds it
+// with one atomic per word (256 atomics: a one-block reduction of the 32 k
+// counts at 100 M rows took 5-10 us); with a keyless sink (XSink, E rows)
+// block j also moves the 16 wave segments of first-pass block j (valid
+// keyless rows, who = rank: own Objects) to who[K + (rows of the segments
+// before) ...], one wave per segment.
 __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict__ lcnt,
                                                       uint32_t nb, uint32_t* __restrict__ counts,
                                                       uint32_t* __restrict__ who, XSink xs) {
-  __shared__ uint32_t sw[16], sb[16], sseg[kSinkWaves];
+  __shared__ uint32_t sl[16], se[16], sb[16], sseg[kSinkWaves];
   const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6, K = lcnt[nb];
-  uint32_t E = 0, before = 0;  // the sink's rows: all, in the segments before this block's
+  const uint32_t per = (nb + gridDim.x - 1) / gridDim.x, b0 = min(nb, blockIdx.x * per),
+                 b1 = min(nb, b0 + per);
+  uint32_t l = 0, e = 0, bf = 0;  // linked rows of the slice; sink rows: all, before this block's
+  for (uint32_t i = b0 + threadIdx.x; i < b1; i += 1024) l += lcnt[i];
   if (xs.st) {
     constexpr uint32_t nseg = kPartBlocks * kSinkWaves;
     const uint32_t seg0 = blockIdx.x * kSinkWaves;
-    uint32_t e = 0, bf = 0;
     for (uint32_t g = threadIdx.x; g < nseg; g += 1024) {
       const uint32_t c = xs.cnt[g];
       e += c;
       if (g < seg0) bf += c;
       if (g >= seg0 && g < seg0 + kSinkWaves) sseg[g - seg0] = c;
     }
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-      e += __shfl_xor(e, d);
-      bf += __shfl_xor(bf, d);
-    }
-    if (lane == 0) {
-      sw[wv] = e;
-      sb[wv] = bf;
-    }
-    __syncthreads();
-    for (uint32_t w = 0; w < 16; ++w) {
-      E += sw[w];
-      before += sb[w];
-    }
-    __syncthreads();  // sw is reused below
   }
-  if (blockIdx.x == 0) {
-    uint32_t t = 0;
-    for (uint32_t i = threadIdx.x; i < nb; i += 1024) t += lcnt[i];
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d);
-    if (lane == 0) sw[wv] = t;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t l = 0;
-      for (int w = 0; w < 16; ++w) l += sw[w];
-      counts[1] = l;
-      counts[0] = K - l + E;
+  for (int d = 32; d > 0; d >>= 1) {
+    l += __shfl_xor(l, d);
+    e += __shfl_xor(e, d);
+    bf += __shfl_xor(bf, d);
+  }
+  if (lane == 0) {
+    sl[wv] = l;
+    se[wv] = e;
+    sb[wv] = bf;
+  }
+  __syncthreads();
+  uint32_t L = 0, E = 0, before = 0;
+  for (uint32_t w = 0; w < 16; ++w) {
+    L += sl[w];
+    E += se[w];
+    before += sb[w];
+  }
+  if (threadIdx.x == 0) {
+    if (L) {
+      atomicAdd(&counts[1], L);
+      atomicSub(&counts[0], L);
+    }
+    if (blockIdx.x == 0) {
+      atomicAdd(&counts[0], K + E);
       counts[2] = K + E;
     }
   }
@@ -1429,7 +1431,8 @@ __device__ __forceinline__ void out_done(const ListOut& o, uint32_t, uint32_t, u
 __device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t,
                                          const uint32_t*) {}
 hipError_t out_finish(const ListOut& o, uint32_t nb, hipStream_t s) {
-  k_list_finish<<<o.x.st ? kPartBlocks : 1u, 1024, 0, s>>>(o.lcnt, nb, o.counts, o.who, o.x);
+  const uint32_t g = o.x.st ? kPartBlocks : std::max(1u, std::min(kPartBlocks, (nb + 255) / 256));
+  k_list_finish<<<g, 1024, 0, s>>>(o.lcnt, nb, o.counts, o.who, o.x);
   return hipGetLastError();
 }
 
