@@ -1327,14 +1327,19 @@ __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict
                  b1 = min(nb, b0 + per);
   uint32_t l = 0, e = 0, bf = 0;  // linked rows of the slice; sink rows: all, before this block's
   for (uint32_t i = b0 + threadIdx.x; i < b1; i += 1024) l += lcnt[i];
-  if (xs.st) {
-    constexpr uint32_t nseg = kPartBlocks * kSinkWaves;
+  if (xs.st) {  // the segment counts loaded together (one memory latency)
+    constexpr uint32_t kPerT = kPartBlocks * kSinkWaves / 1024;
+    static_assert(kPartBlocks * kSinkWaves % 1024 == 0, "segments per thread");
     const uint32_t seg0 = blockIdx.x * kSinkWaves;
-    for (uint32_t g = threadIdx.x; g < nseg; g += 1024) {
-      const uint32_t c = xs.cnt[g];
-      e += c;
-      if (g < seg0) bf += c;
-      if (g >= seg0 && g < seg0 + kSinkWaves) sseg[g - seg0] = c;
+    uint32_t cv[kPerT];
+#pragma unroll
+    for (uint32_t k = 0; k < kPerT; ++k) cv[k] = xs.cnt[threadIdx.x + k * 1024];
+#pragma unroll
+    for (uint32_t k = 0; k < kPerT; ++k) {
+      const uint32_t g = threadIdx.x + k * 1024;
+      e += cv[k];
+      if (g < seg0) bf += cv[k];
+      if (g - seg0 < kSinkWaves) sseg[g - seg0] = cv[k];
     }
   }
 #pragma unroll
