@@ -1310,27 +1310,34 @@ struct RepOut {
     (void)r;
   }
 };
-// counts[] (zero on entry) from the buckets' linked counts lcnt[] and K =
-// the keyed entries, lcnt[nb] (the last bucket's end): counts[1] = L, [0] =
-// K - L + E, [2] = K + E.  Every block reduces a slice of lcnt and adds it
-// with one atomic per word (256 atomics: a one-block reduction of the 32 k
-// counts at 100 M rows took 5-10 us); with a keyless sink (XSink, E rows)
-// block j also moves the 16 wave segments of first-pass block j (valid
-// keyless rows, who = rank: own Objects) to who[K + (rows of the segments
-// before) ...], one wave per segment.
+// Block 0 sets counts[] from the buckets' linked counts lcnt[] and K = the
+// keyed entries, lcnt[nb] (the last bucket's end): counts[1] = L, [0] = K - L
+// + E, [2] = K + E -- loads issued 8 at a time (a plain loop over the 32 k
+// counts of 100 M rows took ~10 us).  With a keyless sink (XSink, E rows)
+// block 1 + j moves the 16 wave segments of first-pass block j (valid keyless
+// rows, who = rank: own Objects) to who[K + (rows of the segments before)
+// ...], one wave per segment.  (Every block reducing a slice and adding it
+// with atomics took 9 us: 512 same-address atomics, r4zd.)
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* sw) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+  if (__lane_id() == 0) sw[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (uint32_t w = 0; w < blockDim.x / 64; ++w) t += sw[w];
+  __syncthreads();  // sw reusable
+  return t;
+}
 __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict__ lcnt,
                                                       uint32_t nb, uint32_t* __restrict__ counts,
                                                       uint32_t* __restrict__ who, XSink xs) {
-  __shared__ uint32_t sl[16], se[16], sb[16], sseg[kSinkWaves];
-  const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6, K = lcnt[nb];
-  const uint32_t per = (nb + gridDim.x - 1) / gridDim.x, b0 = min(nb, blockIdx.x * per),
-                 b1 = min(nb, b0 + per);
-  uint32_t l = 0, e = 0, bf = 0;  // linked rows of the slice; sink rows: all, before this block's
-  for (uint32_t i = b0 + threadIdx.x; i < b1; i += 1024) l += lcnt[i];
-  if (xs.st) {  // the segment counts loaded together (one memory latency)
-    constexpr uint32_t kPerT = kPartBlocks * kSinkWaves / 1024;
-    static_assert(kPartBlocks * kSinkWaves % 1024 == 0, "segments per thread");
-    const uint32_t seg0 = blockIdx.x * kSinkWaves;
+  __shared__ uint32_t sw[16], sseg[kSinkWaves];
+  constexpr uint32_t kPerT = kPartBlocks * kSinkWaves / 1024;
+  static_assert(kPartBlocks * kSinkWaves % 1024 == 0, "segments per thread");
+  const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
+  const uint32_t seg0 = blockIdx.x ? (blockIdx.x - 1) * kSinkWaves : 0u;
+  uint32_t e = 0, bf = 0;  // sink rows: all, in the segments before this block's
+  if (xs.st) {             // the segment counts loaded together (one latency)
     uint32_t cv[kPerT];
 #pragma unroll
     for (uint32_t k = 0; k < kPerT; ++k) cv[k] = xs.cnt[threadIdx.x + k * 1024];
@@ -1339,42 +1346,36 @@ __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict
       const uint32_t g = threadIdx.x + k * 1024;
       e += cv[k];
       if (g < seg0) bf += cv[k];
-      if (g - seg0 < kSinkWaves) sseg[g - seg0] = cv[k];
+      if (blockIdx.x && g - seg0 < kSinkWaves) sseg[g - seg0] = cv[k];
     }
   }
+  if (blockIdx.x == 0) {
+    const uint32_t K = lcnt[nb];
+    uint32_t l = 0;
+    constexpr uint32_t kB = 8;
+    for (uint32_t i0 = 0; i0 < nb; i0 += kB * 1024) {
+      uint32_t v[kB];
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) {
-    l += __shfl_xor(l, d);
-    e += __shfl_xor(e, d);
-    bf += __shfl_xor(bf, d);
-  }
-  if (lane == 0) {
-    sl[wv] = l;
-    se[wv] = e;
-    sb[wv] = bf;
-  }
-  __syncthreads();
-  uint32_t L = 0, E = 0, before = 0;
-  for (uint32_t w = 0; w < 16; ++w) {
-    L += sl[w];
-    E += se[w];
-    before += sb[w];
-  }
-  if (threadIdx.x == 0) {
-    if (L) {
-      atomicAdd(&counts[1], L);
-      atomicSub(&counts[0], L);
+      for (uint32_t k = 0; k < kB; ++k) {
+        const uint32_t i = i0 + threadIdx.x + k * 1024;
+        v[k] = i < nb ? lcnt[i] : 0u;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kB; ++k) l += v[k];
     }
-    if (blockIdx.x == 0) {
-      atomicAdd(&counts[0], K + E);
+    const uint32_t L = block_sum(l, sw), E = block_sum(e, sw);
+    if (threadIdx.x == 0) {
+      counts[1] = L;
+      counts[0] = K - L + E;
       counts[2] = K + E;
     }
+    return;
   }
-  if (!xs.st) return;
-  uint32_t o = K + before;  // wave wv copies segment wv of this block
+  const uint32_t before = block_sum(bf, sw);
+  uint32_t o = lcnt[nb] + before;  // wave wv copies segment wv of first-pass block j
   for (uint32_t w = 0; w < wv; ++w) o += sseg[w];
   const uint32_t c = sseg[wv];
-  const uint32_t* src = xs.st + (static_cast<uint64_t>(blockIdx.x) * kSinkWaves + wv) * xs.cap;
+  const uint32_t* src = xs.st + static_cast<uint64_t>(seg0 + wv) * xs.cap;
   for (uint32_t k = lane; k < c; k += 64) who[o + k] = src[k];
 }
 hipError_t out_finish(const RepOut&, uint32_t, hipStream_t) { return hipSuccess; }
@@ -1436,8 +1437,7 @@ __device__ __forceinline__ void out_done(const ListOut& o, uint32_t, uint32_t, u
 __device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t,
                                          const uint32_t*) {}
 hipError_t out_finish(const ListOut& o, uint32_t nb, hipStream_t s) {
-  const uint32_t g = o.x.st ? kPartBlocks : std::max(1u, std::min(kPartBlocks, (nb + 255) / 256));
-  k_list_finish<<<g, 1024, 0, s>>>(o.lcnt, nb, o.counts, o.who, o.x);
+  k_list_finish<<<o.x.st ? 1 + kPartBlocks : 1u, 1024, 0, s>>>(o.lcnt, nb, o.counts, o.who, o.x);
   return hipGetLastError();
 }
 
