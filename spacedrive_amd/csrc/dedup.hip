@@ -217,7 +217,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
       }
       const uint4* __restrict__ k4 = reinterpret_cast<const uint4*>(in.key);
       const uint16_t* __restrict__ v2 = reinterpret_cast<const uint16_t*>(in.valid);
-      constexpr int kP = kUnroll;  // row pairs per thread per step
+      constexpr int kP = kUnroll / 2;
       for (uint64_t q0 = p0 + threadIdx.x; q0 < p1; q0 += kP * kPartThreads) {
         uint4 kk[kP];
         uint32_t vv[kP];
@@ -2014,11 +2014,10 @@ struct GroupLayout {
 
 // Rows per XSink wave segment: at least the rows one wave of a first-pass
 // block reads -- a 16th of the block's tile plus one step of rows
-// (k_part_private: 256 per round; k_part_hist: 1024 per paired step, 512 per
-// row step, +2 edge rows).
+// (k_part_private: 256 per round; k_part_hist: 512 per step, +2 edge rows).
 uint32_t sink_cap(uint64_t n) {
   const uint64_t tile = (n + kPartBlocks - 1) / kPartBlocks;
-  return static_cast<uint32_t>((tile + kSinkWaves - 1) / kSinkWaves + 1040);
+  return static_cast<uint32_t>((tile + kSinkWaves - 1) / kSinkWaves + 520);
 }
 
 GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
