@@ -234,19 +234,19 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
           count((static_cast<uint64_t>(kk[u].y) << 32) | kk[u].x, (vv[u] & 0xFFu) != 0);
           count((static_cast<uint64_t>(kk[u].w) << 32) | kk[u].z, (vv[u] >> 8) != 0);
         }
-        if constexpr (kX) {  // one wave-uniform test per step: keyless rows are rare
-          bool any = false;
+        if constexpr (kX) {  // keyless rows are rare: bit 2 u + h = row 2 q_u + h
+          uint32_t km = 0;
 #pragma unroll
           for (int u = 0; u < kP; ++u)
-            any |= q0 + static_cast<uint64_t>(u) * kPartThreads < p1 &&
-                   ((vv[u] & 0xFFu) == 0 || (vv[u] & 0xFF00u) == 0);
-          if (__ballot(any)) {
-#pragma unroll
-            for (int u = 0; u < kP; ++u) {
-              const uint64_t q = q0 + static_cast<uint64_t>(u) * kPartThreads;
-              sink_keyless(xs, in, q < p1 && (vv[u] & 0xFFu) == 0, 2 * q, wn);
-              sink_keyless(xs, in, q < p1 && (vv[u] >> 8) == 0, 2 * q + 1, wn);
-            }
+            if (q0 + static_cast<uint64_t>(u) * kPartThreads < p1)
+              km |= (static_cast<uint32_t>((vv[u] & 0xFFu) == 0) |
+                     (static_cast<uint32_t>((vv[u] & 0xFF00u) == 0) << 1)) << (2 * u);
+          // one pass per bit position some lane has (usually none, else one)
+          for (uint64_t b = __ballot(km != 0); b; b = __ballot(km != 0)) {
+            const uint32_t p = __ffs(__shfl(km, __ffsll(static_cast<unsigned long long>(b)) - 1)) - 1;
+            const uint64_t q = q0 + static_cast<uint64_t>(p >> 1) * kPartThreads;
+            sink_keyless(xs, in, (km >> p) & 1u, 2 * q + (p & 1u), wn);
+            km &= ~(1u << p);
           }
         }
       }
