@@ -19,10 +19,11 @@ def get_shard_hex(cas_id: str) -> str:
     return cas_id[0:2]
 
 
-def orphan_objects(object_ids, fp_object_ids, max_object_id: int, ctx=None):
+def orphan_objects(object_ids, fp_object_ids, max_object_id: int, ctx=None, trim: bool = True):
     """int32 device tensor of the Object ids (from `object_ids`) that no
     file_path's object_id (`fp_object_ids`, negative = NULL) references, in
-    list order."""
+    list order.  trim=False: the full-length list and the device count [1],
+    no synchronisation."""
     import torch
     dev = object_ids.device
     ctx = ctx or default_context(dev.index)
@@ -33,12 +34,16 @@ def orphan_objects(object_ids, fp_object_ids, max_object_id: int, ctx=None):
         ctx.h, object_ids.data_ptr(), object_ids.numel(), fp_object_ids.data_ptr(),
         fp_object_ids.numel(), max_object_id, out.data_ptr(), cnt.data_ptr(), s),
         "sdgpu_orphan_objects_device")
+    if not trim:
+        return out, cnt
     return out[:int(cnt.item())]
 
 
-def thumbnail_shards(cas8, valid=None, ctx=None):
+def thumbnail_shards(cas8, valid=None, ctx=None, trim: bool = True):
     """(order, counts): rows with a cas_id ordered by thumbnail directory
-    (stable inside a directory), and rows per directory (256)."""
+    (stable inside a directory), and rows per directory (256).  trim=False:
+    the full-length order (its first sum(counts) entries), no
+    synchronisation."""
     import torch
     dev = cas8.device
     ctx = ctx or default_context(dev.index)
@@ -49,5 +54,7 @@ def thumbnail_shards(cas8, valid=None, ctx=None):
     check(ctx.lib.sdgpu_thumbnail_shards_device(
         ctx.h, cas8.data_ptr(), valid.data_ptr() if valid is not None else None, n,
         order.data_ptr(), counts.data_ptr(), s), "sdgpu_thumbnail_shards_device")
+    if not trim:
+        return order, counts
     total = int(counts.sum().item())
     return order[:total], counts

@@ -21,6 +21,9 @@ def test_orphan_objects(ctx, n_obj, n_fp):
     got = consumers.orphan_objects(torch.from_numpy(objs).cuda(), torch.from_numpy(fp).cuda(),
                                    maxid, ctx)
     np.testing.assert_array_equal(got.cpu().numpy(), O.orphan_objects(objs, fp))
+    out, cnt = consumers.orphan_objects(torch.from_numpy(objs).cuda(),
+                                        torch.from_numpy(fp).cuda(), maxid, ctx, trim=False)
+    np.testing.assert_array_equal(out[:int(cnt.item())].cpu().numpy(), O.orphan_objects(objs, fp))
 
 
 def test_orphans_after_an_identifier_run(ctx):
@@ -51,5 +54,9 @@ def test_thumbnail_shards(ctx, n):
     eo, ec = O.thumbnail_shards(cas8, valid)
     np.testing.assert_array_equal(counts.cpu().numpy(), ec)
     np.testing.assert_array_equal(order.cpu().numpy(), eo)
+    o2, c2 = consumers.thumbnail_shards(torch.from_numpy(cas8).cuda(),
+                                        torch.from_numpy(valid).cuda(), ctx, trim=False)
+    np.testing.assert_array_equal(c2.cpu().numpy(), ec)
+    np.testing.assert_array_equal(o2[:int(ec.sum())].cpu().numpy(), eo)
     if n:
         assert consumers.get_shard_hex(bytes(cas8[0]).hex()) == f"{cas8[0, 0]:02x}"
