@@ -242,11 +242,13 @@ class Runner:
             return "none (one GPU: local grouping)"
         return f"torch.distributed {self.backend} all-to-all over libsdgpu steps (rehearsal)"
 
-    def group(self, key, has, rank, timings=None):
-        """The cas_id -> Object grouping of this rank's rows against all ranks."""
+    def group(self, key, has, rank, timings=None, wait=True):
+        """The cas_id -> Object grouping of this rank's rows against all ranks.
+        wait=False (timed loops): a padded exchange call is resolved by the
+        next call or the barrier's Comm.wait(), not here."""
         from spacedrive_amd import dedup
         if self.comm is not None:
-            return dedup.group_sharded(key, has, rank, self.comm, None, 100)
+            return dedup.group_sharded(key, has, rank, self.comm, None, 100, wait=wait)
         if self.world == 1:
             return self.ops.group_rows(key, has, rank, 100, 0)
         return dedup.sharded_group_reps(key, has, rank, 100, ops=self.ops, timings=timings)
@@ -462,6 +464,8 @@ class Runner:
                                                         ctx=self.ctx, trim=False, index=index)
                 return ("lists", who, obj, cnt)
             if self.comm is not None:
+                # resolved before the link batch reads rep (a padded call that
+                # overflowed is re-run counted first)
                 rep = dedup.group_sharded(key, has, ranks[s], self.comm, index, 100)
             else:  # gloo rehearsal: the exchange has no index
                 rep = self.group(key, has, ranks[s])
@@ -692,11 +696,12 @@ class Runner:
                                                           device=rank.device)).all())
         grank = None if implicit else rank
         self.group(key, has, grank)  # first launches (lazy code-object loads) untimed
-        t, kt = self.timed_kernels(lambda: self.group(key, has, grank), steps, warmup)
+        t, kt = self.timed_kernels(lambda: self.group(key, has, grank, wait=False), steps, warmup)
         explicit_ms = None
         if implicit and not self.args.no_explicit_rank:
             self.group(key, has, rank)
-            explicit_ms = 1e3 * self.timed(lambda: self.group(key, has, rank), steps, warmup) / steps
+            explicit_ms = 1e3 * self.timed(lambda: self.group(key, has, rank, wait=False), steps,
+                                           warmup) / steps
         xchg = None
         if self.world > 1:
             # payload of one step on this rank: (key, rank) 12-B records out to
@@ -818,90 +823,122 @@ class Runner:
     # ASSUMPTION of the model below, not a measurement (no 8-GPU node here)
     XGMI_LINK_GBPS = 100.0
 
+    @staticmethod
+    def padded_slots(rows: int, n_ranks: int) -> int:
+        """Slots (header included) of one padded exchange message at n_ranks
+        ranks of `rows` rows each (csrc/shard.cpp padded_slots)."""
+        c = rows if n_ranks == 1 else min(rows, rows // n_ranks + rows // (128 * n_ranks) + 4096)
+        return -(-(c + 1) // 64) * 64
+
     def exchange_model(self, key, has, rank, steps, warmup, local_ms):
         """Predicted per-GPU config-4 step at N = 2 / 4 / 8 (DESIGN.md §6;
-        VERDICT r3 item 4).  The whole exchange path runs on this GPU through
-        a ONE-rank RCCL communicator -- partition by owner, count exchange +
-        host synchronisation, the records' all-to-all (a self send), the local
-        grouping of as many received rows as one GPU gets at any N (weak
-        scaling: every GPU sends its rows and receives ~as many), the compact
-        return (second count exchange + pairs) and the gather -- timed with
-        its kernels; only the xGMI time of the remote share is modelled:
-        every GPU sends rows/N of its rows to each peer over that peer's own
-        link (fully connected node), 12 B per record plus 8 B per returned
-        pair in the same direction."""
+        VERDICT r3 item 4, r4 item 1).  The whole exchange path runs on this
+        GPU through a ONE-rank RCCL communicator -- partition by owner, the
+        records' all-to-all (a self send), the local grouping of as many
+        received rows as one GPU gets at any N (weak scaling: every GPU sends
+        its rows and receives ~as many), the return leg and the gather --
+        timed with its kernels; only the xGMI time of the remote share is
+        modelled: every GPU sends one message per peer over that peer's own
+        link (fully connected node).  Since round 5 the default exchange is
+        PADDED (fixed-capacity messages, no host synchronisation; sdgpu.h):
+        its messages carry the padded slot count, 12 B each (+ 4 B back for
+        the rep form).  The counted forms (count exchange + host sync; the
+        compact return) are rehearsed beside it for the A/B."""
         from spacedrive_amd import dedup
         per = int(key.numel())
         comm = dedup.Comm.init_rank(self.ctx, 1, 0, dedup.Comm.unique_id(),
                                     timeout_ms=self.comm_timeout_ms)
-        try:
-            comm.set_return(dedup.RETURN_COMPACT)
-            fn = lambda: dedup.group_sharded(key, has, rank, comm, None, 100)  # noqa: E731
+        stats = {}
+
+        def rehearse(name, fn, kernels=False):
             fn()
             comm.wait()
             s0 = comm.stats()
-            t, kt = self.timed_kernels(fn, steps, warmup)
+            if kernels:
+                t_, kt_ = self.timed_kernels(fn, steps, warmup)
+            else:
+                t_, kt_ = self.timed(fn, steps, warmup), None
             comm.wait()
             s1 = comm.stats()
             calls = max(1, s1["calls"] - s0["calls"])
-            linked_frac = (s1["rows_returned"] - s0["rows_returned"]) / max(
-                1, s1["rows_received"] - s0["rows_received"])
+            stats[name] = {
+                "ms_per_step": 1e3 * t_ / steps,
+                "count_wait_ms_per_call": (s1["count_wait_ms"] - s0["count_wait_ms"]) / calls,
+                "host_ms_per_call": (s1["host_ms"] - s0["host_ms"]) / calls,
+                "padded_calls": s1["padded_calls"] - s0["padded_calls"],
+                "overflow_reruns": s1["overflow_reruns"] - s0["overflow_reruns"],
+                "resolve_wait_ms_per_call": (s1["resolve_wait_ms"] - s0["resolve_wait_ms"]) / calls,
+                "bytes_sent_per_row": (s1["bytes_sent"] - s0["bytes_sent"]) / max(
+                    1, s1["rows_sent"] - s0["rows_sent"]),
+                "rows_returned": s1["rows_returned"] - s0["rows_returned"],
+                "rows_received": s1["rows_received"] - s0["rows_received"]}
+            if kt_ is not None:
+                stats[name]["kernels"] = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
+                                          for k, v in kt_.items()}
+            return 1e3 * t_ / steps
+
+        try:
+            # the rep form, counted with the compact return (explicit setting)
+            comm.set_return(dedup.RETURN_COMPACT)
+            rep_compact = rehearse("rep_counted_compact", lambda: dedup.group_sharded(
+                key, has, rank, comm, None, 100, wait=False))
+            st = stats["rep_counted_compact"]
+            linked_frac = st["rows_returned"] / max(1, st["rows_received"])
+            # the rep form, full return: padded (the default) and counted
+            comm.set_return(dedup.RETURN_AUTO)
+            rep_padded = rehearse("rep_padded", lambda: dedup.group_sharded(
+                key, has, rank, comm, None, 100, wait=False), kernels=True)
+            comm.set_exchange(dedup.EXCHANGE_COUNTED)
             comm.set_return(dedup.RETURN_FULL)
-            fn()
-            comm.wait()
-            t_full = self.timed(fn, steps, warmup)
-            comm.wait()
-            # the write-set form (sdgpu_group_link_sharded_device): no return leg
+            rep_counted = rehearse("rep_counted_full", lambda: dedup.group_sharded(
+                key, has, rank, comm, None, 100, wait=False))
+            comm.set_return(dedup.RETURN_AUTO)
+            # the write-set form (sdgpu_group_link_sharded_device): counted, then
+            # padded (the N > 1 identifier step's path)
             fl = lambda: dedup.group_link_sharded(key, has, None, rank, comm, 100,  # noqa: E731
                                                   trim=False)
-            fl()
-            comm.wait()
-            t_lists = self.timed(fl, steps, warmup)
-            comm.wait()
+            ws_counted = rehearse("write_set_counted", fl)
+            comm.set_exchange(dedup.EXCHANGE_AUTO)
+            ws_padded = rehearse("write_set_padded", fl, kernels=True)
         finally:
             comm.close()
-        reh = 1e3 * t / steps
-        reh_full = 1e3 * t_full / steps
-        pred = {}
+        pred, pred_lists = {}, {}
         for n_ in (2, 4, 8):
-            # the library's default (SDGPU_RETURN_AUTO): compact iff rows / N >= 4 Mi
-            compact = per // n_ >= (4 << 20)
-            ret_b = 8 * linked_frac if compact else 4.0
-            link_b = per / n_ * (12 + ret_b)  # bytes per link direction
+            c1 = self.padded_slots(per, n_)
+            link_b = c1 * 16  # 12-B records out, 4-B reps back, per link direction
             x_ms = link_b / (self.XGMI_LINK_GBPS * 1e9) * 1e3
-            step = (reh if compact else reh_full) + x_ms
-            pred[str(n_)] = {"return_leg": "compact" if compact else "full",
+            step = rep_padded + x_ms
+            pred[str(n_)] = {"exchange": "padded, full return", "slots_per_message": c1,
                              "step_ms": step, "xgmi_ms": x_ms, "bytes_per_link": int(link_b),
                              "rows_per_s_total": n_ * per / (step * 1e-3),
                              "weak_scaling_efficiency": local_ms / step}
-        reh_lists = 1e3 * t_lists / steps
-        pred_lists = {}
-        for n_ in (2, 4, 8):
-            link_b = per / n_ * 12
+            link_b = c1 * 12
             x_ms = link_b / (self.XGMI_LINK_GBPS * 1e9) * 1e3
-            step = reh_lists + x_ms
-            pred_lists[str(n_)] = {"step_ms": step, "xgmi_ms": x_ms, "bytes_per_link": int(link_b),
+            step = ws_padded + x_ms
+            pred_lists[str(n_)] = {"slots_per_message": c1, "step_ms": step, "xgmi_ms": x_ms,
+                                   "bytes_per_link": int(link_b),
                                    "rows_per_s_total": n_ * per / (step * 1e-3)}
-        return {"rehearsal_ms_per_step": reh, "rehearsal_full_return_ms_per_step": reh_full,
-                "rehearsal_write_set_ms_per_step": reh_lists,
+        return {"rehearsal_ms_per_step": rep_padded,
+                "rehearsal_full_return_counted_ms_per_step": rep_counted,
+                "rehearsal_compact_counted_ms_per_step": rep_compact,
+                "rehearsal_write_set_ms_per_step": ws_padded,
+                "rehearsal_write_set_counted_ms_per_step": ws_counted,
                 "per_n_write_set": pred_lists,
                 "write_set_note": "grouping + Object write set with no return leg "
                                   "(sdgpu_group_link_sharded_device, the N > 1 identifier "
-                                  "step's path): 12 B per row on the wire; against "
-                                  "fused_job.ms_per_step at N = 1",
-                "count_wait_ms_per_call": (s1["count_wait_ms"] - s0["count_wait_ms"]) / calls,
-                "host_ms_per_call": (s1["host_ms"] - s0["host_ms"]) / calls,
-                "bytes_sent_per_row": (s1["bytes_sent"] - s0["bytes_sent"]) / max(
-                    1, s1["rows_sent"] - s0["rows_sent"]),
+                                  "step's path), padded exchange: 12 B per slot on the wire; "
+                                  "against fused_job.ms_per_step at N = 1",
+                "count_wait_ms_per_call": stats["write_set_padded"]["count_wait_ms_per_call"],
+                "host_ms_per_call": stats["write_set_padded"]["host_ms_per_call"],
                 "linked_fraction": linked_frac, "local_only_ms_per_step": local_ms,
                 "xgmi_link_GBps_assumed": self.XGMI_LINK_GBPS, "per_n": pred,
-                "kernels": {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]}
-                            for k, v in kt.items()},
+                "legs": stats,
                 "note": "PREDICTION (unmeasured on hardware at N > 1): the exchange path "
-                        "rehearsed on one GPU (one-rank RCCL: partition, count exchange + "
-                        "sync, records, local grouping of the received rows, the return "
-                        "leg SDGPU_RETURN_AUTO picks at that N, gather) + the modelled "
-                        "xGMI time of rows/N per link"}
+                        "rehearsed on one GPU (one-rank RCCL: partition, padded records (no "
+                        "host synchronisation), local grouping of the received rows, full "
+                        "return, gather) + the modelled xGMI time of one padded message per "
+                        "link; at one rank a message has no slack slots, at N ranks "
+                        "slots_per_message ~1.6 % over rows/N (the model's bytes)"}
 
     def staged_oracle(self):
         """Config 5's parity at full size: the reps of the batched 50 M-file run

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SDGPU_ABI_VERSION 4
+#define SDGPU_ABI_VERSION 5
 
 /* cas.rs:10-15 */
 #define SDGPU_CAS_SAMPLE_COUNT 4u
@@ -258,7 +258,12 @@ int sdgpu_dedup_batch(sdgpu_ctx *ctx, sdgpu_index *idx, const uint64_t *key,
  * shards s with s * world / 256 == d); each GPU sends its keyed rows to their
  * owners as packed 12-byte {key, rank} records, the owners group their rows
  * (and probe their share of the Object index), and the reps return (4 B per
- * row).  One host synchronisation per call (the count exchange).
+ * row).  Two exchanges (sdgpu_comm_set_exchange): COUNTED -- a count
+ * all-to-all sizes the messages, one host synchronisation per call; PADDED
+ * (ABI 5, the default once a communicator has run one call) -- every
+ * (source, owner) message has a fixed capacity agreed by all ranks, its
+ * real count travels in its first slot and is read on the device, and the
+ * call enqueues everything without waiting for the host.
  * Transports: SDGPU_TRANSPORT_RCCL (grouped ncclSend/ncclRecv; one rank per
  * GPU), SDGPU_TRANSPORT_PEER (device-to-device copies between contexts of one
  * process; also contexts sharing a GPU), AUTO = RCCL unless devices repeat. */
@@ -292,20 +297,54 @@ int sdgpu_comm_info(sdgpu_comm *comm, int *nranks, int *rank, int *transport);
 int sdgpu_comm_set_timeout(sdgpu_comm *comm, int timeout_ms);
 /* Waits, bounded by the timeout, until `stream` (NULL: the stream of the
  * communicator's last exchange) has drained -- i.e. the reps of the last
- * sdgpu_group_sharded_device are written.  -ETIMEDOUT (communicator aborted)
- * if a peer never completes its side. */
+ * sdgpu_group_sharded_device are written -- and resolves a padded exchange
+ * (below): if any message of it overflowed, the call is re-run through the
+ * counted exchange before this returns.  Returns that call's result (e.g.
+ * -ENOSPC of a write set that did not fit).  -ETIMEDOUT (communicator
+ * aborted) if a peer never completes its side. */
 int sdgpu_comm_wait(sdgpu_comm *comm, void *stream);
+/* Exchange of the one-process-per-GPU calls (sdgpu_group_sharded_device,
+ * sdgpu_group_link_sharded_device; ABI 5):
+ *   COUNTED: counts first, then the records; one host synchronisation per
+ *     call, the results final when the stream reaches them.
+ *   PADDED: no host synchronisation.  The message from each source to each
+ *     owner holds C = min(B, B / nranks + B / (128 nranks) + 4096) records
+ *     (a little over its expected share; B = the largest n of the ranks'
+ *     previous call, which every rank learns from the headers, or rows_hint)
+ *     plus a header slot; the owners drop the padding on the device.  A
+ *     message that needed more than C records (a cas_id held by many rows,
+ *     a rank with more rows than B) sets an overflow bit every rank sees.
+ *     The call is RESOLVED at the next exchange call on the communicator,
+ *     sdgpu_comm_wait or destroy: overflowed calls are then re-run through
+ *     the counted exchange on the same stream, on every rank alike.  Until
+ *     it is resolved, the call's inputs must not change and its outputs are
+ *     not final (read them after sdgpu_comm_wait).  The rep form with an
+ *     explicit SDGPU_RETURN_COMPACT stays counted.
+ *   AUTO (default): PADDED once B is known (after the first call), else
+ *     COUNTED.
+ * Every rank of a communicator must set the same mode (and rows_hint, which
+ * sets B when > 0).  The _all entry points (one process, all ranks) resolve
+ * a padded call before they return. */
+#define SDGPU_EXCHANGE_AUTO 0
+#define SDGPU_EXCHANGE_COUNTED 1
+#define SDGPU_EXCHANGE_PADDED 2
+int sdgpu_comm_set_exchange(sdgpu_comm *comm, int mode, uint64_t rows_hint);
 /* Cumulative exchange volume of this rank (bytes = 12-B records + 4-B reps). */
 typedef struct sdgpu_comm_stats_t {
   uint64_t calls;
   uint64_t rows_sent, rows_received;      /* keyed rows to / from every rank incl. self */
   uint64_t bytes_sent, bytes_received;    /* payload incl. the self share: 12-B records,
                                              plus the reps this rank returned as an owner
-                                             (sent) / got back as a source (received) */
+                                             (sent) / got back as a source (received);
+                                             padded calls: the whole fixed-size messages */
   uint64_t bytes_remote;                  /* payload that crossed to / from other ranks */
-  double count_wait_ms;                   /* host ms until the counts were known */
+  double count_wait_ms;                   /* host ms until the counts were known (0 for
+                                             padded calls) */
   double host_ms;                         /* host ms inside the exchange calls */
   uint64_t rows_returned;                 /* (ABI 4) received rows whose rep went back */
+  uint64_t padded_calls;                  /* (ABI 5) calls through the padded exchange */
+  uint64_t overflow_reruns;               /* (ABI 5) padded calls re-run counted */
+  double resolve_wait_ms;                 /* (ABI 5) host ms waiting to resolve them */
 } sdgpu_comm_stats_t;
 /* Return leg of the exchange (ABI 4).  COMPACT: an owner sends back only the
  * received rows whose rep is not their own rank, as 8-B {index, rep} pairs
@@ -343,9 +382,12 @@ int sdgpu_group_sharded_all_device(sdgpu_ctx *const *ctx, sdgpu_comm *const *com
  * its own valid keyless rows.  The union over the ranks is the write set of
  * all rows (a set, mod.rs:189-333), so only the 12-B records cross xGMI.
  * Global ranks in d_rank (required, < 2^31).  d_who / d_obj hold cap
- * entries: -ENOSPC (after the exchange, before any list is written; the
- * peers are unaffected) when this rank's owned rows + own keyless rows
- * exceed cap -- up to nranks x n when every row shares one cas_id.
+ * entries: -ENOSPC (the peers are unaffected; the lists are not valid) when
+ * this rank's owned keyed rows + own keyless rows exceed cap -- up to
+ * nranks x n when every row shares one cas_id.  The counted exchange
+ * returns it from the call, before any list is written; the padded one
+ * finds it on the device (no entry is written past cap) and returns it when
+ * the call is resolved (sdgpu_comm_wait).
  * d_counts (device) = [creators, linked, entries].  No Object index (use
  * sdgpu_group_sharded_device with one). */
 int sdgpu_group_link_sharded_device(sdgpu_ctx *ctx, sdgpu_comm *comm, const uint64_t *d_key,

@@ -81,6 +81,7 @@ def _proto(L):
         "sdgpu_dedup_batch": (i32, [ctx, c_vp, c_vp, c_vp, u32, u32, u32, c_vp]),
         "sdgpu_comm_unique_id": (i32, [c_vp]),
         "sdgpu_comm_set_return": (i32, [c_vp, i32]),
+        "sdgpu_comm_set_exchange": (i32, [c_vp, i32, u64]),
         "sdgpu_comm_init_rank": (i32, [ctx, i32, i32, c_vp, P(c_vp)]),
         "sdgpu_comm_init_all": (i32, [c_vp, i32, i32, c_vp]),
         "sdgpu_comm_destroy": (i32, [c_vp]),

@@ -290,6 +290,8 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
 //           reps come back through a gather (k_gather_rep);
 //   else:   separate key / rank arrays and out_pos[p] = source row of packed
 //           row p (the single-step ABI for hosts with their own collectives).
+// kRec12 with out_pos null: the write-set form, which needs no send
+// positions (no rep comes back).
 template <typename In, bool kRec12>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
     In in, uint64_t n, uint32_t skip, uint32_t bits, uint32_t world,
@@ -314,18 +316,113 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
       const uint32_t d = v ? part_digit(in_hash<In>(k), skip, bits, world) : 0u;
       const uint32_t p = world ? wave_add(cur, d, v) : (v ? atomicAdd(&cur[d], 1u) : 0u);
       if (!v) {
-        if (kRec12 && q.in[u]) out_pos[i] = 0xFFFFFFFFu;
+        if (kRec12 && q.in[u] && out_pos) out_pos[i] = 0xFFFFFFFFu;
         continue;
       }
       const uint32_t r = in.rank_of(q, u);
       if (kRec12) {
         out_rec[p] = make_uint3(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32), r);
-        out_pos[i] = p;
+        if (out_pos) out_pos[i] = p;
       } else {
         out_key[p] = k;
         out_rank[p] = r;
         out_pos[p] = static_cast<uint32_t>(i);
       }
+    }
+  }
+}
+
+// Padded exchange partition (round 5; shard.cpp padded exchange): ONE pass
+// over the caller's rows, no histogram or scan.  Each round of kPadR rows a
+// block counting-sorts its keyed rows by owner in LDS, reserves each owner's
+// run inside that owner's fixed-capacity message with ONE global atomic per
+// owner (cursor[d], zeroed before the launch), and copies the runs out
+// coalesced.  Message d = slots d * (cap + 1) .. of the send buffer (slot 0
+// its header, k_pad_fill); the message to this rank itself (d == me) is
+// written straight into the receive buffer (self_out, same slots): no copy.
+// The order of the rows inside a message follows the reservations, not row
+// order -- the grouping reads ranks, not positions.  Slots past cap are not
+// written (cursor[d] > cap: k_pad_fill raises the overflow bit).  out_pos
+// (rep form; null for the write set): the send slot of row i, ~0 for keyless
+// or unsent rows.  Round r + 1's rows are loaded before round r's atomics.
+constexpr int kPadU = 4;
+constexpr uint32_t kPadR = kPadU * kPartThreads;
+constexpr uint32_t kXShardBitsDev = 8;  // shard = top 8 hash bits (shard.cpp kXShardBits)
+__global__ __launch_bounds__(kPartThreads) void k_part_padded(
+    RowsIn in, uint64_t n, uint32_t world, uint32_t me, uint32_t cap, uint3* __restrict__ out,
+    uint3* __restrict__ self_out, uint32_t* __restrict__ out_pos,
+    uint32_t* __restrict__ cursor) {
+  __shared__ uint3 buf[kPadR];
+  __shared__ uint32_t cnt[kMaxWorld], lb[kMaxWorld + 1], gb[kMaxWorld];
+  const uint64_t c1 = cap + 1ull;
+  uint64_t t0, t1;
+  tile_of(n, gridDim.x, t0, t1);
+  auto round = [&](const RowBatch<kPadU>& q, uint64_t i0) {
+    if (threadIdx.x < world) cnt[threadIdx.x] = 0;
+    lds_barrier();
+    uint32_t dg[kPadU], lr[kPadU];
+#pragma unroll
+    for (int u = 0; u < kPadU; ++u) {
+      const bool v = in.valid_of(q, u);
+      const uint32_t d = v ? part_digit(row_hash(in.key_of(q, u)), 0, kXShardBitsDev, world) : 0u;
+      lr[u] = wave_add(cnt, d, v);
+      dg[u] = v ? d : ~0u;
+    }
+    lds_barrier();
+    if (threadIdx.x < 64) {  // one wave: the round's run starts and the reservations
+      const uint32_t lane = threadIdx.x;
+      const uint32_t c = lane < world ? cnt[lane] : 0u;
+      uint32_t inc = c;
+#pragma unroll
+      for (int s = 1; s < 64; s <<= 1) {
+        const uint32_t o = __shfl_up(inc, s);
+        if (lane >= static_cast<uint32_t>(s)) inc += o;
+      }
+      if (lane < world) lb[lane] = inc - c;
+      if (lane == world - 1) lb[world] = inc;
+      if (lane < world && c) gb[lane] = atomicAdd(&cursor[lane], c);
+    }
+    lds_barrier();
+#pragma unroll
+    for (int u = 0; u < kPadU; ++u) {
+      const uint64_t i = i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads;
+      if (dg[u] == ~0u) {
+        if (out_pos && q.in[u]) out_pos[i] = 0xFFFFFFFFu;
+        continue;
+      }
+      const uint32_t d = dg[u];
+      const uint64_t k = in.key_of(q, u);
+      buf[lb[d] + lr[u]] = make_uint3(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32),
+                                      in.rank_of(q, u));
+      if (out_pos) {
+        const uint32_t pos = gb[d] + lr[u];
+        out_pos[i] = pos < cap ? static_cast<uint32_t>(d * c1 + 1 + pos) : 0xFFFFFFFFu;
+      }
+    }
+    lds_barrier();
+    const uint32_t total = lb[world];
+    for (uint32_t k = threadIdx.x; k < total; k += kPartThreads) {
+      uint32_t lo = 0, hi = world - 1;  // the owner of slot k: last d with lb[d] <= k
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (lb[mid] <= k) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint32_t pos = gb[lo] + (k - lb[lo]);
+      if (pos < cap) (lo == me ? self_out : out)[lo * c1 + 1 + pos] = buf[k];
+    }
+    lds_barrier();  // buf, cnt and lb are rewritten by the next round
+  };
+  if (t0 < t1) {
+    RowBatch<kPadU> qa, qb;
+    in.template load_many<kPadU>(t0 + threadIdx.x, kPartThreads, t1, t0, qa);
+    for (uint64_t i0 = t0;; i0 += 2 * kPadR) {  // uniform trip count
+      in.template load_many<kPadU>(i0 + kPadR + threadIdx.x, kPartThreads, t1, t0, qb);
+      round(qa, i0);
+      if (i0 + kPadR >= t1) break;
+      in.template load_many<kPadU>(i0 + 2 * kPadR + threadIdx.x, kPartThreads, t1, t0, qa);
+      round(qb, i0 + kPadR);
+      if (i0 + 2 * kPadR >= t1) break;
     }
   }
 }
@@ -1121,9 +1218,11 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
 // (profiles/r3/exp_scatter_align/run.log).
 constexpr uint32_t kWsProd = 512;   // producer threads (waves 0-7)
 constexpr int kWsRows = 4;          // rows per producer thread per round
-template <bool kInitRep>
+// In: the caller's rows (RowsIn, rank = rank_base + row) or received exchange
+// records (RecRankIn: the rank in the record's third word).
+template <typename In, bool kInitRep>
 __global__ __launch_bounds__(kPartThreads) void k_part_scatter_ws(
-    RowsIn in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ offs,
+    In in, uint64_t n, uint32_t skip, const uint32_t* __restrict__ offs,
     const uint32_t* __restrict__ ftot, uint3* __restrict__ out, uint32_t* __restrict__ rep,
     uint32_t* __restrict__ fbase) {
   constexpr uint32_t nbins = 1u << kStageBits;
@@ -1183,7 +1282,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_ws(
 #pragma unroll
       for (int u = 0; u < kWsRows; ++u) {
         if (!in.valid_of(q, u)) continue;
-        const uint64_t h = row_hash(in.key_of(q, u));
+        const uint64_t h = in_hash<In>(in.key_of(q, u));
         const uint32_t b = digit_of(h, skip, kStageBits);
         const uint3 rq = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32),
                                     in.row_of(q, u));
@@ -1394,11 +1493,20 @@ struct ListOut {
   uint32_t* counts;
   uint32_t* lcnt;  // [bucket]: linked rows; [buckets]: the keyed total
   XSink x;         // the valid keyless rows, when the partition collects them
+  // entries who / obj hold (the sharded write set's caller capacity): a
+  // bucket ending past it writes nothing and sets *nospc (the call then
+  // fails with -ENOSPC); ~0: unbounded (n entries at most)
+  uint32_t cap = 0xFFFFFFFFu;
+  uint32_t* nospc = nullptr;
   template <int kSteps>
   __device__ __forceinline__ void emit(const bool (&live)[kSteps], const bool (&lk)[kSteps],
                                        const uint32_t (&r)[kSteps], const uint32_t (&w)[kSteps],
                                        const uint32_t (&f)[kSteps], uint32_t start, uint32_t end,
                                        uint32_t&, uint32_t&, uint32_t* scr, bool) const {
+    if (end > cap) {  // uniform per bucket
+      if (threadIdx.x == 0) *nospc = 1u;
+      return;
+    }
     const uint32_t lane = __lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
@@ -1841,35 +1949,123 @@ __global__ void k_copy_counts(const uint32_t* __restrict__ offs, uint32_t nbins,
 
 // Rows per destination rank of the exchange, from the scanned offsets of the
 // destination-digit partition.
-// msgs (may be NULL): the count messages of the exchange, {rows for d, n}
-// per destination d (every rank learns every rank's n with the counts).
+// msgs (may be NULL): the count messages of the exchange, {rows for d, n,
+// code} per destination d (every rank learns every rank's n with the counts;
+// code = the call's form and return leg, which every rank must share --
+// checked by the receivers).
 __global__ void k_dest_counts(const uint32_t* __restrict__ offs, uint32_t world,
                               int64_t* __restrict__ counts, int64_t* __restrict__ msgs,
-                              int64_t n) {
+                              int64_t n, int64_t code) {
   const uint32_t d = threadIdx.x;
   if (d < world) {
     const int64_t c = static_cast<int64_t>(offs[static_cast<uint64_t>(d + 1) * kPartBlocks]) -
                       offs[static_cast<uint64_t>(d) * kPartBlocks];
     counts[d] = c;
     if (msgs) {
-      msgs[2 * d] = c;
-      msgs[2 * d + 1] = n;
+      msgs[3 * d] = c;
+      msgs[3 * d + 1] = n;
+      msgs[3 * d + 2] = code;
     }
   }
 }
 
 // rep[i] of the sender's rows from the reps returned in send order: row i was
-// sent at position pos[i] (~0: no key, it keeps its own rank); back[p] == ~0
-// (compact return: no pair came back for it) also keeps the rank.
+// sent at position pos[i] (~0: no key, it keeps its own rank).  Every sent
+// position holds a rep: the full return writes all of them, the compact one
+// starts from each record's own rank (k_back_init).  (Round 4 marked "no
+// pair came back" with back == ~0, which is also the legal rep
+// SDGPU_REP_EXISTING | 0x7FFFFFFF: ADVICE r4.)
+// Positions in [self_lo, self_hi) read self[p]: the padded exchange's
+// message to this rank itself, whose reps the owner side wrote locally.
 __global__ __launch_bounds__(256) void k_gather_rep(const uint32_t* __restrict__ back,
                                                     const uint32_t* __restrict__ pos,
                                                     const uint32_t* __restrict__ rank, uint64_t n,
-                                                    uint32_t* __restrict__ rep) {
+                                                    uint32_t* __restrict__ rep,
+                                                    const uint32_t* __restrict__ self,
+                                                    uint32_t self_lo, uint32_t self_hi) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) {
     const uint32_t p = pos[i];
-    const uint32_t b = back[p == 0xFFFFFFFFu ? 0u : p];
-    rep[i] = (p == 0xFFFFFFFFu || b == 0xFFFFFFFFu) ? rank[i] : b;
+    const bool mine = p - self_lo < self_hi - self_lo;  // never for p == ~0 (< 2^32 slots)
+    const uint32_t b = (mine ? self : back)[p == 0xFFFFFFFFu ? 0u : p];
+    rep[i] = p == 0xFFFFFFFFu ? rank[i] : b;
+  }
+}
+
+// Compact return leg, source side: back[p] = the rank in send record p (a
+// row whose rep is its own rank gets no pair back).
+__global__ __launch_bounds__(256) void k_back_init(const uint3* __restrict__ srec, uint64_t n,
+                                                   uint32_t* __restrict__ back) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride)
+    back[i] = srec[i].z;
+}
+
+// Fixed-capacity exchange messages (shard.cpp, padded exchange): the message
+// to rank d is C1 = cap + 1 12-byte slots at d * C1 of the send buffer --
+// slot 0 the header {rows for d | this source's overflow bit << 31, this
+// source's n, kPadRank}, slots 1..cap the records (k_part_scatter with
+// k_part_padded), the rest padding {0, 0, kPadRank}; the message to this
+// rank itself lives in the receive buffer (self_out).  The owner's grouping drops
+// every kPadRank record (RecIn::valid_of).  The overflow bit (some count of
+// this source > cap: rows were not sent) goes to EVERY owner, so all ranks
+// learn the same "some message overflowed" from their headers.  Block (0, 0)
+// also writes summary[3] = rows this source sent, clears summary[4] (the
+// list kernels' -ENOSPC flag) and zero3[0..2] (the write set's counts).
+// counts (cnt: the reservation cursors) < 2^31 (n < 2^31 on this path).
+__global__ __launch_bounds__(256) void k_pad_fill(const uint32_t* __restrict__ cnt, uint32_t world,
+                                                  uint32_t me, uint32_t cap, uint32_t n,
+                                                  uint3* __restrict__ out,
+                                                  uint3* __restrict__ self_out,
+                                                  uint32_t* __restrict__ summary,
+                                                  uint32_t* __restrict__ zero3) {
+  const uint32_t d = blockIdx.y;
+  bool ovf = false;
+  uint32_t sent = 0;
+  for (uint32_t p = 0; p < world; ++p) {
+    const uint32_t c = cnt[p];
+    ovf |= c > cap;
+    sent += min(c, cap);
+  }
+  uint3* rec = d == me ? self_out : out;
+  const uint64_t base = static_cast<uint64_t>(d) * (cap + 1ull);
+  const uint32_t c = cnt[d];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    rec[base] = make_uint3(c | (ovf ? 0x80000000u : 0u), n, kPadRank);
+    if (d == 0) {
+      summary[3] = sent;
+      summary[4] = 0u;
+      if (zero3) zero3[0] = zero3[1] = zero3[2] = 0u;
+    }
+  }
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+  for (uint64_t j = min(c, cap) + static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; j < cap;
+       j += stride)
+    rec[base + 1 + j] = make_uint3(0u, 0u, kPadRank);
+}
+
+// Owner side, after the records arrived: summary[0] = some source overflowed
+// (the same on every rank), [1] = the largest source n, [2] = rows received.
+__global__ void k_recv_summary(const uint3* __restrict__ rrec, uint32_t world, uint32_t cap,
+                               uint32_t* __restrict__ summary) {
+  const uint32_t p = threadIdx.x;
+  uint32_t ovf = 0, nmax = 0, rows = 0;
+  if (p < world) {
+    const uint3 h = rrec[static_cast<uint64_t>(p) * (cap + 1ull)];
+    ovf = h.x >> 31;
+    nmax = h.y;
+    rows = min(h.x & 0x7FFFFFFFu, cap);
+  }
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    ovf |= __shfl_xor(ovf, s);
+    nmax = max(nmax, __shfl_xor(nmax, s));
+    rows += __shfl_xor(rows, s);
+  }
+  if (p == 0) {
+    summary[0] = ovf;
+    summary[1] = nmax;
+    summary[2] = rows;
   }
 }
 
@@ -2020,9 +2216,15 @@ uint32_t sink_cap(uint64_t n) {
   return static_cast<uint32_t>((tile + kSinkWaves - 1) / kSinkWaves + 520);
 }
 
-GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
+// bits_rows (0: n): the rows the buckets are sized for -- the keyed rows of a
+// padded exchange receive, whose n counts the padding slots too (buckets
+// over the LDS capacity stay correct through the global table, so the hint
+// only chooses the layout).  with_sink: room for ListOut's keyless sink
+// (~4 B per row; only the fused call without an index uses it).
+GroupLayout group_layout(uint64_t n, uint64_t bits_rows = 0, bool with_sink = false) {
+  constexpr uint32_t b2 = kStage2Bits;
   GroupLayout L;
-  L.bits = bucket_bits_for(n);
+  L.bits = bucket_bits_for(bits_rows && bits_rows < n ? bits_rows : n);
   L.cbits = L.bits > kStageBits ? L.bits - b2 : 0;
   const uint64_t nh = (static_cast<uint64_t>(1) << L.bits) * kMaxPartBlocks;
   const uint64_t nh1 = (static_cast<uint64_t>(1) << L.cbits) * kMaxPartBlocks;
@@ -2048,8 +2250,10 @@ GroupLayout group_layout(uint64_t n, uint32_t b2 = kStage2Bits) {
   L.run_l = o; o = align_up(o + 4 * nrun, 256);
   L.segtot = o; o = align_up(o + 4 * kRunMaxBins, 256);
   L.lcnt = o; o = align_up(o + 4 * (nf + 1), 256);  // ListOut: linked rows per bucket, keyed total
-  L.xst = o; o = align_up(o + 4 * static_cast<uint64_t>(kPartBlocks) * kSinkWaves * sink_cap(n), 256);
-  L.xcnt = o; o = align_up(o + 4 * kPartBlocks * kSinkWaves, 256);
+  L.xst = o;
+  if (with_sink) o = align_up(o + 4 * static_cast<uint64_t>(kPartBlocks) * kSinkWaves * sink_cap(n), 256);
+  L.xcnt = o;
+  if (with_sink) o = align_up(o + 4 * kPartBlocks * kSinkWaves, 256);
   L.total = o;
   return L;
 }
@@ -2216,10 +2420,24 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
   return out_finish(out, nfine, s);
 }
 
+// Rows whose bucket records can be 12 bytes {hash, z} with rank = rank_base
+// + z: the caller's rows without a rank array (z = row), and received
+// exchange records for an output that needs no row (RecRankIn: z = rank).
+template <typename In>
+bool rank_in_z(const In& in) {
+  if constexpr (std::is_same<In, RowsIn>::value) return !in.rank;
+  else return std::is_same<In, RecRankIn>::value;
+}
+template <typename In>
+uint32_t z_rank_base(const In& in) {
+  if constexpr (std::is_same<In, RowsIn>::value) return in.rank_base;
+  else return 0u;
+}
+
 template <typename In, typename Out>
 hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, bool init_rep,
-                        Out out, void* ws, hipStream_t s, KTimer* timer) {
-  const GroupLayout L = group_layout(n);
+                        Out out, void* ws, hipStream_t s, KTimer* timer, uint64_t bits_rows = 0) {
+  const GroupLayout L = group_layout(n, bits_rows, sink_of(out).st != nullptr);
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(w + L.hist);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(w + L.tiles);
@@ -2231,11 +2449,11 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
   const uint64_t nh = (static_cast<uint64_t>(1) << bits) * P;
   const size_t lds = sizeof(uint32_t) << bits;
   if (L.cbits) {
-    if constexpr (std::is_same<In, RowsIn>::value) {
-      if (!in.rank)  // rank = rank_base + row: 12-byte records
+    if constexpr (std::is_same<In, RowsIn>::value || std::is_same<In, RecRankIn>::value) {
+      if (rank_in_z(in))  // 12-byte records
         return two_level_launch<In, kStage2Bits, kStage2Slots, kStage2Rows, kStage2Blocks, true,
                                 kStage2Slots>(in, n, L, chunk_rows, rep, init_rep, out, ws, s,
-                                              timer, in.rank_base);
+                                              timer, z_rank_base(in));
     }
     return two_level_launch<In, kStage2Bits, kStage2Slots, kStage2Rows, kStage2Blocks, false,
                             kStage2Slots>(in, n, L, chunk_rows, rep, init_rep, out, ws, s, timer);
@@ -2256,21 +2474,23 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
       hist_launch(sink_of(out), lds, s, in, n, kShardBits, bits, fine, nullptr, true);
       k_fine_scan<kPartBlocks, 1><<<nb / 64, 1024, 0, s>>>(fine, nb, fE, ftot, ovf);
     }
-    if constexpr (std::is_same<In, RowsIn>::value) {
-      if (!in.rank) {  // rank = rank_base + row: 12-byte records
+    if constexpr (std::is_same<In, RowsIn>::value || std::is_same<In, RecRankIn>::value) {
+      if (rank_in_z(in)) {  // rank = rank_base + z: 12-byte records
         {
           KScope k(timer, "bucket_scatter", s);
           uint3* rec12 = reinterpret_cast<uint3*>(rec);
-          if (init_rep)
-            k_part_scatter_ws<true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, fE, ftot, rec12,
-                                                               rep, fbase);
-          else
-            k_part_scatter_ws<false><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, fE, ftot, rec12,
-                                                                rep, fbase);
+          if (init_rep) {
+            if constexpr (std::is_same<In, RowsIn>::value)
+              k_part_scatter_ws<In, true><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, fE, ftot,
+                                                                     rec12, rep, fbase);
+          } else {
+            k_part_scatter_ws<In, false><<<P, kPartThreads, 0, s>>>(in, n, kShardBits, fE, ftot,
+                                                                    rec12, rep, fbase);
+          }
         }
         KScope k(timer, "bucket_group", s);
         k_bucket_group12_pk<Out><<<nb, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
-                                                              in.rank_base, fbase, kStageBits,
+                                                              z_rank_base(in), fbase, kStageBits,
                                                               ChunkOf::make(chunk_rows), gkey, gmin,
                                                               out);
         return out_finish(out, nb, s);
@@ -2331,7 +2551,7 @@ hipError_t shard_partition(const RowsIn& in, uint64_t n, uint32_t shard_bits, ui
     k_part_hist<RowsIn><<<kPartBlocks, kPartThreads, lds, s>>>(in, n, 0, shard_bits, world, hist);
   }
   scan::exclusive(hist, nh, hist, tiles, nullptr, s);
-  if (opos) {
+  if (opos || orec) {
     KScope k(timer, "shard_scatter", s);
     if (orec)
       k_part_scatter<RowsIn, true><<<kPartBlocks, kPartThreads, lds, s>>>(
@@ -2345,36 +2565,44 @@ hipError_t shard_partition(const RowsIn& in, uint64_t n, uint32_t shard_bits, ui
 
 }  // namespace
 
-size_t dedup_workspace_bytes(uint64_t n) { return group_layout(n).total; }
+size_t dedup_workspace_bytes(uint64_t n, bool with_sink) {
+  return group_layout(n, 0, with_sink).total;
+}
 
 hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* rep,
                               bool init_rep, void* ws, hipStream_t s, KTimer* timer) {
   if (in.n == 0) return hipSuccess;
   if (in.rec12)
     return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
-                        chunk_rows, rep, init_rep, RepOut{rep}, ws, s, timer);
+                        chunk_rows, rep, init_rep, RepOut{rep}, ws, s, timer, in.bits_rows);
   return group_launch(RowsIn{in.key, in.valid, in.rank, in.rank_base}, in.n, chunk_rows, rep,
-                      init_rep, RepOut{rep}, ws, s, timer);
+                      init_rep, RepOut{rep}, ws, s, timer, in.bits_rows);
 }
 
 hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* who,
                              uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
-                             KTimer* timer, bool sink_keyless, const uint8_t* keyless_valid) {
+                             KTimer* timer, bool sink_keyless, const uint8_t* keyless_valid,
+                             uint32_t cap, uint32_t* nospc) {
   if (in.n == 0) return hipSuccess;
   uint8_t* w = static_cast<uint8_t*>(ws);
-  const GroupLayout L = group_layout(in.n);
+  const bool sink = sink_keyless && !in.rec12 && in.valid;
+  const GroupLayout L = group_layout(in.n, in.bits_rows, sink);
   ListOut out{who, obj, counts, reinterpret_cast<uint32_t*>(w + L.lcnt), XSink{}};
-  if (sink_keyless && !in.rec12 && in.valid) {
+  if (nospc) {
+    out.cap = cap;
+    out.nospc = nospc;
+  }
+  if (sink) {
     out.x.valid = keyless_valid;
     out.x.st = reinterpret_cast<uint32_t*>(w + L.xst);
     out.x.cnt = reinterpret_cast<uint32_t*>(w + L.xcnt);
     out.x.cap = sink_cap(in.n);
   }
-  if (in.rec12)
-    return group_launch(RecIn{reinterpret_cast<const uint3*>(in.rec12), in.valid}, in.n,
-                        chunk_rows, nullptr, false, out, ws, s, timer);
+  if (in.rec12)  // the list needs no row index: 12-byte bucket records carrying the rank
+    return group_launch(RecRankIn{{reinterpret_cast<const uint3*>(in.rec12), in.valid}}, in.n,
+                        chunk_rows, nullptr, false, out, ws, s, timer, in.bits_rows);
   return group_launch(RowsIn{in.key, in.valid, in.rank, in.rank_base}, in.n, chunk_rows, nullptr,
-                      false, out, ws, s, timer);
+                      false, out, ws, s, timer, in.bits_rows);
 }
 
 size_t shard_workspace_bytes(uint32_t shard_bits) {
@@ -2410,7 +2638,8 @@ hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
                                  const uint32_t* rank, uint64_t n, uint32_t shard_bits,
                                  uint32_t world, uint64_t* out_key, uint32_t* out_rank,
                                  uint32_t* out_rec12, uint32_t* out_pos, int64_t* d_dest_counts,
-                                 void* ws, hipStream_t s, KTimer* timer, int64_t* d_count_msgs) {
+                                 void* ws, hipStream_t s, KTimer* timer, int64_t* d_count_msgs,
+                                 int64_t msg_code) {
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(w);
   uint32_t* tiles = reinterpret_cast<uint32_t*>(w + shard_hist_bytes(shard_bits));
@@ -2419,7 +2648,7 @@ hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
                                  s, timer);
   if (e != hipSuccess) return e;
   k_dest_counts<<<1, 64, 0, s>>>(hist, world, d_dest_counts, d_count_msgs,
-                                 static_cast<int64_t>(n));
+                                 static_cast<int64_t>(n), msg_code);
   return hipGetLastError();
 }
 
@@ -2450,10 +2679,11 @@ hipError_t ret_compact_launch(const RetTiles& st, const uint32_t* rrec, const ui
 }
 
 hipError_t ret_apply_launch(const RetApply& ap, const uint2* rback, uint32_t* back,
-                            uint64_t n_back, hipStream_t s) {
+                            uint64_t n_back, const uint32_t* srec12, hipStream_t s) {
   if (n_back) {
-    const hipError_t e = hipMemsetAsync(back, 0xFF, 4 * n_back, s);
-    if (e != hipSuccess) return e;
+    const uint64_t g = std::min<uint64_t>((n_back + 255) / 256, 16384);
+    k_back_init<<<static_cast<uint32_t>(g), 256, 0, s>>>(reinterpret_cast<const uint3*>(srec12),
+                                                         n_back, back);
   }
   const uint64_t total = ap.poff[ap.world];
   if (total) {
@@ -2464,11 +2694,46 @@ hipError_t ret_apply_launch(const RetApply& ap, const uint2* rback, uint32_t* ba
 }
 
 hipError_t gather_rep_launch(const uint32_t* back, const uint32_t* pos, const uint32_t* rank,
-                             uint64_t n, uint32_t* rep, hipStream_t s) {
+                             uint64_t n, uint32_t* rep, hipStream_t s, const uint32_t* self,
+                             uint64_t self_lo, uint64_t self_hi) {
   if (n) {
     const uint64_t g = std::min<uint64_t>((n + 255) / 256, 16384);
-    k_gather_rep<<<static_cast<uint32_t>(g), 256, 0, s>>>(back, pos, rank, n, rep);
+    k_gather_rep<<<static_cast<uint32_t>(g), 256, 0, s>>>(
+        back, pos, rank, n, rep, self ? self : back, static_cast<uint32_t>(self_lo),
+        static_cast<uint32_t>(self ? self_hi : self_lo));
   }
+  return hipGetLastError();
+}
+
+hipError_t padded_partition_launch(const uint64_t* key, const uint8_t* has_key,
+                                   const uint32_t* rank, uint64_t n, uint32_t world, uint32_t me,
+                                   uint32_t cap, uint32_t* out_rec12, uint32_t* self_rec12,
+                                   uint32_t* out_pos, uint32_t* cursor, hipStream_t s,
+                                   KTimer* timer) {
+  hipError_t e = hipMemsetAsync(cursor, 0, 4ull * world, s);
+  if (e != hipSuccess) return e;
+  if (n) {
+    KScope k(timer, "shard_padded", s);
+    k_part_padded<<<kPartBlocks, kPartThreads, 0, s>>>(
+        RowsIn{key, has_key, rank, 0}, n, world, me, cap, reinterpret_cast<uint3*>(out_rec12),
+        reinterpret_cast<uint3*>(self_rec12), out_pos, cursor);
+  }
+  return hipGetLastError();
+}
+
+hipError_t pad_fill_launch(const uint32_t* cursor, uint32_t world, uint32_t me, uint32_t cap,
+                           uint64_t n, uint32_t* rec12, uint32_t* self_rec12, uint32_t* summary,
+                           uint32_t* zero3, hipStream_t s) {
+  const uint32_t bx = std::min<uint32_t>(64u, (cap + 1023u) / 1024u + 1u);
+  k_pad_fill<<<dim3(bx, world), 256, 0, s>>>(cursor, world, me, cap, static_cast<uint32_t>(n),
+                                             reinterpret_cast<uint3*>(rec12),
+                                             reinterpret_cast<uint3*>(self_rec12), summary, zero3);
+  return hipGetLastError();
+}
+
+hipError_t recv_summary_launch(const uint32_t* rrec12, uint32_t world, uint32_t cap,
+                               uint32_t* summary, hipStream_t s) {
+  k_recv_summary<<<1, 64, 0, s>>>(reinterpret_cast<const uint3*>(rrec12), world, cap, summary);
   return hipGetLastError();
 }
 

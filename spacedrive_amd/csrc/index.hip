@@ -167,10 +167,15 @@ __global__ __launch_bounds__(kThreads) void k_index_probe(IndexRef t, In in, uin
 }
 
 // After the grouping: rows that created an Object (grouped, rep == rank).
+// skip (may be null): *skip != 0 -- the rows of a padded exchange that
+// overflowed, whose grouping is re-run through the counted exchange -- inserts
+// nothing (the index must not learn creators of an incomplete grouping).
 template <typename In>
 __global__ __launch_bounds__(kThreads) void k_index_creators(IndexRef t, In in, uint64_t n,
                                                              const uint32_t* __restrict__ rep,
-                                                             const uint8_t* __restrict__ grouped) {
+                                                             const uint8_t* __restrict__ grouped,
+                                                             const uint32_t* __restrict__ skip) {
+  if (skip && *skip) return;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
   uint32_t added = 0;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n;
@@ -224,15 +229,16 @@ hipError_t index_probe_launch(const IndexRef& t, const GroupInput& in, uint32_t 
 }
 
 hipError_t index_creators_launch(const IndexRef& t, const GroupInput& in, const uint32_t* rep,
-                                 const uint8_t* grouped, hipStream_t s, KTimer* timer) {
+                                 const uint8_t* grouped, hipStream_t s, KTimer* timer,
+                                 const uint32_t* skip) {
   if (in.n == 0) return hipSuccess;
   KScope k(timer, "index_insert", s);
   if (in.rec12)
     k_index_creators<<<grid_for(in.n), kThreads, 0, s>>>(
-        t, RecIn{reinterpret_cast<const uint3*>(in.rec12), nullptr}, in.n, rep, grouped);
+        t, RecIn{reinterpret_cast<const uint3*>(in.rec12), nullptr}, in.n, rep, grouped, skip);
   else
     k_index_creators<<<grid_for(in.n), kThreads, 0, s>>>(
-        t, RowsIn{in.key, nullptr, in.rank, in.rank_base}, in.n, rep, grouped);
+        t, RowsIn{in.key, nullptr, in.rank, in.rank_base}, in.n, rep, grouped, skip);
   return hipGetLastError();
 }
 

@@ -149,8 +149,13 @@ struct GroupInput {
   const uint32_t* rank = nullptr;
   uint32_t rank_base = 0;
   uint64_t n = 0;
+  // rows the buckets are sized for (0: n) -- a padded exchange receive's n
+  // counts its header and padding slots, which the grouping drops
+  uint64_t bits_rows = 0;
 };
-size_t dedup_workspace_bytes(uint64_t n);
+// with_sink: room for the fused call's keyless sink (sdgpu_group_link_device
+// without an index)
+size_t dedup_workspace_bytes(uint64_t n, bool with_sink = false);
 // rep[i] for row i of `in` (the canonical rule over ranks; rows without a key
 // get rep = their rank when init_rep, and are left untouched otherwise).
 hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* rep,
@@ -163,10 +168,14 @@ hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_
 // partition pass also lists the valid keyless rows (keyless_valid[i] != 0,
 // null: all) as creators behind the keyed entries -- what extra_list_launch
 // does without an index, with no pass of its own.
+// nospc (non-null): who / obj hold cap entries; a bucket past them writes
+// nothing and sets *nospc (the sharded write set's -ENOSPC, decided on the
+// device).
 hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* who,
                              uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
                              KTimer* timer = nullptr, bool sink_keyless = false,
-                             const uint8_t* keyless_valid = nullptr);
+                             const uint8_t* keyless_valid = nullptr, uint32_t cap = 0xFFFFFFFFu,
+                             uint32_t* nospc = nullptr);
 // extra_list_launch then appends, in row order, the valid keyless rows and
 // (with an index: grouped = the probe's mask, hitrep = its reps) the keyed
 // rows the probe decided -- the index path, the owner's keyless rows of the
@@ -175,7 +184,8 @@ size_t extra_workspace_bytes(uint64_t n);
 hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uint8_t* grouped,
                              const uint32_t* hitrep, const uint32_t* rank, uint32_t first_rank,
                              uint64_t n, uint32_t* who, uint32_t* obj, uint32_t* counts, void* ws,
-                             hipStream_t s, KTimer* timer = nullptr);
+                             hipStream_t s, KTimer* timer = nullptr, uint32_t cap = 0xFFFFFFFFu,
+                             uint32_t* nospc = nullptr);
 // Compact return leg of the exchange (dedup.hip): the received rows are cut
 // into tiles of 4096 that never straddle a source's segment [roff[p],
 // roff[p + 1]); tstart[p] = first tile of segment p, tstart[world] = tiles.
@@ -201,9 +211,11 @@ size_t ret_workspace_bytes(uint32_t tiles);
 hipError_t ret_compact_launch(const RetTiles& st, const uint32_t* rrec, const uint32_t* rrep,
                               uint2* ret, int64_t* retcnt, void* ws, hipStream_t s,
                               KTimer* timer = nullptr);
-// back[0..n_back) = ~0, then back[soff[d] + idx] = rep for every received pair
+// back[p] = the rank of send record p (srec12, p < n_back: a row no pair
+// came back for keeps its own Object), then back[soff[d] + idx] = rep for
+// every received pair
 hipError_t ret_apply_launch(const RetApply& ap, const uint2* rback, uint32_t* back,
-                            uint64_t n_back, hipStream_t s);
+                            uint64_t n_back, const uint32_t* srec12, hipStream_t s);
 size_t shard_workspace_bytes(uint32_t shard_bits);
 // Shard of a key = top shard_bits bits of mix64(key) (rows_device.hpp row_hash).
 hipError_t shard_count_launch(const uint64_t* key, const uint8_t* has_key, uint64_t n,
@@ -223,10 +235,33 @@ hipError_t shard_exchange_launch(const uint64_t* key, const uint8_t* has_key,
                                  uint32_t world, uint64_t* out_key, uint32_t* out_rank,
                                  uint32_t* out_rec12, uint32_t* out_pos, int64_t* d_dest_counts,
                                  void* ws, hipStream_t s, KTimer* timer = nullptr,
-                                 int64_t* d_count_msgs = nullptr);
-// rep[i] = pos[i] == ~0 ? rank[i] : back[pos[i]] (the exchange's return path)
+                                 int64_t* d_count_msgs = nullptr, int64_t msg_code = 0);
+// rep[i] = pos[i] == ~0 ? rank[i] : back[pos[i]] (the exchange's return
+// path); positions in [self_lo, self_hi) read self[pos] instead (the padded
+// exchange's message to this rank itself: its reps never travel)
 hipError_t gather_rep_launch(const uint32_t* back, const uint32_t* pos, const uint32_t* rank,
-                             uint64_t n, uint32_t* rep, hipStream_t s);
+                             uint64_t n, uint32_t* rep, hipStream_t s, const uint32_t* self = nullptr,
+                             uint64_t self_lo = 0, uint64_t self_hi = 0);
+// Padded exchange (fixed-capacity messages of cap + 1 12-byte slots per
+// destination rank, dedup.hip k_part_padded / k_pad_fill): one pass writes
+// the keyed rows into their owners' messages -- the message to rank `me`
+// into self_rec12 (the receive buffer), the others into rec12 -- reserving
+// slots through cursor[world] (device u32, zeroed here); out_pos (may be
+// null): send slot of each row, ~0 for keyless / unsent rows.  Then the
+// headers + padding from the cursors; summary (device u32[8]): [3] rows
+// sent, [4] = 0; zero3 (may be null) zeroed.
+hipError_t padded_partition_launch(const uint64_t* key, const uint8_t* has_key,
+                                   const uint32_t* rank, uint64_t n, uint32_t world, uint32_t me,
+                                   uint32_t cap, uint32_t* out_rec12, uint32_t* self_rec12,
+                                   uint32_t* out_pos, uint32_t* cursor, hipStream_t s,
+                                   KTimer* timer = nullptr);
+hipError_t pad_fill_launch(const uint32_t* cursor, uint32_t world, uint32_t me, uint32_t cap,
+                           uint64_t n, uint32_t* rec12, uint32_t* self_rec12, uint32_t* summary,
+                           uint32_t* zero3, hipStream_t s);
+// summary [0] some message overflowed (every rank alike), [1] largest source
+// n, [2] rows received, from the received headers.
+hipError_t recv_summary_launch(const uint32_t* rrec12, uint32_t world, uint32_t cap,
+                               uint32_t* summary, hipStream_t s);
 hipError_t scatter_rep_launch(const uint32_t* src, const uint32_t* pos, uint64_t n, uint32_t* dst,
                               uint64_t n_dst, const uint32_t* init, bool do_init, hipStream_t s);
 
@@ -248,8 +283,11 @@ hipError_t index_objects_launch(const IndexRef& t, const uint64_t* key, const ui
 hipError_t index_probe_launch(const IndexRef& t, const GroupInput& in, uint32_t chunk_rows,
                               uint32_t* rep, uint8_t* valid_out, hipStream_t s,
                               KTimer* timer = nullptr);
+// skip (device, may be null): nothing is inserted when *skip != 0 (a padded
+// exchange that overflowed: re-run counted).
 hipError_t index_creators_launch(const IndexRef& t, const GroupInput& in, const uint32_t* rep,
-                                 const uint8_t* grouped, hipStream_t s, KTimer* timer = nullptr);
+                                 const uint8_t* grouped, hipStream_t s, KTimer* timer = nullptr,
+                                 const uint32_t* skip = nullptr);
 
 // ---- downstream consumers (consumers.hip) ---------------------------------------
 size_t orphan_workspace_bytes(uint64_t n_obj, uint32_t max_id);

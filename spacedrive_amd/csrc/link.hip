@@ -302,7 +302,9 @@ constexpr int kScanThreads = 1024;
 __global__ __launch_bounds__(kScanThreads) void k_extra_scan(uint32_t* __restrict__ cnt,
                                                              const uint32_t* __restrict__ lk,
                                                              uint32_t nb, uint32_t* __restrict__ kx,
-                                                             uint32_t* __restrict__ counts) {
+                                                             uint32_t* __restrict__ counts,
+                                                             uint32_t cap,
+                                                             uint32_t* __restrict__ nospc) {
   __shared__ uint32_t sw[kScanThreads / 64], slk[kScanThreads / 64];
   const uint32_t per = (nb + kScanThreads - 1) / kScanThreads;
   const uint32_t b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
@@ -342,6 +344,9 @@ __global__ __launch_bounds__(kScanThreads) void k_extra_scan(uint32_t* __restric
     counts[0] += tot - ltot;
     counts[1] += ltot;
     counts[2] = K + tot;
+    // the caller's capacity (the sharded write set): k_extra_write skips
+    // entries past it and the call fails with -ENOSPC
+    if (nospc && static_cast<uint64_t>(K) + tot > cap) *nospc = 1u;
   }
 }
 
@@ -350,7 +355,7 @@ __global__ __launch_bounds__(kThreads) void k_extra_write(
     const uint8_t* __restrict__ grouped, const uint32_t* __restrict__ hitrep,
     const uint32_t* __restrict__ rank, uint32_t first_rank, uint64_t n, ExtraSegs g,
     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ kx, uint32_t* __restrict__ who,
-    uint32_t* __restrict__ obj) {
+    uint32_t* __restrict__ obj, uint32_t cap) {
   __shared__ uint32_t sw[kWaves];
   const uint32_t lane = __lane_id(), wv = threadIdx.x >> 6;
   uint32_t base = kx[0] + cnt[blockIdx.x];  // this segment's first entry
@@ -380,11 +385,13 @@ __global__ __launch_bounds__(kThreads) void k_extra_write(
       const uint64_t i = i0 + k;
       const uint32_t r = rank_of(rank, first_rank, i);
       uint32_t o, w = r;
+      const bool room = pos < cap;
       if (extra_linked((hm >> k) & 1u, hitrep, i, r, o)) {  // keyed: decided by the probe
         w = r | kLinkedBit;
-        obj[pos] = o;
+        if (room) obj[pos] = o;
       }
-      who[pos++] = w;
+      if (room) who[pos] = w;
+      ++pos;
     }
   }
 }
@@ -409,7 +416,7 @@ size_t extra_workspace_bytes(uint64_t) {
 hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uint8_t* grouped,
                              const uint32_t* hitrep, const uint32_t* rank, uint32_t first_rank,
                              uint64_t n, uint32_t* who, uint32_t* obj, uint32_t* counts, void* ws,
-                             hipStream_t s, KTimer* timer) {
+                             hipStream_t s, KTimer* timer, uint32_t cap, uint32_t* nospc) {
   if (n == 0 || (!has && !grouped)) return hipSuccess;  // every row keyed, no probe: nothing extra
   const ExtraSegs g = extra_segs(n);
   uint8_t* b = static_cast<uint8_t*>(ws);
@@ -420,9 +427,9 @@ hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uin
   KScope k(timer, "extra_list", s);
   k_extra_count<<<g.nseg, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, g,
                                             cnt, lk);
-  k_extra_scan<<<1, kScanThreads, 0, s>>>(cnt, lk, g.nseg, kx, counts);
+  k_extra_scan<<<1, kScanThreads, 0, s>>>(cnt, lk, g.nseg, kx, counts, cap, nospc);
   k_extra_write<<<g.nseg, kThreads, 0, s>>>(has, valid, grouped, hitrep, rank, first_rank, n, g,
-                                            cnt, kx, who, obj);
+                                            cnt, kx, who, obj, nospc ? cap : 0xFFFFFFFFu);
   return hipGetLastError();
 }
 

@@ -120,6 +120,11 @@ struct RowsIn {
     return q.row[u];
   }
 };
+// A record whose rank is kPadRank is not a row: the padding and the header
+// slot of a fixed-capacity exchange message (shard.cpp).  Row ranks are below
+// 2^31 on every path that builds records, so no row carries it.
+constexpr uint32_t kPadRank = 0xFFFFFFFFu;
+
 struct RecIn {
   static constexpr bool kHashed = false;
   const uint3* rec;
@@ -128,7 +133,7 @@ struct RecIn {
     const uint3 q = rec[i];
     k = (static_cast<uint64_t>(q.y) << 32) | q.x;
     r = q.z;
-    v = !valid || valid[i] != 0;
+    v = q.z != kPadRank && (!valid || valid[i] != 0);
   }
   __device__ __forceinline__ void get_row(uint64_t i, uint64_t& k, uint32_t& r, uint32_t& row,
                                           bool& v) const {
@@ -157,11 +162,21 @@ struct RecIn {
   __device__ __forceinline__ uint32_t rank_of(const RowBatch<U>& q, int u) const { return q.a[u]; }
   template <int U>
   __device__ __forceinline__ bool valid_of(const RowBatch<U>& q, int u) const {
-    return q.in[u] && (!valid || (q.b[u] & 0xFFu) != 0);
+    return q.in[u] && q.a[u] != kPadRank && (!valid || (q.b[u] & 0xFFu) != 0);
   }
   template <int U>
   __device__ __forceinline__ uint32_t row_of(const RowBatch<U>& q, int u) const {
     return q.row[u];
+  }
+};
+// RecRankIn: exchange records grouped for an output that needs no row index
+// (the Object write set, ListOut): the 12-byte bucket records carry the RANK
+// in their third word (rank_base 0), so the owner's partition moves 12 bytes
+// per row instead of 16 (the Rec12 paths of dedup.hip).
+struct RecRankIn : RecIn {
+  template <int U>
+  __device__ __forceinline__ uint32_t row_of(const RowBatch<U>& q, int u) const {
+    return q.a[u];
   }
 };
 struct Rec16In {

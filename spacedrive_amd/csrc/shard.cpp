@@ -36,6 +36,51 @@
 
 using namespace sdgpu;
 
+namespace {
+
+// One rank's side of one exchange call (all the call's arguments, so a padded
+// call can be re-run through the counted exchange when it is resolved).
+struct RankJob {
+  sdgpu_ctx* c = nullptr;
+  sdgpu_comm* comm = nullptr;
+  sdgpu_index* idx = nullptr;
+  hipStream_t s = nullptr;
+  const uint64_t* key = nullptr;
+  const uint8_t* has = nullptr;
+  const uint32_t* rank = nullptr;
+  uint64_t n = 0;
+  uint32_t* rep = nullptr;
+  // write-set form (sdgpu_group_link_sharded_device): lists of the owned rows
+  const uint8_t* valid = nullptr;
+  uint32_t* who = nullptr;
+  uint32_t* obj = nullptr;
+  uint32_t* counts = nullptr;
+  uint64_t cap = 0;
+  // device workspace
+  uint32_t* srec = nullptr;   // [n][3], or padded [W][C1][3]
+  uint32_t* spos = nullptr;   // [n] send position of row i (~0: keyless / not sent)
+  int64_t* dcnt = nullptr;    // [W] rows to each owner
+  int64_t* xmsg = nullptr;    // [W][3] count messages: {rows to the owner, this rank's n, code}
+  int64_t* rcnt_d = nullptr;  // [W][3] from each source
+  uint32_t* summ = nullptr;   // [8] padded call summary (pad_fill_launch / recv_summary_launch)
+  uint32_t* rrec = nullptr;   // [m][3]
+  uint32_t* rrep = nullptr;   // [m]
+  uint8_t* rvalid = nullptr;  // [m]
+  uint32_t* back = nullptr;   // [total] reps of the sent rows, in send order
+  int64_t* h = nullptr;       // pinned [6W]: send counts, receive messages; pairs out, pairs in
+  std::vector<uint64_t> scnt, rcnt, soff, roff;
+  uint64_t total = 0, m = 0;
+  uint64_t c1 = 0;            // slots per padded message (header included); 0: counted
+  // compact return leg
+  uint2* ret = nullptr;       // [m] pairs this owner returns, grouped by source
+  uint2* rback = nullptr;     // pairs returned to this source
+  int64_t* retcnt = nullptr;  // [W] pairs to each source (device)
+  int64_t* rretcnt = nullptr; // [W] pairs from each owner (device)
+  std::vector<uint64_t> pcnt, pin, poff, pioff;
+};
+
+}  // namespace
+
 struct sdgpu_comm {
   int nranks = 1;
   int rank = 0;
@@ -53,6 +98,23 @@ struct sdgpu_comm {
   // second synchronisation) or SDGPU_RETURN_AUTO (per call, see
   // compact_pays).  Every rank of a communicator must agree.
   int return_mode = SDGPU_RETURN_AUTO;
+  // -ENOSPC of a padded write set resolved at the next call (not that call's
+  // result): returned by the next sdgpu_comm_wait
+  int deferred_rc = 0;
+  // exchange: SDGPU_EXCHANGE_COUNTED / PADDED / AUTO (sdgpu.h).  agreed_n =
+  // B, the largest n of the ranks' last call (every rank learns the same
+  // value: from the count messages, or from the padded messages' headers
+  // when the call is resolved); 0 = unknown (the next call is counted)
+  int exchange = SDGPU_EXCHANGE_AUTO;
+  uint64_t agreed_n = 0;
+  // the padded call not yet resolved: its arguments, and its summary (copied
+  // to pinned memory at the end of the call, summ_evt recorded after it)
+  bool pending = false;
+  bool pending_list = false;
+  uint32_t pending_chunk_rows = 0;
+  RankJob pend;
+  sdgpu::PinBuf summ;
+  hipEvent_t summ_evt = nullptr;
   sdgpu_comm_stats_t stats{};
 };
 
@@ -209,8 +271,11 @@ int index_reserve(sdgpu_index* x, uint64_t add, hipStream_t s) {
 
 // Grouping of one GPU's rows (`in`) with optional Object index: probe, group
 // the rest, insert the creators.  rep[i] for every row.
+// overflow (device, may be null): a padded exchange's "some message
+// overflowed" -- the creators are then not inserted (the call is re-run).
 int group_with_index(sdgpu_ctx* c, sdgpu_index* idx, GroupInput in, uint32_t chunk_rows,
-                     uint32_t* rep, uint8_t* valid_scratch, hipStream_t s) {
+                     uint32_t* rep, uint8_t* valid_scratch, hipStream_t s,
+                     const uint32_t* overflow = nullptr) {
   if (in.n == 0) return 0;
   SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(in.n)));
   if (!idx) {
@@ -222,48 +287,36 @@ int group_with_index(sdgpu_ctx* c, sdgpu_index* idx, GroupInput in, uint32_t chu
   GroupInput g = in;
   g.valid = valid_scratch;
   SD_TRY(dedup_local_launch(g, chunk_rows, rep, false, c->dedup_ws.p, s, c->kt()));
-  SD_TRY(index_creators_launch(idx->ref, in, rep, valid_scratch, s, c->kt()));
+  SD_TRY(index_creators_launch(idx->ref, in, rep, valid_scratch, s, c->kt(), overflow));
   return 0;
 }
 
 // ---- the sharded grouping engine ------------------------------------------------
 
-struct RankJob {
-  sdgpu_ctx* c = nullptr;
-  sdgpu_comm* comm = nullptr;
-  sdgpu_index* idx = nullptr;
-  hipStream_t s = nullptr;
-  const uint64_t* key = nullptr;
-  const uint8_t* has = nullptr;
-  const uint32_t* rank = nullptr;
-  uint64_t n = 0;
-  uint32_t* rep = nullptr;
-  // write-set form (sdgpu_group_link_sharded_device): lists of the owned rows
-  const uint8_t* valid = nullptr;
-  uint32_t* who = nullptr;
-  uint32_t* obj = nullptr;
-  uint32_t* counts = nullptr;
-  uint64_t cap = 0;
-  // device workspace
-  uint32_t* srec = nullptr;   // [n][3]
-  uint32_t* spos = nullptr;   // [n] send position of row i (~0: keyless)
-  int64_t* dcnt = nullptr;    // [W] rows to each owner
-  int64_t* xmsg = nullptr;    // [W][2] count messages: {rows to the owner, this rank's n}
-  int64_t* rcnt_d = nullptr;  // [W][2] from each source: {rows, its n}
-  uint32_t* rrec = nullptr;   // [m][3]
-  uint32_t* rrep = nullptr;   // [m]
-  uint8_t* rvalid = nullptr;  // [m]
-  uint32_t* back = nullptr;   // [total] reps of the sent rows, in send order
-  int64_t* h = nullptr;       // pinned [4W]: send, receive counts; pairs out, pairs in
-  std::vector<uint64_t> scnt, rcnt, soff, roff;
-  uint64_t total = 0, m = 0;
-  // compact return leg
-  uint2* ret = nullptr;       // [m] pairs this owner returns, grouped by source
-  uint2* rback = nullptr;     // pairs returned to this source
-  int64_t* retcnt = nullptr;  // [W] pairs to each source (device)
-  int64_t* rretcnt = nullptr; // [W] pairs from each owner (device)
-  std::vector<uint64_t> pcnt, pin, poff, pioff;
-};
+// Count-message code: the call's form and return setting, which every rank
+// must share (a rank posting the rep return while another does not would
+// leave the collectives unmatched until the deadline): checked by every
+// receiver of the counts, -EPROTO on a mismatch.
+int64_t call_code(const sdgpu_comm* m, bool list) {
+  return (list ? 32 : 16) + m->return_mode;
+}
+
+// Slots per (source, owner) message of a padded exchange, header included;
+// 0 = counted.  C records = a little over the expected share of the largest
+// rank's rows, B / W (binomial spread ~sqrt(B / W), a few thousand rows at
+// config 4), never more than B (a source cannot send more); C + 1 rounded
+// up to 64 slots.  Depends only on what every rank shares (B, W and the
+// modes every rank must set alike), so every rank picks the same layout.
+uint64_t padded_slots(const sdgpu_comm* m, int W, bool rep_form) {
+  if (m->exchange == SDGPU_EXCHANGE_COUNTED) return 0;
+  if (rep_form && m->return_mode == SDGPU_RETURN_COMPACT) return 0;
+  const uint64_t B = m->agreed_n, w = static_cast<uint64_t>(W);
+  if (B == 0 || B >= (1ull << 31)) return 0;
+  const uint64_t C = w == 1 ? B : std::min<uint64_t>(B, B / w + B / (128 * w) + 4096);
+  const uint64_t c1 = align_up(C + 1, 64);
+  if (w * c1 >= (1ull << 32)) return 0;  // slot indices are 32-bit
+  return c1;
+}
 
 // One all-to-all round: rank j sends bytes(j, p) from sendp(j, p) to every p
 // and receives rbytes(j, p) into recvp(j, p) from every p.
@@ -279,6 +332,8 @@ int alltoallv(std::vector<RankJob>& J, int W, Clock::time_point deadline, SP sen
     bool fail = false;
     for (auto& j : J) {
       for (int p = 0; p < W && !fail; ++p) {
+        // a padded exchange's message to this rank itself is already in place
+        if (p == j.comm->rank && sbytes(j, p) == 0 && rbytes(j, p) == 0) continue;
         fail |= !ok(ncclSend(sendp(j, p), sbytes(j, p), ncclUint8, p, j.comm->nccl, j.s));
         fail |= !ok(ncclRecv(recvp(j, p), rbytes(j, p), ncclUint8, p, j.comm->nccl, j.s));
       }
@@ -338,38 +393,46 @@ int alltoallv(std::vector<RankJob>& J, int W, Clock::time_point deadline, SP sen
   return rc;
 }
 
-int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows);
-
-// One exchange step; any failure on an RCCL rank aborts its communicator
-// (bounded failure for the peers) and is returned.
-int run_sharded(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
-  for (auto& j : J)
-    if (j.comm->aborted || (j.comm->transport == SDGPU_TRANSPORT_RCCL && !j.comm->nccl))
-      return -ECONNABORTED;
-  const int rc = run_sharded_impl(J, W, chunk_rows);
-  if (rc != 0)
-    for (auto& j : J)
-      if (j.comm->transport == SDGPU_TRANSPORT_RCCL) comm_fail(j.comm, rc);
-  return rc;
-}
-
 // Steps 1-3 of an exchange, shared by the rep and the write-set forms: every
-// rank's keyed rows partitioned by owner, the count messages (with every
-// rank's n -> n_max, the same on all ranks), the host synchronisation, the
-// records to their owners.  count_ms: host time until the counts were known.
+// rank's keyed rows partitioned by owner, then either
+//   counted (c1 == 0): the count messages (with every rank's n -> n_max, the
+//     same on all ranks, and the call code), the host synchronisation, the
+//     records to their owners in messages of their exact size; or
+//   padded (c1 > 0): the records at fixed slots of c1-slot messages, their
+//     headers and padding written on the device, all messages of one size,
+//     the owners' summary of what arrived (rows, overflow, n_max) left on
+//     the device -- no host synchronisation.
+// count_ms: host time until the counts were known (0 when padded).
 int exchange_forward(std::vector<RankJob>& J, int W, Clock::time_point t_start,
-                     Clock::time_point deadline, uint64_t& n_max, double& count_ms) {
-  // 1. send side: packed records by owner + per-owner counts, on each GPU
+                     Clock::time_point deadline, int64_t code, uint64_t c1, bool list,
+                     uint64_t& n_max, double& count_ms) {
+  auto recv_bufs = [&](RankJob& j) -> int {
+    const size_t o_rep = align_up(12 * j.m, 256);
+    const size_t o_val = align_up(o_rep + 4 * j.m, 256);
+    SD_TRY_RC(ensure_dev(j.c, j.c->xs_recv, o_val + j.m + 256));
+    SD_TRY_RC(ensure_dev(j.c, j.c->xs_back, 4 * j.total + 256));
+    uint8_t* r = static_cast<uint8_t*>(j.c->xs_recv.p);
+    j.rrec = reinterpret_cast<uint32_t*>(r);
+    j.rrep = reinterpret_cast<uint32_t*>(r + o_rep);
+    j.rvalid = r + o_val;
+    j.back = static_cast<uint32_t*>(j.c->xs_back.p);
+    return 0;
+  };
+  // 1. send side: the keyed rows by owner, on each GPU
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
     const uint64_t n = j.n;
-    const size_t o_pos = align_up(12 * n, 256);
+    j.c1 = c1;
+    const uint64_t srecs = c1 ? static_cast<uint64_t>(W) * c1 : n;
+    const size_t o_pos = align_up(12 * srecs, 256);
     const size_t o_dcnt = align_up(o_pos + 4 * n, 256);
     const size_t o_xmsg = align_up(o_dcnt + 8ull * W, 256);
-    const size_t o_rcnt = align_up(o_xmsg + 16ull * W, 256);
-    const size_t o_pcnt = align_up(o_rcnt + 16ull * W, 256);
+    const size_t o_rcnt = align_up(o_xmsg + 24ull * W, 256);
+    const size_t o_pcnt = align_up(o_rcnt + 24ull * W, 256);
     const size_t o_rpcnt = align_up(o_pcnt + 8ull * W, 256);
-    SD_TRY_RC(ensure_dev(j.c, j.c->xs_send, o_rpcnt + 8ull * W));
+    const size_t o_summ = align_up(o_rpcnt + 8ull * W, 256);
+    const size_t o_cur = align_up(o_summ + 32, 256);
+    SD_TRY_RC(ensure_dev(j.c, j.c->xs_send, o_cur + 4ull * W));
     SD_TRY_RC(ensure_dev(j.c, j.c->shard_ws, shard_workspace_bytes(kXShardBits)));
     SD_TRY_RC(ensure_pin(j.c->xs_counts, 64ull * W));
     uint8_t* b = static_cast<uint8_t*>(j.c->xs_send.p);
@@ -380,84 +443,151 @@ int exchange_forward(std::vector<RankJob>& J, int W, Clock::time_point t_start,
     j.rcnt_d = reinterpret_cast<int64_t*>(b + o_rcnt);
     j.retcnt = reinterpret_cast<int64_t*>(b + o_pcnt);
     j.rretcnt = reinterpret_cast<int64_t*>(b + o_rpcnt);
+    j.summ = reinterpret_cast<uint32_t*>(b + o_summ);
+    uint32_t* cursor = reinterpret_cast<uint32_t*>(b + o_cur);
     j.h = static_cast<int64_t*>(j.c->xs_counts.p);
-    SD_TRY(shard_exchange_launch(j.key, j.has, j.rank, n, kXShardBits, W, nullptr, nullptr,
-                                 j.srec, j.spos, j.dcnt, j.c->shard_ws.p, j.s, j.c->kt(),
-                                 j.xmsg));
-  }
-  // 2. count messages all-to-all ({rows for the peer, my n}), then the host
-  // synchronisation
-  SD_TRY_RC(alltoallv(
-      J, W, deadline, [](RankJob& j, int p) -> void* { return j.xmsg + 2 * p; },
-      [](RankJob& j, int p) -> void* { return j.rcnt_d + 2 * p; },
-      [](RankJob&, int) -> size_t { return 16; }, [](RankJob&, int) -> size_t { return 16; }));
-  for (auto& j : J) {
-    SD_TRY(hipSetDevice(j.c->device));
-    SD_TRY(hipMemcpyAsync(j.h, j.dcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
-    SD_TRY(hipMemcpyAsync(j.h + W, j.rcnt_d, 16ull * W, hipMemcpyDeviceToHost, j.s));
-  }
-  n_max = 0;  // every rank's n arrived with the counts: the same on all ranks
-  for (auto& j : J) {
-    SD_TRY(hipSetDevice(j.c->device));
-    if (j.comm->transport == SDGPU_TRANSPORT_RCCL) {
-      SD_TRY_RC(stream_wait(j.comm, j.s, deadline));
+    if (c1) {
+      // fixed slots: the receive buffer is sized now, and the message to
+      // this rank itself is written straight into it (no self copy)
+      j.total = j.m = static_cast<uint64_t>(W) * c1;
+      SD_TRY_RC(recv_bufs(j));
+      const uint32_t me = static_cast<uint32_t>(j.comm->rank), cap = static_cast<uint32_t>(c1 - 1);
+      SD_TRY(padded_partition_launch(j.key, j.has, j.rank, n, static_cast<uint32_t>(W), me, cap,
+                                     j.srec, j.rrec, list ? nullptr : j.spos, cursor, j.s,
+                                     j.c->kt()));
+      SD_TRY(pad_fill_launch(cursor, static_cast<uint32_t>(W), me, cap, n, j.srec, j.rrec, j.summ,
+                             list ? j.counts : nullptr, j.s));
     } else {
-      SD_TRY(hipStreamSynchronize(j.s));
+      SD_TRY(shard_exchange_launch(j.key, j.has, j.rank, n, kXShardBits, W, nullptr, nullptr,
+                                   j.srec, list ? nullptr : j.spos, j.dcnt, j.c->shard_ws.p, j.s,
+                                   j.c->kt(), j.xmsg, code));
     }
-    j.scnt.assign(W, 0);
-    j.rcnt.assign(W, 0);
-    j.soff.assign(W + 1, 0);
-    j.roff.assign(W + 1, 0);
-    for (int p = 0; p < W; ++p) {
-      const int64_t rc = j.h[W + 2 * p], np = j.h[W + 2 * p + 1];
-      if (j.h[p] < 0 || rc < 0 || np < 0) return -EPROTO;
-      n_max = std::max(n_max, static_cast<uint64_t>(np));
-      j.scnt[p] = static_cast<uint64_t>(j.h[p]);
-      j.rcnt[p] = static_cast<uint64_t>(rc);
-      j.soff[p + 1] = j.soff[p] + j.scnt[p];
-      j.roff[p + 1] = j.roff[p] + j.rcnt[p];
-    }
-    j.total = j.soff[W];
-    j.m = j.roff[W];
-    if (j.total > j.n || j.m >= (1ull << 32)) return -EPROTO;
-    const size_t o_rep = align_up(12 * j.m, 256);
-    const size_t o_val = align_up(o_rep + 4 * j.m, 256);
-    SD_TRY_RC(ensure_dev(j.c, j.c->xs_recv, o_val + j.m + 256));
-    SD_TRY_RC(ensure_dev(j.c, j.c->xs_back, 4 * j.total + 256));
-    uint8_t* r = static_cast<uint8_t*>(j.c->xs_recv.p);
-    j.rrec = reinterpret_cast<uint32_t*>(r);
-    j.rrep = reinterpret_cast<uint32_t*>(r + o_rep);
-    j.rvalid = r + o_val;
-    j.back = static_cast<uint32_t*>(j.c->xs_back.p);
   }
-  count_ms = std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
+  if (c1) {
+    n_max = 0;  // known on the device only (resolution)
+    count_ms = 0;
+    for (auto& j : J) {
+      const int me = j.comm->rank;
+      j.scnt.assign(W, c1);
+      j.rcnt.assign(W, c1);
+      j.scnt[me] = j.rcnt[me] = 0;  // already in place
+      j.soff.assign(W + 1, 0);
+      j.roff.assign(W + 1, 0);
+      for (int p = 0; p < W; ++p) {
+        j.soff[p + 1] = j.soff[p] + c1;
+        j.roff[p + 1] = j.roff[p] + c1;
+      }
+    }
+  } else {
+    // 2. count messages all-to-all ({rows for the peer, my n, code}), then the
+    // host synchronisation
+    SD_TRY_RC(alltoallv(
+        J, W, deadline, [](RankJob& j, int p) -> void* { return j.xmsg + 3 * p; },
+        [](RankJob& j, int p) -> void* { return j.rcnt_d + 3 * p; },
+        [](RankJob&, int) -> size_t { return 24; }, [](RankJob&, int) -> size_t { return 24; }));
+    for (auto& j : J) {
+      SD_TRY(hipSetDevice(j.c->device));
+      SD_TRY(hipMemcpyAsync(j.h, j.dcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
+      SD_TRY(hipMemcpyAsync(j.h + W, j.rcnt_d, 24ull * W, hipMemcpyDeviceToHost, j.s));
+    }
+    n_max = 0;  // every rank's n arrived with the counts: the same on all ranks
+    for (auto& j : J) {
+      SD_TRY(hipSetDevice(j.c->device));
+      if (j.comm->transport == SDGPU_TRANSPORT_RCCL) {
+        SD_TRY_RC(stream_wait(j.comm, j.s, deadline));
+      } else {
+        SD_TRY(hipStreamSynchronize(j.s));
+      }
+      j.scnt.assign(W, 0);
+      j.rcnt.assign(W, 0);
+      j.soff.assign(W + 1, 0);
+      j.roff.assign(W + 1, 0);
+      for (int p = 0; p < W; ++p) {
+        const int64_t* msg = j.h + W + 3 * p;
+        const int64_t rc = msg[0], np = msg[1];
+        if (j.h[p] < 0 || rc < 0 || np < 0) return -EPROTO;
+        if (msg[2] != code) return -EPROTO;  // ranks disagree on the form / return leg
+        n_max = std::max(n_max, static_cast<uint64_t>(np));
+        j.scnt[p] = static_cast<uint64_t>(j.h[p]);
+        j.rcnt[p] = static_cast<uint64_t>(rc);
+        j.soff[p + 1] = j.soff[p] + j.scnt[p];
+        j.roff[p + 1] = j.roff[p] + j.rcnt[p];
+      }
+      j.total = j.soff[W];
+      j.m = j.roff[W];
+      if (j.total > j.n || j.m >= (1ull << 32)) return -EPROTO;
+      SD_TRY_RC(recv_bufs(j));
+    }
+    count_ms = std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
+    for (auto& j : J) j.comm->agreed_n = n_max;
+  }
   // 3. the rows, one message per (source, owner) pair
   SD_TRY_RC(alltoallv(
       J, W, deadline, [](RankJob& j, int p) -> void* { return j.srec + 3 * j.soff[p]; },
       [](RankJob& j, int p) -> void* { return j.rrec + 3 * j.roff[p]; },
       [](RankJob& j, int p) -> size_t { return 12 * j.scnt[p]; },
       [](RankJob& j, int p) -> size_t { return 12 * j.rcnt[p]; }));
+  if (c1)
+    for (auto& j : J) {
+      SD_TRY(hipSetDevice(j.c->device));
+      SD_TRY(recv_summary_launch(j.rrec, static_cast<uint32_t>(W), static_cast<uint32_t>(c1 - 1),
+                                 j.summ, j.s));
+    }
   return 0;
 }
 
-int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
+// The received rows of a padded exchange, for the grouping: every slot of
+// the W messages (the grouping drops headers and padding), buckets sized for
+// the rows the ranks hold (B).
+GroupInput received_rows(const RankJob& j) {
+  GroupInput in;
+  in.rec12 = j.rrec;
+  in.n = j.m;
+  if (j.c1) in.bits_rows = std::max<uint64_t>(j.comm->agreed_n, 1);
+  return in;
+}
+
+// Padded call: its summary to pinned memory behind everything it enqueued,
+// and the call pending until resolved (single rank per process), or the
+// payload counted into the stats now (the caller resolves at once).
+int padded_epilogue(std::vector<RankJob>& J, int W, bool rep_form) {
+  for (auto& j : J) {
+    SD_TRY(hipSetDevice(j.c->device));
+    sdgpu_comm* m = j.comm;
+    SD_TRY_RC(ensure_pin(m->summ, 64));
+    if (!m->summ_evt) SD_TRY(hipEventCreateWithFlags(&m->summ_evt, hipEventDisableTiming));
+    SD_TRY(hipMemcpyAsync(m->summ.p, j.summ, 32, hipMemcpyDeviceToHost, j.s));
+    SD_TRY(hipEventRecord(m->summ_evt, j.s));
+    const uint64_t slots = static_cast<uint64_t>(W) * j.c1, mine = j.c1;
+    const uint64_t ret = rep_form ? 4 : 0;
+    sdgpu_comm_stats_t& st = m->stats;
+    st.padded_calls += 1;
+    st.bytes_sent += 12 * slots + ret * slots;
+    st.bytes_received += 12 * slots + ret * slots;
+    st.bytes_remote += 2 * (12 + ret) * (slots - mine);
+    if (rep_form) st.rows_returned += 0;  // counted at resolution (rows received)
+  }
+  return 0;
+}
+
+int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows, uint64_t c1) {
   const auto t_start = Clock::now();
   const Clock::time_point deadline = deadline_of(J[0].comm->timeout_ms);
   uint64_t n_max = 0;
   double count_ms = 0;
-  SD_TRY_RC(exchange_forward(J, W, t_start, deadline, n_max, count_ms));
+  SD_TRY_RC(exchange_forward(J, W, t_start, deadline, call_code(J[0].comm, false), c1, false,
+                             n_max, count_ms));
   // 4. local grouping of the received rows (every key's rows are all here)
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
-    GroupInput in;
-    in.rec12 = j.rrec;
-    in.n = j.m;
-    SD_TRY_RC(group_with_index(j.c, j.idx, in, chunk_rows, j.rrep, j.rvalid, j.s));
+    SD_TRY_RC(group_with_index(j.c, j.idx, received_rows(j), chunk_rows, j.rrep, j.rvalid, j.s,
+                               c1 ? j.summ : nullptr));
   }
-  // 5. reps back to their sources, gathered to row order
+  // 5. reps back to their sources, gathered to row order (a padded call
+  // returns in full: its messages are fixed-size, the compact leg's are not)
   const int mode = J[0].comm->return_mode;
-  const bool compact =
-      mode == SDGPU_RETURN_COMPACT || (mode == SDGPU_RETURN_AUTO && compact_pays(n_max, W));
+  const bool compact = !c1 && (mode == SDGPU_RETURN_COMPACT ||
+                               (mode == SDGPU_RETURN_AUTO && compact_pays(n_max, W)));
   if (!compact) {
     SD_TRY_RC(alltoallv(
         J, W, deadline, [](RankJob& j, int p) -> void* { return j.rrep + j.roff[p]; },
@@ -492,8 +622,8 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
         [](RankJob&, int) -> size_t { return 8; }, [](RankJob&, int) -> size_t { return 8; }));
     for (auto& j : J) {
       SD_TRY(hipSetDevice(j.c->device));
-      SD_TRY(hipMemcpyAsync(j.h + 3 * W, j.retcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
-      SD_TRY(hipMemcpyAsync(j.h + 4 * W, j.rretcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
+      SD_TRY(hipMemcpyAsync(j.h + 4 * W, j.retcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
+      SD_TRY(hipMemcpyAsync(j.h + 5 * W, j.rretcnt, 8ull * W, hipMemcpyDeviceToHost, j.s));
     }
     for (auto& j : J) {
       SD_TRY(hipSetDevice(j.c->device));
@@ -507,7 +637,7 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
       j.poff.assign(W + 1, 0);
       j.pioff.assign(W + 1, 0);
       for (int p = 0; p < W; ++p) {
-        const int64_t a = j.h[3 * W + p], b = j.h[4 * W + p];
+        const int64_t a = j.h[4 * W + p], b = j.h[5 * W + p];
         if (a < 0 || b < 0 || static_cast<uint64_t>(a) > j.rcnt[p] ||
             static_cast<uint64_t>(b) > j.scnt[p])
           return -EPROTO;
@@ -532,23 +662,29 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
         ap.poff[p] = j.pioff[p];
         ap.soff[p] = static_cast<uint32_t>(j.soff[p]);
       }
-      SD_TRY(ret_apply_launch(ap, j.rback, j.back, j.total, j.s));
+      SD_TRY(ret_apply_launch(ap, j.rback, j.back, j.total, j.srec, j.s));
     }
   }
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
-    SD_TRY(gather_rep_launch(j.back, j.spos, j.rank, j.n, j.rep, j.s));
+    const uint64_t me = static_cast<uint64_t>(j.comm->rank);
+    SD_TRY(gather_rep_launch(j.back, j.spos, j.rank, j.n, j.rep, j.s, c1 ? j.rrep : nullptr,
+                             me * c1, (me + 1) * c1));
   }
+  if (c1) SD_TRY_RC(padded_epilogue(J, W, true));
   const double call_ms =
       std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
   for (auto& j : J) {
+    sdgpu_comm_stats_t& st = j.comm->stats;
+    st.calls += 1;
+    st.host_ms += call_ms;
+    j.comm->last_stream = j.s;
+    if (c1) continue;  // the rows are counted when the call is resolved
     // payload of this rank: the 12-B records it sent, the reps it returned
     // as an owner (4 B per received row, or 8-B pairs for the linked ones),
     // and the same for what it received
     const int me = j.comm->rank;
     const uint64_t self_rows = j.scnt[me];
-    sdgpu_comm_stats_t& st = j.comm->stats;
-    st.calls += 1;
     st.rows_sent += j.total;
     st.rows_received += j.m;
     if (compact) {
@@ -566,8 +702,6 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
                          12 * (j.m - j.rcnt[me]) + 4 * (j.total - self_rows);
     }
     st.count_wait_ms += count_ms;
-    st.host_ms += call_ms;
-    j.comm->last_stream = j.s;
   }
   return 0;
 }
@@ -577,52 +711,171 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
 // group kernel of sdgpu_group_link_device, ranks from the records), then
 // appends its OWN valid keyless rows.  No return leg, no gather: the union of
 // the ranks' lists is the write set of all rows (a set, mod.rs:189-333).
-int run_lists_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
+int run_lists_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows, uint64_t c1) {
   const auto t_start = Clock::now();
   const Clock::time_point deadline = deadline_of(J[0].comm->timeout_ms);
   uint64_t n_max = 0;
   double count_ms = 0;
-  SD_TRY_RC(exchange_forward(J, W, t_start, deadline, n_max, count_ms));
-  // no collective follows: a rank whose lists do not fit fails alone
+  SD_TRY_RC(exchange_forward(J, W, t_start, deadline, call_code(J[0].comm, true), c1, true,
+                             n_max, count_ms));
+  // no collective follows: a rank whose lists do not fit fails alone.
+  // Counted: every rank's capacity (owned keyed rows + own keyless rows,
+  // i.e. the rows it did not send) is checked before any list kernel runs,
+  // with every rank's counts zeroed first.  Padded: the owned
+  // rows are known on the device only; the list kernels write nothing past
+  // cap and flag it (summary[4]), the call returns -ENOSPC when resolved.
+  bool nospc = false;
+  for (auto& j : J) {  // (padded: k_pad_fill zeroed the counts)
+    SD_TRY(hipSetDevice(j.c->device));
+    if (c1) continue;
+    SD_TRY(hipMemsetAsync(j.counts, 0, 3 * sizeof(uint32_t), j.s));
+    if (j.m + (j.n - j.total) > j.cap) nospc = true;
+  }
+  if (nospc) return -ENOSPC;
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
-    if (j.m + j.n > j.cap) return -ENOSPC;
-    SD_TRY(hipMemsetAsync(j.counts, 0, 3 * sizeof(uint32_t), j.s));
     SD_TRY_RC(ensure_dev(j.c, j.c->dedup_ws, dedup_workspace_bytes(std::max<uint64_t>(j.m, 1))));
     SD_TRY_RC(ensure_dev(j.c, j.c->link_ws, extra_workspace_bytes(j.n)));
-    GroupInput in;
-    in.rec12 = j.rrec;  // {key, global rank}: 16-B bucket records
-    in.n = j.m;
+    const GroupInput in = received_rows(j);  // {key, global rank}: 12-B bucket records
+    const uint32_t cap32 = static_cast<uint32_t>(std::min<uint64_t>(j.cap, 0xFFFFFFFFull));
+    uint32_t* flag = c1 ? j.summ + 4 : nullptr;
     SD_TRY(dedup_list_launch(in, chunk_rows, j.who, j.obj, j.counts, j.c->dedup_ws.p, j.s,
-                             j.c->kt()));
+                             j.c->kt(), false, nullptr, cap32, flag));
     SD_TRY(extra_list_launch(j.has, j.valid, nullptr, nullptr, j.rank, 0, j.n, j.who, j.obj,
-                             j.counts, j.c->link_ws.p, j.s, j.c->kt()));
+                             j.counts, j.c->link_ws.p, j.s, j.c->kt(), cap32, flag));
   }
+  if (c1) SD_TRY_RC(padded_epilogue(J, W, false));
   const double call_ms =
       std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
   for (auto& j : J) {
-    const int me = j.comm->rank;
     sdgpu_comm_stats_t& st = j.comm->stats;
     st.calls += 1;
+    st.host_ms += call_ms;
+    j.comm->last_stream = j.s;
+    if (c1) continue;
+    const int me = j.comm->rank;
     st.rows_sent += j.total;
     st.rows_received += j.m;
     st.bytes_sent += 12 * j.total;
     st.bytes_received += 12 * j.m;
     st.bytes_remote += 12 * (j.total - j.scnt[me]) + 12 * (j.m - j.rcnt[me]);
     st.count_wait_ms += count_ms;
-    st.host_ms += call_ms;
-    j.comm->last_stream = j.s;
   }
-  (void)n_max;
   return 0;
 }
 
-int run_lists(std::vector<RankJob>& J, int W, uint32_t chunk_rows) {
+// Waits (bounded, the communicator's errors polled) for event ev.
+int event_wait(sdgpu_comm* m, hipEvent_t ev, Clock::time_point deadline) {
+  if (!m->nccl) return hipEventSynchronize(ev) == hipSuccess ? 0 : -EIO;
+  int spins = 0;
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return comm_fail(m, map_err(q));
+    ncclResult_t a = ncclSuccess;
+    if (ncclCommGetAsyncError(m->nccl, &a) != ncclSuccess ||
+        (a != ncclSuccess && a != ncclInProgress))
+      return comm_fail(m, -EIO);
+    if (Clock::now() > deadline) return comm_fail(m, -ETIMEDOUT);
+    backoff(spins);
+  }
+}
+
+// What a finished padded call left in m->summ: the rows it moved are
+// counted, B is updated (every rank read the same headers).  Returns
+// 1 when some message overflowed (re-run counted), -ENOSPC when this rank's
+// lists did not fit, else 0.
+int padded_outcome(sdgpu_comm* m, bool list) {
+  const uint32_t* sm = static_cast<const uint32_t*>(m->summ.p);
+  m->agreed_n = sm[1];
+  sdgpu_comm_stats_t& st = m->stats;
+  st.rows_sent += sm[3];
+  st.rows_received += sm[2];
+  if (!list) st.rows_returned += sm[2];
+  if (sm[0]) return 1;
+  return list && sm[4] ? -ENOSPC : 0;
+}
+
+int run_counted(std::vector<RankJob>& J, int W, uint32_t chunk_rows, bool list) {
+  return list ? run_lists_impl(J, W, chunk_rows, 0) : run_sharded_impl(J, W, chunk_rows, 0);
+}
+
+// Resolves the communicator's pending padded call (single rank per process;
+// the caller holds the call's context lock): waits for its summary, and
+// re-runs it through the counted exchange if some message overflowed --
+// every rank reads the same overflow bit and does the same.  Returns the
+// call's result.
+int resolve_pending(sdgpu_comm* m) {
+  if (!m->pending) return 0;
+  m->pending = false;
+  if (m->aborted) return -ECONNABORTED;
+  const auto t0 = Clock::now();
+  SD_TRY(hipSetDevice(m->device));
+  SD_TRY_RC(event_wait(m, m->summ_evt, deadline_of(m->timeout_ms)));
+  m->stats.resolve_wait_ms += std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+  const int o = padded_outcome(m, m->pending_list);
+  if (o <= 0) return o;
+  m->stats.overflow_reruns += 1;
+  std::vector<RankJob> J(1, m->pend);
+  J[0].s = pick(J[0].c, J[0].s);  // after whatever the context ran since
+  const int rc = run_counted(J, m->nranks, m->pending_chunk_rows, m->pending_list);
+  if (rc != 0 && rc != -ENOSPC && m->transport == SDGPU_TRANSPORT_RCCL) comm_fail(m, rc);
+  return rc;
+}
+
+// One exchange call over J (every rank of the call: one for a process per
+// GPU, all for the _all entry points).  Any failure on an RCCL rank aborts
+// its communicator (bounded failure for the peers) and is
+// returned; -ENOSPC of the write set comes after the last collective and
+// leaves the peers fine.
+int run_call(std::vector<RankJob>& J, int W, uint32_t chunk_rows, bool list) {
   for (auto& j : J)
     if (j.comm->aborted || (j.comm->transport == SDGPU_TRANSPORT_RCCL && !j.comm->nccl))
       return -ECONNABORTED;
-  const int rc = run_lists_impl(J, W, chunk_rows);
-  if (rc != 0 && rc != -ENOSPC)  // -ENOSPC: after the last collective, the peers are fine
+  const bool single = J.size() == 1 && W > 0 && J[0].comm->transport == SDGPU_TRANSPORT_RCCL;
+  if (single) {
+    // the previous call of this communicator first (its overflow re-run, if
+    // any, keeps the collectives in the same order on every rank)
+    const int prc = resolve_pending(J[0].comm);
+    if (prc == -ENOSPC) J[0].comm->deferred_rc = prc;
+    if (prc != 0 && prc != -ENOSPC) return prc;
+    if (J[0].comm->aborted) return -ECONNABORTED;
+  }
+  uint64_t c1 = padded_slots(J[0].comm, W, !list);
+  for (auto& j : J)  // the _all forms: every rank's settings must agree
+    if (padded_slots(j.comm, W, !list) != c1 || j.comm->exchange != J[0].comm->exchange ||
+        j.comm->return_mode != J[0].comm->return_mode)
+      return -EINVAL;
+  int rc = list ? run_lists_impl(J, W, chunk_rows, c1) : run_sharded_impl(J, W, chunk_rows, c1);
+  if (rc == 0 && c1) {
+    if (single) {
+      sdgpu_comm* m = J[0].comm;
+      m->pending = true;
+      m->pending_list = list;
+      m->pending_chunk_rows = chunk_rows;
+      m->pend = J[0];
+      return 0;
+    }
+    // all ranks in this process: resolve now (wait, and re-run counted on
+    // an overflow, which every rank's summary shows alike)
+    bool over = false;
+    int local = 0;
+    for (auto& j : J) {
+      SD_TRY(hipSetDevice(j.c->device));
+      rc = event_wait(j.comm, j.comm->summ_evt, deadline_of(j.comm->timeout_ms));
+      if (rc) break;
+      const int o = padded_outcome(j.comm, list);
+      if (o > 0) over = true;
+      if (o < 0) local = o;
+    }
+    if (rc == 0 && over) {
+      for (auto& j : J) j.comm->stats.overflow_reruns += 1;
+      rc = run_counted(J, W, chunk_rows, list);
+    } else if (rc == 0) {
+      rc = local;
+    }
+  }
+  if (rc != 0 && rc != -ENOSPC)
     for (auto& j : J)
       if (j.comm->transport == SDGPU_TRANSPORT_RCCL) comm_fail(j.comm, rc);
   return rc;
@@ -700,13 +953,34 @@ int sdgpu_comm_set_timeout(sdgpu_comm* m, int timeout_ms) {
 
 int sdgpu_comm_wait(sdgpu_comm* m, void* stream) {
   if (!m) return -EINVAL;
+  if (m->pending) {
+    // the padded call's summary, and its counted re-run on an overflow
+    sdgpu_ctx* c = m->pend.c;
+    std::lock_guard<std::mutex> g(c->mu);
+    const int rc = resolve_pending(m);
+    if (rc != 0) return rc;
+  }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : m->last_stream;
-  if (!s) return 0;
   if (m->aborted) return -ECONNABORTED;
+  if (m->deferred_rc) {
+    const int rc = m->deferred_rc;
+    m->deferred_rc = 0;
+    return rc;
+  }
+  if (!s) return 0;
   SD_TRY(hipSetDevice(m->device));
   if (m->transport != SDGPU_TRANSPORT_RCCL || !m->nccl)
     return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
   return stream_wait(m, s, deadline_of(m->timeout_ms));
+}
+
+int sdgpu_comm_set_exchange(sdgpu_comm* m, int mode, uint64_t rows_hint) {
+  if (!m || (mode != SDGPU_EXCHANGE_AUTO && mode != SDGPU_EXCHANGE_COUNTED &&
+             mode != SDGPU_EXCHANGE_PADDED))
+    return -EINVAL;
+  m->exchange = mode;
+  if (rows_hint) m->agreed_n = rows_hint;
+  return 0;
 }
 
 int sdgpu_comm_set_return(sdgpu_comm* m, int mode) {
@@ -771,6 +1045,18 @@ int sdgpu_comm_init_all(sdgpu_ctx* const* ctx, int ngpu, int transport, sdgpu_co
 
 int sdgpu_comm_destroy(sdgpu_comm* m) {
   if (!m) return -EINVAL;
+  // a pending padded call is dropped (its outputs were never final): its
+  // summary copy is waited for, not re-run (the peers are going away too)
+  if (m->summ_evt) {
+    (void)hipSetDevice(m->device);
+    if (m->pending && m->nccl)
+      (void)event_wait(m, m->summ_evt, deadline_of(m->timeout_ms > 0 ? m->timeout_ms : 10000));
+    else
+      (void)hipEventSynchronize(m->summ_evt);
+    (void)hipEventDestroy(m->summ_evt);
+    m->summ_evt = nullptr;
+  }
+  m->pending = false;
   if (m->nccl) {
     (void)hipSetDevice(m->device);
     // non-blocking communicator: finalize (may report ncclInProgress while
@@ -789,6 +1075,7 @@ int sdgpu_comm_destroy(sdgpu_comm* m) {
     }
     m->nccl = nullptr;
   }
+  if (m->summ.p) (void)hipHostFree(m->summ.p);
   delete m;
   return 0;
 }
@@ -915,7 +1202,7 @@ int sdgpu_group_link_device(sdgpu_ctx* c, sdgpu_index* x, const uint64_t* d_key,
   hipStream_t s = pick(c, stream);
   SD_TRY(hipMemsetAsync(d_counts, 0, 3 * sizeof(uint32_t), s));
   if (n == 0) return 0;
-  SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(n)));
+  SD_TRY_RC(ensure_dev(c, c->dedup_ws, dedup_workspace_bytes(n, !x && d_has_key)));
   SD_TRY_RC(ensure_dev(c, c->link_ws, extra_workspace_bytes(n)));
   GroupInput in;
   in.key = d_key;
@@ -1013,7 +1300,7 @@ int sdgpu_group_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, sdgpu_index* x,
   j.rank = d_rank;
   j.n = n;
   j.rep = d_rep;
-  return run_sharded(J, comm->nranks, chunk_rows);
+  return run_call(J, comm->nranks, chunk_rows, false);
 }
 
 int sdgpu_group_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* comm,
@@ -1056,7 +1343,7 @@ int sdgpu_group_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* com
     j.n = n[r];
     j.rep = d_rep[r];
   }
-  return run_sharded(J, ngpu, chunk_rows);
+  return run_call(J, ngpu, chunk_rows, false);
 }
 
 int sdgpu_group_link_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, const uint64_t* d_key,
@@ -1086,7 +1373,7 @@ int sdgpu_group_link_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, const uint64
   j.obj = d_obj;
   j.counts = d_counts;
   j.cap = cap;
-  return run_lists(J, comm->nranks, chunk_rows);
+  return run_call(J, comm->nranks, chunk_rows, true);
 }
 
 int sdgpu_group_link_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* comm, int ngpu,
@@ -1129,7 +1416,7 @@ int sdgpu_group_link_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const
     j.counts = d_counts[r];
     j.cap = cap[r];
   }
-  return run_lists(J, ngpu, chunk_rows);
+  return run_call(J, ngpu, chunk_rows, true);
 }
 
 int sdgpu_dedup_sharded(sdgpu_ctx* const* ctx, int ngpu, const uint64_t* key,

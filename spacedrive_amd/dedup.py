@@ -275,6 +275,7 @@ TRANSPORT_AUTO, TRANSPORT_RCCL, TRANSPORT_PEER = 0, 1, 2
 
 
 RETURN_FULL, RETURN_COMPACT, RETURN_AUTO = 0, 1, 2  # SDGPU_RETURN_*
+EXCHANGE_AUTO, EXCHANGE_COUNTED, EXCHANGE_PADDED = 0, 1, 2  # SDGPU_EXCHANGE_*
 
 
 class CommStats(ctypes.Structure):
@@ -283,7 +284,8 @@ class CommStats(ctypes.Structure):
                 ("rows_received", ctypes.c_uint64), ("bytes_sent", ctypes.c_uint64),
                 ("bytes_received", ctypes.c_uint64), ("bytes_remote", ctypes.c_uint64),
                 ("count_wait_ms", ctypes.c_double), ("host_ms", ctypes.c_double),
-                ("rows_returned", ctypes.c_uint64)]
+                ("rows_returned", ctypes.c_uint64), ("padded_calls", ctypes.c_uint64),
+                ("overflow_reruns", ctypes.c_uint64), ("resolve_wait_ms", ctypes.c_double)]
 
 
 class Comm:
@@ -323,7 +325,9 @@ class Comm:
               "sdgpu_comm_set_timeout")
 
     def wait(self, stream=None):
-        """Bounded wait for the last exchange's stream (sdgpu_comm_wait)."""
+        """Bounded wait for the last exchange's stream, resolving a padded
+        call (re-run counted on an overflow; its -ENOSPC raised here)
+        (sdgpu_comm_wait)."""
         check(self.ctx.lib.sdgpu_comm_wait(self.h, stream), "sdgpu_comm_wait")
 
     def set_return(self, mode: int):
@@ -331,6 +335,15 @@ class Comm:
         more count exchange), SDGPU_RETURN_FULL (4 B per row) or
         SDGPU_RETURN_AUTO (the default: compact for large calls, sdgpu.h)."""
         check(self.ctx.lib.sdgpu_comm_set_return(self.h, mode), "sdgpu_comm_set_return")
+
+    def set_exchange(self, mode: int, rows_hint: int = 0):
+        """SDGPU_EXCHANGE_PADDED (fixed-capacity messages, no host
+        synchronisation; an overflowed call is re-run counted when resolved),
+        SDGPU_EXCHANGE_COUNTED or SDGPU_EXCHANGE_AUTO (the default: padded
+        once the ranks' row count is known).  rows_hint > 0 sets that count
+        (every rank alike)."""
+        check(self.ctx.lib.sdgpu_comm_set_exchange(self.h, mode, int(rows_hint)),
+              "sdgpu_comm_set_exchange")
 
     def stats(self) -> dict:
         """Cumulative exchange volume / host time of this rank (sdgpu_comm_stats)."""
@@ -367,9 +380,12 @@ class Comm:
 
 
 def group_sharded(key, has_key, rank, comm: Comm, index: ObjectIndex | None = None,
-                  chunk_rows: int = CHUNK_SIZE, out=None):
+                  chunk_rows: int = CHUNK_SIZE, out=None, wait: bool = True):
     """This rank's rep (int32, device) of the grouping over all ranks of `comm`
-    (collective; sdgpu_group_sharded_device: RCCL all-to-all inside libsdgpu)."""
+    (collective; sdgpu_group_sharded_device: RCCL all-to-all inside libsdgpu).
+    wait=True resolves the call before returning (sdgpu_comm_wait: a padded
+    exchange that overflowed is re-run counted); wait=False leaves it to the
+    next exchange call or Comm.wait() -- rep is final only then."""
     import torch
     ctx = comm.ctx
     rep = out if out is not None else torch.empty(key.numel(), dtype=torch.int32,
@@ -379,6 +395,8 @@ def group_sharded(key, has_key, rank, comm: Comm, index: ObjectIndex | None = No
         ctx.h, comm.h, index.h if index is not None else None, key.data_ptr(),
         has_key.data_ptr() if has_key is not None else None, rank.data_ptr(), key.numel(),
         chunk_rows, rep.data_ptr(), s), "sdgpu_group_sharded_device")
+    if wait:
+        comm.wait(s)
     return rep
 
 
@@ -504,8 +522,11 @@ def group_link_sharded(key, has_key, valid, rank, comm, chunk_rows: int = 100,
     the keyed rows it OWNS (hash shard) and of its own valid keyless rows; the
     union over the ranks is the write set of all rows.  rank: int32 global
     ranks (required).  cap: list capacity (default nranks x n + n: enough
-    when every row shares one cas_id and the ranks hold equal shares).  Returns (who, obj, (c, l)) trimmed,
-    or full-length tensors + device counts with trim=False."""
+    when every row shares one cas_id and the ranks hold equal shares).
+    Returns (who, obj, (c, l)) trimmed after resolving the call (Comm.wait:
+    a padded exchange that overflowed is re-run counted, -ENOSPC raised), or
+    full-length tensors + device counts with trim=False (final after the
+    next exchange call or Comm.wait())."""
     import torch
     dev = key.device
     ctx = comm.ctx
@@ -524,6 +545,7 @@ def group_link_sharded(key, has_key, valid, rank, comm, chunk_rows: int = 100,
           "sdgpu_group_link_sharded_device")
     if not trim:
         return who, obj, counts
+    comm.wait(s)
     c, l, e = (int(x) for x in counts.cpu().tolist())
     return who[:e], obj[:e], (c, l)
 

@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     lib = _native.load()
-    assert lib.sdgpu_abi_version() == 4
+    assert lib.sdgpu_abi_version() == 5
     assert lib.sdgpu_strerror(0) == b"success"
     assert lib.sdgpu_strerror(-22) == b"Invalid argument"
 

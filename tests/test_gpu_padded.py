@@ -1,0 +1,184 @@
+"""GPU parity of the padded exchange (round 5): fixed-
+capacity (source, owner) messages whose real counts travel in their first
+slot and are read on the device, so an exchange call enqueues everything
+with no host synchronisation; a call whose messages overflowed is re-run
+through the counted exchange when it is resolved (shard.cpp run_call /
+resolve_pending).  Every result is compared with the oracle's grouping of
+all rows (file_identifier/mod.rs:136-333 canonical rule):
+uniform keys (no overflow), one key repeated 40 k times and an all-one-key
+batch (overflow, re-run) at 1 / 2 / 3 / 8 ranks (peer transport: contexts
+sharing the one GPU) and through a one-rank RCCL communicator."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    from spacedrive_amd._native import Context
+    cs = [Context(0) for _ in range(8)]
+    yield cs
+    for c in cs:
+        c.close()
+
+
+def _rows(case, total, seed):
+    rng = np.random.default_rng(seed)
+    if case == "uniform":
+        k, h, _ = O.synth_dedup_rows(seed, total, int(total * 0.8), 0, total)
+        return k, h
+    pool = rng.integers(0, 2**64 - 1, total, dtype=np.uint64, endpoint=True)
+    k = pool[rng.integers(0, pool.size // 2, total)]
+    if case == "one_key_40k":
+        k[rng.choice(total, 40_000, replace=False)] = pool[7]
+    else:  # all_one_key
+        k[:] = pool[7]
+    h = (rng.random(total) > 0.01).astype(np.uint8)
+    return k, h
+
+
+def _split(k, h, world):
+    import torch
+    keys, hass, ranks, spans = [], [], [], []
+    total = k.size
+    for r in range(world):  # uneven shares
+        a = total * r * (r + 1) // (world * (world + 1))
+        b = total * (r + 1) * (r + 2) // (world * (world + 1))
+        spans.append((a, b))
+        keys.append(torch.from_numpy(k[a:b].view(np.int64)).cuda())
+        hass.append(torch.from_numpy(h[a:b]).cuda())
+        ranks.append(torch.arange(a, b, dtype=torch.int64).to(torch.int32).cuda())
+    return keys, hass, ranks, spans
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("case", ["uniform", "one_key_40k", "all_one_key"])
+def test_padded_rep_form(ctxs, world, case):
+    """sdgpu_group_sharded_all_device through the padded exchange: the reps
+    equal the oracle's; messages overflow exactly when a (source, owner)
+    share exceeds the agreed capacity, and then the call is re-run counted."""
+    from spacedrive_amd import dedup
+    total = 300_000
+    k, h = _rows(case, total, 50 + world)
+    keys, hass, ranks, spans = _split(k, h, world)
+    ref = O.group_reps(k, h, 100)
+    comms = dedup.Comm.init_all(ctxs[:world])
+    B = max(x.numel() for x in keys)
+    for c in comms:
+        c.set_exchange(dedup.EXCHANGE_PADDED, B)
+    reps = dedup.group_sharded_all(keys, hass, ranks, comms, None, 100)
+    out = np.zeros(total, np.uint32)
+    for (a, b), rp in zip(spans, reps):
+        out[a:b] = rp.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(out, ref)
+    sts = [c.stats() for c in comms]
+    assert all(st["padded_calls"] == 1 for st in sts)
+    reruns = {st["overflow_reruns"] for st in sts}
+    assert len(reruns) == 1  # every rank saw the same overflow bit
+    if case == "uniform" or world == 1:
+        assert reruns == {0}
+    else:
+        assert reruns == {1}
+    # the rows actually sent / received (summary words) balance over the ranks
+    assert sum(st["rows_sent"] for st in sts) == sum(st["rows_received"] for st in sts)
+    for c in comms:
+        c.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_padded_with_index_and_overflow(ctxs, world):
+    """Batches through per-rank Object indexes with the padded exchange; the
+    second batch overflows (a key repeated 40 k times): its creators must not
+    reach the index before the counted re-run, and the third batch (padded
+    again, B from the re-run) still equals the oracle over the union --
+    with pre-existing Objects, one of them handle 0x7FFFFFFF (ADVICE r4:
+    SDGPU_REP_EXISTING | 0x7FFFFFFF == ~0 is a legal rep), in the full and
+    the compact return legs."""
+    import torch
+    from spacedrive_amd import dedup
+    total, batch = 450_000, 150_000
+    k, h, _ = O.synth_dedup_rows(61 + world, total, 280_000, 0, total)
+    rng = np.random.default_rng(world)
+    k[batch + rng.choice(batch, 40_000, replace=False)] = k[5]
+    ek = rng.choice(k, 1500)
+    ek[0] = k[5]
+    eh = (np.arange(ek.size, dtype=np.uint32) + 3)
+    eh[0] = 0x7FFFFFFF
+    ref = O.group_reps_existing(k, h, 100, ek, eh)
+    for ret in (dedup.RETURN_FULL, dedup.RETURN_COMPACT):
+        comms = dedup.Comm.init_all(ctxs[:world])
+        for c in comms:
+            c.set_return(ret)  # COMPACT: counted exchange, compact return leg
+            c.set_exchange(dedup.EXCHANGE_AUTO, batch // world + 1)
+        idxs = [dedup.ObjectIndex(c, 1000) for c in ctxs[:world]]
+        for r, ix in enumerate(idxs):
+            ix.add_objects(torch.from_numpy(ek.view(np.int64)).cuda(),
+                           torch.from_numpy(eh.view(np.int32)).cuda(), world, r)
+        torch.cuda.synchronize()
+        out = np.zeros(total, np.uint32)
+        for b0 in range(0, total, batch):
+            keys, hass, ranks, spans = [], [], [], []
+            for r in range(world):
+                a, b = b0 + batch * r // world, b0 + batch * (r + 1) // world
+                spans.append((a, b))
+                keys.append(torch.from_numpy(k[a:b].view(np.int64)).cuda())
+                hass.append(torch.from_numpy(h[a:b]).cuda())
+                ranks.append(torch.arange(a, b, dtype=torch.int64).to(torch.int32).cuda())
+            reps = dedup.group_sharded_all(keys, hass, ranks, comms, idxs, 100)
+            for (a, b), rp in zip(spans, reps):
+                out[a:b] = rp.cpu().numpy().view(np.uint32)
+            bad = np.flatnonzero(out[b0:b0 + batch] != ref[b0:b0 + batch])
+            assert bad.size == 0, (ret, b0, bad.size, bad[:5] + b0, out[b0 + bad[:5]],
+                                   ref[b0 + bad[:5]], comms[0].stats())
+        st = comms[0].stats()
+        if ret == dedup.RETURN_FULL:
+            assert st["padded_calls"] == 3 and st["overflow_reruns"] == 1
+        else:
+            assert st["padded_calls"] == 0
+        for c in comms:
+            c.close()
+
+
+def test_padded_one_rank_rccl_rep_form(ctx):
+    """The rep form through a one-rank RCCL communicator: counted first (B
+    learned), then padded calls back to back with no wait in between
+    (resolved by the next call), an index batch, and a call whose rows
+    exceed B (overflow, re-run counted at resolution); every rep equals the
+    oracle's."""
+    import torch
+    from spacedrive_amd import dedup
+    comm = dedup.Comm.init_rank(ctx, 1, 0, dedup.Comm.unique_id())
+    n = 600_000
+    k, h, rk = O.synth_dedup_rows(67, n, 480_000, 0, n)
+    dk = torch.from_numpy(k.view(np.int64)).cuda()
+    dh = torch.from_numpy(h).cuda()
+    dr = torch.from_numpy(rk.view(np.int32)).cuda()
+    ref = O.group_reps(k, h, 100)
+    rep = dedup.group_sharded(dk, dh, dr, comm, None, 100)  # counted: B unknown
+    np.testing.assert_array_equal(rep.cpu().numpy().view(np.uint32), ref)
+    assert comm.stats()["padded_calls"] == 0
+    outs = [dedup.group_sharded(dk, dh, dr, comm, None, 100, wait=False) for _ in range(3)]
+    comm.wait()
+    for rep in outs:
+        np.testing.assert_array_equal(rep.cpu().numpy().view(np.uint32), ref)
+    st = comm.stats()
+    assert st["padded_calls"] == 3 and st["overflow_reruns"] == 0
+    keyed = int(h.sum())
+    assert st["rows_sent"] == st["rows_received"] == 4 * keyed
+    # B = n now; an index over two batches (the first smaller than B)
+    idx = dedup.ObjectIndex(ctx)
+    out = []
+    for a, b in ((0, 200_000), (200_000, n)):
+        out.append(dedup.group_sharded(dk[a:b], dh[a:b], dr[a:b], comm, idx, 100).cpu().numpy())
+    np.testing.assert_array_equal(np.concatenate(out).view(np.uint32), ref)
+    # after the 400 k-row call B = 400 k: a 600 k-row call overflows, re-run counted
+    s0 = comm.stats()
+    rep = dedup.group_sharded(dk, dh, dr, comm, None, 100)
+    np.testing.assert_array_equal(rep.cpu().numpy().view(np.uint32), ref)
+    s1 = comm.stats()
+    assert s1["padded_calls"] - s0["padded_calls"] == 1
+    assert s1["overflow_reruns"] - s0["overflow_reruns"] == 1
+    comm.close()

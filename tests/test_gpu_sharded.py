@@ -98,6 +98,8 @@ def test_auto_return_takes_the_compact_leg_for_large_calls(ctxs):
     k, h, _ = O.synth_dedup_rows(37, total, int(total * 0.8), 0, total)
     ref = O.group_reps(k, h, 100)
     comms = dedup.Comm.init_all(ctxs[:2])
+    for c in comms:  # the counted exchange's return legs (a padded call returns in full)
+        c.set_exchange(dedup.EXCHANGE_COUNTED)
 
     def run(bounds):
         keys, hass, ranks = [], [], []
@@ -137,7 +139,9 @@ def test_link_sharded_union_is_the_write_set(ctxs, world):
     process): each rank lists the rows it owns + its own keyless rows; the
     union over the ranks equals the oracle's link batch over the grouping of
     all rows, as sets -- uneven shares, keyless and invalid rows, a key
-    repeated 40 k times (one owner gets all its rows)."""
+    repeated 40 k times (one owner gets all its rows).  Once through the
+    counted exchange, once through the padded one (round 5), whose messages
+    overflow on the 40 k-row key at 2 / 3 / 8 ranks and are re-run counted."""
     import torch
     from spacedrive_amd import dedup
     total = 400_000
@@ -155,24 +159,37 @@ def test_link_sharded_union_is_the_write_set(ctxs, world):
         hass.append(torch.from_numpy(h[a:b]).cuda())
         vals.append(torch.from_numpy(valid[a:b]).cuda())
         ranks.append(torch.arange(a, b, dtype=torch.int64).to(torch.int32).cuda())
-    parts = dedup.group_link_sharded_all(keys, hass, vals, ranks, comms, 100)
-    (c, lr, lo), nc, nl = _lists_union(parts)
     rc, rlr, rlo = O.link_batch(O.group_reps(k, h, 100), None, valid, 0)
-    assert (nc, nl) == (rc.size, rlr.size)
-    np.testing.assert_array_equal(c, rc)
-    np.testing.assert_array_equal(lr, rlr)
-    np.testing.assert_array_equal(lo, rlo)
+    for mode in (dedup.EXCHANGE_COUNTED, dedup.EXCHANGE_PADDED):
+        for cm in comms:
+            cm.set_exchange(mode, max(x.numel() for x in keys))
+        before = [cm.stats() for cm in comms]
+        parts = dedup.group_link_sharded_all(keys, hass, vals, ranks, comms, 100)
+        (c, lr, lo), nc, nl = _lists_union(parts)
+        assert (nc, nl) == (rc.size, rlr.size)
+        np.testing.assert_array_equal(c, rc)
+        np.testing.assert_array_equal(lr, rlr)
+        np.testing.assert_array_equal(lo, rlo)
+        for cm, b in zip(comms, before):
+            st = cm.stats()
+            d = {x: st[x] - b[x] for x in st}
+            assert d["rows_returned"] == 0
+            if mode == dedup.EXCHANGE_COUNTED:
+                assert d["bytes_sent"] == 12 * d["rows_sent"] and d["padded_calls"] == 0
+            else:
+                assert d["padded_calls"] == 1
+                assert d["overflow_reruns"] == (1 if world > 1 else 0)
     for cm in comms:
-        st = cm.stats()
-        assert st["rows_returned"] == 0 and st["bytes_sent"] == 12 * st["rows_sent"]
         cm.close()
 
 
 def test_link_sharded_one_rank_rccl(ctx):
     """The write-set form through a one-rank RCCL communicator (the N > 1
-    headline step's code path): equal to the oracle, 12 B per row on the
-    wire, and -ENOSPC for lists that do not fit leaves the communicator
-    usable."""
+    headline step's code path): equal to the oracle, counted (12 B per row on
+    the wire) and padded (round 5: no count exchange, no host wait), and
+    -ENOSPC for lists that do not fit -- from the call when counted, from
+    Comm.wait() when padded (the list kernels write nothing past cap) --
+    leaves the communicator usable."""
     import errno
     import torch
     from spacedrive_amd import dedup
@@ -184,21 +201,46 @@ def test_link_sharded_one_rank_rccl(ctx):
     dh = torch.from_numpy(h).cuda()
     dr = torch.from_numpy(rk.view(np.int32)).cuda()
     rc, rlr, rlo = O.link_batch(O.group_reps(k, h, 100), None, None, 0)
-    for _ in range(2):
-        who, obj, (c, l) = dedup.group_link_sharded(dk, dh, None, dr, comm, 100)
-        torch.cuda.synchronize()
+
+    def check(who, obj, c, l):
         fc, flr, flo = dedup.split_link_lists(who.cpu().numpy(), obj.cpu().numpy())
         assert (c, l) == (rc.size, rlr.size)
         np.testing.assert_array_equal(fc, rc)
         np.testing.assert_array_equal(flr, rlr)
         np.testing.assert_array_equal(flo, rlo)
-    with pytest.raises(SdgpuError) as e:
-        dedup.group_link_sharded(dk, dh, None, dr, comm, 100, cap=1000)
-    assert e.value.rc == -errno.ENOSPC
+
+    for mode in (dedup.EXCHANGE_COUNTED, dedup.EXCHANGE_AUTO):
+        comm.set_exchange(mode)
+        s0 = comm.stats()
+        for _ in range(2):
+            who, obj, (c, l) = dedup.group_link_sharded(dk, dh, None, dr, comm, 100)
+            check(who, obj, c, l)
+        d = {x: comm.stats()[x] - s0[x] for x in s0}
+        if mode == dedup.EXCHANGE_COUNTED:
+            assert d["rows_returned"] == 0 and d["bytes_sent"] == 12 * d["rows_sent"]
+        else:  # one rank: the message holds all n rows, header + 64-slot rounding
+            assert d["padded_calls"] == 2 and d["overflow_reruns"] == 0
+            assert d["count_wait_ms"] == 0
+            assert d["bytes_sent"] == 2 * 12 * ((n + 1 + 63) // 64 * 64)
+        with pytest.raises(SdgpuError) as e:
+            dedup.group_link_sharded(dk, dh, None, dr, comm, 100, cap=1000)
+        assert e.value.rc == -errno.ENOSPC
+        who, obj, (c, l) = dedup.group_link_sharded(dk, dh, None, dr, comm, 100)
+        check(who, obj, c, l)
+    # trim=False calls back to back, resolved by the next call / wait
+    comm.set_exchange(dedup.EXCHANGE_AUTO)
+    outs = [dedup.group_link_sharded(dk, dh, None, dr, comm, 100, trim=False) for _ in range(3)]
+    comm.wait()
+    for who, obj, cnt in outs[-1:]:
+        c, l, e = (int(x) for x in cnt.cpu().tolist())
+        check(who[:e], obj[:e], c, l)
+    # a padded message too small (B below this call's rows): overflow, re-run counted
+    comm.set_exchange(dedup.EXCHANGE_PADDED, n // 2)
+    s0 = comm.stats()
     who, obj, (c, l) = dedup.group_link_sharded(dk, dh, None, dr, comm, 100)
-    assert (c, l) == (rc.size, rlr.size)
-    st = comm.stats()
-    assert st["rows_returned"] == 0 and st["bytes_sent"] == 12 * st["rows_sent"]
+    check(who, obj, c, l)
+    d = {x: comm.stats()[x] - s0[x] for x in s0}
+    assert d["padded_calls"] == 1 and d["overflow_reruns"] == 1
     comm.close()
 
 
@@ -212,6 +254,7 @@ def test_rccl_transport_one_rank(ctx):
     uid = dedup.Comm.unique_id()
     comm = dedup.Comm.init_rank(ctx, 1, 0, uid)
     assert comm.info() == (1, 0, dedup.TRANSPORT_RCCL)
+    comm.set_exchange(dedup.EXCHANGE_COUNTED)  # the padded exchange: test_gpu_padded.py
     comm.set_return(dedup.RETURN_COMPACT)  # the default (AUTO) picks FULL at this size
     k, h, rk = O.synth_dedup_rows(29, 500_000, 400_000, 0, 500_000)
     dk = torch.from_numpy(k.view(np.int64)).cuda()
