@@ -366,6 +366,24 @@ class Runner:
             log(f"bench: identifier job step failed: {e!r}")
             res["job"] = {"error": repr(e)[:400]}
             return self._finish_cas(res, lens, blk, par)
+        if self.world == 1 and self.comm is not None:
+            # one-rank rehearsal (SD_BENCH_FORCE_COMM=1): the step through the
+            # communicator against the fused one-GPU step in the SAME process,
+            # interleaved A B A B ... so K1's clock (which ramps after every
+            # idle gap by more than the exchange costs) cancels out
+            def job_fused():
+                k1()
+                dedup.group_link_device(out.view(torch.int64).view(-1), has, None, None, 0, 100,
+                                        ctx=self.ctx, trim=False)
+            ab = {"comm": [], "fused": []}
+            for _ in range(3):
+                ab["comm"].append(1e3 * self.timed(job, steps, warmup) / steps)
+                ab["fused"].append(1e3 * self.timed(job_fused, steps, warmup) / steps)
+            med = {k: sorted(v)[len(v) // 2] for k, v in ab.items()}
+            res["job"]["vs_fused_same_process"] = {
+                "comm_ms_per_step": med["comm"], "fused_ms_per_step": med["fused"],
+                "delta_ms": med["comm"] - med["fused"], "rounds": ab,
+                "note": "medians of 3 interleaved rounds of `steps` steps each"}
         if self.world == 1 and self.comm is None:
             # the same step captured once into a HIP graph and replayed (fixed
             # buffers and shapes: what a host re-running same-size device

@@ -169,6 +169,12 @@ struct sdgpu_ctx {
   // records, their reps, the returned reps; host copies of the counts
   DevBuf xs_send, xs_recv, xs_back, xs_ret, xs_rback;
   PinBuf xs_counts;
+  // padded exchange: two sets of 64 reservation cursors used alternately
+  // (each call's k_pad_fill zeroes the other set for the next call), and the
+  // keyless-row segments of the write set's partition
+  DevBuf xs_cursor, xs_sink;
+  uint32_t xs_parity = 0;
+  bool xs_cursor_clean = false;
   bool timing = false;
   bool io_uring = false;  // sdgpu_identify_files reads through io_uring (uring.hpp)
   EventTimer timer;

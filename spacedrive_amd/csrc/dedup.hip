@@ -344,17 +344,21 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
 // order -- the grouping reads ranks, not positions.  Slots past cap are not
 // written (cursor[d] > cap: k_pad_fill raises the overflow bit).  out_pos
 // (rep form; null for the write set): the send slot of row i, ~0 for keyless
-// or unsent rows.  Round r + 1's rows are loaded before round r's atomics.
+// or unsent rows.  xs (the write set): the valid keyless rows are collected
+// into the XSink segments on the way (as the fused call's first pass does),
+// for the owner's k_list_finish -- no extra-entry pass.  Round r + 1's rows
+// are loaded before round r's atomics.
 constexpr int kPadU = 4;
 constexpr uint32_t kPadR = kPadU * kPartThreads;
 constexpr uint32_t kXShardBitsDev = 8;  // shard = top 8 hash bits (shard.cpp kXShardBits)
 __global__ __launch_bounds__(kPartThreads) void k_part_padded(
     RowsIn in, uint64_t n, uint32_t world, uint32_t me, uint32_t cap, uint3* __restrict__ out,
     uint3* __restrict__ self_out, uint32_t* __restrict__ out_pos,
-    uint32_t* __restrict__ cursor) {
+    uint32_t* __restrict__ cursor, XSink xs) {
   __shared__ uint3 buf[kPadR];
   __shared__ uint32_t cnt[kMaxWorld], lb[kMaxWorld + 1], gb[kMaxWorld];
   const uint64_t c1 = cap + 1ull;
+  uint32_t wn = 0;  // the wave's keyless rows (XSink)
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
   auto round = [&](const RowBatch<kPadU>& q, uint64_t i0) {
@@ -367,6 +371,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part_padded(
       const uint32_t d = v ? part_digit(row_hash(in.key_of(q, u)), 0, kXShardBitsDev, world) : 0u;
       lr[u] = wave_add(cnt, d, v);
       dg[u] = v ? d : ~0u;
+      if (xs.st)  // uniform; a ballot, and a store only for the rare valid keyless row
+        sink_keyless(xs, in, q.in[u] && !v, i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads,
+                     wn);
     }
     lds_barrier();
     if (threadIdx.x < 64) {  // one wave: the round's run starts and the reservations
@@ -425,6 +432,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_padded(
       if (i0 + 2 * kPadR >= t1) break;
     }
   }
+  if (xs.st) sink_count(xs, wn);
 }
 
 // Bucket partition writing ONE 16-byte record {hash lo, hash hi, rank, row}
@@ -1427,9 +1435,12 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* sw) {
   __syncthreads();  // sw reusable
   return t;
 }
+// cap / nospc: the caller's list capacity (ListOut); sink rows past it are
+// not written and the total past it raises *nospc.
 __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict__ lcnt,
                                                       uint32_t nb, uint32_t* __restrict__ counts,
-                                                      uint32_t* __restrict__ who, XSink xs) {
+                                                      uint32_t* __restrict__ who, XSink xs,
+                                                      uint32_t cap, uint32_t* __restrict__ nospc) {
   __shared__ uint32_t sw[16], sseg[kSinkWaves];
   constexpr uint32_t kPerT = kPartBlocks * kSinkWaves / 1024;
   static_assert(kPartBlocks * kSinkWaves % 1024 == 0, "segments per thread");
@@ -1467,6 +1478,7 @@ __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict
       counts[1] = L;
       counts[0] = K - L + E;
       counts[2] = K + E;
+      if (nospc && static_cast<uint64_t>(K) + E > cap) *nospc = 1u;
     }
     return;
   }
@@ -1475,7 +1487,8 @@ __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict
   for (uint32_t w = 0; w < wv; ++w) o += sseg[w];
   const uint32_t c = sseg[wv];
   const uint32_t* src = xs.st + static_cast<uint64_t>(seg0 + wv) * xs.cap;
-  for (uint32_t k = lane; k < c; k += 64) who[o + k] = src[k];
+  for (uint32_t k = lane; k < c; k += 64)
+    if (o + k < cap) who[o + k] = src[k];
 }
 hipError_t out_finish(const RepOut&, uint32_t, hipStream_t) { return hipSuccess; }
 // ListOut: each wave's entries are placed by ONE LDS atomic per (step, list)
@@ -1545,7 +1558,8 @@ __device__ __forceinline__ void out_done(const ListOut& o, uint32_t, uint32_t, u
 __device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t,
                                          const uint32_t*) {}
 hipError_t out_finish(const ListOut& o, uint32_t nb, hipStream_t s) {
-  k_list_finish<<<o.x.st ? 1 + kPartBlocks : 1u, 1024, 0, s>>>(o.lcnt, nb, o.counts, o.who, o.x);
+  k_list_finish<<<o.x.st ? 1 + kPartBlocks : 1u, 1024, 0, s>>>(o.lcnt, nb, o.counts, o.who, o.x,
+                                                                 o.cap, o.nospc);
   return hipGetLastError();
 }
 
@@ -2018,7 +2032,8 @@ __global__ __launch_bounds__(256) void k_pad_fill(const uint32_t* __restrict__ c
                                                   uint3* __restrict__ out,
                                                   uint3* __restrict__ self_out,
                                                   uint32_t* __restrict__ summary,
-                                                  uint32_t* __restrict__ zero3) {
+                                                  uint32_t* __restrict__ zero3,
+                                                  uint32_t* __restrict__ next_cursor) {
   const uint32_t d = blockIdx.y;
   bool ovf = false;
   uint32_t sent = 0;
@@ -2035,9 +2050,17 @@ __global__ __launch_bounds__(256) void k_pad_fill(const uint32_t* __restrict__ c
     if (d == 0) {
       summary[3] = sent;
       summary[4] = 0u;
+      if (world == 1) {  // nothing to receive: the owner's summary is this one
+        summary[0] = ovf ? 1u : 0u;
+        summary[1] = n;
+        summary[2] = sent;
+      }
       if (zero3) zero3[0] = zero3[1] = zero3[2] = 0u;
     }
   }
+  // the next call's reservation cursors (the previous call used them; this
+  // call's stay untouched while its blocks read them)
+  if (blockIdx.x == 0 && threadIdx.x == 0) next_cursor[d] = 0u;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
   for (uint64_t j = min(c, cap) + static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; j < cap;
        j += stride)
@@ -2582,7 +2605,7 @@ hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_
 hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* who,
                              uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
                              KTimer* timer, bool sink_keyless, const uint8_t* keyless_valid,
-                             uint32_t cap, uint32_t* nospc) {
+                             uint32_t cap, uint32_t* nospc, const KeylessSink* moved) {
   if (in.n == 0) return hipSuccess;
   uint8_t* w = static_cast<uint8_t*>(ws);
   const bool sink = sink_keyless && !in.rec12 && in.valid;
@@ -2597,6 +2620,11 @@ hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t
     out.x.st = reinterpret_cast<uint32_t*>(w + L.xst);
     out.x.cnt = reinterpret_cast<uint32_t*>(w + L.xcnt);
     out.x.cap = sink_cap(in.n);
+  } else if (moved) {  // segments filled by the exchange's partition (k_part_padded)
+    out.x.valid = moved->valid;
+    out.x.st = moved->st;
+    out.x.cnt = moved->cnt;
+    out.x.cap = moved->cap;
   }
   if (in.rec12)  // the list needs no row index: 12-byte bucket records carrying the rank
     return group_launch(RecRankIn{{reinterpret_cast<const uint3*>(in.rec12), in.valid}}, in.n,
@@ -2708,26 +2736,39 @@ hipError_t gather_rep_launch(const uint32_t* back, const uint32_t* pos, const ui
 hipError_t padded_partition_launch(const uint64_t* key, const uint8_t* has_key,
                                    const uint32_t* rank, uint64_t n, uint32_t world, uint32_t me,
                                    uint32_t cap, uint32_t* out_rec12, uint32_t* self_rec12,
-                                   uint32_t* out_pos, uint32_t* cursor, hipStream_t s,
-                                   KTimer* timer) {
-  hipError_t e = hipMemsetAsync(cursor, 0, 4ull * world, s);
-  if (e != hipSuccess) return e;
+                                   uint32_t* out_pos, uint32_t* cursor, const KeylessSink* sink,
+                                   hipStream_t s, KTimer* timer) {
+  XSink xs{};
+  if (sink) {
+    xs.valid = sink->valid;
+    xs.st = sink->st;
+    xs.cnt = sink->cnt;
+    xs.cap = sink->cap;
+  }
   if (n) {
     KScope k(timer, "shard_padded", s);
     k_part_padded<<<kPartBlocks, kPartThreads, 0, s>>>(
         RowsIn{key, has_key, rank, 0}, n, world, me, cap, reinterpret_cast<uint3*>(out_rec12),
-        reinterpret_cast<uint3*>(self_rec12), out_pos, cursor);
+        reinterpret_cast<uint3*>(self_rec12), out_pos, cursor, xs);
+  } else if (sink) {  // no rows: the segments are empty
+    const hipError_t e =
+        hipMemsetAsync(sink->cnt, 0, 4ull * keyless_sink_segments(), s);
+    if (e != hipSuccess) return e;
   }
   return hipGetLastError();
 }
 
+uint32_t keyless_sink_segments() { return kPartBlocks * kSinkWaves; }
+uint32_t keyless_sink_cap(uint64_t n) { return sink_cap(n); }
+
 hipError_t pad_fill_launch(const uint32_t* cursor, uint32_t world, uint32_t me, uint32_t cap,
                            uint64_t n, uint32_t* rec12, uint32_t* self_rec12, uint32_t* summary,
-                           uint32_t* zero3, hipStream_t s) {
+                           uint32_t* zero3, uint32_t* next_cursor, hipStream_t s) {
   const uint32_t bx = std::min<uint32_t>(64u, (cap + 1023u) / 1024u + 1u);
   k_pad_fill<<<dim3(bx, world), 256, 0, s>>>(cursor, world, me, cap, static_cast<uint32_t>(n),
                                              reinterpret_cast<uint3*>(rec12),
-                                             reinterpret_cast<uint3*>(self_rec12), summary, zero3);
+                                             reinterpret_cast<uint3*>(self_rec12), summary, zero3,
+                                             next_cursor);
   return hipGetLastError();
 }
 

@@ -168,14 +168,27 @@ hipError_t dedup_local_launch(const GroupInput& in, uint32_t chunk_rows, uint32_
 // partition pass also lists the valid keyless rows (keyless_valid[i] != 0,
 // null: all) as creators behind the keyed entries -- what extra_list_launch
 // does without an index, with no pass of its own.
+// The valid keyless rows of a write set collected by a partition pass into
+// per-wave segments (dedup.hip XSink): kPartBlocks x 16 segments of cap rows
+// (keyless_sink_cap of the partitioned rows), their counts in cnt.
+struct KeylessSink {
+  const uint8_t* valid = nullptr;  // null: every keyless row is valid
+  uint32_t* st = nullptr;
+  uint32_t* cnt = nullptr;
+  uint32_t cap = 0;
+};
+uint32_t keyless_sink_segments();
+uint32_t keyless_sink_cap(uint64_t n);
 // nospc (non-null): who / obj hold cap entries; a bucket past them writes
 // nothing and sets *nospc (the sharded write set's -ENOSPC, decided on the
-// device).
+// device).  moved (may be null): keyless-row segments filled earlier (the
+// padded exchange's partition) that the list's finish moves behind the keyed
+// entries.
 hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t* who,
                              uint32_t* obj, uint32_t* counts, void* ws, hipStream_t s,
                              KTimer* timer = nullptr, bool sink_keyless = false,
                              const uint8_t* keyless_valid = nullptr, uint32_t cap = 0xFFFFFFFFu,
-                             uint32_t* nospc = nullptr);
+                             uint32_t* nospc = nullptr, const KeylessSink* moved = nullptr);
 // extra_list_launch then appends, in row order, the valid keyless rows and
 // (with an index: grouped = the probe's mask, hitrep = its reps) the keyed
 // rows the probe decided -- the index path, the owner's keyless rows of the
@@ -246,18 +259,20 @@ hipError_t gather_rep_launch(const uint32_t* back, const uint32_t* pos, const ui
 // destination rank, dedup.hip k_part_padded / k_pad_fill): one pass writes
 // the keyed rows into their owners' messages -- the message to rank `me`
 // into self_rec12 (the receive buffer), the others into rec12 -- reserving
-// slots through cursor[world] (device u32, zeroed here); out_pos (may be
-// null): send slot of each row, ~0 for keyless / unsent rows.  Then the
-// headers + padding from the cursors; summary (device u32[8]): [3] rows
-// sent, [4] = 0; zero3 (may be null) zeroed.
+// slots through cursor[world] (device u32, zero on entry); out_pos (may be
+// null): send slot of each row, ~0 for keyless / unsent rows; sink (may be
+// null, the write set): the valid keyless rows collected.  Then the headers
+// + padding from the cursors; summary (device u32[8]): [3] rows sent, [4] =
+// 0 (one rank: [0..2] too, nothing is received); zero3 (may be null) and
+// next_cursor[world] (the next call's cursors) zeroed.
 hipError_t padded_partition_launch(const uint64_t* key, const uint8_t* has_key,
                                    const uint32_t* rank, uint64_t n, uint32_t world, uint32_t me,
                                    uint32_t cap, uint32_t* out_rec12, uint32_t* self_rec12,
-                                   uint32_t* out_pos, uint32_t* cursor, hipStream_t s,
-                                   KTimer* timer = nullptr);
+                                   uint32_t* out_pos, uint32_t* cursor, const KeylessSink* sink,
+                                   hipStream_t s, KTimer* timer = nullptr);
 hipError_t pad_fill_launch(const uint32_t* cursor, uint32_t world, uint32_t me, uint32_t cap,
                            uint64_t n, uint32_t* rec12, uint32_t* self_rec12, uint32_t* summary,
-                           uint32_t* zero3, hipStream_t s);
+                           uint32_t* zero3, uint32_t* next_cursor, hipStream_t s);
 // summary [0] some message overflowed (every rank alike), [1] largest source
 // n, [2] rows received, from the received headers.
 hipError_t recv_summary_launch(const uint32_t* rrec12, uint32_t world, uint32_t cap,

@@ -71,6 +71,7 @@ struct RankJob {
   std::vector<uint64_t> scnt, rcnt, soff, roff;
   uint64_t total = 0, m = 0;
   uint64_t c1 = 0;            // slots per padded message (header included); 0: counted
+  KeylessSink sink;           // padded write set: this rank's valid keyless rows
   // compact return leg
   uint2* ret = nullptr;       // [m] pairs this owner returns, grouped by source
   uint2* rback = nullptr;     // pairs returned to this source
@@ -431,8 +432,7 @@ int exchange_forward(std::vector<RankJob>& J, int W, Clock::time_point t_start,
     const size_t o_pcnt = align_up(o_rcnt + 24ull * W, 256);
     const size_t o_rpcnt = align_up(o_pcnt + 8ull * W, 256);
     const size_t o_summ = align_up(o_rpcnt + 8ull * W, 256);
-    const size_t o_cur = align_up(o_summ + 32, 256);
-    SD_TRY_RC(ensure_dev(j.c, j.c->xs_send, o_cur + 4ull * W));
+    SD_TRY_RC(ensure_dev(j.c, j.c->xs_send, o_summ + 32));
     SD_TRY_RC(ensure_dev(j.c, j.c->shard_ws, shard_workspace_bytes(kXShardBits)));
     SD_TRY_RC(ensure_pin(j.c->xs_counts, 64ull * W));
     uint8_t* b = static_cast<uint8_t*>(j.c->xs_send.p);
@@ -444,7 +444,6 @@ int exchange_forward(std::vector<RankJob>& J, int W, Clock::time_point t_start,
     j.retcnt = reinterpret_cast<int64_t*>(b + o_pcnt);
     j.rretcnt = reinterpret_cast<int64_t*>(b + o_rpcnt);
     j.summ = reinterpret_cast<uint32_t*>(b + o_summ);
-    uint32_t* cursor = reinterpret_cast<uint32_t*>(b + o_cur);
     j.h = static_cast<int64_t*>(j.c->xs_counts.p);
     if (c1) {
       // fixed slots: the receive buffer is sized now, and the message to
@@ -452,11 +451,34 @@ int exchange_forward(std::vector<RankJob>& J, int W, Clock::time_point t_start,
       j.total = j.m = static_cast<uint64_t>(W) * c1;
       SD_TRY_RC(recv_bufs(j));
       const uint32_t me = static_cast<uint32_t>(j.comm->rank), cap = static_cast<uint32_t>(c1 - 1);
+      // reservation cursors: two sets used alternately, each call's pad
+      // fill zeroing the next call's (no memset launch per call)
+      sdgpu_ctx* c = j.c;
+      SD_TRY_RC(ensure_dev(c, c->xs_cursor, 2 * 64 * sizeof(uint32_t)));
+      if (!c->xs_cursor_clean) {
+        SD_TRY(hipMemsetAsync(c->xs_cursor.p, 0, 2 * 64 * sizeof(uint32_t), j.s));
+        c->xs_cursor_clean = true;
+      }
+      uint32_t* cur = static_cast<uint32_t*>(c->xs_cursor.p) + 64 * c->xs_parity;
+      uint32_t* next = static_cast<uint32_t*>(c->xs_cursor.p) + 64 * (c->xs_parity ^ 1u);
+      j.sink = KeylessSink{};
+      if (list) {  // the valid keyless rows, collected by the partition
+        const uint32_t segs = keyless_sink_segments(), scap = keyless_sink_cap(n);
+        const size_t o_cnt = align_up(4ull * segs * scap, 256);
+        SD_TRY_RC(ensure_dev(c, c->xs_sink, o_cnt + 4ull * segs));
+        j.sink.valid = j.valid;
+        j.sink.st = static_cast<uint32_t*>(c->xs_sink.p);
+        j.sink.cnt = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(c->xs_sink.p) + o_cnt);
+        j.sink.cap = scap;
+      }
+      c->xs_cursor_clean = false;  // until the pad fill below is queued
       SD_TRY(padded_partition_launch(j.key, j.has, j.rank, n, static_cast<uint32_t>(W), me, cap,
-                                     j.srec, j.rrec, list ? nullptr : j.spos, cursor, j.s,
-                                     j.c->kt()));
-      SD_TRY(pad_fill_launch(cursor, static_cast<uint32_t>(W), me, cap, n, j.srec, j.rrec, j.summ,
-                             list ? j.counts : nullptr, j.s));
+                                     j.srec, j.rrec, list ? nullptr : j.spos, cur,
+                                     list ? &j.sink : nullptr, j.s, j.c->kt()));
+      SD_TRY(pad_fill_launch(cur, static_cast<uint32_t>(W), me, cap, n, j.srec, j.rrec, j.summ,
+                             list ? j.counts : nullptr, next, j.s));
+      c->xs_cursor_clean = true;
+      c->xs_parity ^= 1u;
     } else {
       SD_TRY(shard_exchange_launch(j.key, j.has, j.rank, n, kXShardBits, W, nullptr, nullptr,
                                    j.srec, list ? nullptr : j.spos, j.dcnt, j.c->shard_ws.p, j.s,
@@ -527,7 +549,7 @@ int exchange_forward(std::vector<RankJob>& J, int W, Clock::time_point t_start,
       [](RankJob& j, int p) -> void* { return j.rrec + 3 * j.roff[p]; },
       [](RankJob& j, int p) -> size_t { return 12 * j.scnt[p]; },
       [](RankJob& j, int p) -> size_t { return 12 * j.rcnt[p]; }));
-  if (c1)
+  if (c1 && W > 1)  // (one rank: the pad fill wrote the summary)
     for (auto& j : J) {
       SD_TRY(hipSetDevice(j.c->device));
       SD_TRY(recv_summary_launch(j.rrec, static_cast<uint32_t>(W), static_cast<uint32_t>(c1 - 1),
@@ -739,10 +761,13 @@ int run_lists_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows, uint64_t
     const GroupInput in = received_rows(j);  // {key, global rank}: 12-B bucket records
     const uint32_t cap32 = static_cast<uint32_t>(std::min<uint64_t>(j.cap, 0xFFFFFFFFull));
     uint32_t* flag = c1 ? j.summ + 4 : nullptr;
+    // padded: the own valid keyless rows were collected by the partition and
+    // the list's finish moves them; counted: the extra-entry pass lists them
     SD_TRY(dedup_list_launch(in, chunk_rows, j.who, j.obj, j.counts, j.c->dedup_ws.p, j.s,
-                             j.c->kt(), false, nullptr, cap32, flag));
-    SD_TRY(extra_list_launch(j.has, j.valid, nullptr, nullptr, j.rank, 0, j.n, j.who, j.obj,
-                             j.counts, j.c->link_ws.p, j.s, j.c->kt(), cap32, flag));
+                             j.c->kt(), false, nullptr, cap32, flag, c1 ? &j.sink : nullptr));
+    if (!c1)
+      SD_TRY(extra_list_launch(j.has, j.valid, nullptr, nullptr, j.rank, 0, j.n, j.who, j.obj,
+                               j.counts, j.c->link_ws.p, j.s, j.c->kt()));
   }
   if (c1) SD_TRY_RC(padded_epilogue(J, W, false));
   const double call_ms =
