@@ -1208,6 +1208,24 @@ class Runner:
         if lv[0] > 0:
             res["leaf_valu_frac_spec"] = comp * ISA_PER_COMPRESSION / (lv[0] / lv[1] * 1e-3) \
                 / VALU_PEAK_SPEC
+        if not self.args.no_cpu and files:
+            # parity of the timed batch (after the timing):
+            # the first, the last and two middle digests of the ONE plan the
+            # bench times (cross-file offsets past 2^32 bytes) against the
+            # oracle's multi-threaded AVX-512 hasher over the same bytes
+            from oracle import oracle as O
+            threads, _ = host_cores()
+            picks = sorted({0, len(files) // 3, 2 * len(files) // 3, len(files) - 1})
+            got = out.cpu().numpy()
+            bad, t0 = 0, time.perf_counter()
+            for i in picks:
+                host = files[i].cpu().numpy()
+                bad += int(bytes(got[i]) != O.blake3(host, threads=threads))
+                del host
+            res["gpu_digest_mismatches"] = bad
+            res["digests_checked"] = {"files": picks, "threads": threads,
+                                      "seconds": time.perf_counter() - t0,
+                                      "checker": "oracle blake3 (AVX-512 16-way, multi-threaded)"}
         del files
         return res
 
@@ -1393,7 +1411,9 @@ def start_watchdog(writer: LineWriter, seconds: float, state: dict):
         writer.emit()
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0 if writer.line.get("value") is not None else 3)
+        # non-zero either way (a hung leg must not look
+        # green): 4 = the headline was measured and is in the line, 3 = not
+        os._exit(4 if writer.line.get("value") is not None else 3)
 
     t = threading.Timer(seconds, fire)
     t.daemon = True

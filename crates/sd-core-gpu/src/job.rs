@@ -35,14 +35,31 @@ pub struct Orphan {
     pub size: u64,
 }
 
+/// One page of the library's file_paths already linked to an Object.
+pub struct ExistingPage {
+    /// (file_path id, cas key as LE u64, object id), ascending file_path id
+    pub rows: Vec<(i32, u64, u32)>,
+}
+
 /// The reference's queries and writes for this job (prisma in sd-core).
+/// `sub_path` is the materialized-path prefix of the job's sub directory
+/// (`materialized_path_for_children`, file_identifier_job.rs:94-117, 259-264);
+/// None = the whole location.
 pub trait OrphanTable {
-    /// Orphans (object_id NULL, !is_dir) of the location with id >= cursor
-    /// (all if None), ascending id, at most `limit`.
-    fn orphans(&self, cursor: Option<i32>, limit: usize) -> io::Result<Vec<Orphan>>;
-    /// (cas key as LE u64, object id) of every file_path already linked to an
-    /// Object, library-wide (mod.rs:168-185).
-    fn existing_objects(&self) -> io::Result<(Vec<u64>, Vec<u32>)>;
+    /// count_orphan_file_paths (file_identifier_job.rs:270-284): orphans
+    /// (object_id NULL, !is_dir, this location, under sub_path).
+    fn count_orphans(&self, sub_path: Option<&str>) -> io::Result<usize>;
+    /// The first orphan's id: `find_first(orphan_path_filters(.., None, ..))`
+    /// selecting `id` only (:140-151).
+    fn first_orphan(&self, sub_path: Option<&str>) -> io::Result<Option<i32>>;
+    /// get_orphan_file_paths (:286-309): orphans with id >= cursor, ascending
+    /// id, at most `limit`.
+    fn orphans(&self, cursor: i32, limit: usize, sub_path: Option<&str>) -> io::Result<Vec<Orphan>>;
+    /// Library-wide file_paths linked to an Object and carrying a cas_id, id >
+    /// after, ascending, at most `limit` (what mod.rs:168-175's find_many can
+    /// return), so the Object index is filled in pages rather than from one
+    /// materialised table.
+    fn existing_objects_page(&self, after: Option<i32>, limit: usize) -> io::Result<ExistingPage>;
     /// `file_path.cas_id` of a row (mod.rs:144-165).
     fn set_cas_id(&mut self, id: i32, cas_id: Option<&str>) -> io::Result<()>;
     /// `object::create_many` of `n` Objects (mod.rs:243-297); returns their ids.
@@ -51,9 +68,14 @@ pub trait OrphanTable {
     fn connect(&mut self, links: &[(i32, u32)]) -> io::Result<()>;
 }
 
+/// Rows per page of existing Objects loaded into the index.
+pub const EXISTING_PAGE: usize = 1 << 20;
+
 /// FileIdentifierJobRunMetadata (file_identifier_job.rs:52-70) + the job state.
 #[derive(Clone, Debug, Default, Serialize, Deserialize)]
 pub struct JobState {
+    /// the sub directory's materialized path for children (None: the location)
+    pub sub_path: Option<String>,
     pub cursor: Option<i32>,
     pub total_orphan_paths: usize,
     pub total_objects_created: usize,
@@ -78,18 +100,29 @@ pub struct FileIdentifierJob<'a, T: OrphanTable> {
 pub struct EarlyFinish(pub &'static str);
 
 impl<'a, T: OrphanTable> FileIdentifierJob<'a, T> {
-    /// init (file_identifier_job.rs:80-172): count the orphans, task_count =
-    /// ceil(n / 100), cursor = first orphan id; the Object index gets every
-    /// Object the library already has.
-    pub fn init(gpu: &'a Gpu, table: T, chunks_per_step: usize) -> io::Result<Result<Self, EarlyFinish>> {
-        let all = table.orphans(None, usize::MAX)?;
-        if all.is_empty() {
+    /// init (file_identifier_job.rs:80-172): count the orphans (early finish
+    /// if none), task_count = ceil(n / 100), cursor = the first orphan's id
+    /// (a `count` and a `find_first`, not the rows); the Object index gets the
+    /// library's existing Objects page by page.
+    pub fn init(
+        gpu: &'a Gpu,
+        table: T,
+        sub_path: Option<String>,
+        chunks_per_step: usize,
+    ) -> io::Result<Result<Self, EarlyFinish>> {
+        let sp = sub_path.as_deref();
+        let count = table.count_orphans(sp)?;
+        if count == 0 {
             return Ok(Err(EarlyFinish("Found no orphan file paths to process")));
         }
+        let first = table.first_orphan(sp)?.ok_or_else(|| {
+            io::Error::new(io::ErrorKind::Other, "orphans counted but none found")
+        })?;
         let state = JobState {
-            cursor: Some(all[0].id),
-            total_orphan_paths: all.len(),
-            task_count: (all.len() + CHUNK_SIZE - 1) / CHUNK_SIZE,
+            sub_path,
+            cursor: Some(first),
+            total_orphan_paths: count,
+            task_count: (count + CHUNK_SIZE - 1) / CHUNK_SIZE,
             chunks_per_step: chunks_per_step.max(1),
             ..Default::default()
         };
@@ -103,9 +136,19 @@ impl<'a, T: OrphanTable> FileIdentifierJob<'a, T> {
     }
 
     fn open(gpu: &'a Gpu, table: T, state: JobState) -> io::Result<Self> {
-        let (ek, eh) = table.existing_objects()?;
-        let index = ObjectIndex::new(gpu, (2 * (state.total_orphan_paths + ek.len())).max(1024) as u64)?;
-        index.add_objects(gpu, &ek, &eh)?;
+        let index = ObjectIndex::new(gpu, (2 * state.total_orphan_paths).max(1024) as u64)?;
+        let mut after = None;
+        loop {
+            let page = table.existing_objects_page(after, EXISTING_PAGE)?;
+            let Some(&(last, _, _)) = page.rows.last() else { break };
+            let keys: Vec<u64> = page.rows.iter().map(|r| r.1).collect();
+            let objs: Vec<u32> = page.rows.iter().map(|r| r.2).collect();
+            index.add_objects(gpu, &keys, &objs)?;  // grows the table as it fills
+            if page.rows.len() < EXISTING_PAGE {
+                break;
+            }
+            after = Some(last);
+        }
         Ok(FileIdentifierJob { gpu, table, index, state, creator_object: HashMap::new() })
     }
 
@@ -121,7 +164,10 @@ impl<'a, T: OrphanTable> FileIdentifierJob<'a, T> {
             return Ok(Ok(()));
         }
         let nchunks = self.state.chunks_per_step.min(self.state.task_count - self.state.step_number);
-        let cand = self.table.orphans(self.state.cursor, nchunks * CHUNK_SIZE + nchunks)?;
+        let Some(cur0) = self.state.cursor else {
+            return Ok(Err(EarlyFinish("Expected orphan Paths not returned from database query for this chunk")));
+        };
+        let cand = self.table.orphans(cur0, nchunks * CHUNK_SIZE + nchunks, self.state.sub_path.as_deref())?;
         if cand.is_empty() {
             return Ok(Err(EarlyFinish("Expected orphan Paths not returned from database query for this chunk")));
         }

@@ -17,10 +17,11 @@ struct KTimer {
   virtual void end(hipStream_t s) = 0;
   virtual ~KTimer() = default;
 };
+// name null: no scope (a launch sequence timed as a whole elsewhere)
 struct KScope {
   KTimer* t;
   hipStream_t s;
-  KScope(KTimer* t_, const char* name, hipStream_t s_) : t(t_), s(s_) {
+  KScope(KTimer* t_, const char* name, hipStream_t s_) : t(name ? t_ : nullptr), s(s_) {
     if (t) t->begin(name, s);
   }
   ~KScope() {

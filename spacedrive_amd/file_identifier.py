@@ -199,19 +199,64 @@ class FilePaths:
                 break
         return out
 
-    def existing_objects(self):
-        """(key, object id) of every row linked to an Object and carrying a
-        cas_id, library-wide (what mod.rs:168-175's find_many can return)."""
+    def count_orphans(self, location_id: int, children_of: str | None = None,
+                      under: str | None = None) -> int:
+        """count_orphan_file_paths (file_identifier_job.rs:270-284): a count,
+        no rows returned."""
+        rows = self._file_rows.get(location_id, [])
+        n = 0
+        for fid in rows:
+            i = fid - 1
+            if self.object_id[i] is not None:
+                continue
+            mp = self.materialized_path[i]
+            if (children_of is not None and mp != children_of) or \
+                    (under is not None and not mp.startswith(under)):
+                continue
+            n += 1
+        return n
+
+    def first_orphan(self, location_id: int, children_of: str | None = None,
+                     under: str | None = None) -> int | None:
+        """find_first(orphan_path_filters(.., None, ..)) selecting the id
+        (file_identifier_job.rs:140-151)."""
+        first = self.orphans(location_id, None, children_of, under, limit=1)
+        return first[0] if first else None
+
+    def existing_objects_page(self, after: int | None = None, limit: int = 1 << 20):
+        """(ids, keys, object ids) of the rows linked to an Object and carrying
+        a cas_id, library-wide (what mod.rs:168-175's find_many can return),
+        id > after in ascending id, at most `limit`: the Object index is
+        filled page by page, never from one materialised table."""
         from .cas import keys_of
-        keys, objs = [], []
-        for c, o in zip(self.cas_id, self.object_id):
+        ids, keys, objs = [], [], []
+        for i in range(after or 0, len(self.name)):
+            c, o = self.cas_id[i], self.object_id[i]
             if c is not None and o is not None:
+                ids.append(i + 1)
                 keys.append(bytes.fromhex(c))
                 objs.append(o)
+                if len(ids) >= limit:
+                    break
         if not keys:
-            return np.zeros(0, np.uint64), np.zeros(0, np.uint32)
+            return np.zeros(0, np.int64), np.zeros(0, np.uint64), np.zeros(0, np.uint32)
         k = keys_of(np.frombuffer(b"".join(keys), np.uint8).reshape(-1, 8))
-        return k, np.asarray(objs, np.uint32)
+        return np.asarray(ids, np.int64), k, np.asarray(objs, np.uint32)
+
+    def existing_objects(self):
+        """(key, object id) of every row linked to an Object (all pages)."""
+        ks, os_ = [], []
+        after = None
+        while True:
+            ids, k, o = self.existing_objects_page(after)
+            if not ids.size:
+                break
+            ks.append(k)
+            os_.append(o)
+            after = int(ids[-1])
+        if not ks:
+            return np.zeros(0, np.uint64), np.zeros(0, np.uint32)
+        return np.concatenate(ks), np.concatenate(os_)
 
 
 @dataclass
@@ -264,26 +309,36 @@ class FileIdentifierJob:
 
     # ---- reference: init (file_identifier_job.rs:80-172) -------------------------
     def init(self) -> "FileIdentifierJob":
-        orphans = self._orphans(None)
-        if not orphans:
+        # a count and a find_first (file_identifier_job.rs:120-156), not the rows
+        count = self.table.count_orphans(self.location_id, self._children_of, self._under)
+        if count == 0:
             raise EarlyFinish("Found no orphan file paths to process")
-        self.meta = IdentifierRunMetadata(cursor=orphans[0], total_orphan_paths=len(orphans))
-        self.task_count = -(-len(orphans) // CHUNK_SIZE)
+        first = self.table.first_orphan(self.location_id, self._children_of, self._under)
+        self.meta = IdentifierRunMetadata(cursor=first, total_orphan_paths=count)
+        self.task_count = -(-count // CHUNK_SIZE)
         self._open_index()
         return self
 
     def _orphans(self, cursor, limit=None):
         return self.table.orphans(self.location_id, cursor, self._children_of, self._under, limit)
 
-    def _open_index(self):
+    def _open_index(self, page: int = 1 << 20):
+        """The library's existing Objects into the device index, page by page
+        (the index grows as it fills)."""
         import torch
-        ek, eh = self.table.existing_objects()
-        self.index = _dedup.ObjectIndex(self.ctx, max(1024, 2 * (len(self.table) + ek.size)))
-        if ek.size:
-            dev = torch.device("cuda", self.ctx.device)
+        self.index = _dedup.ObjectIndex(self.ctx, max(1024, 2 * self.meta.total_orphan_paths))
+        dev = torch.device("cuda", self.ctx.device)
+        after = None
+        while True:
+            ids, ek, eh = self.table.existing_objects_page(after, page)
+            if not ids.size:
+                break
             # copies: the views may be read-only (torch.from_numpy warns on them)
             self.index.add_objects(torch.from_numpy(ek.view(np.int64).copy()).to(dev),
                                    torch.from_numpy(eh.view(np.int32).copy()).to(dev))
+            if ids.size < page:
+                break
+            after = int(ids[-1])
 
     def done(self) -> bool:
         return self.step_number >= self.task_count

@@ -126,3 +126,28 @@ def test_rust_job_step_mirrors_the_reference_job():
                   "total_objects_linked", "total_objects_ignored", "chunks_per_step"):
         assert field in job, field
     assert "identify(self.gpu" in job and "group(self.gpu" in job
+
+
+def test_rust_job_queries_mirror_the_python_job():
+    """the Rust job's table trait has the reference's query
+    set -- a count and a find_first at init (file_identifier_job.rs:120-156),
+    the cursor fetch with the sub_path filter (:245-309), the existing Objects
+    in pages (mod.rs:168-175) -- and the Python stand-in table the GPU tests
+    drive has the same queries, so the two job loops read the same way."""
+    import os
+    import re
+    from spacedrive_amd.file_identifier import FilePaths
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    job = open(os.path.join(root, "crates", "sd-core-gpu", "src", "job.rs")).read()
+    trait = job[job.index("pub trait OrphanTable"):]
+    trait = trait[:trait.index("\n}\n")]
+    methods = set(re.findall(r"fn (\w+)\(", trait))
+    queries = {"count_orphans", "first_orphan", "orphans", "existing_objects_page"}
+    assert queries <= methods, queries - methods
+    for q in queries:
+        assert callable(getattr(FilePaths, q)), q
+    # the sub_path filter travels with every orphan query, and init reads no rows
+    assert re.search(r"fn orphans\(&self, cursor: i32, limit: usize, sub_path: Option<&str>\)", trait)
+    init = job[job.index("pub fn init("):job.index("pub fn resume(")]
+    assert "count_orphans(" in init and "first_orphan(" in init and ".orphans(" not in init
+    assert "existing_objects_page(" in job and "fn existing_objects(" not in trait

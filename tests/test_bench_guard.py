@@ -107,7 +107,7 @@ def test_raising_legs_keep_the_headline():
 
 def test_hanging_leg_hits_the_deadline():
     p, lines, dt = _run("staged_hangs", deadline="3")
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode == 4, p.stderr[-3000:]  # the line is printed, the exit is not green
     assert len(lines) == 1, p.stdout
     d = json.loads(lines[0])
     assert d["value"] == 7.4e7
