@@ -1944,6 +1944,174 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12_pk(
                       out, tab, lmin, special_min, scr);
 }
 
+// K5 over 12-byte records as a persistent, LDS-staged loop (round 5; VERDICT
+// r4 item 3).  One workgroup per CU walks buckets b = blockIdx.x, + gridDim.x,
+// ...: the NEXT bucket's records are copied global -> LDS with
+// global_load_lds (no VGPRs, no per-record wait) while the current bucket is
+// grouped, so the group-by's LDS phases no longer wait out the record loads
+// -- the one-bucket-per-workgroup kernel waits two dependent memory latencies
+// per bucket (its bounds, then its records) with only two buckets per CU to
+// overlap them.  All of LDS is one dynamic array (a second __shared__ object
+// can make hipcc drain vmcnt before LDS reads), the barriers are raw
+// (lgkmcnt only: __syncthreads would drain the copy in flight), and the only
+// vmcnt wait is the explicit one at the top of a bucket.  Double-buffered
+// stage 2 x 4096 records + a 5120-slot packed table (load <= 0.8 at the
+// 4095-row cap, ~0.6 at the mean bucket) + lmin: 152 KiB, one workgroup per
+// CU.  Buckets over the cap take group_bucket_global as before.
+constexpr uint32_t kGlSlots = 5120;  // 2^10 * 5: probe steps odd and prime to 3 and 5
+constexpr uint32_t kGlStageB = (kPkCap + 1) * 12;
+constexpr uint32_t kGlTabOff = 2 * kGlStageB;
+constexpr uint32_t kGlMinOff = kGlTabOff + kGlSlots * 8;
+constexpr uint32_t kGlMiscOff = kGlMinOff + (kPkCap + 1) * 4;
+constexpr uint32_t kGlLdsBytes = kGlMiscOff + 64;
+static_assert(kGlLdsBytes <= 160u * 1024u, "one workgroup per CU");
+
+__device__ __forceinline__ void glds_done(const RepOut&, uint32_t, uint32_t, uint32_t,
+                                          const uint32_t*) {}
+__device__ __forceinline__ void glds_done(const ListOut& o, uint32_t b, uint32_t nb, uint32_t end,
+                                          const uint32_t* scr) {
+  if (threadIdx.x == 0) {
+    o.lcnt[b] = scr[1];
+    if (b == nb - 1) o.lcnt[nb] = end;
+  }
+}
+
+template <typename Out>
+__global__ __launch_bounds__(kGroupThreads, 1) void k_bucket_group12_glds(
+    const uint3* __restrict__ rec, uint32_t rank_base, const uint32_t* __restrict__ offs,
+    uint32_t nb, uint32_t bits, ChunkOf chunk_of, uint64_t* __restrict__ gkey,
+    uint32_t* __restrict__ gmin, Out out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint64_t* tab = reinterpret_cast<uint64_t*>(lds + kGlTabOff);
+  uint32_t* lmin = reinterpret_cast<uint32_t*>(lds + kGlMinOff);
+  uint32_t* scr = reinterpret_cast<uint32_t*>(lds + kGlMiscOff);  // [0..1] Out's, [4] special
+  constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
+  const uint32_t G = gridDim.x, wv = threadIdx.x >> 6, lane = __lane_id();
+  const uint32_t nb_all = out.nbuckets ? out.nbuckets : nb;
+  // stage buffer `buf` <- records [s, s + m) (m <= kPkCap)
+  // Issued as inline asm: with the builtin, hipcc cannot tell the copy's LDS
+  // range from the stage being read, the tables or lmin, and waits vmcnt(0)
+  // before every LDS access after it (draining the copy at once).  The
+  // compiler's own vector loads (only in the rare over-cap path) return in
+  // order behind it, so its counted waits stay correct.
+  const uint32_t lds0 = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds));
+  // The records are copied as a flat run of 3m dwords, one dword per lane
+  // (LDS address = m0 + 4 * lane, the long-standing LDS-DMA rule).
+  auto issue = [&](uint32_t buf, uint32_t s, uint32_t m) {
+    const uint32_t u = 3 * m;
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(rec + s);
+    for (uint32_t i0 = wv * 64; i0 < u; i0 += kGroupThreads) {  // wave-uniform
+      const uint32_t* src = base + min(i0 + lane, u - 1);
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + buf * kGlStageB + i0 * 4u);
+      uint32_t keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(src), "s"(dst)
+          : "memory");
+    }
+  };
+  uint32_t b = blockIdx.x;
+  if (b >= nb) return;
+  uint32_t s0 = offs[b], e0 = offs[b + 1], p = 0;
+  if (e0 - s0 <= kPkCap) issue(0, s0, e0 - s0);
+  for (;;) {
+    const uint32_t bn = b + G;
+    uint32_t s1 = 0, e1 = 0;
+    if (bn < nb) {
+      s1 = offs[bn];
+      e1 = offs[bn + 1];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage[p] has landed
+    lds_barrier();  // ...for every wave; the previous bucket's LDS reads are done
+    if (bn < nb && e1 - s1 <= kPkCap) issue(p ^ 1u, s1, e1 - s1);
+    const uint32_t m = e0 - s0, bg = out.bucket0 + b;
+    if (m > kPkCap) {
+      Out ob = out;  // out_done there names the bucket by blockIdx.x
+      ob.bucket0 = bg - blockIdx.x;
+      ob.nbuckets = nb_all;
+      group_bucket_global(Rec12Src{rec, rank_base}, s0, e0, chunk_of, gkey, gmin, ob, scr[4], scr);
+    } else {
+      const uint3* st = reinterpret_cast<const uint3*>(lds + p * kGlStageB);
+      uint4 q[kP];
+#pragma unroll
+      for (int j = 0; j < kP; ++j) {
+        const uint32_t idx = threadIdx.x + j * kGroupThreads;
+        const uint3 v = st[min(idx, kPkCap)];
+        q[j] = idx < m ? make_uint4(v.x, v.y, rank_base + v.z, v.z)
+                       : make_uint4(0, 0, kPadRow, kPadRow);
+      }
+      for (uint32_t t = threadIdx.x; t < kGlSlots; t += kGroupThreads) tab[t] = 0ull;
+      for (uint32_t t = threadIdx.x; t <= kPkCap; t += kGroupThreads) lmin[t] = 0xFFFFFFFFu;
+      out_init(out, scr);
+      lds_barrier();
+      uint32_t slot[kP], step[kP], owner[kP];
+      uint64_t mine[kP];
+      uint32_t pend = 0;
+#pragma unroll
+      for (int j = 0; j < kP; ++j) {
+        const uint64_t h = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
+        const uint32_t idx = threadIdx.x + j * kGroupThreads;
+        mine[j] = (key_rest(h, bits) << 12) | (idx + 1);
+        slot[j] = static_cast<uint32_t>((static_cast<uint64_t>(static_cast<uint32_t>(h)) * kGlSlots) >> 32);
+        uint32_t sp = 1u + 2u * static_cast<uint32_t>((h >> 40) & 1023u);  // odd, prime to 5
+        sp += (sp % 5u == 0) ? 2u : 0u;
+        step[j] = sp;
+        owner[j] = idx;
+        if (q[j].w != kPadRow) pend |= 1u << j;
+      }
+      const uint32_t live = pend;
+      while (pend) {  // a thread's records probe in lock step
+        uint64_t prev[kP];
+#pragma unroll
+        for (int j = 0; j < kP; ++j)
+          prev[j] = (pend >> j & 1u)
+                        ? atomicCAS(reinterpret_cast<unsigned long long*>(&tab[slot[j]]), 0ull,
+                                    static_cast<unsigned long long>(mine[j]))
+                        : 0ull;
+#pragma unroll
+        for (int j = 0; j < kP; ++j) {
+          if (!(pend >> j & 1u)) continue;
+          if (prev[j] == 0ull) {
+            pend &= ~(1u << j);
+          } else if ((prev[j] >> 12) == (mine[j] >> 12)) {
+            owner[j] = static_cast<uint32_t>(prev[j] & 0xFFFu) - 1;
+            pend &= ~(1u << j);
+          } else {
+            const uint32_t sn = slot[j] + step[j];
+            slot[j] = sn >= kGlSlots ? sn - kGlSlots : sn;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kP; ++j)
+        if (live >> j & 1u) atomicMin(&lmin[owner[j]], q[j].z);
+      lds_barrier();
+      bool lv[kP], lk[kP];
+      uint32_t r[kP], w[kP], f[kP];
+#pragma unroll
+      for (int j = 0; j < kP; ++j) {
+        lv[j] = live >> j & 1u;
+        r[j] = q[j].z;
+        w[j] = q[j].w;
+        f[j] = lmin[owner[j]];
+        lk[j] = lv[j] && chunk_of(r[j]) != chunk_of(f[j]);
+      }
+      uint32_t c_run = 0, l_run = 0;
+      out.template emit<kP>(lv, lk, r, w, f, s0, e0, c_run, l_run, scr, false);
+      lds_barrier();  // every wave's counter atomics
+      glds_done(out, bg, nb_all, e0, scr);
+    }
+    if (bn >= nb) break;
+    b = bn;
+    s0 = s1;
+    e0 = e1;
+    p ^= 1u;
+  }
+}
+
 // the segment sizes k_part_private adds to, and the fine-count overflow flag
 __global__ void k_zero_runs(uint32_t* __restrict__ segtot, uint32_t* __restrict__ ovf) {
   if (threadIdx.x < kRunMaxBins) segtot[threadIdx.x] = 0;
@@ -2301,6 +2469,32 @@ void allow_lds(K kernel, size_t bytes) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
 }
 
+
+// K5 over 12-byte records: the one-bucket-per-workgroup kernel, or with
+// SDGPU_GROUP_GLDS=1 the LDS-staged persistent kernel (round 5 A/B: 2.2x
+// slower).  nb buckets starting at out.bucket0 (offs indexed
+// globally).
+bool group_glds_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("SDGPU_GROUP_GLDS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+template <typename Out>
+void group12_launch(const uint3* rec, uint32_t rank_base, const uint32_t* offs, uint32_t nb,
+                    uint32_t bits, ChunkOf chunk_of, uint64_t* gkey, uint32_t* gmin, const Out& out,
+                    hipStream_t s) {
+  if (group_glds_on()) {
+    allow_lds(k_bucket_group12_glds<Out>, kGlLdsBytes);
+    k_bucket_group12_glds<Out><<<std::min<uint32_t>(nb, kPartBlocks), kGroupThreads, kGlLdsBytes, s>>>(
+        rec, rank_base, offs + out.bucket0, nb, bits, chunk_of, gkey, gmin, out);
+    return;
+  }
+  k_bucket_group12_pk<Out><<<nb, kGroupThreads, 0, s>>>(rec, rank_base, offs, bits, chunk_of, gkey,
+                                                        gmin, out);
+}
+
 XSink sink_of(const RepOut&) { return XSink{}; }
 XSink sink_of(const ListOut& o) { return o.x; }
 
@@ -2413,9 +2607,8 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
       o.nbuckets = nfine;
       const uint32_t nbk = (s1 - s0) << kB2;
       if constexpr (kRec12)
-        k_bucket_group12_pk<Out><<<nbk, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
-                                                               rank_base, fbase, bits,
-                                                               ChunkOf::make(chunk_rows), gkey, gmin, o);
+        group12_launch(reinterpret_cast<const uint3*>(rec), rank_base, fbase, nbk, bits,
+                       ChunkOf::make(chunk_rows), gkey, gmin, o, s);
       else
         k_bucket_group_pk<Out><<<nbk, kGroupThreads, 0, s>>>(rec, fbase, 1, bits,
                                                              ChunkOf::make(chunk_rows), gkey, gmin, o);
@@ -2465,9 +2658,8 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
   }
   KScope k(timer, "bucket_group", s);
   if constexpr (kRec12)
-    k_bucket_group12_pk<Out><<<nfine, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
-                                                             rank_base, fbase, bits,
-                                                             ChunkOf::make(chunk_rows), gkey, gmin, out);
+    group12_launch(reinterpret_cast<const uint3*>(rec), rank_base, fbase, nfine, bits,
+                   ChunkOf::make(chunk_rows), gkey, gmin, out, s);
   else
     k_bucket_group_pk<Out><<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits,
                                                            ChunkOf::make(chunk_rows), gkey, gmin, out);
@@ -2543,10 +2735,8 @@ hipError_t group_launch(In in, uint64_t n, uint32_t chunk_rows, uint32_t* rep, b
           }
         }
         KScope k(timer, "bucket_group", s);
-        k_bucket_group12_pk<Out><<<nb, kGroupThreads, 0, s>>>(reinterpret_cast<const uint3*>(rec),
-                                                              z_rank_base(in), fbase, kStageBits,
-                                                              ChunkOf::make(chunk_rows), gkey, gmin,
-                                                              out);
+        group12_launch(reinterpret_cast<const uint3*>(rec), z_rank_base(in), fbase, nb, kStageBits,
+                       ChunkOf::make(chunk_rows), gkey, gmin, out, s);
         return out_finish(out, nb, s);
       }
     }
