@@ -17,6 +17,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 
 def main():
     import torch
+    if os.environ.get("AB_LIB"):  # A/B against another build of libsdgpu (scripts/gpu_r5_pk.sh)
+        from spacedrive_amd import _native
+        _native.LIB_PATH = os.path.abspath(os.environ["AB_LIB"])
     from spacedrive_amd import corpus, dedup
     from spacedrive_amd._native import default_context
     rows = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
@@ -45,7 +48,7 @@ def main():
     w = who[:e].to(torch.int64) & 0xFFFFFFFF
     o = torch.where(w >= 2**31, obj[:e].to(torch.int64) & 0xFFFFFFFF, torch.zeros_like(w))
     packed = torch.sort((w << 32) | o).values.cpu().numpy()
-    print(json.dumps({"G": os.environ.get("SDGPU_SEG_GROUPS", "1"), "rows": rows,
+    print(json.dumps({"G": os.environ.get("SDGPU_SEG_GROUPS", "1"), "lib": os.environ.get("AB_LIB", "tree"), "rows": rows,
                       "ms_per_call": sorted(ts)[1], "rounds_ms": ts, "counts": [c, l, e],
                       "digest": hashlib.sha1(packed.tobytes()).hexdigest(),
                       "kernels": {k: v[0] / max(v[1], 1) for k, v in kt.items()}}))

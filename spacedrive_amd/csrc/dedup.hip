@@ -1499,13 +1499,16 @@ __global__ __launch_bounds__(1024) void k_list_finish(const uint32_t* __restrict
     if (o + k < cap) who[o + k] = src[k];
 }
 hipError_t out_finish(const RepOut&, uint32_t, hipStream_t) { return hipSuccess; }
-// ListOut: each wave's entries are placed by ONE LDS atomic per (step, list)
-// on the bucket's creator / linked counters (scr[0..1], zeroed with the
-// table): no barrier in emit, one at the end for the linked total.  The
-// entries' order inside a bucket depends on wave timing (not part of the
-// contract).  Workgroup-wide ranks in record order (two barriers + a one-wave
-// scan per emit) measured slower: 100 M rows 1.870 -> 1.850 ms, 12.5 M rows
-// 0.246 -> 0.244 ms (profiles/r4/listranks_ab/).
+// ListOut: each wave reserves the slots of ALL its entries with ONE LDS
+// atomic per list on the bucket's creator / linked counters (scr[0..1],
+// zeroed with the table) and places step j's entries after those of steps
+// < j (round 5: one atomic round trip per wave instead of one per step and
+// list -- the group kernel is VALU-issue bound).  No barrier
+// in emit, one at the end for the linked total.  The entries' order inside a
+// bucket depends on wave timing (not part of the contract).  Workgroup-wide
+// ranks in record order (two barriers + a one-wave scan per emit) measured
+// slower: 100 M rows 1.870 -> 1.850 ms, 12.5 M rows 0.246 -> 0.244 ms
+// (profiles/r4/listranks_ab/).
 constexpr uint32_t kLinkedBit = 0x80000000u;
 struct ListOut {
   static constexpr int kScratch = 2;
@@ -1531,25 +1534,36 @@ struct ListOut {
       if (threadIdx.x == 0) *nospc = 1u;
       return;
     }
-    const uint32_t lane = __lane_id();
-    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t bc[kSteps], bl[kSteps];
+    uint32_t nc = 0, nl = 0;
 #pragma unroll
     for (int j = 0; j < kSteps; ++j) {
-      const bool c = live[j] && !lk[j], l = lk[j];
-      const uint64_t bc = __ballot(c), bl = __ballot(l);
-      uint32_t cb = 0, lb = 0;
-      if (lane == 0) {
-        if (bc) cb = atomicAdd(&scr[0], static_cast<uint32_t>(__popcll(bc)));
-        if (bl) lb = atomicAdd(&scr[1], static_cast<uint32_t>(__popcll(bl)));
-      }
-      cb = __shfl(cb, 0);
-      lb = __shfl(lb, 0);
-      if (c) who[start + cb + __popcll(bc & lt)] = r[j];
-      if (l) {
-        const uint32_t p = end - 1 - (lb + __popcll(bl & lt));
+      bc[j] = __ballot(live[j] && !lk[j]);
+      bl[j] = __ballot(lk[j]);
+      nc += static_cast<uint32_t>(__popcll(bc[j]));
+      nl += static_cast<uint32_t>(__popcll(bl[j]));
+    }
+    uint32_t cb = 0, lb = 0;
+    if (__lane_id() == 0) {
+      if (nc) cb = atomicAdd(&scr[0], nc);
+      if (nl) lb = atomicAdd(&scr[1], nl);
+    }
+    cb = __builtin_amdgcn_readfirstlane(cb);  // lane 0 is active here
+    lb = __builtin_amdgcn_readfirstlane(lb);
+#pragma unroll
+    for (int j = 0; j < kSteps; ++j) {
+      const uint32_t bc_lo = static_cast<uint32_t>(bc[j]), bc_hi = static_cast<uint32_t>(bc[j] >> 32);
+      const uint32_t bl_lo = static_cast<uint32_t>(bl[j]), bl_hi = static_cast<uint32_t>(bl[j] >> 32);
+      if (live[j] && !lk[j])
+        who[start + cb + __builtin_amdgcn_mbcnt_hi(bc_hi, __builtin_amdgcn_mbcnt_lo(bc_lo, 0u))] = r[j];
+      if (lk[j]) {
+        const uint32_t p =
+            end - 1 - (lb + __builtin_amdgcn_mbcnt_hi(bl_hi, __builtin_amdgcn_mbcnt_lo(bl_lo, 0u)));
         who[p] = r[j] | kLinkedBit;
         obj[p] = f[j];
       }
+      cb += static_cast<uint32_t>(__popcll(bc[j]));
+      lb += static_cast<uint32_t>(__popcll(bl[j]));
     }
     (void)w;
   }
@@ -1767,23 +1781,101 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
   out_done(out, c_run, l_run, end, scr);
 }
 
-// K5 with a PACKED 8-byte LDS table, for buckets of >= 12 digit bits (the
-// one-level 12-bit path and the two-level 15-bit path).  Inside a bucket the
-// digit bits of h are implied, so a key is known by its other 64 - bits
-// (<= 52) bits; with the record's index in the bucket + 1 (12 bits, 0 =
-// empty) a slot is ONE 64-bit word.  The CAS that places or finds a key also
-// names the record that owns it, the group minimum lives per owner
-// (lmin[4096]), and 7680 slots fit where 6144 twelve-byte ones did: load
-// ~0.4 instead of ~0.5, shorter probe chains.  scripts/exp/exp_group_packed.hip:
-// 12.5 M rows 0.078 -> 0.072 ms (profiles/r3/exp_group_packed/run.log).
+// K5 with a PACKED 8-byte LDS table, for buckets of 12-15 digit bits (the
+// one-level 12-bit path and the two-level path).  Inside a bucket the digit
+// bits of h are implied, so a key is known by its other 64 - bits (<= 52)
+// bits; with the record's index in the bucket + 1 (12 bits, 0 = empty) a
+// slot is ONE 64-bit word.  The CAS that places or finds a key also names the
+// record that owns it, the group minimum lives per owner (lmin[4096]), and
+// 7680 slots fit where 6144 twelve-byte ones did: load ~0.4 instead of ~0.5,
+// shorter probe chains.  scripts/exp/exp_group_packed.hip: 12.5 M rows 0.078
+// -> 0.072 ms (profiles/r3/exp_group_packed/run.log).
+// Round 5: the kernel is VALU-issue bound (SQ counters,
+// VALU busy 73 % of the SIMD cycles at 12.5 M rows, 82 % at
+// 100 M), so the per-record setup was cut: the word is assembled with 32-bit
+// operations (lo = h lo, hi = the remaining hi bits | (index + 1) << 20) and
+// the double-hashing step (coprime with 2^9 * 15) is 30 k + r, r one of the
+// 8 residues prime to 30 read from a nibble table -- ~6 VALU where the odd
+// step with its mod-3 / mod-5 corrections took ~16.  (Linear probing, step
+// 1, cut more VALU but lengthened the probe chains: 12.5 M rows 0.079 ->
+// 0.085 ms, profiles/r5/pmc_group/.)
 // Buckets above 4095 records take the global table; pads (row ~0) are skipped.
-constexpr uint32_t kPkSlots = 7680;  // 2^9 * 15: probe steps odd and prime to 3 and 5
+constexpr uint32_t kPkSlots = 7680;  // 2^9 * 15
 constexpr uint32_t kPkCap = 4095;
 
-// h without its `bits` digit bits [64 - kShardBits - bits, 64 - kShardBits)
-__device__ __forceinline__ uint64_t key_rest(uint64_t h, uint32_t bits) {
-  const uint32_t lo = 64 - kShardBits - bits;
-  return (h & ((1ull << lo) - 1)) | ((h >> (64 - kShardBits)) << lo);
+// The packed group-by of one bucket whose records are in registers (q[j] =
+// {h lo, h hi, rank, row}, row kPadRow past the end), m = end - start <=
+// kPkCap.  kRaw: barriers without a vmcnt drain (the LDS-staged kernel).
+template <bool kRaw, int kP, typename Out>
+__device__ __forceinline__ void group_packed_regs(const uint4 (&q)[kP], uint32_t start, uint32_t end,
+                                                  uint32_t bits, ChunkOf chunk_of, const Out& out,
+                                                  uint64_t* tab, uint32_t* lmin, uint32_t* scr) {
+  auto barrier = [] {
+    if constexpr (kRaw) lds_barrier();
+    else __syncthreads();
+  };
+  for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
+  for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
+  out_init(out, scr);
+  barrier();
+  // word hi: the 24 - bits hi-word bits below the digit, the 8 shard bits
+  // above it, then index + 1 in bits 20..31 (bits in 12..15: <= 20 key bits)
+  const uint32_t kb = 24u - bits, lowm = (1u << kb) - 1u;
+  uint32_t whi[kP], slot[kP], step[kP], owner[kP];
+  uint32_t pend = 0;
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    const uint32_t idx = threadIdx.x + j * kGroupThreads;
+    whi[j] = (q[j].y & lowm) | ((q[j].y >> 24) << kb) | ((idx + 1) << 20);
+    slot[j] = __umulhi(q[j].x, kPkSlots);  // the top bits of h lo
+    // (r - 1) / 2 for r = 1 7 11 13 17 19 23 29, one nibble each; k and the
+    // residue from the low bits of h lo
+    const uint32_t nib = __builtin_amdgcn_ubfe(0xEB986530u, ((q[j].x >> 6) & 7u) << 2, 4);
+    step[j] = 30u * (q[j].x & 63u) + 2u * nib + 1u;
+    owner[j] = idx;
+    if (q[j].w != kPadRow) pend |= 1u << j;
+  }
+  const uint32_t live = pend;
+  // the records of a thread probe in lock step (their LDS round trips overlap)
+  while (pend) {
+    uint64_t prev[kP];
+#pragma unroll
+    for (int j = 0; j < kP; ++j)
+      prev[j] = (pend >> j & 1u)
+                    ? atomicCAS(reinterpret_cast<unsigned long long*>(&tab[slot[j]]), 0ull,
+                                (static_cast<unsigned long long>(whi[j]) << 32) | q[j].x)
+                    : 0ull;
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      if (!(pend >> j & 1u)) continue;
+      const uint32_t plo = static_cast<uint32_t>(prev[j]), phi = static_cast<uint32_t>(prev[j] >> 32);
+      if ((plo | phi) == 0u) {
+        pend &= ~(1u << j);  // placed: owns its key
+      } else if ((((phi ^ whi[j]) & 0xFFFFFu) | (plo ^ q[j].x)) == 0u) {
+        owner[j] = (phi >> 20) - 1;
+        pend &= ~(1u << j);
+      } else {
+        const uint32_t sn = slot[j] + step[j];
+        slot[j] = sn >= kPkSlots ? sn - kPkSlots : sn;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kP; ++j)
+    if (live >> j & 1u) atomicMin(&lmin[owner[j]], q[j].z);
+  barrier();
+  bool lv[kP], lk[kP];
+  uint32_t r[kP], w[kP], f[kP];
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    lv[j] = live >> j & 1u;
+    r[j] = q[j].z;
+    w[j] = q[j].w;
+    f[j] = lmin[owner[j]];
+    lk[j] = lv[j] && r[j] != f[j] && chunk_of(r[j]) != chunk_of(f[j]);
+  }
+  uint32_t c_run = 0, l_run = 0;
+  out.template emit<kP>(lv, lk, r, w, f, start, end, c_run, l_run, scr, false);
 }
 
 template <typename Src, typename Out>
@@ -1814,69 +1906,8 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
 #pragma unroll
   for (int j = 0; j < kP; ++j)
     if (start + threadIdx.x + j * kGroupThreads >= end) q[j] = make_uint4(0, 0, kPadRow, kPadRow);
-  for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
-  for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
-  out_init(out, scr);
-  __syncthreads();
-  uint32_t slot[kP], step[kP], owner[kP];
-  uint64_t mine[kP];
-  uint32_t pend = 0;
-#pragma unroll
-  for (int j = 0; j < kP; ++j) {
-    const uint64_t h = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
-    const uint32_t idx = threadIdx.x + j * kGroupThreads;
-    mine[j] = (key_rest(h, bits) << 12) | (idx + 1);
-    slot[j] = static_cast<uint32_t>((static_cast<uint64_t>(static_cast<uint32_t>(h)) * kPkSlots) >> 32);
-    // double hashing: an odd step prime to 3 and 5 is coprime with 2^9 * 15
-    uint32_t st = 1u + 2u * static_cast<uint32_t>((h >> 40) & 1023u);
-    st += (st % 3u == 0) ? 2u : 0u;
-    st += (st % 5u == 0) ? 2u : 0u;
-    st += (st % 3u == 0) ? 2u : 0u;
-    step[j] = st;
-    owner[j] = idx;
-    if (q[j].w != kPadRow) pend |= 1u << j;
-  }
-  const uint32_t live = pend;
-  // the records of a thread probe in lock step (their LDS round trips overlap)
-  while (pend) {
-    uint64_t prev[kP];
-#pragma unroll
-    for (int j = 0; j < kP; ++j)
-      prev[j] = (pend >> j & 1u)
-                    ? atomicCAS(reinterpret_cast<unsigned long long*>(&tab[slot[j]]), 0ull,
-                                static_cast<unsigned long long>(mine[j]))
-                    : 0ull;
-#pragma unroll
-    for (int j = 0; j < kP; ++j) {
-      if (!(pend >> j & 1u)) continue;
-      if (prev[j] == 0ull) {
-        pend &= ~(1u << j);  // placed: owns its key
-      } else if ((prev[j] >> 12) == (mine[j] >> 12)) {
-        owner[j] = static_cast<uint32_t>(prev[j] & 0xFFFu) - 1;
-        pend &= ~(1u << j);
-      } else {
-        const uint32_t sn = slot[j] + step[j];
-        slot[j] = sn >= kPkSlots ? sn - kPkSlots : sn;
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < kP; ++j)
-    if (live >> j & 1u) atomicMin(&lmin[owner[j]], q[j].z);
-  __syncthreads();
-  bool lv[kP], lk[kP];
-  uint32_t r[kP], w[kP], f[kP];
-#pragma unroll
-  for (int j = 0; j < kP; ++j) {
-    lv[j] = live >> j & 1u;
-    r[j] = q[j].z;
-    w[j] = q[j].w;
-    f[j] = lmin[owner[j]];
-    lk[j] = lv[j] && chunk_of(r[j]) != chunk_of(f[j]);
-  }
-  uint32_t c_run = 0, l_run = 0;
-  out.template emit<kP>(lv, lk, r, w, f, start, end, c_run, l_run, scr, false);
-  out_done(out, c_run, l_run, end, scr);
+  group_packed_regs<false>(q, start, end, bits, chunk_of, out, tab, lmin, scr);
+  out_done(out, 0u, 0u, end, scr);
 }
 
 
@@ -1942,174 +1973,6 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12_pk(
   const uint32_t b = out.bucket0 + blockIdx.x;
   group_bucket_packed(Rec12Src{rec, rank_base}, offs[b], offs[b + 1], bits, chunk_of, gkey, gmin,
                       out, tab, lmin, special_min, scr);
-}
-
-// K5 over 12-byte records as a persistent, LDS-staged loop (round 5; VERDICT
-// r4 item 3).  One workgroup per CU walks buckets b = blockIdx.x, + gridDim.x,
-// ...: the NEXT bucket's records are copied global -> LDS with
-// global_load_lds (no VGPRs, no per-record wait) while the current bucket is
-// grouped, so the group-by's LDS phases no longer wait out the record loads
-// -- the one-bucket-per-workgroup kernel waits two dependent memory latencies
-// per bucket (its bounds, then its records) with only two buckets per CU to
-// overlap them.  All of LDS is one dynamic array (a second __shared__ object
-// can make hipcc drain vmcnt before LDS reads), the barriers are raw
-// (lgkmcnt only: __syncthreads would drain the copy in flight), and the only
-// vmcnt wait is the explicit one at the top of a bucket.  Double-buffered
-// stage 2 x 4096 records + a 5120-slot packed table (load <= 0.8 at the
-// 4095-row cap, ~0.6 at the mean bucket) + lmin: 152 KiB, one workgroup per
-// CU.  Buckets over the cap take group_bucket_global as before.
-constexpr uint32_t kGlSlots = 5120;  // 2^10 * 5: probe steps odd and prime to 3 and 5
-constexpr uint32_t kGlStageB = (kPkCap + 1) * 12;
-constexpr uint32_t kGlTabOff = 2 * kGlStageB;
-constexpr uint32_t kGlMinOff = kGlTabOff + kGlSlots * 8;
-constexpr uint32_t kGlMiscOff = kGlMinOff + (kPkCap + 1) * 4;
-constexpr uint32_t kGlLdsBytes = kGlMiscOff + 64;
-static_assert(kGlLdsBytes <= 160u * 1024u, "one workgroup per CU");
-
-__device__ __forceinline__ void glds_done(const RepOut&, uint32_t, uint32_t, uint32_t,
-                                          const uint32_t*) {}
-__device__ __forceinline__ void glds_done(const ListOut& o, uint32_t b, uint32_t nb, uint32_t end,
-                                          const uint32_t* scr) {
-  if (threadIdx.x == 0) {
-    o.lcnt[b] = scr[1];
-    if (b == nb - 1) o.lcnt[nb] = end;
-  }
-}
-
-template <typename Out>
-__global__ __launch_bounds__(kGroupThreads, 1) void k_bucket_group12_glds(
-    const uint3* __restrict__ rec, uint32_t rank_base, const uint32_t* __restrict__ offs,
-    uint32_t nb, uint32_t bits, ChunkOf chunk_of, uint64_t* __restrict__ gkey,
-    uint32_t* __restrict__ gmin, Out out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint64_t* tab = reinterpret_cast<uint64_t*>(lds + kGlTabOff);
-  uint32_t* lmin = reinterpret_cast<uint32_t*>(lds + kGlMinOff);
-  uint32_t* scr = reinterpret_cast<uint32_t*>(lds + kGlMiscOff);  // [0..1] Out's, [4] special
-  constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
-  const uint32_t G = gridDim.x, wv = threadIdx.x >> 6, lane = __lane_id();
-  const uint32_t nb_all = out.nbuckets ? out.nbuckets : nb;
-  // stage buffer `buf` <- records [s, s + m) (m <= kPkCap)
-  // Issued as inline asm: with the builtin, hipcc cannot tell the copy's LDS
-  // range from the stage being read, the tables or lmin, and waits vmcnt(0)
-  // before every LDS access after it (draining the copy at once).  The
-  // compiler's own vector loads (only in the rare over-cap path) return in
-  // order behind it, so its counted waits stay correct.
-  const uint32_t lds0 = static_cast<uint32_t>(
-      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds));
-  // The records are copied as a flat run of 3m dwords, one dword per lane
-  // (LDS address = m0 + 4 * lane, the long-standing LDS-DMA rule).
-  auto issue = [&](uint32_t buf, uint32_t s, uint32_t m) {
-    const uint32_t u = 3 * m;
-    const uint32_t* base = reinterpret_cast<const uint32_t*>(rec + s);
-    for (uint32_t i0 = wv * 64; i0 < u; i0 += kGroupThreads) {  // wave-uniform
-      const uint32_t* src = base + min(i0 + lane, u - 1);
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + buf * kGlStageB + i0 * 4u);
-      uint32_t keep;
-      asm volatile(
-          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-          "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-          : "=&s"(keep)
-          : "v"(src), "s"(dst)
-          : "memory");
-    }
-  };
-  uint32_t b = blockIdx.x;
-  if (b >= nb) return;
-  uint32_t s0 = offs[b], e0 = offs[b + 1], p = 0;
-  if (e0 - s0 <= kPkCap) issue(0, s0, e0 - s0);
-  for (;;) {
-    const uint32_t bn = b + G;
-    uint32_t s1 = 0, e1 = 0;
-    if (bn < nb) {
-      s1 = offs[bn];
-      e1 = offs[bn + 1];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage[p] has landed
-    lds_barrier();  // ...for every wave; the previous bucket's LDS reads are done
-    if (bn < nb && e1 - s1 <= kPkCap) issue(p ^ 1u, s1, e1 - s1);
-    const uint32_t m = e0 - s0, bg = out.bucket0 + b;
-    if (m > kPkCap) {
-      Out ob = out;  // out_done there names the bucket by blockIdx.x
-      ob.bucket0 = bg - blockIdx.x;
-      ob.nbuckets = nb_all;
-      group_bucket_global(Rec12Src{rec, rank_base}, s0, e0, chunk_of, gkey, gmin, ob, scr[4], scr);
-    } else {
-      const uint3* st = reinterpret_cast<const uint3*>(lds + p * kGlStageB);
-      uint4 q[kP];
-#pragma unroll
-      for (int j = 0; j < kP; ++j) {
-        const uint32_t idx = threadIdx.x + j * kGroupThreads;
-        const uint3 v = st[min(idx, kPkCap)];
-        q[j] = idx < m ? make_uint4(v.x, v.y, rank_base + v.z, v.z)
-                       : make_uint4(0, 0, kPadRow, kPadRow);
-      }
-      for (uint32_t t = threadIdx.x; t < kGlSlots; t += kGroupThreads) tab[t] = 0ull;
-      for (uint32_t t = threadIdx.x; t <= kPkCap; t += kGroupThreads) lmin[t] = 0xFFFFFFFFu;
-      out_init(out, scr);
-      lds_barrier();
-      uint32_t slot[kP], step[kP], owner[kP];
-      uint64_t mine[kP];
-      uint32_t pend = 0;
-#pragma unroll
-      for (int j = 0; j < kP; ++j) {
-        const uint64_t h = (static_cast<uint64_t>(q[j].y) << 32) | q[j].x;
-        const uint32_t idx = threadIdx.x + j * kGroupThreads;
-        mine[j] = (key_rest(h, bits) << 12) | (idx + 1);
-        slot[j] = static_cast<uint32_t>((static_cast<uint64_t>(static_cast<uint32_t>(h)) * kGlSlots) >> 32);
-        uint32_t sp = 1u + 2u * static_cast<uint32_t>((h >> 40) & 1023u);  // odd, prime to 5
-        sp += (sp % 5u == 0) ? 2u : 0u;
-        step[j] = sp;
-        owner[j] = idx;
-        if (q[j].w != kPadRow) pend |= 1u << j;
-      }
-      const uint32_t live = pend;
-      while (pend) {  // a thread's records probe in lock step
-        uint64_t prev[kP];
-#pragma unroll
-        for (int j = 0; j < kP; ++j)
-          prev[j] = (pend >> j & 1u)
-                        ? atomicCAS(reinterpret_cast<unsigned long long*>(&tab[slot[j]]), 0ull,
-                                    static_cast<unsigned long long>(mine[j]))
-                        : 0ull;
-#pragma unroll
-        for (int j = 0; j < kP; ++j) {
-          if (!(pend >> j & 1u)) continue;
-          if (prev[j] == 0ull) {
-            pend &= ~(1u << j);
-          } else if ((prev[j] >> 12) == (mine[j] >> 12)) {
-            owner[j] = static_cast<uint32_t>(prev[j] & 0xFFFu) - 1;
-            pend &= ~(1u << j);
-          } else {
-            const uint32_t sn = slot[j] + step[j];
-            slot[j] = sn >= kGlSlots ? sn - kGlSlots : sn;
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kP; ++j)
-        if (live >> j & 1u) atomicMin(&lmin[owner[j]], q[j].z);
-      lds_barrier();
-      bool lv[kP], lk[kP];
-      uint32_t r[kP], w[kP], f[kP];
-#pragma unroll
-      for (int j = 0; j < kP; ++j) {
-        lv[j] = live >> j & 1u;
-        r[j] = q[j].z;
-        w[j] = q[j].w;
-        f[j] = lmin[owner[j]];
-        lk[j] = lv[j] && chunk_of(r[j]) != chunk_of(f[j]);
-      }
-      uint32_t c_run = 0, l_run = 0;
-      out.template emit<kP>(lv, lk, r, w, f, s0, e0, c_run, l_run, scr, false);
-      lds_barrier();  // every wave's counter atomics
-      glds_done(out, bg, nb_all, e0, scr);
-    }
-    if (bn >= nb) break;
-    b = bn;
-    s0 = s1;
-    e0 = e1;
-    p ^= 1u;
-  }
 }
 
 // the segment sizes k_part_private adds to, and the fine-count overflow flag
@@ -2470,27 +2333,16 @@ void allow_lds(K kernel, size_t bytes) {
 }
 
 
-// K5 over 12-byte records: the one-bucket-per-workgroup kernel, or with
-// SDGPU_GROUP_GLDS=1 the LDS-staged persistent kernel (round 5 A/B: 2.2x
-// slower).  nb buckets starting at out.bucket0 (offs indexed
-// globally).
-bool group_glds_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("SDGPU_GROUP_GLDS");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
+// K5 over 12-byte records, one workgroup per bucket.  nb buckets starting at
+// out.bucket0 (offs indexed globally).  Round 5 measured a persistent,
+// LDS-staged variant (one workgroup per CU copying the next bucket's records
+// to LDS with global_load_lds while grouping the current one): 2.2x slower
+// (it halves the resident workgroups of a VALU-bound kernel; DESIGN.md 4.3,
+// commit 1346212).
 template <typename Out>
 void group12_launch(const uint3* rec, uint32_t rank_base, const uint32_t* offs, uint32_t nb,
                     uint32_t bits, ChunkOf chunk_of, uint64_t* gkey, uint32_t* gmin, const Out& out,
                     hipStream_t s) {
-  if (group_glds_on()) {
-    allow_lds(k_bucket_group12_glds<Out>, kGlLdsBytes);
-    k_bucket_group12_glds<Out><<<std::min<uint32_t>(nb, kPartBlocks), kGroupThreads, kGlLdsBytes, s>>>(
-        rec, rank_base, offs + out.bucket0, nb, bits, chunk_of, gkey, gmin, out);
-    return;
-  }
   k_bucket_group12_pk<Out><<<nb, kGroupThreads, 0, s>>>(rec, rank_base, offs, bits, chunk_of, gkey,
                                                         gmin, out);
 }
