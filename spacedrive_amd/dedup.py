@@ -293,6 +293,7 @@ class Comm:
 
     def __init__(self, ctx, handle):
         self.ctx, self.h = ctx, handle
+        self._hold = None  # an unresolved padded call's tensors (_held)
 
     @staticmethod
     def unique_id() -> bytes:
@@ -329,6 +330,7 @@ class Comm:
         call (re-run counted on an overflow; its -ENOSPC raised here)
         (sdgpu_comm_wait)."""
         check(self.ctx.lib.sdgpu_comm_wait(self.h, stream), "sdgpu_comm_wait")
+        self._hold = None  # the resolved call's tensors (see _held)
 
     def set_return(self, mode: int):
         """SDGPU_RETURN_COMPACT (only the linked rows' reps travel back, one
@@ -371,12 +373,21 @@ class Comm:
         if self.h:
             self.ctx.lib.sdgpu_comm_destroy(self.h)
             self.h = None
+        self._hold = None
 
     def __del__(self):
         try:
             self.close()
         except Exception:
             pass
+
+
+def _held(comm: Comm, tensors):
+    """Keeps an unresolved padded call's tensors alive until the call is
+    resolved (sdgpu.h: until then its inputs must not change, and an overflow
+    re-run, enqueued by the next exchange call or Comm.wait(), still reads and
+    writes them): held on the communicator until the next call or wait."""
+    comm._hold = tensors
 
 
 def group_sharded(key, has_key, rank, comm: Comm, index: ObjectIndex | None = None,
@@ -395,6 +406,7 @@ def group_sharded(key, has_key, rank, comm: Comm, index: ObjectIndex | None = No
         ctx.h, comm.h, index.h if index is not None else None, key.data_ptr(),
         has_key.data_ptr() if has_key is not None else None, rank.data_ptr(), key.numel(),
         chunk_rows, rep.data_ptr(), s), "sdgpu_group_sharded_device")
+    _held(comm, (key, has_key, rank, rep, index))
     if wait:
         comm.wait(s)
     return rep
@@ -543,6 +555,7 @@ def group_link_sharded(key, has_key, valid, rank, comm, chunk_rows: int = 100,
                                                   who.data_ptr(), obj.data_ptr(), cap,
                                                   counts.data_ptr(), s),
           "sdgpu_group_link_sharded_device")
+    _held(comm, (key, has_key, valid, rank, who, obj, counts))
     if not trim:
         return who, obj, counts
     comm.wait(s)
