@@ -1545,8 +1545,9 @@ def main(argv=None, runner_cls=None, out=None):
                  "data": "synthetic (BASELINE configs 2/3/4 shapes, generated in HBM)",
                  "config": {"workload": "identifier job step: config2 (1M files/GPU) cas_id + "
                                         "cas_id->Object grouping + Object write set (one fused "
-                                        "pass on one GPU; hash-sharded over RCCL + link batch "
-                                        "at N > 1)",
+                                        "pass on one GPU; at N > 1 hash-sharded over RCCL, each "
+                                        "owner writing its share of the write set, padded "
+                                        "exchange)",
                             "files_per_gpu": args.files, "global_files": args.files * R.world,
                             "parallelism": f"dp{R.world} (files) + hash-sharded dedup, "
                                            "RCCL all-to-all"},
