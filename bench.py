@@ -577,6 +577,10 @@ class Runner:
             # the listing encoded once for the C ABI (as a host holds its
             # CStrings); the CPU port below gets the same pre-encoded array
             paths = fi.PathList(paths)
+            # the files were just written: flush them first, so the kernel's
+            # writeback of ~0.6 GB of dirty pages does not run under the timed
+            # reads (it made the first timed call ~35 % slower, r5s step_ms)
+            os.sync()
             fi.identify(paths, sizes=sizes, ctx=self.ctx)  # warm page cache
             self.barrier()
             # each call timed on its own: one call is ~15 ms of host reads,
