@@ -1,5 +1,6 @@
-# Round 5: correctness of the LDS-staged group kernel (k_bucket_group12_glds,
-# default on), then an interleaved A/B against SDGPU_GROUP_GLDS=0 at 100 M
+# Round 5 (historical: run on commit 1346212, where the LDS-staged group
+# kernel k_bucket_group12_glds existed; it was removed after this A/B):
+# correctness, then an interleaved A/B against SDGPU_GROUP_GLDS=0 at 100 M
 # and 12.5 M rows (exp_seg_groups.py; the digest must match between legs).
 #   TAG=r5n [TESTS=...] bash scripts/gpu_r5_glds.sh
 set -o pipefail

@@ -19,7 +19,8 @@ for rows in 100000000 12500000; do
       || { echo "set $i rows $rows failed"; tail -5 "$OUT/r${rows}_s$i.log"; }
   done
 done
-# the LDS-staged persistent variant (SDGPU_GROUP_GLDS=1, negative A/B), set 1
+# the LDS-staged persistent variant (SDGPU_GROUP_GLDS=1, negative A/B; the
+# knob existed until commit 1346212's kernel was removed), set 1
 SDGPU_GROUP_GLDS=1 timeout -s KILL 120 rocprofv3 --pmc ${SETS[0]} -d "$OUT/glds_r12500000_s1" -o pmc \
   --output-format csv -- python3 scripts/exp/exp_seg_groups.py 12500000 2 > "$OUT/glds_s1.log" 2>&1 \
   || { echo "glds set failed"; tail -5 "$OUT/glds_s1.log"; }
