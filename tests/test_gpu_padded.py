@@ -182,3 +182,42 @@ def test_padded_one_rank_rccl_rep_form(ctx):
     assert s1["padded_calls"] - s0["padded_calls"] == 1
     assert s1["overflow_reruns"] - s0["overflow_reruns"] == 1
     comm.close()
+
+
+@pytest.mark.parametrize("shares", [(0, 5, 120_000), (60_000, 0, 0), (1, 0, 90_000, 7)])
+def test_padded_empty_and_tiny_ranks(ctxs, shares):
+    """Ragged padded calls: ranks holding no rows or a handful send only
+    headers and padding, and still receive their owned rows; the rep form
+    and the write-set form both equal the oracle."""
+    import torch
+    from spacedrive_amd import dedup
+    world, total = len(shares), sum(shares)
+    k, h, _ = O.synth_dedup_rows(71 + world, total, max(1, int(total * 0.8)), 0, total)
+    valid = np.ones(total, np.uint8)
+    bounds = np.concatenate([[0], np.cumsum(shares)]).astype(np.int64)
+    dev = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    keys = [dev(k[bounds[r]:bounds[r + 1]].view(np.int64)) for r in range(world)]
+    hass = [dev(h[bounds[r]:bounds[r + 1]]) for r in range(world)]
+    vals = [dev(valid[bounds[r]:bounds[r + 1]]) for r in range(world)]
+    ranks = [torch.arange(int(bounds[r]), int(bounds[r + 1]), dtype=torch.int64).to(torch.int32).cuda()
+             for r in range(world)]
+    ref = O.group_reps(k, h, 100)
+    comms = dedup.Comm.init_all(ctxs[:world])
+    for c in comms:
+        c.set_exchange(dedup.EXCHANGE_PADDED, max(shares))
+    reps = dedup.group_sharded_all(keys, hass, ranks, comms, None, 100)
+    out = np.concatenate([rp.cpu().numpy().view(np.uint32) for rp in reps])
+    np.testing.assert_array_equal(out, ref)
+    parts = dedup.group_link_sharded_all(keys, hass, vals, ranks, comms, 100)
+    w = np.concatenate([p[0].cpu().numpy() for p in parts])
+    o = np.concatenate([p[1].cpu().numpy() for p in parts])
+    c, lr, lo = dedup.split_link_lists(w, o)
+    rc, rlr, rlo = O.link_batch(ref, None, valid, 0)
+    np.testing.assert_array_equal(c, rc)
+    np.testing.assert_array_equal(lr, rlr)
+    np.testing.assert_array_equal(lo, rlo)
+    sts = [cm.stats() for cm in comms]
+    assert all(st["padded_calls"] == 2 for st in sts)
+    assert len({st["overflow_reruns"] for st in sts}) == 1
+    for cm in comms:
+        cm.close()
