@@ -578,8 +578,9 @@ class Runner:
             # CStrings); the CPU port below gets the same pre-encoded array
             paths = fi.PathList(paths)
             # the files were just written: flush them first, so the kernel's
-            # writeback of ~0.6 GB of dirty pages does not run under the timed
-            # reads (it made the first timed call ~35 % slower, r5s step_ms)
+            # writeback of their dirty pages does not run under the timed reads
+            # (the first timed call stays ~35 % slower either way, r5s / r5x
+            # step_ms: hence the median)
             os.sync()
             fi.identify(paths, sizes=sizes, ctx=self.ctx)  # warm page cache
             self.barrier()
