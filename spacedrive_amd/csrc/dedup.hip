@@ -1373,14 +1373,17 @@ __device__ __forceinline__ uint32_t lds_slot(uint64_t h) {
   return static_cast<uint32_t>((static_cast<uint64_t>(static_cast<uint32_t>(h)) * kLdsSlots) >> 32);
 }
 
-// Double hashing: a key's probe step is 1 + 6 * (10 hash bits above the slot
-// bits), coprime with the 6144 (= 2^11 * 3) slots, so every probe sequence
+// Double hashing: a key's probe step is 1 + 6 * (10 low hash bits, below the
+// slot's), coprime with the 6144 (= 2^11 * 3) slots, so every probe sequence
 // visits every slot and sequences of different keys do not run together in
 // clusters.  A wave probes until its longest chain is placed; with linear
 // probing those chains were clustered: 12.5 M rows 0.099 -> 0.081 ms
 // (scripts/exp_group_persist.hip, profiles/r2/exp_group_persist_r2AG.log).
+// (Round 5: the 10 bits are the LOW bits of h lo -- bits 40-49 overlapped the
+// bucket's own digit bits, so inside a bucket the step took only 2^(10 -
+// overlap) values; the slot comes from the top bits of h lo.)
 __device__ __forceinline__ uint32_t lds_step(uint64_t h) {
-  return 1u + 6u * static_cast<uint32_t>((h >> 40) & 1023u);
+  return 1u + 6u * (static_cast<uint32_t>(h) & 1023u);
 }
 
 __device__ __forceinline__ uint32_t next_slot(uint32_t h, uint32_t step) {
