@@ -1222,8 +1222,9 @@ class Runner:
         if lv[0] > 0:
             res["leaf_valu_frac_spec"] = comp * ISA_PER_COMPRESSION / (lv[0] / lv[1] * 1e-3) \
                 / VALU_PEAK_SPEC
-        if not self.args.no_cpu and files:
-            # parity of the timed batch (after the timing):
+        if self.world == 1 and not self.args.no_cpu and files:
+            # parity of the timed batch (after the timing; VERDICT r4 item 4;
+            # at N = 1 only, like every oracle check of the bench):
             # the first, the last and two middle digests of the ONE plan the
             # bench times (cross-file offsets past 2^32 bytes) against the
             # oracle's multi-threaded AVX-512 hasher over the same bytes
