@@ -1808,19 +1808,16 @@ constexpr uint32_t kPkCap = 4095;
 
 // The packed group-by of one bucket whose records are in registers (q[j] =
 // {h lo, h hi, rank, row}, row kPadRow past the end), m = end - start <=
-// kPkCap.  kRaw: barriers without a vmcnt drain (the LDS-staged kernel).
-template <bool kRaw, int kP, typename Out>
+// kPkCap, bits in 12..15 (the word's key field; group_launch picks this
+// kernel only for those).
+template <int kP, typename Out>
 __device__ __forceinline__ void group_packed_regs(const uint4 (&q)[kP], uint32_t start, uint32_t end,
                                                   uint32_t bits, ChunkOf chunk_of, const Out& out,
                                                   uint64_t* tab, uint32_t* lmin, uint32_t* scr) {
-  auto barrier = [] {
-    if constexpr (kRaw) lds_barrier();
-    else __syncthreads();
-  };
   for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
   for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
   out_init(out, scr);
-  barrier();
+  __syncthreads();
   // word hi: the 24 - bits hi-word bits below the digit, the 8 shard bits
   // above it, then index + 1 in bits 20..31 (bits in 12..15: <= 20 key bits)
   const uint32_t kb = 24u - bits, lowm = (1u << kb) - 1u;
@@ -1866,7 +1863,7 @@ __device__ __forceinline__ void group_packed_regs(const uint4 (&q)[kP], uint32_t
 #pragma unroll
   for (int j = 0; j < kP; ++j)
     if (live >> j & 1u) atomicMin(&lmin[owner[j]], q[j].z);
-  barrier();
+  __syncthreads();
   bool lv[kP], lk[kP];
   uint32_t r[kP], w[kP], f[kP];
 #pragma unroll
@@ -1909,7 +1906,7 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
 #pragma unroll
   for (int j = 0; j < kP; ++j)
     if (start + threadIdx.x + j * kGroupThreads >= end) q[j] = make_uint4(0, 0, kPadRow, kPadRow);
-  group_packed_regs<false>(q, start, end, bits, chunk_of, out, tab, lmin, scr);
+  group_packed_regs(q, start, end, bits, chunk_of, out, tab, lmin, scr);
   out_done(out, 0u, 0u, end, scr);
 }
 
