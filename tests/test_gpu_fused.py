@@ -291,3 +291,29 @@ def test_fused_two_level_path_all_keyless_tiles(ctx):
     valid = np.ones(n, np.uint8)
     valid[n // 8: n // 8 + 5000] = 0
     _check(ctx, key, has, valid=valid)
+
+
+@pytest.mark.parametrize("t,distinct", [(4095, 4095), (4095, 1500), (4096, 4096), (4096, 2000)])
+def test_fused_packed_bucket_at_capacity(ctx, t, distinct):
+    """One 12-bit bucket of exactly kPkCap = 4095 records among 12.5 M rows --
+    the packed table's last record index (the word's index field 0xFFF) --
+    or one more (the global table), with all-distinct or repeated keys: keys
+    built from hashes whose digit bits (44-55) name the bucket."""
+    n, D = 12_500_000, 1234
+    rng = np.random.default_rng(t * 7 + distinct)
+    sh8, sh52 = np.uint64(8), np.uint64(52)
+    key = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    dig = (O.mix64(key) << sh8) >> sh52
+    bad = np.flatnonzero(dig == D)
+    while bad.size:  # every other row outside bucket D
+        key[bad] = rng.integers(0, 2**64 - 1, bad.size, dtype=np.uint64, endpoint=True)
+        dig[bad] = (O.mix64(key[bad]) << sh8) >> sh52
+        bad = bad[dig[bad] == D]
+    mask = np.uint64(0xFFF << 44)
+    hs = (rng.integers(0, 2**63, distinct, dtype=np.uint64) & ~mask) | (np.uint64(D) << np.uint64(44))
+    ks = np.array([inv_mix64(int(h)) for h in hs], np.uint64)
+    assert np.all(((O.mix64(ks) << sh8) >> sh52) == D)
+    pick = ks[rng.integers(0, distinct, t)]
+    pick[:distinct] = ks
+    key[rng.choice(n, t, replace=False)] = pick
+    _check(ctx, key, np.ones(n, np.uint8), chunk=100)
