@@ -293,26 +293,30 @@ def test_fused_two_level_path_all_keyless_tiles(ctx):
     _check(ctx, key, has, valid=valid)
 
 
-@pytest.mark.parametrize("t,distinct", [(4095, 4095), (4095, 1500), (4096, 4096), (4096, 2000)])
-def test_fused_packed_bucket_at_capacity(ctx, t, distinct):
-    """One 12-bit bucket of exactly kPkCap = 4095 records among 12.5 M rows --
-    the packed table's last record index (the word's index field 0xFFF) --
-    or one more (the global table), with all-distinct or repeated keys: keys
-    built from hashes whose digit bits (44-55) name the bucket."""
-    n, D = 12_500_000, 1234
-    rng = np.random.default_rng(t * 7 + distinct)
-    sh8, sh52 = np.uint64(8), np.uint64(52)
+@pytest.mark.parametrize("n,bits,t,distinct", [
+    (12_500_000, 12, 4095, 4095), (12_500_000, 12, 4095, 1500), (12_500_000, 12, 4096, 4096),
+    (12_500_000, 12, 4096, 2000), (13_000_000, 13, 4095, 4095), (13_000_000, 13, 4096, 3000)])
+def test_fused_packed_bucket_at_capacity(ctx, n, bits, t, distinct):
+    """One bucket of exactly kPkCap = 4095 records -- the packed table's last
+    record index (the word's index field 0xFFF) -- or one more (the global
+    table), with all-distinct or repeated keys, on the one-level 12-bit path
+    (12.5 M rows) and the two-level path (13 M rows: 13 digit bits): keys
+    built from hashes whose digit bits (56 - bits .. 55) name the bucket."""
+    D = 1234
+    rng = np.random.default_rng(t * 7 + distinct + bits)
+    sh8, shd = np.uint64(8), np.uint64(64 - bits)
     key = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
-    dig = (O.mix64(key) << sh8) >> sh52
+    dig = (O.mix64(key) << sh8) >> shd
     bad = np.flatnonzero(dig == D)
     while bad.size:  # every other row outside bucket D
         key[bad] = rng.integers(0, 2**64 - 1, bad.size, dtype=np.uint64, endpoint=True)
-        dig[bad] = (O.mix64(key[bad]) << sh8) >> sh52
+        dig[bad] = (O.mix64(key[bad]) << sh8) >> shd
         bad = bad[dig[bad] == D]
-    mask = np.uint64(0xFFF << 44)
-    hs = (rng.integers(0, 2**63, distinct, dtype=np.uint64) & ~mask) | (np.uint64(D) << np.uint64(44))
+    lo = 56 - bits
+    mask = np.uint64(((1 << bits) - 1) << lo)
+    hs = (rng.integers(0, 2**63, distinct, dtype=np.uint64) & ~mask) | (np.uint64(D) << np.uint64(lo))
     ks = np.array([inv_mix64(int(h)) for h in hs], np.uint64)
-    assert np.all(((O.mix64(ks) << sh8) >> sh52) == D)
+    assert np.all(((O.mix64(ks) << sh8) >> shd) == D)
     pick = ks[rng.integers(0, distinct, t)]
     pick[:distinct] = ks
     key[rng.choice(n, t, replace=False)] = pick
