@@ -189,9 +189,9 @@ __global__ __launch_bounds__(kThreads) void k_thumb_hist(const uint8_t* __restri
 
 // Stable within a block's tile: one round of kThreads rows at a time.  A row's
 // place in its bin = cursor + rows with the same byte in earlier waves of the
-// round + earlier lanes of its own wave with the same byte (a ballot per
-// distinct byte in the wave: ~57 for random bytes, instead of a scan of the
-// whole round per row).
+// round + earlier lanes of its own wave with the same byte.  The lanes holding
+// the same byte are found with 8 ballots, one per bit of the byte (round 5;
+// a ballot per distinct byte in the wave took ~57 passes for random bytes).
 __global__ __launch_bounds__(kThreads) void k_thumb_scatter(const uint8_t* __restrict__ cas8,
                                                             const uint8_t* __restrict__ valid,
                                                             uint64_t n,
@@ -211,16 +211,15 @@ __global__ __launch_bounds__(kThreads) void k_thumb_scatter(const uint8_t* __res
     const uint32_t b = i < t1 ? cas8[8 * i] : 0u;
     for (uint32_t k = threadIdx.x; k < kWaves * kShardBins; k += kThreads) (&wcnt[0][0])[k] = 0;
     __syncthreads();
-    uint64_t rem = __ballot(v);
-    uint32_t rank = 0;
-    while (rem) {  // wave-uniform
-      const int leader = __ffsll(static_cast<unsigned long long>(rem)) - 1;
-      const uint32_t bl = __shfl(b, leader);
-      const uint64_t m = __ballot(v && b == bl);
-      if (v && b == bl) rank = __popcll(m & ((1ull << lane) - 1ull));
-      if (lane == static_cast<uint32_t>(leader)) wcnt[wave][bl] = __popcll(m);
-      rem &= ~m;
+    uint64_t peers = __ballot(v);  // the valid lanes whose byte equals this lane's
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool bit = (b >> k) & 1u;
+      const uint64_t mk = __ballot(bit);
+      peers &= bit ? mk : ~mk;
     }
+    const uint32_t rank = static_cast<uint32_t>(__popcll(peers & ((1ull << lane) - 1ull)));
+    if (v && rank == 0) wcnt[wave][b] = static_cast<uint32_t>(__popcll(peers));
     __syncthreads();
     if (v) {
       uint32_t p = cur[b] + rank;

@@ -60,3 +60,21 @@ def test_thumbnail_shards(ctx, n):
     np.testing.assert_array_equal(o2[:int(ec.sum())].cpu().numpy(), eo)
     if n:
         assert consumers.get_shard_hex(bytes(cas8[0]).hex()) == f"{cas8[0, 0]:02x}"
+
+
+@pytest.mark.parametrize("values", [(0x5A,), (7, 200), (0, 1, 2, 3, 128, 255)])
+def test_thumbnail_shards_skewed_bytes(ctx, values):
+    """Few distinct first bytes, so every wave holds long runs of equal bytes
+    (the same-byte lane masks of k_thumb_scatter), keyless rows between."""
+    import torch
+    from spacedrive_amd import consumers
+    n = 300_007
+    rng = np.random.default_rng(len(values))
+    cas8 = rng.integers(0, 256, (n, 8), dtype=np.uint8)
+    cas8[:, 0] = np.asarray(values, np.uint8)[rng.integers(0, len(values), n)]
+    valid = (rng.random(n) > 0.1).astype(np.uint8)
+    order, counts = consumers.thumbnail_shards(torch.from_numpy(cas8).cuda(),
+                                               torch.from_numpy(valid).cuda(), ctx)
+    eo, ec = O.thumbnail_shards(cas8, valid)
+    np.testing.assert_array_equal(counts.cpu().numpy(), ec)
+    np.testing.assert_array_equal(order.cpu().numpy(), eo)
