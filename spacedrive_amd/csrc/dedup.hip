@@ -117,24 +117,30 @@ __device__ __forceinline__ uint32_t part_digit(uint64_t h, uint32_t skip, uint32
 
 // Wave-aggregated LDS counter add for few, heavily shared bins (the exchange's
 // W destination ranks): one atomic per distinct digit in the wave instead of
-// one per row.  Every active lane of the wave must call it (v = row counts);
-// returns the row's slot (base of its bin + its rank among the wave's lanes
-// with the same digit).
-__device__ __forceinline__ uint32_t wave_add(uint32_t* cnt, uint32_t d, bool v) {
+// one per row.  Every active lane of the wave must call it (v = row counts;
+// digits d < 2^nbits); returns the row's slot (base of its bin + its rank
+// among the wave's lanes with the same digit).  The lanes sharing a digit
+// come from nbits ballots, one per digit bit, and the groups' atomics issue
+// together (round 5: a loop over the distinct digits took up to W dependent
+// atomic round trips per row step).
+__device__ __forceinline__ uint32_t wave_add(uint32_t* cnt, uint32_t d, bool v, uint32_t nbits) {
   const uint32_t lane = __lane_id();
-  uint64_t pending = __ballot(v);
-  uint32_t slot = 0;
-  while (pending) {
-    const int leader = __ffsll(static_cast<unsigned long long>(pending)) - 1;
-    const uint32_t dl = __shfl(d, leader);
-    const uint64_t m = __ballot(v && d == dl);
-    uint32_t base = 0;
-    if (lane == static_cast<uint32_t>(leader)) base = atomicAdd(&cnt[dl], __popcll(m));
-    base = __shfl(base, leader);
-    if ((m >> lane) & 1ull) slot = base + __popcll(m & ((1ull << lane) - 1ull));
-    pending &= ~m;
+  uint64_t peers = __ballot(v);
+  for (uint32_t k = 0; k < nbits; ++k) {  // wave-uniform
+    const bool bit = (d >> k) & 1u;
+    const uint64_t mk = __ballot(bit);
+    peers &= bit ? mk : ~mk;
   }
-  return slot;
+  const uint32_t rank = static_cast<uint32_t>(__popcll(peers & ((1ull << lane) - 1ull)));
+  uint32_t base = 0;
+  if (v && rank == 0) base = atomicAdd(&cnt[d], static_cast<uint32_t>(__popcll(peers)));
+  const int leader = __ffsll(static_cast<unsigned long long>(peers)) - 1;
+  base = __shfl(base, v ? leader : static_cast<int>(lane));
+  return v ? base + rank : 0u;
+}
+// digit bits of bins 0 .. world - 1
+__device__ __forceinline__ uint32_t world_bits(uint32_t world) {
+  return world > 1 ? 32u - static_cast<uint32_t>(__clz(world - 1)) : 0u;
 }
 
 // The valid keyless rows of a fused grouping call (ListOut without an Object
@@ -267,7 +273,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(In in, uint64_t n, u
       const uint64_t k = in.key_of(q, u);
       if constexpr (kX) sink_keyless(xs, in, q.in[u] && !v, q.row[u], wn);
       if (world) {
-        (void)wave_add(cnt, v ? part_digit(in_hash<In>(k), skip, bits, world) : 0u, v);
+        (void)wave_add(cnt, v ? part_digit(in_hash<In>(k), skip, bits, world) : 0u, v, world_bits(world));
       } else if (v) {
         atomicAdd(&cnt[part_digit(in_hash<In>(k), skip, bits, world)], 1u);
       }
@@ -314,7 +320,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(
       const bool v = in.valid_of(q, u);
       const uint64_t k = in.key_of(q, u);
       const uint32_t d = v ? part_digit(in_hash<In>(k), skip, bits, world) : 0u;
-      const uint32_t p = world ? wave_add(cur, d, v) : (v ? atomicAdd(&cur[d], 1u) : 0u);
+      const uint32_t p = world ? wave_add(cur, d, v, world_bits(world)) : (v ? atomicAdd(&cur[d], 1u) : 0u);
       if (!v) {
         if (kRec12 && q.in[u] && out_pos) out_pos[i] = 0xFFFFFFFFu;
         continue;
@@ -369,7 +375,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_padded(
     for (int u = 0; u < kPadU; ++u) {
       const bool v = in.valid_of(q, u);
       const uint32_t d = v ? part_digit(row_hash(in.key_of(q, u)), 0, kXShardBitsDev, world) : 0u;
-      lr[u] = wave_add(cnt, d, v);
+      lr[u] = wave_add(cnt, d, v, world_bits(world));
       dg[u] = v ? d : ~0u;
       if (xs.st)  // uniform; a ballot, and a store only for the rare valid keyless row
         sink_keyless(xs, in, q.in[u] && !v, i0 + threadIdx.x + static_cast<uint64_t>(u) * kPartThreads,
