@@ -1801,16 +1801,22 @@ __device__ __forceinline__ void group_bucket(Src rec, uint32_t start,
 // -> 0.072 ms (profiles/r3/exp_group_packed/run.log).
 // Round 5: the kernel is VALU-issue bound (SQ counters,
 // VALU busy 73 % of the SIMD cycles at 12.5 M rows, 82 % at
-// 100 M), so the per-record setup was cut: the word is assembled with 32-bit
-// operations (lo = h lo, hi = the remaining hi bits | (index + 1) << 20) and
-// the double-hashing step (coprime with 2^9 * 15) is 30 k + r, r one of the
-// 8 residues prime to 30 read from a nibble table -- ~6 VALU where the odd
-// step with its mod-3 / mod-5 corrections took ~16.  (Linear probing, step
-// 1, cut more VALU but lengthened the probe chains: 12.5 M rows 0.079 ->
-// 0.085 ms, profiles/r5/pmc_group/.)
-// Buckets above 4095 records take the global table; pads (row ~0) are skipped.
-constexpr uint32_t kPkSlots = 7680;  // 2^9 * 15
-constexpr uint32_t kPkCap = 4095;
+// 100 M), so the VALU per record was cut twice.  First: the word assembled
+// from 32-bit halves, and a double-hashing step from the LOW bits of h lo
+// (the old one overlapped the digit bits: nearly linear probing).  Second:
+// 2^13 slots (a step wraps as a 16-bit add of byte offsets; the odd step
+// from the 13 low bits of h lo, the slot from its 13 top bits); the probe
+// loop without branches per record (see below); the owner read from the
+// record's final slot after the loop.  Probe-loop VALU per record and round
+// ~16 -> 7.  64 KiB of table + a 4096-word area = exactly half the CU's LDS
+// (two workgroups per CU, as before); the area holds lmin[kPkCap],
+// special_min and the output's scratch, so kPkCap = 4093.  (Linear probing,
+// step 1, lengthened the probe chains: 12.5 M rows 0.079 -> 0.085 ms,
+// profiles/r5/pk_ab/.)
+// Buckets above kPkCap records take the global table; pads (row ~0) are skipped.
+constexpr uint32_t kPkSlots = 8192;  // 2^13
+constexpr uint32_t kPkWords = 4096;  // lmin[kPkCap] | special_min | scr[2]
+constexpr uint32_t kPkCap = kPkWords - 3;
 
 // The packed group-by of one bucket whose records are in registers (q[j] =
 // {h lo, h hi, rank, row}, row kPadRow past the end), m = end - start <=
@@ -1821,67 +1827,89 @@ __device__ __forceinline__ void group_packed_regs(const uint4 (&q)[kP], uint32_t
                                                   uint32_t bits, ChunkOf chunk_of, const Out& out,
                                                   uint64_t* tab, uint32_t* lmin, uint32_t* scr) {
   for (uint32_t s = threadIdx.x; s < kPkSlots; s += kGroupThreads) tab[s] = 0ull;
-  for (uint32_t s = threadIdx.x; s <= kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
+  for (uint32_t s = threadIdx.x; s < kPkCap; s += kGroupThreads) lmin[s] = 0xFFFFFFFFu;
   out_init(out, scr);
   __syncthreads();
   // word hi: the 24 - bits hi-word bits below the digit, the 8 shard bits
   // above it, then index + 1 in bits 20..31 (bits in 12..15: <= 20 key bits)
   const uint32_t kb = 24u - bits, lowm = (1u << kb) - 1u;
-  uint32_t whi[kP], slot[kP], step[kP], owner[kP];
-  uint32_t pend = 0;
+  uint32_t sa[kP], sst[kP], own1[kP], khi[kP];
+  uint64_t word[kP];  // the record's word; 0 for a pad
+  bool live[kP];
 #pragma unroll
   for (int j = 0; j < kP; ++j) {
-    const uint32_t idx = threadIdx.x + j * kGroupThreads;
-    whi[j] = (q[j].y & lowm) | ((q[j].y >> 24) << kb) | ((idx + 1) << 20);
-    slot[j] = __umulhi(q[j].x, kPkSlots);  // the top bits of h lo
-    // (r - 1) / 2 for r = 1 7 11 13 17 19 23 29, one nibble each; k and the
-    // residue from the low bits of h lo
-    const uint32_t nib = __builtin_amdgcn_ubfe(0xEB986530u, ((q[j].x >> 6) & 7u) << 2, 4);
-    step[j] = 30u * (q[j].x & 63u) + 2u * nib + 1u;
-    owner[j] = idx;
-    if (q[j].w != kPadRow) pend |= 1u << j;
+    const uint32_t idx1 = threadIdx.x + j * kGroupThreads + 1u;
+    khi[j] = (q[j].y & lowm) | ((q[j].y >> 24) << kb);
+    live[j] = q[j].w != kPadRow;
+    word[j] = live[j] ? (static_cast<uint64_t>(khi[j] | (idx1 << 20)) << 32) | q[j].x : 0ull;
+    // byte offsets: the slot from the top 13 bits of h lo, the (odd) step
+    // from its low 13 bits -- both independent of the digit bits (h hi)
+    // (a pad: a slot of its own lane -- pads share the last record's h, and
+    // 64 lanes CASing one word serialise)
+    sa[j] = live[j] ? (q[j].x >> 16) & 0xFFF8u : threadIdx.x << 3;
+    sst[j] = ((q[j].x << 3) | 8u) & 0xFFF8u;
   }
-  const uint32_t live = pend;
-  // the records of a thread probe in lock step (their LDS round trips overlap)
-  while (pend) {
+  // The records of a thread probe in lock step, without branches: every
+  // round CASes all four words and the round's results decide.  A record
+  // that has found its key CASes the same slot again, which holds that key
+  // (its own word or its owner's) and so leaves it unchanged and finds it
+  // again; a pad's word is 0, and CAS(0 -> 0) changes nothing.  Branches
+  // per record (the lanes' pending masks) made the compiler wait out each
+  // CAS before issuing the next.
+  for (;;) {
     uint64_t prev[kP];
 #pragma unroll
     for (int j = 0; j < kP; ++j)
-      prev[j] = (pend >> j & 1u)
-                    ? atomicCAS(reinterpret_cast<unsigned long long*>(&tab[slot[j]]), 0ull,
-                                (static_cast<unsigned long long>(whi[j]) << 32) | q[j].x)
-                    : 0ull;
+      prev[j] = atomicCAS(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(tab) + sa[j]),
+                          0ull, static_cast<unsigned long long>(word[j]));
+    bool all = true;
 #pragma unroll
     for (int j = 0; j < kP; ++j) {
-      if (!(pend >> j & 1u)) continue;
       const uint32_t plo = static_cast<uint32_t>(prev[j]), phi = static_cast<uint32_t>(prev[j] >> 32);
-      if ((plo | phi) == 0u) {
-        pend &= ~(1u << j);  // placed: owns its key
-      } else if ((((phi ^ whi[j]) & 0xFFFFFu) | (plo ^ q[j].x)) == 0u) {
-        owner[j] = (phi >> 20) - 1;
-        pend &= ~(1u << j);
-      } else {
-        const uint32_t sn = slot[j] + step[j];
-        slot[j] = sn >= kPkSlots ? sn - kPkSlots : sn;
-      }
+      const bool hit = !live[j] || prev[j] == 0ull || (plo == q[j].x && (phi & 0xFFFFFu) == khi[j]);
+      sa[j] = static_cast<uint16_t>(sa[j] + (hit ? 0u : sst[j]));  // 2^13 slots x 8 B
+      all = all && hit;
     }
+    if (all) break;
   }
+  // each record's slot now holds its key's word: the owner's index + 1
 #pragma unroll
   for (int j = 0; j < kP; ++j)
-    if (live >> j & 1u) atomicMin(&lmin[owner[j]], q[j].z);
+    own1[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + sa[j] + 4) >> 20;
+#pragma unroll
+  for (int j = 0; j < kP; ++j)
+    if (live[j]) atomicMin(&lmin[own1[j] - 1u], q[j].z);
   __syncthreads();
-  bool lv[kP], lk[kP];
+  bool lk[kP];
   uint32_t r[kP], w[kP], f[kP];
 #pragma unroll
   for (int j = 0; j < kP; ++j) {
-    lv[j] = live >> j & 1u;
     r[j] = q[j].z;
     w[j] = q[j].w;
-    f[j] = lmin[owner[j]];
-    lk[j] = lv[j] && r[j] != f[j] && chunk_of(r[j]) != chunk_of(f[j]);
+    f[j] = lmin[own1[j] - 1u];
+    lk[j] = live[j] && r[j] != f[j] && chunk_of(r[j]) != chunk_of(f[j]);
   }
   uint32_t c_run = 0, l_run = 0;
-  out.template emit<kP>(lv, lk, r, w, f, start, end, c_run, l_run, scr, false);
+  out.template emit<kP>(live, lk, r, w, f, start, end, c_run, l_run, scr, false);
+}
+
+// Records of a bucket into registers, kP per thread: every load issued
+// unconditionally (past the end: the bucket's last record) and the pad
+// selected after -- a guarded `i < end ? rec(i) : pad` made the compiler
+// branch around each load and wait out its latency before the next one
+// (four serial memory latencies per workgroup).  Only the row marks a pad:
+// nothing reads a pad's other fields.
+template <int kP, typename Src, typename Out>
+__device__ __forceinline__ void group_packed_load(Src rec, uint32_t start, uint32_t end,
+                                                  uint32_t bits, ChunkOf chunk_of, const Out& out,
+                                                  uint64_t* tab, uint32_t* lmin, uint32_t* scr) {
+  uint4 q[kP];
+#pragma unroll
+  for (int j = 0; j < kP; ++j) q[j] = rec(min(start + threadIdx.x + j * kGroupThreads, end - 1));
+#pragma unroll
+  for (int j = 0; j < kP; ++j)
+    if (start + threadIdx.x + j * kGroupThreads >= end) q[j].w = kPadRow;
+  group_packed_regs(q, start, end, bits, chunk_of, out, tab, lmin, scr);
 }
 
 template <typename Src, typename Out>
@@ -1891,7 +1919,6 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
                                                     uint32_t* __restrict__ gmin, const Out& out,
                                                     uint64_t* tab, uint32_t* lmin,
                                                     uint32_t& special_min, uint32_t* scr) {
-  constexpr int kP = (kPkCap + kGroupThreads) / kGroupThreads;  // 4
   const uint32_t m = end - start;
   if (m == 0) {
     out_init(out, scr);  // an empty bucket: counters zeroed for done
@@ -1902,17 +1929,13 @@ __device__ __forceinline__ void group_bucket_packed(Src rec, uint32_t start, uin
     group_bucket_global(rec, start, end, chunk_of, gkey, gmin, out, special_min, scr);
     return;
   }
-  // every load issued unconditionally (past the end: the bucket's last record)
-  // and the pad selected after: a guarded `i < end ? rec(i) : pad` made the
-  // compiler branch around each load and wait out its latency before the
-  // next one (four serial memory latencies per workgroup)
-  uint4 q[kP];
-#pragma unroll
-  for (int j = 0; j < kP; ++j) q[j] = rec(min(start + threadIdx.x + j * kGroupThreads, end - 1));
-#pragma unroll
-  for (int j = 0; j < kP; ++j)
-    if (start + threadIdx.x + j * kGroupThreads >= end) q[j] = make_uint4(0, 0, kPadRow, kPadRow);
-  group_packed_regs(q, start, end, bits, chunk_of, out, tab, lmin, scr);
+  // three records per thread when they suffice (uniform per bucket; ~3 k
+  // records is the mean bucket): a fourth of pads would still probe
+  static_assert(kPkCap <= 4 * kGroupThreads, "four records per thread hold a bucket");
+  if (m <= 3 * kGroupThreads)
+    group_packed_load<3>(rec, start, end, bits, chunk_of, out, tab, lmin, scr);
+  else
+    group_packed_load<4>(rec, start, end, bits, chunk_of, out, tab, lmin, scr);
   out_done(out, 0u, 0u, end, scr);
 }
 
@@ -1958,9 +1981,11 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group_pk(
     const uint4* __restrict__ rec, const uint32_t* __restrict__ offs, uint32_t P, uint32_t bits,
     ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin, Out out) {
   __shared__ uint64_t tab[kPkSlots];
-  __shared__ uint32_t lmin[kPkCap + 1];
-  __shared__ uint32_t special_min;
-  __shared__ uint32_t scr[Out::kScratch];
+  __shared__ uint32_t lw[kPkWords];  // lmin | special_min | scr (80 KiB in all)
+  static_assert(Out::kScratch <= 2, "scratch fits the word area");
+  uint32_t* lmin = lw;
+  uint32_t& special_min = lw[kPkCap];
+  uint32_t* scr = lw + kPkCap + 1;
   const uint32_t b = out.bucket0 + blockIdx.x;
   group_bucket_packed(Rec16Src{rec}, offs[static_cast<uint64_t>(b) * P],
                       offs[static_cast<uint64_t>(b + 1) * P], bits, chunk_of, gkey, gmin, out, tab,
@@ -1973,9 +1998,11 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12_pk(
     uint32_t bits, ChunkOf chunk_of, uint64_t* __restrict__ gkey, uint32_t* __restrict__ gmin,
     Out out) {
   __shared__ uint64_t tab[kPkSlots];
-  __shared__ uint32_t lmin[kPkCap + 1];
-  __shared__ uint32_t special_min;
-  __shared__ uint32_t scr[Out::kScratch];
+  __shared__ uint32_t lw[kPkWords];  // lmin | special_min | scr (80 KiB in all)
+  static_assert(Out::kScratch <= 2, "scratch fits the word area");
+  uint32_t* lmin = lw;
+  uint32_t& special_min = lw[kPkCap];
+  uint32_t* scr = lw + kPkCap + 1;
   const uint32_t b = out.bucket0 + blockIdx.x;
   group_bucket_packed(Rec12Src{rec, rank_base}, offs[b], offs[b + 1], bits, chunk_of, gkey, gmin,
                       out, tab, lmin, special_min, scr);

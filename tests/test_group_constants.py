@@ -20,18 +20,23 @@ def _const(text, name):
 
 def test_packed_table_steps_are_coprime_with_its_slots():
     text = open(SRC).read()
-    slots, cap = _const(text, "kPkSlots"), _const(text, "kPkCap")
-    m = re.search(r"__builtin_amdgcn_ubfe\((0x[0-9A-Fa-f]+)u,", text)
-    assert m
-    nibbles = int(m.group(1), 16)
-    assert "step[j] = 30u * (q[j].x & 63u) + 2u * nib + 1u;" in text
-    steps = {30 * k + 2 * ((nibbles >> (4 * i)) & 15) + 1 for k in range(64) for i in range(8)}
-    assert len(steps) == 512
-    assert all(math.gcd(s, slots) == 1 and 0 < s < slots for s in steps)
+    slots, words = _const(text, "kPkSlots"), _const(text, "kPkWords")
+    assert "constexpr uint32_t kPkCap = kPkWords - 3;" in text
+    cap = words - 3
+    # a power-of-two table probed with odd steps: every step is coprime
+    assert slots & (slots - 1) == 0
+    assert "sst[j] = ((q[j].x << 3) | 8u) & 0xFFF8u;" in text
+    steps = {((x << 3) | 8) & 0xFFF8 for x in range(1 << 13)}
+    assert all((s // 8) % 2 == 1 and 0 < s < slots * 8 for s in steps)
+    # byte offsets wrap at 16 bits: exactly the table
+    assert "static_cast<uint16_t>(sa[j] + (hit ? 0u : sst[j]))" in text and slots * 8 == 1 << 16
+    assert "sa[j] = live[j] ? (q[j].x >> 16) & 0xFFF8u : threadIdx.x << 3;" in text
     # load: the largest bucket held in LDS against the table
     assert cap / slots <= 0.55
-    # the word's index field (12 bits, index + 1) holds every record of a bucket
+    # the word's index field (12 bits, index + 1, bits 20..31) holds every record
     assert cap + 1 <= 0xFFF + 1
+    # table + word area = half of the CU's 160 KiB (two workgroups per CU)
+    assert slots * 8 + words * 4 == 160 * 1024 // 2
 
 
 def test_small_table_steps_are_coprime_with_its_slots():
