@@ -1872,10 +1872,12 @@ __device__ __forceinline__ void group_packed_regs(const uint4 (&q)[kP], uint32_t
     }
     if (all) break;
   }
-  // each record's slot now holds its key's word: the owner's index + 1
+  // each record's slot now holds its key's word: the owner's index + 1 (a
+  // pad's slot may be empty: index 0 then, so that its unused lmin read
+  // stays inside lmin)
 #pragma unroll
   for (int j = 0; j < kP; ++j)
-    own1[j] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + sa[j] + 4) >> 20;
+    own1[j] = max(1u, *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + sa[j] + 4) >> 20);
 #pragma unroll
   for (int j = 0; j < kP; ++j)
     if (live[j]) atomicMin(&lmin[own1[j] - 1u], q[j].z);

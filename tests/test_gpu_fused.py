@@ -296,14 +296,16 @@ def test_fused_two_level_path_all_keyless_tiles(ctx):
 @pytest.mark.parametrize("n,bits,t,distinct", [
     (12_500_000, 12, 4093, 4093), (12_500_000, 12, 4093, 1500), (12_500_000, 12, 4094, 4094),
     (12_500_000, 12, 4094, 2000), (12_500_000, 12, 4095, 4095), (13_000_000, 13, 4093, 4093),
-    (13_000_000, 13, 4094, 3000)])
+    (13_000_000, 13, 4094, 3000), (12_500_000, 12, 3072, 3072), (12_500_000, 12, 3073, 1000),
+    (13_000_000, 13, 3073, 3073)])
 def test_fused_packed_bucket_at_capacity(ctx, n, bits, t, distinct):
     """One bucket of exactly kPkCap = 4093 records -- the packed table's
     last record index (lmin's last entry, beside special_min and the output
     scratch in the kernel's word area) -- or more (the global table), with
     all-distinct or repeated keys, on the one-level 12-bit path (12.5 M rows)
     and the two-level path (13 M rows: 13 digit bits): keys built from hashes
-    whose digit bits (56 - bits .. 55) name the bucket."""
+    whose digit bits (56 - bits .. 55) name the bucket.  3072 / 3073: the
+    last bucket grouped with three records per thread, the first with four."""
     D = 1234
     rng = np.random.default_rng(t * 7 + distinct + bits)
     sh8, shd = np.uint64(8), np.uint64(64 - bits)
