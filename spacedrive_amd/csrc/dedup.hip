@@ -591,38 +591,56 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_runs(
 // pass (k_part2_runs) reads a segment's records as those runs, so no global
 // offsets -- and no k_part_hist pass over all rows -- are needed.  Fine
 // counts per final bucket as in k_part_scatter_runs.
+// Rows per thread per round of k_part_private: 12-byte records take 8192-row
+// rounds (96 KiB of sort buffer beside 8-bit fine counters): half the runs of
+// 4096-row rounds, each twice as long, for the second pass to read.  16-byte
+// records keep 4096-row rounds and 16-bit counters (64 KiB + 64 KiB).
+template <bool kRec12>
+constexpr int priv_rows() { return kRec12 ? 8 : 4; }
+template <bool kRec12>
+constexpr uint32_t priv_round() { return static_cast<uint32_t>(priv_rows<kRec12>()) * kPartThreads; }
+
 template <typename In, bool kInitRep, bool kRec12 = false, bool kX = false>
 __global__ __launch_bounds__(kPartThreads) void k_part_private(
     In in, uint64_t n, uint32_t skip, uint32_t bits, uint4* __restrict__ rec,
     uint32_t* __restrict__ rep, uint32_t fbits, uint32_t* __restrict__ fine,
     uint32_t* __restrict__ ovf, uint32_t* __restrict__ run_start, uint32_t* __restrict__ run_len,
     uint32_t max_rounds, uint32_t* __restrict__ segtot, XSink xs = XSink{}) {
-  constexpr int U = 4;
-  constexpr uint32_t R = U * kPartThreads;
+  constexpr int U = priv_rows<kRec12>();
+  constexpr uint32_t R = priv_round<kRec12>();
   using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
   __shared__ RecT buf[R];
   RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
   __shared__ uint32_t cnt[kRunMaxBins], base[kRunMaxBins + 1];
-  __shared__ uint32_t fc[1u << (kMaxBucketBits - 1)];  // 2 x 16-bit counters per word
+  // fine counters, kFc bits each, 32 / kFc per word.  One that would wrap
+  // (a key filling 255 / 65535 rows of one tile's final bucket) sets the
+  // overflow flag, and k_fine_recount_runs rebuilds every count from the
+  // records; a carry into the neighbouring counter is rebuilt with them.
+  constexpr uint32_t kFc = kRec12 ? 8u : 16u, kFcPer = 32u / kFc, kFcMax = (1u << kFc) - 1u;
+  constexpr uint32_t kFcShift = kRec12 ? 2u : 1u;
+  static_assert((1u << kFcShift) == kFcPer, "counters per word");
+  __shared__ uint32_t fc[(1u << kMaxBucketBits) / kFcPer];
   const uint32_t nbins = 1u << bits, nfine = 1u << fbits;
   const uint32_t blk = part_block();
   uint32_t wn = 0;  // the wave's keyless rows (XSink)
-  for (uint32_t b = threadIdx.x; b < nfine / 2; b += kPartThreads) fc[b] = 0;
+  for (uint32_t b = threadIdx.x; b < nfine / kFcPer; b += kPartThreads) fc[b] = 0;
   bool over = false;
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
   uint32_t acc = 0, r = 0, dsum = 0;  // records written, rounds done; wave 0: its digit's total
-  // XSink: the keyless rows of 8 rounds as bits of km (bit 4 k + u: round
-  // rbase + k, the thread's row u), sunk together -- the rounds' own loops
-  // carry one OR on their rare keyless branch, nothing else (a ballot test
-  // per round measured +0.02 ms at 100 M rows)
+  // XSink: the keyless rows of kKmRounds rounds as bits of km (bit U k + u:
+  // round rbase + k, the thread's row u), sunk together -- the rounds' own
+  // loops carry one OR on their rare keyless branch, nothing else (a ballot
+  // test per round measured +0.02 ms at 100 M rows)
+  constexpr uint32_t kKmRounds = 32u / U;
+  static_assert((kKmRounds & (kKmRounds - 1)) == 0, "rounds per sink flush: a power of two");
   uint32_t km = 0;
   auto flush = [&](uint32_t rbase) {
     if constexpr (kX) {
       for (uint64_t b = __ballot(km != 0); b; b = __ballot(km != 0)) {
         const uint32_t p = __ffs(__shfl(km, __ffsll(static_cast<unsigned long long>(b)) - 1)) - 1;
-        const uint64_t i = t0 + static_cast<uint64_t>(rbase + p / 4) * R + threadIdx.x +
-                           static_cast<uint64_t>(p % 4) * kPartThreads;
+        const uint64_t i = t0 + static_cast<uint64_t>(rbase + p / U) * R + threadIdx.x +
+                           static_cast<uint64_t>(p % U) * kPartThreads;
         sink_keyless<kRec12>(xs, in, (km >> p) & 1u, i, wn);
         km &= ~(1u << p);
       }
@@ -642,14 +660,14 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
       const uint32_t rk = in.rank_of(q, u);
       if (kInitRep) rep[i] = rk;
       if (!in.valid_of(q, u)) {
-        if constexpr (kX) km |= 1u << (4 * (r & 7u) + u);  // sunk every 8 rounds
+        if constexpr (kX) km |= 1u << (U * (r & (kKmRounds - 1)) + u);  // sunk every kKmRounds
         continue;
       }
       const uint64_t h = in_hash<In>(in.key_of(q, u));
       dg[u] = digit_of(h, skip, bits);
       lr[u] = atomicAdd(&cnt[dg[u]], 1u);
-      const uint32_t fb = digit_of(h, skip, fbits), sh = (fb & 1u) << 4;
-      over |= ((atomicAdd(&fc[fb >> 1], 1u << sh) >> sh) & 0xFFFFu) == 0xFFFFu;
+      const uint32_t fb = digit_of(h, skip, fbits), sh = (fb & (kFcPer - 1u)) * kFc;
+      over |= ((atomicAdd(&fc[fb >> kFcShift], 1u << sh) >> sh) & kFcMax) == kFcMax;
       if constexpr (kRec12)
         rq[u] = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), in.row_of(q, u));
       else
@@ -684,7 +702,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
     acc += total;
     ++r;
     if constexpr (kX)
-      if ((r & 7u) == 0) flush(r - 8);
+      if ((r & (kKmRounds - 1)) == 0) flush(r - kKmRounds);
     lds_barrier();
   };
   constexpr uint64_t kStep = R;
@@ -700,7 +718,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
       if (i0 + 2 * kStep >= t1) break;
     }
   }
-  if constexpr (kX) flush(r & ~7u);
+  if constexpr (kX) flush(r & ~(kKmRounds - 1));
   if (threadIdx.x < 64) {  // rounds this tile did not have: empty runs
     for (uint32_t rr = r; rr < max_rounds; ++rr)
       run_len[(static_cast<uint64_t>(blk) * max_rounds + rr) * kRunMaxBins + threadIdx.x] = 0u;
@@ -711,7 +729,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
   if constexpr (kX) sink_count(xs, wn);
   uint32_t* f = fine + static_cast<uint64_t>(blk) * nfine;
   for (uint32_t b = threadIdx.x; b < nfine; b += kPartThreads)
-    f[b] = (fc[b >> 1] >> ((b & 1u) << 4)) & 0xFFFFu;
+    f[b] = (fc[b >> kFcShift] >> ((b & (kFcPer - 1u)) * kFc)) & kFcMax;
 }
 
 // Only after a 16-bit counter overflow in k_part_scatter_runs (*ovf): for
@@ -1065,7 +1083,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
 // but measured slower at 100 M rows (2.02 ms at 16, 2.06 at 12, 2.10 at 8,
 // profiles/r3/exp_twolevel_s2/run_r3I.log): a block's stores into one bucket
 // fill one contiguous range, so the L2 merges the single stores anyway.
-constexpr uint32_t kMaxRuns = 512;  // R x max_rounds (host: two_level_runs_ok)
+constexpr uint32_t kMaxRuns = 512;  // R x max_rounds (host: two_level_launch)
 template <bool kRec12, uint32_t kB2, uint32_t kS2, int kRows, uint32_t kF = kS2>
 __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
     const uint4* __restrict__ rec1, uint32_t skip, const uint32_t* __restrict__ offs,
@@ -2343,9 +2361,10 @@ GroupLayout group_layout(uint64_t n, uint64_t bits_rows = 0, bool with_sink = fa
   L.ftot = o; o = align_up(o + 4 * nf, 256);
   L.fbase = o; o = align_up(o + 4 * (nf + 1), 256);
   L.ovf = o; o = align_up(o + 4, 256);
-  // rounds of 4096 rows in the largest coarse tile (kPartBlocks tiles)
+  // rounds in the largest coarse tile (kPartBlocks tiles), sized for the
+  // shorter 4096-row rounds (k_part_private: priv_round)
   const uint64_t tile = (n + kPartBlocks - 1) / kPartBlocks;
-  L.max_rounds = L.cbits ? static_cast<uint32_t>((tile + 4095) / 4096) : 0u;
+  L.max_rounds = L.cbits ? static_cast<uint32_t>((tile + priv_round<false>() - 1) / priv_round<false>()) : 0u;
   const uint64_t nrun = static_cast<uint64_t>(kPartBlocks) * L.max_rounds * kRunMaxBins;
   L.run_s = o; o = align_up(o + 4 * nrun, 256);
   L.run_l = o; o = align_up(o + 4 * nrun, 256);
@@ -2432,7 +2451,11 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
   static_assert(kMaxBucketBits - kB2 <= 6, "coarse digits fit k_part_scatter_runs");
   static_assert(kP2 <= kPartBlocks && kPartBlocks % kP2 == 0, "second-pass blocks per segment");
   static_assert((1u << kB2) <= kPartThreads, "second-pass bucket starts: one bucket per thread");
-  if (kPartBlocks / kP2 * L.max_rounds <= kMaxRuns) {
+  // rounds of the coarse pass in the largest tile (the layout sized the run
+  // table for 4096-row rounds, the most this variant can have)
+  const uint64_t tile = (n + P - 1) / P;
+  const uint32_t mr = static_cast<uint32_t>((tile + priv_round<kRec12>() - 1) / priv_round<kRec12>());
+  if (kPartBlocks / kP2 * mr <= kMaxRuns) {
     // no histogram pass: the coarse pass writes each block's records into its
     // own tile range as runs, the second pass reads segments as run lists
     uint32_t* run_s = reinterpret_cast<uint32_t*>(w + L.run_s);
@@ -2448,7 +2471,7 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
         const XSink xs = sink_of(out);
         if (xs.st) {
           k_part_private<In, false, kRec12, true><<<P, kPartThreads, 0, s>>>(
-              in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, L.max_rounds,
+              in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, mr,
               segtot, xs);
           sunk = true;
         }
@@ -2456,16 +2479,16 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
       if (sunk) {
       } else if (init_rep) {
         k_part_private<In, true, kRec12><<<P, kPartThreads, 0, s>>>(
-            in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, L.max_rounds, segtot);
+            in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, mr, segtot);
       } else {
         k_part_private<In, false, kRec12><<<P, kPartThreads, 0, s>>>(
-            in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, L.max_rounds, segtot);
+            in, n, kShardBits, L.cbits, rec1, rep, bits, fine, ovf, run_s, run_l, mr, segtot);
       }
     }
     {
       KScope k(timer, "bucket_fine_scan", s);
       k_fine_recount_runs<kB2, RecT><<<kPartBlocks, kPartThreads, 0, s>>>(
-          reinterpret_cast<const RecT*>(rec1), skip2, run_s, run_l, L.max_rounds, P, nseg, bits, fine,
+          reinterpret_cast<const RecT*>(rec1), skip2, run_s, run_l, mr, P, nseg, bits, fine,
           ovf);
       k_fine_scan<kP2, kPartBlocks / kP2><<<(nfine + 63) / 64, 1024, 0, s>>>(fine, nfine, fE, ftot, ovf);
     }
@@ -2485,7 +2508,7 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
       {
         KScope k(timer, G > 1 ? nullptr : "bucket_scatter", s);
         k_part2_runs<kRec12, kB2, kS2, kR2, kF2><<<dim3(kP2, s1 - s0), kPartThreads, 0, s>>>(
-            rec1, skip2, fE, rec, run_s, run_l, L.max_rounds, P, kPartBlocks / kP2, segtot, ftot,
+            rec1, skip2, fE, rec, run_s, run_l, mr, P, kPartBlocks / kP2, segtot, ftot,
             fbase, s0, nseg);
       }
       KScope k(timer, G > 1 ? nullptr : "bucket_group", s);

@@ -349,3 +349,16 @@ def test_two_level_34m_rows_both_record_sizes(ctx, chunk):
     dr = torch.arange(n, dtype=torch.int32, device="cuda")
     explicit = ops.group_rows(dk, dh, dr, chunk, 0).cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(explicit, ref)
+
+
+def test_two_level_8bit_fine_count_overflow_rep_api(ctx):
+    """The rep API over 12-byte records (implicit ranks, two-level at 13 M
+    rows): 8-bit fine counters of the 8192-row coarse rounds wrap on a key
+    repeated 1000 times in the first tile; reps bit-exact with the oracle."""
+    from spacedrive_amd import dedup
+    n = 13_000_000
+    rng = np.random.default_rng(1000)
+    key = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    key[:1000] = np.uint64(0xC0FFEE)
+    has = (rng.random(n) > 0.001).astype(np.uint8)
+    np.testing.assert_array_equal(dedup.group_reps(key, has, 100, ctx), O.group_reps(key, has, 100))

@@ -325,3 +325,22 @@ def test_fused_packed_bucket_at_capacity(ctx, n, bits, t, distinct):
     pick[:distinct] = ks
     key[rng.choice(n, t, replace=False)] = pick
     _check(ctx, key, np.ones(n, np.uint8), chunk=100)
+
+
+@pytest.mark.parametrize("reps,keyless", [(255, False), (256, False), (300, True), (70_000, False)])
+def test_fused_two_level_8bit_fine_count_overflow(ctx, reps, keyless):
+    """12-byte records (rows in rank order) take 8192-row coarse rounds and
+    8-bit fine counters in k_part_private: one key on the first `reps` rows
+    puts that many rows of one final bucket in the first coarse tile, so from
+    256 on its counter wraps, the flag is set and k_fine_recount_runs
+    rebuilds every count from the records.  255 fills the counter exactly.
+    13 M rows (two-level), with and without keyless rows beside (the sink)."""
+    n = 13_000_000
+    rng = np.random.default_rng(reps)
+    key = rng.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+    key[: n // 8] = key[rng.integers(0, n, n // 8)]  # duplicates elsewhere too
+    key[:reps] = np.uint64(0x5EED)
+    has = (rng.random(n) > 0.01).astype(np.uint8) if keyless else np.ones(n, np.uint8)
+    has[:reps] = 1
+    _check(ctx, key, has)
+    _check(ctx, key, has)  # the flag was reset
