@@ -48,7 +48,7 @@ def main():
     paths, sizes = fi.PathList(m["paths"]), np.array(m["sizes"], np.uint64)
     ctx = default_context()
     cpus = os.sched_getaffinity(0)
-    info = {"io_threads_env": os.environ.get("SDGPU_IO_THREADS"), "cpus": len(cpus),
+    info = {"io": os.environ.get("SDGPU_IO", "pread"), "io_threads_env": os.environ.get("SDGPU_IO_THREADS"), "cpus": len(cpus),
             "nodes": nodes_of(cpus), "bytes": None}
     fi.identify(paths, sizes=sizes, ctx=ctx)  # warm
     ts, fills = [], []

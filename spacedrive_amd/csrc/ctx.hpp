@@ -177,6 +177,7 @@ struct sdgpu_ctx {
   bool xs_cursor_clean = false;
   bool timing = false;
   bool io_uring = false;  // sdgpu_identify_files reads through io_uring (uring.hpp)
+  bool io_bounce = true;   // ... or through a per-thread buffer, streamed into the slab
   EventTimer timer;
   KTimer* kt() { return timing ? &timer : nullptr; }
   // resident latency service (f3, sdgpu_latency_service): mailbox + message

@@ -11,7 +11,9 @@
 #include <stdlib.h>
 #include <stdint.h>
 #include <sys/stat.h>
+#include <string.h>
 #include <unistd.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -112,6 +114,52 @@ inline int64_t read_cas_message(const char* path, uint64_t size, uint8_t* dst, s
   }
   close(fd);
   return rc ? rc : len;
+}
+
+// read_cas_message through a per-thread buffer that stays in the core's
+// cache, then copied into dst with streaming stores (no read-for-ownership of
+// the destination lines: dst is a pinned staging slab, cold, and possibly on
+// the other socket's memory).  Same bytes and results as read_cas_message.
+inline void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+  size_t k = 0;
+  if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+    for (; k + 64 <= n; k += 64) {
+      const __m128i a = _mm_load_si128(reinterpret_cast<const __m128i*>(src + k));
+      const __m128i b = _mm_load_si128(reinterpret_cast<const __m128i*>(src + k + 16));
+      const __m128i c = _mm_load_si128(reinterpret_cast<const __m128i*>(src + k + 32));
+      const __m128i d = _mm_load_si128(reinterpret_cast<const __m128i*>(src + k + 48));
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + k), a);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + k + 16), b);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + k + 32), c);
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + k + 48), d);
+    }
+    _mm_sfence();  // the streamed lines are visible before the slab is handed on
+  }
+  if (k < n) memcpy(dst + k, src + k, n - k);
+}
+
+inline int64_t read_cas_message_bounce(const char* path, uint64_t size, uint8_t* dst, size_t cap) {
+  struct Buf {
+    uint8_t* p = nullptr;
+    size_t n = 0;
+    ~Buf() { free(p); }
+  };
+  thread_local Buf b;
+  if (b.n < cap) {
+    free(b.p);
+    b.n = align_up(cap, 4096);
+    b.p = static_cast<uint8_t*>(aligned_alloc(64, b.n));
+    if (!b.p) {
+      b.n = 0;
+      return read_cas_message(path, size, dst, cap);
+    }
+  }
+  const int64_t r = read_cas_message(path, size, b.p, cap);
+  // a failed read may have written part of the message: dst gets what
+  // read_cas_message would have left there (the caller ignores it anyway)
+  const size_t len = r > 0 ? static_cast<size_t>(r) : 0;
+  stream_copy(dst, b.p, len);
+  return r;
 }
 
 

@@ -38,6 +38,7 @@ using namespace sdgpu;
 using sdgpu::hostio::parallel_for;
 using sdgpu::hostio::pread_exact;
 using sdgpu::hostio::read_cas_message;
+using sdgpu::hostio::read_cas_message_bounce;
 using sdgpu::hostio::read_whole;
 using sdgpu::hostio::read_whole_fd;
 using sdgpu::hostio::slab_layout;
@@ -320,9 +321,14 @@ int sdgpu_open(int device, sdgpu_ctx** out) {
   sdgpu_ctx* c = new (std::nothrow) sdgpu_ctx;
   if (!c) return -ENOMEM;
   c->device = device;
-  {  // staging reads through io_uring (SDGPU_IO=uring) instead of pread
+  {  // staging reads of sdgpu_identify_files: pread into a per-thread buffer
+     // streamed into the slab (default), pread straight into the slab
+     // (SDGPU_IO=pread), or io_uring (SDGPU_IO=uring).  Config 1, one box,
+     // 16 threads (scripts/exp/diag_config1.sh): fill 10.7-10.8 ms against
+     // 12.9-14.8 ms for pread and 17.8 ms for io_uring.
     const char* io = getenv("SDGPU_IO");
     c->io_uring = io && strcmp(io, "uring") == 0;
+    c->io_bounce = !io || (strcmp(io, "uring") != 0 && strcmp(io, "pread") != 0);
   }
   // A BLOCKING stream: callers that pass NULL (e.g. torch's legacy default
   // stream, whose handle is 0) get work ordered with the null stream both ways.
@@ -574,6 +580,7 @@ int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t*
       },
       [&](uint32_t i, uint8_t* dst, size_t cap) -> int64_t {
         if (size[i] == 0) return 0x7fffffff;  // cas_id None (file_identifier/mod.rs:80-88)
+        if (c->io_bounce) return read_cas_message_bounce(paths[i], size[i], dst, cap);
         return read_cas_message(paths[i], size[i], dst, cap);
       },
       [&](uint32_t first, uint32_t cnt, const uint8_t (*o)[8], const int32_t* st) {

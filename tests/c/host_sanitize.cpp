@@ -72,6 +72,15 @@ static void test_cas_reads() {
                                                  buf.size());
     CHECK(got == static_cast<int64_t>(exp.size()), "size %zu: len %lld", n, (long long)got);
     if (got > 0) CHECK(memcmp(buf.data(), exp.data(), exp.size()) == 0, "size %zu bytes", n);
+    // the bounce-buffer reader (per-thread buffer + streaming copy): same
+    // result, into a 16-B aligned and an unaligned destination
+    for (size_t shift : {size_t(0), size_t(3)}) {
+      std::vector<uint8_t> bb(exp.size() + 4096 + 64);
+      uint8_t* d = bb.data() + ((16 - reinterpret_cast<uintptr_t>(bb.data()) % 16) % 16) + shift;
+      const int64_t g2 = hostio::read_cas_message_bounce((dir + "/" + name).c_str(), n, d, exp.size() + 4096);
+      CHECK(g2 == got, "bounce size %zu shift %zu: len %lld", n, shift, (long long)g2);
+      if (g2 > 0) CHECK(memcmp(d, exp.data(), exp.size()) == 0, "bounce size %zu bytes", n);
+    }
     if (n > 102400) {  // capacity below a sampled message
       std::vector<uint8_t> small(1000);
       CHECK(hostio::read_cas_message((dir + "/" + name).c_str(), n, small.data(), small.size()) ==
@@ -83,6 +92,8 @@ static void test_cas_reads() {
   std::vector<uint8_t> b(8 + 5000 + 4096);
   CHECK(hostio::read_cas_message((dir + "/grown").c_str(), 5000, b.data(), b.size()) == -EFBIG,
         "efbig");
+  CHECK(hostio::read_cas_message_bounce((dir + "/grown").c_str(), 5000, b.data(), b.size()) == -EFBIG,
+        "bounce efbig");
   // stale large stat size on a short file: read_exact past EOF
   write_file("short", 50000, 3);
   std::vector<uint8_t> c(60000);
