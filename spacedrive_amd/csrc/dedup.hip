@@ -1065,8 +1065,11 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_rec_staged(
       if (i0 + 2 * kStep >= t1) break;
     }
   }
-  for (uint32_t b = threadIdx.x; b < nbins; b += kPartThreads)
-    for (uint32_t k = 0; k < fill[b]; ++k) out[cur[b] + k] = stage[b][k];
+  // the slots' remainders, kSlots adjacent lanes per bucket (as k_part2_runs)
+  for (uint32_t x = threadIdx.x; x < nbins * kSlots; x += kPartThreads) {
+    const uint32_t b = x / kSlots, k = x % kSlots;
+    if (k < fill[b]) out[cur[b] + k] = stage[b][k];
+  }
 }
 
 // Second pass of the two-level partition over k_part_private's runs: block
@@ -1239,8 +1242,13 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
       if (k0 + 2 * kStep >= T) break;
     }
   }
-  for (uint32_t b = t; b < nbins; b += kPartThreads)
-    for (uint32_t k = 0; k < fill[b]; ++k) out[cur[b] + k] = stage[b][k];
+  // what is left in the slots (< kS2 per bucket, ~40 % of a block's records
+  // at 100 M rows): kS2 adjacent lanes per bucket, so a store instruction
+  // writes a few short runs instead of one record in each of 64 buckets
+  for (uint32_t x = t; x < nbins * kS2; x += kPartThreads) {
+    const uint32_t b = x / kS2, k = x % kS2;
+    if (k < fill[b]) out[cur[b] + k] = stage[b][k];
+  }
 }
 
 // The 12-bit staged scatter of rows in rank order (RowsIn without a rank
