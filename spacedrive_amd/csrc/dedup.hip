@@ -611,7 +611,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
   using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
   __shared__ RecT buf[R];
   RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
-  __shared__ uint32_t cnt[kRunMaxBins], base[kRunMaxBins + 1];
+  __shared__ uint32_t cnt[2][kRunMaxBins];  // digit counts, by round parity
   // fine counters, kFc bits each, 32 / kFc per word.  One that would wrap
   // (a key filling 255 / 65535 rows of one tile's final bucket) sets the
   // overflow flag, and k_fine_recount_runs rebuilds every count from the
@@ -647,9 +647,14 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
     }
     (void)rbase;
   };
+  // Digit counters by round parity: every wave reads round r's after the
+  // first barrier, so wave 0 zeroes the OTHER array (read in round r - 1)
+  // for round r + 1 -- no barrier of its own.  Three barriers per round:
+  // counted, sorted into the buffer, stored.
+  if (threadIdx.x < 2 * kRunMaxBins) (&cnt[0][0])[threadIdx.x] = 0;
+  __syncthreads();
   auto round = [&](const RowBatch<U>& q, uint64_t i0) {
-    if (threadIdx.x < nbins) cnt[threadIdx.x] = 0;
-    lds_barrier();
+    const uint32_t p = r & 1u;
     uint32_t dg[U], lr[U];
     RecT rq[U];
 #pragma unroll
@@ -665,7 +670,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
       }
       const uint64_t h = in_hash<In>(in.key_of(q, u));
       dg[u] = digit_of(h, skip, bits);
-      lr[u] = atomicAdd(&cnt[dg[u]], 1u);
+      lr[u] = atomicAdd(&cnt[p][dg[u]], 1u);
       const uint32_t fb = digit_of(h, skip, fbits), sh = (fb & (kFcPer - 1u)) * kFc;
       over |= ((atomicAdd(&fc[fb >> kFcShift], 1u << sh) >> sh) & kFcMax) == kFcMax;
       if constexpr (kRec12)
@@ -675,29 +680,33 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
                            in.row_of(q, u));
     }
     lds_barrier();
-    if (threadIdx.x < 64) {  // run starts (one wave's shuffle scan) and the run table row
-      static_assert(kRunMaxBins <= 64, "one wave scans the run starts");
-      const uint32_t lane = threadIdx.x;
-      const uint32_t v = lane < nbins ? cnt[lane] : 0u;
-      uint32_t inc = v;
+    // every wave scans the (<= 64) digit counts itself, lane d holding digit
+    // d's run start, so the buffer scatter reads its bases by a lane shuffle
+    // instead of from LDS written behind a second barrier
+    static_assert(kRunMaxBins <= 64, "one wave scans the run starts");
+    const uint32_t lane = __lane_id();
+    const uint32_t v = lane < nbins ? cnt[p][lane] : 0u;
+    uint32_t inc = v;
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(inc, d);
-        if (lane >= static_cast<uint32_t>(d)) inc += o;
-      }
-      if (lane < nbins) base[lane] = inc - v;
-      if (lane == nbins - 1) base[nbins] = inc;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
+    }
+    const uint32_t excl = inc - v;
+    const uint32_t total = __shfl(inc, 63);
+    if (threadIdx.x < 64) {  // the run table row; the other parity's counters zeroed
+      if (lane < nbins) cnt[p ^ 1u][lane] = 0;
       const uint64_t e = (static_cast<uint64_t>(blk) * max_rounds + r) * kRunMaxBins + lane;
-      run_start[e] = static_cast<uint32_t>(t0) + acc + inc - v;
+      run_start[e] = static_cast<uint32_t>(t0) + acc + excl;
       run_len[e] = v;
       dsum += v;
     }
-    lds_barrier();
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (dg[u] != ~0u) buf[base[dg[u]] + lr[u]] = rq[u];
+    for (int u = 0; u < U; ++u) {
+      const uint32_t bb = __shfl(excl, static_cast<int>(dg[u] & 63u));
+      if (dg[u] != ~0u) buf[bb + lr[u]] = rq[u];
+    }
     lds_barrier();
-    const uint32_t total = base[nbins];
     for (uint32_t k = threadIdx.x; k < total; k += kPartThreads) out[t0 + acc + k] = buf[k];
     acc += total;
     ++r;
