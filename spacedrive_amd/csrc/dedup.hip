@@ -1268,8 +1268,11 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
 // round's prefetch and its use, and the waits there drain them too).  Waves
 // 8-15 only store: the full slot pairs, the rows that met a full slot (an LDS
 // overflow list, kept in arrival order per bucket by an LDS cursor) and, with
-// kInitRep, rep = rank of the round's rows (computed, nothing loaded).  Three
-// barriers per round: staged (A), fills read (M), flushed (B).
+// kInitRep, rep = rank of the round's rows (computed, nothing loaded).  Two
+// barriers per round: staged (A), flushed (B) -- the bucket cursors advance
+// atomically and the overflow count alternates by round parity, so the
+// barrier between the pair flush and the overflow rows (round 3-4's M) is
+// gone.
 // scripts/exp_scatter_align.hip: 12.5 M rows 0.136 -> 0.123 ms
 // (profiles/r3/exp_scatter_align/run.log).
 constexpr uint32_t kWsProd = 512;   // producer threads (waves 0-7)
@@ -1287,7 +1290,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_ws(
   __shared__ uint3 stage[nbins][2];
   __shared__ uint32_t fill[nbins], cur[nbins];
   __shared__ uint3 ovf[kRound];
-  __shared__ uint32_t ovf_n;
+  __shared__ uint32_t ovf_n[2];  // by round parity (no barrier to reset it)
   // bucket starts: the segment's sizes scanned here, block 0 publishes them
   constexpr uint32_t kPerT = nbins / kPartThreads;
   const uint32_t t = threadIdx.x, lane = __lane_id();
@@ -1325,7 +1328,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_ws(
     base += v[k];
   }
   if (j == 0 && t == 0) fbase[nbins] = total;
-  if (t == 0) ovf_n = 0;
+  if (t < 2) ovf_n[t] = 0;
   __syncthreads();
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
@@ -1334,7 +1337,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_ws(
     RowBatch<kWsRows> qa, qb;
     in.template load_many<kWsRows>(t0 + t, kWsProd, t1, t0, qa);
     in.template load_many<kWsRows>(t0 + kRound + t, kWsProd, t1, t0, qb);
-    auto stage_round = [&](const RowBatch<kWsRows>& q) {
+    auto stage_round = [&](const RowBatch<kWsRows>& q, uint32_t par) {
 #pragma unroll
       for (int u = 0; u < kWsRows; ++u) {
         if (!in.valid_of(q, u)) continue;
@@ -1346,24 +1349,22 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_ws(
         if (sl < 2)
           stage[b][sl] = rq;
         else
-          ovf[atomicAdd(&ovf_n, 1u)] = rq;
+          ovf[atomicAdd(&ovf_n[par], 1u)] = rq;
       }
     };
-    // per round exactly the consumers' three barriers (A, M, B); the loads
-    // of round r + 2 go out between A and B, while the consumers store
+    // per round exactly the consumers' two barriers (A, B); the loads of
+    // round r + 2 go out between A and B, while the consumers store
     for (uint32_t r = 0; r < rounds; r += 2) {
-      stage_round(qa);
+      stage_round(qa, 0u);
       lds_barrier();  // A
       in.template load_many<kWsRows>(t0 + (r + 2) * static_cast<uint64_t>(kRound) + t, kWsProd, t1,
                                      t0, qa);
-      lds_barrier();  // M
       lds_barrier();  // B
       if (r + 1 >= rounds) break;
-      stage_round(qb);
+      stage_round(qb, 1u);
       lds_barrier();  // A
       in.template load_many<kWsRows>(t0 + (r + 3) * static_cast<uint64_t>(kRound) + t, kWsProd, t1,
                                      t0, qb);
-      lds_barrier();  // M
       lds_barrier();  // B
     }
   } else {
@@ -1384,21 +1385,22 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter_ws(
       for (uint32_t k = 0; k < nbins / kWsProd; ++k) {
         const uint32_t b = c + k * kWsProd;
         if (fill[b] >= 2) {
-          const uint32_t p = cur[b];
+          // an atomic cursor: the overflow rows below advance it too, with
+          // no barrier between (a pair and an overflow row of one bucket may
+          // take either order; every position is taken once)
+          const uint32_t p = atomicAdd(&cur[b], 2u);
           out[p] = stage[b][0];
           out[p + 1] = stage[b][1];
-          cur[b] = p + 2;
           fill[b] = 0;
         }
       }
-      const uint32_t no = ovf_n;
-      lds_barrier();  // M: fills and ovf_n read by every consumer
+      const uint32_t par = r & 1u, no = ovf_n[par];
+      if (c == 0) ovf_n[par ^ 1u] = 0;  // last round's, read by every consumer before its B
       for (uint32_t o = c; o < no; o += kWsProd) {
         const uint3 rq = ovf[o];
         out[atomicAdd(&cur[digit_of((static_cast<uint64_t>(rq.y) << 32) | rq.x, skip, kStageBits)],
                       1u)] = rq;
       }
-      if (c == 0) ovf_n = 0;
       lds_barrier();  // B
     }
   }
