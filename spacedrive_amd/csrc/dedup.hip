@@ -1114,7 +1114,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
   __shared__ uint16_t full[nbins];
   __shared__ uint32_t full_n[2];
   __shared__ uint32_t rpre[kMaxRuns + 1], rst[kMaxRuns];
-  __shared__ uint32_t wsum[kPartThreads / 64];
+  __shared__ uint32_t wsum[kPartThreads / 64], wsumb[kPartThreads / 64];
   __shared__ uint32_t s_segbase, s_segend, s_all;
   const RecT* __restrict__ in = reinterpret_cast<const RecT*>(rec1);
   RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
@@ -1148,36 +1148,34 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
     }
     if (t == 63) s_all = inc;
   }
-  {  // the block's runs and their exclusive prefix (block scan)
+  {  // the block's runs (prefix of their lengths) and its bucket starts
+     // (segment start + the segment's bucket sizes scanned): both block
+     // scans share their barriers (two, not four: a block lives ~2 rounds)
+    static_assert(nbins <= kPartThreads, "one bucket per thread");
     const bool has = t < nr && cb < P1;
     const uint32_t len = has ? len_v : 0u, st = has ? st_v : 0u;
-    uint32_t inc = len;
+    const uint32_t v = t < nbins ? ft_v : 0u;
+    uint32_t inc = len, incb = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = __shfl_up(inc, d);
-      if (lane >= static_cast<uint32_t>(d)) inc += o;
+      const uint32_t o = __shfl_up(inc, d), ob = __shfl_up(incb, d);
+      if (lane >= static_cast<uint32_t>(d)) {
+        inc += o;
+        incb += ob;
+      }
     }
-    if (lane == 63) wsum[t >> 6] = inc;
-    __syncthreads();
-    uint32_t before = 0;
-    for (uint32_t w = 0; w < (t >> 6); ++w) before += wsum[w];
+    if (lane == 63) {
+      wsum[t >> 6] = inc;
+      wsumb[t >> 6] = incb;
+    }
+    __syncthreads();  // wsum, wsumb; s_segbase / s_segend / s_all (wave 0 above)
+    uint32_t before = 0, base = s_segbase + incb - v;
+    for (uint32_t w = 0; w < (t >> 6); ++w) {
+      before += wsum[w];
+      base += wsumb[w];
+    }
     if (t <= kMaxRuns) rpre[t] = before + inc - len;  // rpre[kMaxRuns] = the block's total
     if (t < kMaxRuns) rst[t] = st;
-  }
-  __syncthreads();  // s_segbase, wsum reused below
-  {  // bucket starts: segment start + the segment's bucket sizes scanned
-    static_assert(nbins <= kPartThreads, "one bucket per thread");
-    const uint32_t v = t < nbins ? ft_v : 0u;
-    uint32_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = __shfl_up(inc, d);
-      if (lane >= static_cast<uint32_t>(d)) inc += o;
-    }
-    if (lane == 63) wsum[t >> 6] = inc;
-    __syncthreads();
-    uint32_t base = s_segbase + inc - v;
-    for (uint32_t w = 0; w < (t >> 6); ++w) base += wsum[w];
     if (t < nbins) {
       cur[t] = base + off_v;
       fill[t] = 0;
