@@ -1,7 +1,8 @@
-# Round 5: the leaner packed group kernel (linear probing, 32-bit word, one
-# LDS atomic per wave in the list output).  GPU tests, then an A/B against
-# the previous build (build/ab/libsdgpu_prev.so, AB_LIB) at 100 M and 12.5 M
-# rows, alternating processes, then SQ counters of the new kernel.
+# Round 5: the grouping A/B used for every group-kernel and partition change
+# of the round (first written for the leaner packed group kernel).  Optional
+# GPU tests, then an A/B against a build of the previous tree
+# (build/ab/libsdgpu_prev.so, AB_LIB) at 100 M and 12.5 M rows, alternating
+# processes, then SQ counters of the group kernel.
 #   TAG=r5q [TESTS=...] bash scripts/gpu_r5_pk.sh
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
