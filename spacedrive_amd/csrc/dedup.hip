@@ -612,10 +612,12 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
   __shared__ RecT buf[R];
   RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
   __shared__ uint32_t cnt[2][kRunMaxBins];  // digit counts, by round parity
-  // fine counters, kFc bits each, 32 / kFc per word.  One that would wrap
-  // (a key filling 255 / 65535 rows of one tile's final bucket) sets the
+  // fine counters, kFc bits each, 32 / kFc per word, added to without a
+  // return value.  A counter that wraps (a key filling 256 / 65536 rows of
+  // one tile's final bucket) loses 2^kFc and gives its neighbour at most 1,
+  // so the block's counters then sum to less than its rows: that sets the
   // overflow flag, and k_fine_recount_runs rebuilds every count from the
-  // records; a carry into the neighbouring counter is rebuilt with them.
+  // records.
   constexpr uint32_t kFc = kRec12 ? 8u : 16u, kFcPer = 32u / kFc, kFcMax = (1u << kFc) - 1u;
   constexpr uint32_t kFcShift = kRec12 ? 2u : 1u;
   static_assert((1u << kFcShift) == kFcPer, "counters per word");
@@ -624,7 +626,6 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
   const uint32_t blk = part_block();
   uint32_t wn = 0;  // the wave's keyless rows (XSink)
   for (uint32_t b = threadIdx.x; b < nfine / kFcPer; b += kPartThreads) fc[b] = 0;
-  bool over = false;
   uint64_t t0, t1;
   tile_of(n, gridDim.x, t0, t1);
   uint32_t acc = 0, r = 0, dsum = 0;  // records written, rounds done; wave 0: its digit's total
@@ -672,7 +673,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
       dg[u] = digit_of(h, skip, bits);
       lr[u] = atomicAdd(&cnt[p][dg[u]], 1u);
       const uint32_t fb = digit_of(h, skip, fbits), sh = (fb & (kFcPer - 1u)) * kFc;
-      over |= ((atomicAdd(&fc[fb >> kFcShift], 1u << sh) >> sh) & kFcMax) == kFcMax;
+      atomicAdd(&fc[fb >> kFcShift], 1u << sh);
       if constexpr (kRec12)
         rq[u] = make_uint3(static_cast<uint32_t>(h), static_cast<uint32_t>(h >> 32), in.row_of(q, u));
       else
@@ -733,12 +734,25 @@ __global__ __launch_bounds__(kPartThreads) void k_part_private(
       run_len[(static_cast<uint64_t>(blk) * max_rounds + rr) * kRunMaxBins + threadIdx.x] = 0u;
     if (threadIdx.x < nbins && dsum) atomicAdd(&segtot[threadIdx.x], dsum);
   }
-  if (over) *ovf = 1u;
   __syncthreads();
   if constexpr (kX) sink_count(xs, wn);
   uint32_t* f = fine + static_cast<uint64_t>(blk) * nfine;
-  for (uint32_t b = threadIdx.x; b < nfine; b += kPartThreads)
-    f[b] = (fc[b >> kFcShift] >> ((b & (kFcPer - 1u)) * kFc)) & kFcMax;
+  uint32_t fsum = 0;
+  for (uint32_t b = threadIdx.x; b < nfine; b += kPartThreads) {
+    const uint32_t v = (fc[b >> kFcShift] >> ((b & (kFcPer - 1u)) * kFc)) & kFcMax;
+    f[b] = v;
+    fsum += v;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) fsum += __shfl_xor(fsum, d);
+  __shared__ uint32_t wsum[kPartThreads / 64];
+  if (__lane_id() == 0) wsum[threadIdx.x >> 6] = fsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tsum = 0;
+    for (uint32_t w = 0; w < kPartThreads / 64; ++w) tsum += wsum[w];
+    if (tsum != acc) *ovf = 1u;  // a counter wrapped (see fc)
+  }
 }
 
 // Only after a 16-bit counter overflow in k_part_scatter_runs (*ovf): for
