@@ -90,14 +90,20 @@ pub struct Identified {
     pub status: Vec<i32>,
 }
 
-pub fn identify(gpu: &Gpu, paths: &[PathBuf], sizes: &[u64]) -> io::Result<Identified> {
+/// `sizes` None: the library stats every path itself (ABI 6), as the
+/// reference's FileMetadata::new does (mod.rs:65,80-81).
+pub fn identify(gpu: &Gpu, paths: &[PathBuf], sizes: Option<&[u64]>) -> io::Result<Identified> {
     let n = paths.len();
+    if sizes.map_or(false, |s| s.len() != n) {
+        return Err(io::Error::new(io::ErrorKind::InvalidInput, "one size per path"));
+    }
     let c: Vec<_> = paths.iter().map(|p| cpath(p)).collect();
     let ptrs: Vec<*const c_char> = c.iter().map(|s| s.as_ptr()).collect();
     let mut out = Identified { cas8: vec![[0u8; 8]; n], has_key: vec![0u8; n], status: vec![0i32; n] };
     let ctx = gpu.ctx();
     check(unsafe {
-        sys::sdgpu_identify_files(*ctx, ptrs.as_ptr(), sizes.as_ptr(), n as u32, out.cas8.as_mut_ptr(),
+        sys::sdgpu_identify_files(*ctx, ptrs.as_ptr(), sizes.map_or(std::ptr::null(), |s| s.as_ptr()),
+                                  n as u32, out.cas8.as_mut_ptr(),
                                   out.has_key.as_mut_ptr(), out.status.as_mut_ptr())
     })?;
     Ok(out)
@@ -139,7 +145,7 @@ pub fn group(gpu: &Gpu, idx: &ObjectIndex, rows: &Identified, first_rank: u32) -
 
 /// One job step over `paths` (rows in id order; `sizes` from fs::metadata,
 /// mod.rs:65) whose first row has rank `first_rank`.
-pub fn identify_step(gpu: &Gpu, idx: &ObjectIndex, paths: &[PathBuf], sizes: &[u64],
+pub fn identify_step(gpu: &Gpu, idx: &ObjectIndex, paths: &[PathBuf], sizes: Option<&[u64]>,
                      first_rank: u32) -> io::Result<Vec<IdentifiedRow>> {
     let rows = identify(gpu, paths, sizes)?;
     group(gpu, idx, &rows, first_rank)

@@ -28,11 +28,12 @@ use crate::{
 /// file_identifier/mod.rs:36
 pub const CHUNK_SIZE: usize = sdgpu_sys::SDGPU_IDENTIFIER_CHUNK_SIZE as usize;
 
-/// One orphan row as the job's query returns it (file_path_for_file_identifier).
+/// One orphan row as the job's query returns it (file_path_for_file_identifier,
+/// file_path_helper/mod.rs:32-40: no size -- the size is the file's at
+/// identification time, stat-ed by the library, mod.rs:65,80-81).
 pub struct Orphan {
     pub id: i32,
     pub path: PathBuf,
-    pub size: u64,
 }
 
 /// One page of the library's file_paths already linked to an Object.
@@ -60,8 +61,9 @@ pub trait OrphanTable {
     /// return), so the Object index is filled in pages rather than from one
     /// materialised table.
     fn existing_objects_page(&self, after: Option<i32>, limit: usize) -> io::Result<ExistingPage>;
-    /// `file_path.cas_id` of a row (mod.rs:144-165).
-    fn set_cas_id(&mut self, id: i32, cas_id: Option<&str>) -> io::Result<()>;
+    /// `file_path.cas_id` of the step's rows, all in ONE write
+    /// (mod.rs:144-165: one `write_ops` batch of updates per step).
+    fn set_cas_ids(&mut self, rows: &[(i32, Option<String>)]) -> io::Result<()>;
     /// `object::create_many` of `n` Objects (mod.rs:243-297); returns their ids.
     fn create_objects(&mut self, n: usize) -> io::Result<Vec<u32>>;
     /// `file_path.object_id` connects (mod.rs:189-225, 297-333).
@@ -171,10 +173,11 @@ impl<'a, T: OrphanTable> FileIdentifierJob<'a, T> {
         if cand.is_empty() {
             return Ok(Err(EarlyFinish("Expected orphan Paths not returned from database query for this chunk")));
         }
-        // identify every candidate once (their reads and hashes are independent)
+        // identify every candidate once (their reads and hashes are
+        // independent); sizes None: the library stats every path in its read
+        // pool, the reference's fresh fs::metadata (mod.rs:65,80-81)
         let paths: Vec<PathBuf> = cand.iter().map(|o| o.path.clone()).collect();
-        let sizes: Vec<u64> = cand.iter().map(|o| o.size).collect();
-        let ident = identify(self.gpu, &paths, &sizes)?;
+        let ident = identify(self.gpu, &paths, None)?;
         let ok: Vec<bool> = ident.status.iter().map(|&s| s == 0).collect();
         // replay the reference's fetches
         let mut fetched: Vec<Vec<usize>> = Vec::new();
@@ -211,6 +214,7 @@ impl<'a, T: OrphanTable> FileIdentifierJob<'a, T> {
         let mut creators: Vec<(u32, i32)> = Vec::new(); // (rank, file_path id)
         let mut links: Vec<(i32, u32)> = Vec::new();    // (file_path id, object id)
         let mut to_rows: Vec<(i32, u32)> = Vec::new();  // (file_path id, creator rank)
+        let mut cas_ids: Vec<(i32, Option<String>)> = Vec::with_capacity(out.len());
         let mut ignored = 0;
         for (j, row) in out.iter().enumerate() {
             let id = cand[rows[j]].id;
@@ -223,8 +227,9 @@ impl<'a, T: OrphanTable> FileIdentifierJob<'a, T> {
                 Link::Existing(obj) => links.push((id, obj)),
                 Link::Row(r) => to_rows.push((id, r)),
             }
-            self.table.set_cas_id(id, row.cas_id.as_deref())?;
+            cas_ids.push((id, row.cas_id.clone()));
         }
+        self.table.set_cas_ids(&cas_ids)?;
         let linked = links.len() + to_rows.len();
         let ids = self.table.create_objects(creators.len())?;
         for (&(rank, id), &obj) in creators.iter().zip(&ids) {

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SDGPU_ABI_VERSION 5
+#define SDGPU_ABI_VERSION 6
 
 /* cas.rs:10-15 */
 #define SDGPU_CAS_SAMPLE_COUNT 4u
@@ -118,7 +118,10 @@ int sdgpu_generate_cas_id(sdgpu_ctx *ctx, const char *path, uint64_t size, char 
  * pread into pinned buffers, pipelines H2D copies with K1 in slabs.  size[i] is
  * the fs::metadata length (mod.rs:65,80-81); size 0 yields status 0 and
  * has_key[i] = 0 (cas_id None, mod.rs:80-88); I/O errors yield status -errno
- * and has_key 0 (row dropped, mod.rs:113,127).  has_key may be NULL. */
+ * and has_key 0 (row dropped, mod.rs:113,127).  has_key may be NULL.
+ * size may be NULL (ABI 6): every path is stat-ed by the read pool first --
+ * the reference's fresh fs::metadata(path).len() at identification time, not
+ * a size stored with the row; a failed stat is status -errno. */
 int sdgpu_identify_files(sdgpu_ctx *ctx, const char *const *paths, const uint64_t *size,
                          uint32_t n, uint8_t (*out8)[8], uint8_t *has_key, int32_t *status);
 
@@ -266,11 +269,14 @@ int sdgpu_dedup_batch(sdgpu_ctx *ctx, sdgpu_index *idx, const uint64_t *key,
  * call enqueues everything without waiting for the host.
  * Transports: SDGPU_TRANSPORT_RCCL (grouped ncclSend/ncclRecv; one rank per
  * GPU), SDGPU_TRANSPORT_PEER (device-to-device copies between contexts of one
- * process; also contexts sharing a GPU), AUTO = RCCL unless devices repeat. */
+ * process; also contexts sharing a GPU), AUTO = RCCL unless devices repeat,
+ * SDGPU_TRANSPORT_HOST (ABI 6, sdgpu_comm_init_host: one process per rank on
+ * one host, ranks may share a GPU). */
 #define SDGPU_COMM_ID_BYTES 128
 #define SDGPU_TRANSPORT_AUTO 0
 #define SDGPU_TRANSPORT_RCCL 1
 #define SDGPU_TRANSPORT_PEER 2
+#define SDGPU_TRANSPORT_HOST 3
 typedef struct sdgpu_comm sdgpu_comm;
 /* Failure model (ABI 3).  RCCL communicators are created non-blocking; every
  * wait on a peer (joining, the count exchange's one synchronisation,
@@ -290,6 +296,25 @@ int sdgpu_comm_init_rank_timeout(sdgpu_ctx *ctx, int nranks, int rank,
 /* The same with the timeout from env SDGPU_COMM_TIMEOUT_MS (default 300 s). */
 int sdgpu_comm_init_rank(sdgpu_ctx *ctx, int nranks, int rank,
                          const uint8_t id[SDGPU_COMM_ID_BYTES], sdgpu_comm **out);
+/* One process per rank on one host, through a shared file mapping (ABI 6):
+ * the same messages, in the same order, as the RCCL transport, staged
+ * through host memory -- each rank's outbox of msg_bytes holds its messages
+ * of one all-to-all round; a round waits for the rank's stream, posts the
+ * outbox, waits (bounded by timeout_ms) for every peer's, copies its
+ * inbound messages and waits until every peer has copied its own.  The
+ * exchange calls (sdgpu_group_sharded_device, sdgpu_group_link_sharded_
+ * device) run exactly the per-process state machine they run under RCCL
+ * (a padded call left pending and resolved at the next call / wait / destroy,
+ * the overflow re-run, the deferred -ENOSPC, the bounded failure), so ranks
+ * that share a GPU -- which RCCL refuses -- can exercise it.  Host-
+ * synchronous: a test and fallback transport, not a fast one.  path names a
+ * file every rank opens (created by the first; it must not hold an earlier
+ * communicator's state: -EEXIST); rank 0 unlinks it on destroy.  A round
+ * whose messages exceed msg_bytes fails with -EMSGSIZE.  -ETIMEDOUT when not
+ * every rank joins within timeout_ms (> 0), -EPROTO when the ranks disagree
+ * on nranks or msg_bytes. */
+int sdgpu_comm_init_host(sdgpu_ctx *ctx, int nranks, int rank, const char *path,
+                         uint64_t msg_bytes, int timeout_ms, sdgpu_comm **out);
 /* One process driving ngpu contexts: out[r] is rank r's communicator. */
 int sdgpu_comm_init_all(sdgpu_ctx *const *ctx, int ngpu, int transport, sdgpu_comm **out);
 int sdgpu_comm_destroy(sdgpu_comm *comm);
@@ -324,7 +349,17 @@ int sdgpu_comm_wait(sdgpu_comm *comm, void *stream);
  *     COUNTED.
  * Every rank of a communicator must set the same mode (and rows_hint, which
  * sets B when > 0).  The _all entry points (one process, all ranks) resolve
- * a padded call before they return. */
+ * a padded call before they return.
+ * Agreement (ABI 6): a communicator's first call and its first call after
+ * sdgpu_comm_set_exchange / sdgpu_comm_set_return check that every rank
+ * chose the same layout -- a counted call through the code in its count
+ * messages (form, return mode, exchange mode), a padded call through one
+ * 24-byte agreement message per peer {slots per message, B, code} of the
+ * same shape, before any record moves -- and fail with -EPROTO (communicator
+ * aborted) when they differ, instead of posting messages of different sizes.
+ * -ENOSPC of a padded write set that is resolved by a later call is returned
+ * by the next sdgpu_comm_wait (the earliest unreported one; stats.nospc_call
+ * names the call); a hard error found by the same wait takes precedence. */
 #define SDGPU_EXCHANGE_AUTO 0
 #define SDGPU_EXCHANGE_COUNTED 1
 #define SDGPU_EXCHANGE_PADDED 2
@@ -345,6 +380,9 @@ typedef struct sdgpu_comm_stats_t {
   uint64_t padded_calls;                  /* (ABI 5) calls through the padded exchange */
   uint64_t overflow_reruns;               /* (ABI 5) padded calls re-run counted */
   double resolve_wait_ms;                 /* (ABI 5) host ms waiting to resolve them */
+  uint64_t agreements;                    /* (ABI 6) layout agreement rounds (below) */
+  uint64_t nospc_call;                    /* (ABI 6) `calls` number of the last call that
+                                             failed with -ENOSPC (0: none) */
 } sdgpu_comm_stats_t;
 /* Return leg of the exchange (ABI 4).  COMPACT: an owner sends back only the
  * received rows whose rep is not their own rank, as 8-B {index, rep} pairs

@@ -1,10 +1,10 @@
-"""A/B of the two-level grouping with the second pass and the group kernel
-interleaved per group of coarse segments (SDGPU_SEG_GROUPS, read once per
-process): the fused call (sdgpu_group_link_device) over config-4 rows, timed
-back to back, plus a digest of its write set (sorted who / obj) so runs with
-different G can be compared for equality.
+"""A/B of the fused grouping + write set (sdgpu_group_link_device) over
+config-4 rows: timed back to back, plus a digest of its write set (sorted
+who / obj) so two builds (AB_LIB) or two settings of an env knob can be
+compared for equality.  (Written in round 5 for the SDGPU_SEG_GROUPS
+interleave, deleted in round 6; the file name stayed for the logs.)
 
-    SDGPU_SEG_GROUPS=4 python scripts/exp/exp_seg_groups.py [rows] [steps]
+    python scripts/exp/exp_seg_groups.py [rows] [steps]
 """
 import hashlib
 import json
@@ -48,7 +48,7 @@ def main():
     w = who[:e].to(torch.int64) & 0xFFFFFFFF
     o = torch.where(w >= 2**31, obj[:e].to(torch.int64) & 0xFFFFFFFF, torch.zeros_like(w))
     packed = torch.sort((w << 32) | o).values.cpu().numpy()
-    print(json.dumps({"G": os.environ.get("SDGPU_SEG_GROUPS", "1"), "lib": os.environ.get("AB_LIB", "tree"), "rows": rows,
+    print(json.dumps({"lib": os.environ.get("AB_LIB", "tree"), "rows": rows,
                       "ms_per_call": sorted(ts)[1], "rounds_ms": ts, "counts": [c, l, e],
                       "digest": hashlib.sha1(packed.tobytes()).hexdigest(),
                       "kernels": {k: v[0] / max(v[1], 1) for k, v in kt.items()}}))

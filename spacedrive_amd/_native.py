@@ -88,6 +88,7 @@ def _proto(L):
         "sdgpu_comm_info": (i32, [c_vp, P(i32), P(i32), P(i32)]),
         "sdgpu_comm_init_rank_timeout": (i32, [ctx, i32, i32, c_vp, i32, P(c_vp)]),
         "sdgpu_comm_set_timeout": (i32, [c_vp, i32]),
+        "sdgpu_comm_init_host": (i32, [ctx, i32, i32, ctypes.c_char_p, u64, i32, P(c_vp)]),
         "sdgpu_comm_wait": (i32, [c_vp, c_vp]),
         "sdgpu_comm_stats": (i32, [c_vp, c_vp]),
         "sdgpu_group_sharded_device": (i32, [ctx, c_vp, c_vp, c_vp, c_vp, c_vp, u64, u32, c_vp,

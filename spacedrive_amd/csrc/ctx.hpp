@@ -173,6 +173,8 @@ struct sdgpu_ctx {
   // (each call's k_pad_fill zeroes the other set for the next call), and the
   // keyless-row segments of the write set's partition
   DevBuf xs_cursor, xs_sink;
+  // layout agreement messages (shard.cpp agree_layout): [2][W][3] int64
+  DevBuf xs_agree;
   uint32_t xs_parity = 0;
   bool xs_cursor_clean = false;
   bool timing = false;

@@ -1116,7 +1116,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
     uint4* __restrict__ rec, const uint32_t* __restrict__ run_start,
     const uint32_t* __restrict__ run_len, uint32_t max_rounds, uint32_t P1, uint32_t R,
     const uint32_t* __restrict__ segtot, const uint32_t* __restrict__ ftot,
-    uint32_t* __restrict__ fbase, uint32_t seg0 = 0, uint32_t nseg_all = 0) {
+    uint32_t* __restrict__ fbase) {
   constexpr uint32_t nbins = 1u << kB2;
   using RecT = typename std::conditional<kRec12, uint3, uint4>::type;
   static_assert(nbins < kPartThreads && 64 % kS2 == 0 && kPartThreads % kS2 == 0,
@@ -1129,12 +1129,11 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
   __shared__ uint32_t full_n[2];
   __shared__ uint32_t rpre[kMaxRuns + 1], rst[kMaxRuns];
   __shared__ uint32_t wsum[kPartThreads / 64], wsumb[kPartThreads / 64];
-  __shared__ uint32_t s_segbase, s_segend, s_all;
+  __shared__ uint32_t s_segbase, s_all;
   const RecT* __restrict__ in = reinterpret_cast<const RecT*>(rec1);
   RecT* __restrict__ out = reinterpret_cast<RecT*>(rec);
-  // segments [seg0, seg0 + gridDim.y) of nseg_all (0: the grid's)
-  const uint32_t c = seg0 + blockIdx.y, j = part_block(), t = threadIdx.x, lane = __lane_id();
-  const uint32_t nseg = nseg_all ? nseg_all : gridDim.y;
+  const uint32_t c = blockIdx.y, j = part_block(), t = threadIdx.x, lane = __lane_id();
+  const uint32_t nseg = gridDim.y;
   const uint64_t nfine = static_cast<uint64_t>(nseg) << kB2, b0 = static_cast<uint64_t>(c) << kB2;
   const uint32_t nr = R * max_rounds;
   // Every prologue load is issued here, up front and unconditionally (clamped
@@ -1156,10 +1155,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
       const uint32_t o = __shfl_up(inc, d);
       if (lane >= static_cast<uint32_t>(d)) inc += o;
     }
-    if (t == c) {
-      s_segbase = inc - v;
-      s_segend = inc;
-    }
+    if (t == c) s_segbase = inc - v;
     if (t == 63) s_all = inc;
   }
   {  // the block's runs (prefix of their lengths) and its bucket starts
@@ -1195,10 +1191,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part2_runs(
       fill[t] = 0;
       if (j == 0) fbase[b0 + t] = base;
     }
-    // the end of this segment's last bucket = the next segment's first start
-    // (written here too: a launch over a group of segments groups its last
-    // bucket before the next group's second pass runs; == s_all for the last)
-    if (j == 0 && t == 0) fbase[b0 + nbins] = c == nseg - 1 ? s_all : s_segend;
+    if (j == 0 && c == nseg - 1 && t == 0) fbase[nfine] = s_all;
     if (t == 0) full_n[0] = full_n[1] = 0;
   }
   __syncthreads();
@@ -1470,7 +1463,6 @@ constexpr int kPer = (kLdsCap + kGroupThreads - 1) / kGroupThreads;
 struct RepOut {
   static constexpr int kScratch = 1;
   uint32_t* rep;
-  uint32_t bucket0 = 0, nbuckets = 0;  // as ListOut's
   template <int kSteps>
   __device__ __forceinline__ void emit(const bool (&live)[kSteps], const bool (&lk)[kSteps],
                                        const uint32_t (&r)[kSteps], const uint32_t (&w)[kSteps],
@@ -1580,9 +1572,6 @@ struct ListOut {
   // fails with -ENOSPC); ~0: unbounded (n entries at most)
   uint32_t cap = 0xFFFFFFFFu;
   uint32_t* nospc = nullptr;
-  // a launch over buckets [bucket0, bucket0 + gridDim.x) of nbuckets (the
-  // segment-group launches of the two-level path; nbuckets 0: the whole grid)
-  uint32_t bucket0 = 0, nbuckets = 0;
   template <int kSteps>
   __device__ __forceinline__ void emit(const bool (&live)[kSteps], const bool (&lk)[kSteps],
                                        const uint32_t (&r)[kSteps], const uint32_t (&w)[kSteps],
@@ -1634,9 +1623,8 @@ __device__ __forceinline__ void out_done(const ListOut& o, uint32_t, uint32_t, u
                                          const uint32_t* scr) {
   __syncthreads();  // every wave's atomics on the counters are done
   if (threadIdx.x == 0) {
-    const uint32_t b = o.bucket0 + blockIdx.x, nb = o.nbuckets ? o.nbuckets : gridDim.x;
-    o.lcnt[b] = scr[1];
-    if (b == nb - 1) o.lcnt[nb] = end;
+    o.lcnt[blockIdx.x] = scr[1];
+    if (blockIdx.x == gridDim.x - 1) o.lcnt[gridDim.x] = end;
   }
 }
 __device__ __forceinline__ void out_done(const RepOut&, uint32_t, uint32_t, uint32_t,
@@ -2037,7 +2025,7 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group_pk(
   uint32_t* lmin = lw;
   uint32_t& special_min = lw[kPkCap];
   uint32_t* scr = lw + kPkCap + 1;
-  const uint32_t b = out.bucket0 + blockIdx.x;
+  const uint32_t b = blockIdx.x;
   group_bucket_packed(Rec16Src{rec}, offs[static_cast<uint64_t>(b) * P],
                       offs[static_cast<uint64_t>(b + 1) * P], bits, chunk_of, gkey, gmin, out, tab,
                       lmin, special_min, scr);
@@ -2054,7 +2042,7 @@ __global__ __launch_bounds__(kGroupThreads, 8) void k_bucket_group12_pk(
   uint32_t* lmin = lw;
   uint32_t& special_min = lw[kPkCap];
   uint32_t* scr = lw + kPkCap + 1;
-  const uint32_t b = out.bucket0 + blockIdx.x;
+  const uint32_t b = blockIdx.x;
   group_bucket_packed(Rec12Src{rec, rank_base}, offs[b], offs[b + 1], bits, chunk_of, gkey, gmin,
                       out, tab, lmin, special_min, scr);
 }
@@ -2418,8 +2406,7 @@ void allow_lds(K kernel, size_t bytes) {
 }
 
 
-// K5 over 12-byte records, one workgroup per bucket.  nb buckets starting at
-// out.bucket0 (offs indexed globally).  Round 5 measured a persistent,
+// K5 over 12-byte records, one workgroup per bucket (nb buckets).  Round 5 measured a persistent,
 // LDS-staged variant (one workgroup per CU copying the next bucket's records
 // to LDS with global_load_lds while grouping the current one): 2.2x slower
 // (it halves the resident workgroups of a VALU-bound kernel; DESIGN.md 4.3,
@@ -2523,37 +2510,23 @@ hipError_t two_level_launch(In in, uint64_t n, const GroupLayout& L, uint32_t ch
           ovf);
       k_fine_scan<kP2, kPartBlocks / kP2><<<(nfine + 63) / 64, 1024, 0, s>>>(fine, nfine, fE, ftot, ovf);
     }
-    // second pass and group-by, either over all segments at once or per
-    // group of segments (SDGPU_SEG_GROUPS = G > 1: the group kernel reads
-    // the records its segments' second pass has just written, ~1.2 GB / G at
-    // 100 M rows, while they may still sit in the 256 MiB Infinity Cache)
-    static const uint32_t kGroups = [] {
-      const char* e = std::getenv("SDGPU_SEG_GROUPS");
-      const long v = e ? std::strtol(e, nullptr, 10) : 1;
-      return static_cast<uint32_t>(v >= 1 && v <= 64 ? v : 1);
-    }();
-    const uint32_t G = std::min<uint32_t>(kGroups, nseg);
-    KScope kall(timer, G > 1 ? "bucket_scatter_group" : nullptr, s);
-    for (uint32_t g = 0; g < G; ++g) {
-      const uint32_t s0 = nseg * g / G, s1 = nseg * (g + 1) / G;
-      {
-        KScope k(timer, G > 1 ? nullptr : "bucket_scatter", s);
-        k_part2_runs<kRec12, kB2, kS2, kR2, kF2><<<dim3(kP2, s1 - s0), kPartThreads, 0, s>>>(
-            rec1, skip2, fE, rec, run_s, run_l, mr, P, kPartBlocks / kP2, segtot, ftot,
-            fbase, s0, nseg);
-      }
-      KScope k(timer, G > 1 ? nullptr : "bucket_group", s);
-      Out o = out;
-      o.bucket0 = s0 << kB2;
-      o.nbuckets = nfine;
-      const uint32_t nbk = (s1 - s0) << kB2;
-      if constexpr (kRec12)
-        group12_launch(reinterpret_cast<const uint3*>(rec), rank_base, fbase, nbk, bits,
-                       ChunkOf::make(chunk_rows), gkey, gmin, o, s);
-      else
-        k_bucket_group_pk<Out><<<nbk, kGroupThreads, 0, s>>>(rec, fbase, 1, bits,
-                                                             ChunkOf::make(chunk_rows), gkey, gmin, o);
+    // second pass over all segments, then the group-by over all buckets.
+    // (Round 5 tried the two interleaved per group of segments, so the group
+    // kernel would read records still in the Infinity Cache: slower at every
+    // G, 1.807 -> 1.831-1.990 ms at 100 M rows, and removed in round 6 --
+    // DESIGN.md 4.3, "segment groups".)
+    {
+      KScope k(timer, "bucket_scatter", s);
+      k_part2_runs<kRec12, kB2, kS2, kR2, kF2><<<dim3(kP2, nseg), kPartThreads, 0, s>>>(
+          rec1, skip2, fE, rec, run_s, run_l, mr, P, kPartBlocks / kP2, segtot, ftot, fbase);
     }
+    KScope k(timer, "bucket_group", s);
+    if constexpr (kRec12)
+      group12_launch(reinterpret_cast<const uint3*>(rec), rank_base, fbase, nfine, bits,
+                     ChunkOf::make(chunk_rows), gkey, gmin, out, s);
+    else
+      k_bucket_group_pk<Out><<<nfine, kGroupThreads, 0, s>>>(rec, fbase, 1, bits,
+                                                             ChunkOf::make(chunk_rows), gkey, gmin, out);
     return out_finish(out, nfine, s);
   }
   // pass 1: coarse partition on the top cbits digit bits (rep initialised

@@ -13,7 +13,9 @@
 #include <sys/stat.h>
 #include <string.h>
 #include <unistd.h>
+#if defined(__x86_64__) || defined(__i386__)
 #include <emmintrin.h>
+#endif
 
 #include <algorithm>
 #include <atomic>
@@ -122,6 +124,7 @@ inline int64_t read_cas_message(const char* path, uint64_t size, uint8_t* dst, s
 // the other socket's memory).  Same bytes and results as read_cas_message.
 inline void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
   size_t k = 0;
+#if defined(__x86_64__) || defined(__i386__)
   if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
     for (; k + 64 <= n; k += 64) {
       const __m128i a = _mm_load_si128(reinterpret_cast<const __m128i*>(src + k));
@@ -135,6 +138,7 @@ inline void stream_copy(uint8_t* dst, const uint8_t* src, size_t n) {
     }
     _mm_sfence();  // the streamed lines are visible before the slab is handed on
   }
+#endif  // other hosts: a plain copy
   if (k < n) memcpy(dst + k, src + k, n - k);
 }
 

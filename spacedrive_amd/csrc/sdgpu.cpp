@@ -366,7 +366,8 @@ int sdgpu_close(sdgpu_ctx* c) {
   }
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->plan_pin.p) (void)hipHostFree(c->plan_pin.p);
-  for (DevBuf* b : {&c->xs_send, &c->xs_recv, &c->xs_back, &c->xs_ret, &c->xs_rback})
+  for (DevBuf* b : {&c->xs_send, &c->xs_recv, &c->xs_back, &c->xs_ret, &c->xs_rback,
+                    &c->xs_cursor, &c->xs_sink, &c->xs_agree})
     if (b->p) (void)hipFree(b->p);
   if (c->xs_counts.p) (void)hipHostFree(c->xs_counts.p);
   if (c->handover) (void)hipEventDestroy(c->handover);
@@ -565,20 +566,38 @@ int sdgpu_cas_batch(sdgpu_ctx* c, const uint8_t* msg_arena, const uint64_t* msg_
   return rc;
 }
 
-int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t* size, uint32_t n,
-                         uint8_t (*out8)[8], uint8_t* has_key, int32_t* status) {
-  if (!c || (n && (!paths || !size || !out8))) return -EINVAL;
+int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t* size_in,
+                         uint32_t n, uint8_t (*out8)[8], uint8_t* has_key, int32_t* status) {
+  if (!c || (n && (!paths || !out8))) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
+  // size NULL (ABI 6): the fresh fs::metadata(path).len() of the reference
+  // (file_identifier/mod.rs:65,80-81), stat-ed here by the read pool; a path
+  // whose stat fails gets status -errno and no key (the row is dropped,
+  // mod.rs:113,127)
+  std::vector<uint64_t> fresh;
+  std::vector<int32_t> stat_rc;
+  if (!size_in && n) {
+    fresh.assign(n, 0);
+    stat_rc.assign(n, 0);
+    parallel_for(n, [&](uint32_t i) {
+      struct stat st;
+      if (stat(paths[i], &st) != 0) stat_rc[i] = -errno;
+      else fresh[i] = static_cast<uint64_t>(st.st_size);
+    });
+  }
+  const uint64_t* size = size_in ? size_in : fresh.data();
+  auto failed = [&](uint32_t i) -> int32_t { return stat_rc.empty() ? 0 : stat_rc[i]; };
   std::vector<uint32_t> grown;  // <= 100 KiB at stat, longer than its room at read
   const int rc = run_pipeline(
       c, n,
       [&](uint32_t i) -> uint64_t {
-        if (size[i] == 0) return 16;
+        if (size[i] == 0 || failed(i)) return 16;
         return size[i] <= SDGPU_CAS_MINIMUM_FILE_SIZE ? 8 + size[i] + 4096  // room to grow
                                                       : SDGPU_CAS_SAMPLED_MSG_LEN;
       },
       [&](uint32_t i, uint8_t* dst, size_t cap) -> int64_t {
+        if (failed(i)) return failed(i);
         if (size[i] == 0) return 0x7fffffff;  // cas_id None (file_identifier/mod.rs:80-88)
         if (c->io_bounce) return read_cas_message_bounce(paths[i], size[i], dst, cap);
         return read_cas_message(paths[i], size[i], dst, cap);
@@ -609,6 +628,10 @@ int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t*
           uint32_t idx[kGrain], m = 0;
           for (uint32_t j = j0; j < j1; ++j) {
             const uint32_t i = first + j;
+            if (failed(i)) {
+              settle(j, failed(i));
+              continue;
+            }
             if (size[i] == 0) {
               settle(j, 0x7fffffff);  // cas_id None (file_identifier/mod.rs:80-88)
               continue;

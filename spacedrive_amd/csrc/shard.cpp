@@ -10,22 +10,33 @@
 //   1. partition of the GPU's rows by owner GPU (a W-way scatter) into packed
 //      12-byte send records {key lo, key hi, rank}, each row's send position
 //      (coalesced) and the per-owner counts (device);
-//   2. all-to-all of the counts (8 B per pair), then ONE host synchronisation
-//      that reads the send / receive counts (they size the payload);
-//   3. all-to-all of the records -- one message per (source, owner) pair;
-//   4. local grouping of the received rows (Object-index probe first when an
-//      index is given, creators inserted after);
-//   5. all-to-all of the reps back to the sources (4 B per row), gathered to
-//      row order (keyless rows keep their own rank).
+//   2. the records to their owners: by default (PADDED, ABI 5) in fixed-
+//      capacity messages whose real counts travel in a header slot and are
+//      read on the device -- no host synchronisation, the call's outcome
+//      (an overflow re-run, -ENOSPC) resolved at the next call; else
+//      (COUNTED) an all-to-all of the counts (24 B per pair), one host
+//      synchronisation that sizes the payload, then messages of exact size;
+//   3. local grouping of the received rows (Object-index probe first when an
+//      index is given, creators inserted after), or the write set of the
+//      owned rows (the write-set form: no return leg);
+//   4. rep form: all-to-all of the reps back to the sources (4 B per row),
+//      gathered to row order (keyless rows keep their own rank).
 // Transports: RCCL (ncclSend / ncclRecv in one group, over xGMI; one process
 // per GPU via sdgpu_comm_init_rank, or one process driving all GPUs via
-// sdgpu_comm_init_all), and, for contexts that share a device (RCCL refuses
-// two ranks on one GPU: the one-GPU test box), device-to-device peer copies
-// ordered by events.  Both move the same buffers in the same pattern.
+// sdgpu_comm_init_all); for contexts that share a device (RCCL refuses two
+// ranks on one GPU: the one-GPU test box) device-to-device peer copies
+// ordered by events (one process) or, one process per rank, a shared host
+// mapping (HOST, ABI 6).  All move the same buffers in the same pattern.
+#include <fcntl.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
+#include <atomic>
 #include <chrono>
+#include <string>
 #include <memory>
 #include <thread>
 #include <vector>
@@ -80,6 +91,42 @@ struct RankJob {
   std::vector<uint64_t> pcnt, pin, poff, pioff;
 };
 
+// HOST transport (ABI 6): one rank per process on one host, messages staged
+// through a MAP_SHARED file.  Control page: one HostSlot per rank (its
+// progress words and this round's message table); then one outbox of `obox`
+// bytes per rank.  Round k of a rank: post its messages (posted = k), copy
+// every peer's message to it once they are posted, then consumed = k; its
+// outbox is rewritten only after every peer consumed round k.  The words are
+// lock-free std::atomic in the shared mapping (address-free).
+constexpr int kHostMaxRanks = 64;
+struct HostSlot {
+  std::atomic<uint64_t> joined;    // 1 once the rank has mapped the file
+  std::atomic<uint64_t> posted;    // last round whose outbox is written
+  std::atomic<uint64_t> consumed;  // last round whose inbound messages are copied
+  std::atomic<uint64_t> aborted;   // the rank failed: its peers stop waiting
+  uint64_t nranks, obox;           // what the rank joined with (agreement)
+  uint64_t pad[2];
+  uint64_t off[kHostMaxRanks];     // this round's message to rank p: outbox offset
+  uint64_t bytes[kHostMaxRanks];   //   and size
+};
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory progress words");
+constexpr size_t kHostCtrlBytes = (sizeof(HostSlot) * kHostMaxRanks + 4095) / 4096 * 4096;
+
+struct HostLink {
+  int fd = -1;
+  uint8_t* base = nullptr;
+  size_t size = 0;
+  uint64_t obox = 0;
+  uint64_t round = 0;
+  std::string path;
+  HostSlot* slot(int r) const { return reinterpret_cast<HostSlot*>(base) + r; }
+  uint8_t* outbox(int r) const { return base + kHostCtrlBytes + obox * static_cast<uint64_t>(r); }
+  ~HostLink() {
+    if (base) (void)munmap(base, size);
+    if (fd >= 0) (void)close(fd);
+  }
+};
+
 }  // namespace
 
 struct sdgpu_comm {
@@ -113,10 +160,16 @@ struct sdgpu_comm {
   bool pending = false;
   bool pending_list = false;
   uint32_t pending_chunk_rows = 0;
+  uint64_t pending_call = 0;  // its number in stats.calls
   RankJob pend;
   sdgpu::PinBuf summ;
   hipEvent_t summ_evt = nullptr;
   sdgpu_comm_stats_t stats{};
+  // the layout settings changed since the ranks last agreed on them (every
+  // communicator starts so): the next one-rank-per-process call checks them
+  // with its peers first (agree_layout / the counted call's code)
+  bool layout_dirty = true;
+  std::unique_ptr<HostLink> host;  // SDGPU_TRANSPORT_HOST
 };
 
 struct sdgpu_index {
@@ -182,14 +235,25 @@ void backoff(int& spins) {
 // its kernels still queued on the device exit, its peers see their own
 // deadline pass (a local error becomes a bounded job-wide failure, never a
 // hang).  The communicator is unusable afterwards (-ECONNABORTED).
+// (HOST: the rank's aborted word is raised instead, which its peers poll.)
 int comm_fail(sdgpu_comm* m, int rc) {
   if (m && m->nccl && !m->aborted) {
     (void)hipSetDevice(m->device);
     (void)ncclCommAbort(m->nccl);
     m->nccl = nullptr;
     m->aborted = true;
+  } else if (m && m->host && !m->aborted) {
+    m->host->slot(m->rank)->aborted.store(1, std::memory_order_release);
+    m->aborted = true;
   }
   return rc;
+}
+
+// One rank per process (RCCL, HOST): a call sees only its own rank, its
+// padded outcome is resolved at the next call, a failure aborts the
+// communicator.
+bool per_process(const sdgpu_comm* m) {
+  return m->transport == SDGPU_TRANSPORT_RCCL || m->transport == SDGPU_TRANSPORT_HOST;
 }
 
 // Waits until the communicator's non-blocking operation settles.
@@ -298,9 +362,17 @@ int group_with_index(sdgpu_ctx* c, sdgpu_index* idx, GroupInput in, uint32_t chu
 // must share (a rank posting the rep return while another does not would
 // leave the collectives unmatched until the deadline): checked by every
 // receiver of the counts, -EPROTO on a mismatch.
+// Since round 6 the exchange mode is part of it, so ranks that would pick
+// different layouts (counted vs padded) meet a mismatch, not a hang.
 int64_t call_code(const sdgpu_comm* m, bool list) {
-  return (list ? 32 : 16) + m->return_mode;
+  return (list ? 32 : 16) + m->return_mode + 64 * m->exchange;
 }
+
+// Agreement message of a padded call {slots per message, B, code | tag}
+// (ABI 6; sdgpu.h "Agreement"): 24 B per peer like a count message, and the
+// tag keeps the two from matching, so a rank posting counts where its peer
+// posts an agreement fails with -EPROTO on both sides.
+constexpr int64_t kAgreeTag = int64_t(1) << 40;
 
 // Slots per (source, owner) message of a padded exchange, header included;
 // 0 = counted.  C records = a little over the expected share of the largest
@@ -319,12 +391,81 @@ uint64_t padded_slots(const sdgpu_comm* m, int W, bool rep_form) {
   return c1;
 }
 
+// HOST transport: waits until every rank's progress word `which` reaches k
+// (bounded; a peer that raised its aborted word fails the wait at once).
+int host_wait_all(sdgpu_comm* m, std::atomic<uint64_t> HostSlot::*which, uint64_t k,
+                  Clock::time_point deadline) {
+  HostLink& L = *m->host;
+  int spins = 0;
+  for (int p = 0; p < m->nranks; ++p) {
+    HostSlot* sp = L.slot(p);
+    while ((sp->*which).load(std::memory_order_acquire) < k) {
+      if (sp->aborted.load(std::memory_order_acquire)) return comm_fail(m, -EIO);
+      if (Clock::now() > deadline) return comm_fail(m, -ETIMEDOUT);
+      backoff(spins);
+    }
+  }
+  return 0;
+}
+
+// One all-to-all round over the HOST transport (this process holds one rank,
+// J[0]): the messages leave through the rank's outbox once its stream has
+// produced them, the inbound ones are copied from the peers' outboxes, the
+// self message device to device.  A size that differs from what the peer
+// posted is -EPROTO (the RCCL transport would hang on it until the deadline).
+template <typename SP, typename RP, typename SB, typename RB>
+int host_alltoallv(RankJob& j, int W, Clock::time_point deadline, SP sendp, RP recvp, SB sbytes,
+                   RB rbytes) {
+  sdgpu_comm* m = j.comm;
+  HostLink& L = *m->host;
+  const int me = m->rank;
+  if (W != m->nranks) return -EINVAL;
+  const uint64_t k = ++L.round;
+  SD_TRY(hipSetDevice(j.c->device));
+  if (hipStreamSynchronize(j.s) != hipSuccess) return comm_fail(m, -EIO);
+  HostSlot* mine = L.slot(me);
+  uint64_t off = 0;
+  for (int p = 0; p < W; ++p) {
+    const uint64_t b = p == me ? 0 : sbytes(j, p);
+    if (off + b > L.obox) return comm_fail(m, -EMSGSIZE);
+    if (b && hipMemcpy(L.outbox(me) + off, sendp(j, p), b, hipMemcpyDeviceToHost) != hipSuccess)
+      return comm_fail(m, -EIO);
+    mine->off[p] = off;
+    mine->bytes[p] = b;
+    off = align_up(off + b, 256);
+  }
+  mine->posted.store(k, std::memory_order_release);
+  SD_TRY_RC(host_wait_all(m, &HostSlot::posted, k, deadline));
+  for (int p = 0; p < W; ++p) {
+    const uint64_t rb = rbytes(j, p);
+    if (p == me) {
+      if (sbytes(j, p) != rb) return comm_fail(m, -EPROTO);
+      if (rb && hipMemcpyAsync(recvp(j, p), sendp(j, p), rb, hipMemcpyDeviceToDevice, j.s) !=
+                    hipSuccess)
+        return comm_fail(m, -EIO);
+      continue;
+    }
+    const HostSlot* ps = L.slot(p);
+    if (ps->bytes[me] != rb) return comm_fail(m, -EPROTO);
+    if (rb && hipMemcpyAsync(recvp(j, p), L.outbox(p) + ps->off[me], rb, hipMemcpyHostToDevice,
+                             j.s) != hipSuccess)
+      return comm_fail(m, -EIO);
+  }
+  if (hipStreamSynchronize(j.s) != hipSuccess) return comm_fail(m, -EIO);
+  mine->consumed.store(k, std::memory_order_release);
+  return host_wait_all(m, &HostSlot::consumed, k, deadline);
+}
+
 // One all-to-all round: rank j sends bytes(j, p) from sendp(j, p) to every p
 // and receives rbytes(j, p) into recvp(j, p) from every p.
 template <typename SP, typename RP, typename SB, typename RB>
 int alltoallv(std::vector<RankJob>& J, int W, Clock::time_point deadline, SP sendp, RP recvp,
               SB sbytes, RB rbytes) {
   const int transport = J[0].comm->transport;
+  if (transport == SDGPU_TRANSPORT_HOST) {
+    if (J.size() != 1) return -EINVAL;
+    return host_alltoallv(J[0], W, deadline, sendp, recvp, sbytes, rbytes);
+  }
   if (transport == SDGPU_TRANSPORT_RCCL) {
     // non-blocking communicators: calls inside the group may report
     // ncclInProgress; ncclGroupEnd's completion is polled per communicator
@@ -594,6 +735,7 @@ int padded_epilogue(std::vector<RankJob>& J, int W, bool rep_form) {
 
 int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows, uint64_t c1) {
   const auto t_start = Clock::now();
+  for (auto& j : J) j.comm->stats.calls += 1;  // attempted calls (nospc_call numbers them)
   const Clock::time_point deadline = deadline_of(J[0].comm->timeout_ms);
   uint64_t n_max = 0;
   double count_ms = 0;
@@ -698,7 +840,6 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows, uint64
       std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
   for (auto& j : J) {
     sdgpu_comm_stats_t& st = j.comm->stats;
-    st.calls += 1;
     st.host_ms += call_ms;
     j.comm->last_stream = j.s;
     if (c1) continue;  // the rows are counted when the call is resolved
@@ -735,6 +876,7 @@ int run_sharded_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows, uint64
 // the ranks' lists is the write set of all rows (a set, mod.rs:189-333).
 int run_lists_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows, uint64_t c1) {
   const auto t_start = Clock::now();
+  for (auto& j : J) j.comm->stats.calls += 1;  // attempted calls (nospc_call numbers them)
   const Clock::time_point deadline = deadline_of(J[0].comm->timeout_ms);
   uint64_t n_max = 0;
   double count_ms = 0;
@@ -753,7 +895,11 @@ int run_lists_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows, uint64_t
     SD_TRY(hipMemsetAsync(j.counts, 0, 3 * sizeof(uint32_t), j.s));
     if (j.m + (j.n - j.total) > j.cap) nospc = true;
   }
-  if (nospc) return -ENOSPC;
+  if (nospc) {
+    for (auto& j : J)
+      if (j.m + (j.n - j.total) > j.cap) j.comm->stats.nospc_call = j.comm->stats.calls;
+    return -ENOSPC;
+  }
   for (auto& j : J) {
     SD_TRY(hipSetDevice(j.c->device));
     SD_TRY_RC(ensure_dev(j.c, j.c->dedup_ws, dedup_workspace_bytes(std::max<uint64_t>(j.m, 1))));
@@ -774,7 +920,6 @@ int run_lists_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows, uint64_t
       std::chrono::duration<double, std::milli>(Clock::now() - t_start).count();
   for (auto& j : J) {
     sdgpu_comm_stats_t& st = j.comm->stats;
-    st.calls += 1;
     st.host_ms += call_ms;
     j.comm->last_stream = j.s;
     if (c1) continue;
@@ -786,6 +931,42 @@ int run_lists_impl(std::vector<RankJob>& J, int W, uint32_t chunk_rows, uint64_t
     st.bytes_remote += 12 * (j.total - j.scnt[me]) + 12 * (j.m - j.rcnt[me]);
     st.count_wait_ms += count_ms;
   }
+  return 0;
+}
+
+// The first padded call of a communicator, and its first after a setting
+// changed, checks that every rank chose the same layout before any record
+// moves (one process per rank: J = this rank).  One 24-B message per peer,
+// one host synchronisation; -EPROTO (communicator aborted) on a mismatch.
+int agree_layout(std::vector<RankJob>& J, int W, uint64_t c1, int64_t code) {
+  RankJob& j = J[0];
+  sdgpu_comm* m = j.comm;
+  const Clock::time_point deadline = deadline_of(m->timeout_ms);
+  SD_TRY(hipSetDevice(j.c->device));
+  SD_TRY_RC(ensure_dev(j.c, j.c->xs_agree, 48ull * W));
+  SD_TRY_RC(ensure_pin(j.c->xs_counts, 64ull * W));
+  int64_t* h = static_cast<int64_t*>(j.c->xs_counts.p);
+  int64_t* d = static_cast<int64_t*>(j.c->xs_agree.p);
+  const int64_t mine[3] = {static_cast<int64_t>(c1), static_cast<int64_t>(m->agreed_n),
+                           code | kAgreeTag};
+  for (int p = 0; p < W; ++p)
+    for (int q = 0; q < 3; ++q) h[3 * p + q] = mine[q];
+  SD_TRY(hipMemcpyAsync(d, h, 24ull * W, hipMemcpyHostToDevice, j.s));
+  SD_TRY_RC(alltoallv(
+      J, W, deadline, [d](RankJob&, int p) -> void* { return d + 3 * p; },
+      [d, W](RankJob&, int p) -> void* { return d + 3 * W + 3 * p; },
+      [](RankJob&, int) -> size_t { return 24; }, [](RankJob&, int) -> size_t { return 24; }));
+  SD_TRY(hipMemcpyAsync(h + 3 * W, d + 3 * W, 24ull * W, hipMemcpyDeviceToHost, j.s));
+  if (m->transport == SDGPU_TRANSPORT_RCCL) {
+    SD_TRY_RC(stream_wait(m, j.s, deadline));
+  } else {
+    SD_TRY(hipStreamSynchronize(j.s));
+  }
+  for (int p = 0; p < W; ++p)
+    for (int q = 0; q < 3; ++q)
+      if (h[3 * W + 3 * p + q] != mine[q]) return comm_fail(m, -EPROTO);
+  m->layout_dirty = false;
+  m->stats.agreements += 1;
   return 0;
 }
 
@@ -809,8 +990,8 @@ int event_wait(sdgpu_comm* m, hipEvent_t ev, Clock::time_point deadline) {
 // What a finished padded call left in m->summ: the rows it moved are
 // counted, B is updated (every rank read the same headers).  Returns
 // 1 when some message overflowed (re-run counted), -ENOSPC when this rank's
-// lists did not fit, else 0.
-int padded_outcome(sdgpu_comm* m, bool list) {
+// lists did not fit (stats.nospc_call = call_no, the call's number), else 0.
+int padded_outcome(sdgpu_comm* m, bool list, uint64_t call_no) {
   const uint32_t* sm = static_cast<const uint32_t*>(m->summ.p);
   m->agreed_n = sm[1];
   sdgpu_comm_stats_t& st = m->stats;
@@ -818,7 +999,9 @@ int padded_outcome(sdgpu_comm* m, bool list) {
   st.rows_received += sm[2];
   if (!list) st.rows_returned += sm[2];
   if (sm[0]) return 1;
-  return list && sm[4] ? -ENOSPC : 0;
+  if (!(list && sm[4])) return 0;
+  st.nospc_call = call_no;
+  return -ENOSPC;
 }
 
 int run_counted(std::vector<RankJob>& J, int W, uint32_t chunk_rows, bool list) {
@@ -838,13 +1021,15 @@ int resolve_pending(sdgpu_comm* m) {
   SD_TRY(hipSetDevice(m->device));
   SD_TRY_RC(event_wait(m, m->summ_evt, deadline_of(m->timeout_ms)));
   m->stats.resolve_wait_ms += std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
-  const int o = padded_outcome(m, m->pending_list);
+  const int o = padded_outcome(m, m->pending_list, m->pending_call);
   if (o <= 0) return o;
   m->stats.overflow_reruns += 1;
   std::vector<RankJob> J(1, m->pend);
-  J[0].s = pick(J[0].c, J[0].s);  // after whatever the context ran since
+  // after whatever the context ran since; the caller's next work is ordered
+  // after this stream in turn (run_call picks its own stream again)
+  J[0].s = pick(J[0].c, J[0].s);
   const int rc = run_counted(J, m->nranks, m->pending_chunk_rows, m->pending_list);
-  if (rc != 0 && rc != -ENOSPC && m->transport == SDGPU_TRANSPORT_RCCL) comm_fail(m, rc);
+  if (rc != 0 && rc != -ENOSPC && per_process(m)) comm_fail(m, rc);
   return rc;
 }
 
@@ -852,32 +1037,47 @@ int resolve_pending(sdgpu_comm* m) {
 // GPU, all for the _all entry points).  Any failure on an RCCL rank aborts
 // its communicator (bounded failure for the peers) and is
 // returned; -ENOSPC of the write set comes after the last collective and
-// leaves the peers fine.
+// leaves the peers fine.  J[k].s: the stream the entry point was given (the
+// context's default when NULL); picked here, after the pending call.
 int run_call(std::vector<RankJob>& J, int W, uint32_t chunk_rows, bool list) {
   for (auto& j : J)
     if (j.comm->aborted || (j.comm->transport == SDGPU_TRANSPORT_RCCL && !j.comm->nccl))
       return -ECONNABORTED;
-  const bool single = J.size() == 1 && W > 0 && J[0].comm->transport == SDGPU_TRANSPORT_RCCL;
+  const bool single = J.size() == 1 && W > 0 && per_process(J[0].comm);
   if (single) {
     // the previous call of this communicator first (its overflow re-run, if
-    // any, keeps the collectives in the same order on every rank)
-    const int prc = resolve_pending(J[0].comm);
-    if (prc == -ENOSPC) J[0].comm->deferred_rc = prc;
+    // any, keeps the collectives in the same order on every rank).  Its
+    // -ENOSPC waits for sdgpu_comm_wait (the earliest unreported one stays).
+    sdgpu_comm* m = J[0].comm;
+    const int prc = resolve_pending(m);
+    if (prc == -ENOSPC && !m->deferred_rc) m->deferred_rc = prc;
     if (prc != 0 && prc != -ENOSPC) return prc;
-    if (J[0].comm->aborted) return -ECONNABORTED;
+    if (m->aborted) return -ECONNABORTED;
+  }
+  // This call's stream, picked only now: a re-run above went on the pending
+  // call's stream, which the context's hand-over orders this one after (the
+  // re-run and this call share the exchange buffers and the communicator;
+  // ADVICE r5 high).
+  for (auto& j : J) {
+    SD_TRY(hipSetDevice(j.c->device));
+    j.s = pick(j.c, j.s);
   }
   uint64_t c1 = padded_slots(J[0].comm, W, !list);
   for (auto& j : J)  // the _all forms: every rank's settings must agree
     if (padded_slots(j.comm, W, !list) != c1 || j.comm->exchange != J[0].comm->exchange ||
         j.comm->return_mode != J[0].comm->return_mode)
       return -EINVAL;
+  if (single && c1 && J[0].comm->layout_dirty)
+    SD_TRY_RC(agree_layout(J, W, c1, call_code(J[0].comm, list)));
   int rc = list ? run_lists_impl(J, W, chunk_rows, c1) : run_sharded_impl(J, W, chunk_rows, c1);
+  if (rc == 0 && !c1) J[0].comm->layout_dirty = false;  // the count messages agreed
   if (rc == 0 && c1) {
     if (single) {
       sdgpu_comm* m = J[0].comm;
       m->pending = true;
       m->pending_list = list;
       m->pending_chunk_rows = chunk_rows;
+      m->pending_call = m->stats.calls;
       m->pend = J[0];
       return 0;
     }
@@ -889,7 +1089,7 @@ int run_call(std::vector<RankJob>& J, int W, uint32_t chunk_rows, bool list) {
       SD_TRY(hipSetDevice(j.c->device));
       rc = event_wait(j.comm, j.comm->summ_evt, deadline_of(j.comm->timeout_ms));
       if (rc) break;
-      const int o = padded_outcome(j.comm, list);
+      const int o = padded_outcome(j.comm, list, j.comm->stats.calls);
       if (o > 0) over = true;
       if (o < 0) local = o;
     }
@@ -902,8 +1102,14 @@ int run_call(std::vector<RankJob>& J, int W, uint32_t chunk_rows, bool list) {
   }
   if (rc != 0 && rc != -ENOSPC)
     for (auto& j : J)
-      if (j.comm->transport == SDGPU_TRANSPORT_RCCL) comm_fail(j.comm, rc);
+      if (per_process(j.comm)) comm_fail(j.comm, rc);
   return rc;
+}
+
+// The stream an exchange entry point was given (run_call picks it after
+// resolving the pending call).
+hipStream_t given_stream(sdgpu_ctx* c, void* stream) {
+  return stream ? static_cast<hipStream_t>(stream) : c->stream;
 }
 
 bool same_devices(sdgpu_ctx* const* ctx, int ngpu) {
@@ -970,6 +1176,56 @@ int sdgpu_comm_init_rank(sdgpu_ctx* c, int nranks, int rank, const uint8_t id[SD
   return sdgpu_comm_init_rank_timeout(c, nranks, rank, id, default_timeout_ms(), out);
 }
 
+int sdgpu_comm_init_host(sdgpu_ctx* c, int nranks, int rank, const char* path,
+                         uint64_t msg_bytes, int timeout_ms, sdgpu_comm** out) {
+  if (!c || !path || !*path || !out || nranks < 1 || nranks > kHostMaxRanks || rank < 0 ||
+      rank >= nranks || msg_bytes == 0 || msg_bytes > (1ull << 40) || timeout_ms <= 0)
+    return -EINVAL;
+  *out = nullptr;
+  std::lock_guard<std::mutex> g(c->mu);
+  SD_TRY(hipSetDevice(c->device));
+  std::unique_ptr<HostLink> L(new (std::nothrow) HostLink);
+  if (!L) return -ENOMEM;
+  L->obox = align_up(msg_bytes, 4096);
+  L->size = kHostCtrlBytes + L->obox * static_cast<uint64_t>(nranks);
+  L->path = path;
+  L->fd = open(path, O_RDWR | O_CREAT | O_CLOEXEC, 0600);
+  if (L->fd < 0) return -errno;
+  struct stat st;
+  if (fstat(L->fd, &st) != 0) return -errno;
+  // every rank grows the (fresh, all-zero) file to the same size; a rank
+  // that asked for a different msg_bytes is caught by the agreement below
+  if (static_cast<uint64_t>(st.st_size) < L->size && ftruncate(L->fd, L->size) != 0) return -errno;
+  void* p = mmap(nullptr, L->size, PROT_READ | PROT_WRITE, MAP_SHARED, L->fd, 0);
+  if (p == MAP_FAILED) return -errno;
+  L->base = static_cast<uint8_t*>(p);
+  HostSlot* mine = L->slot(rank);
+  if (mine->joined.load(std::memory_order_acquire)) return -EEXIST;  // an earlier communicator's file
+  mine->nranks = static_cast<uint64_t>(nranks);
+  mine->obox = L->obox;
+  mine->joined.store(1, std::memory_order_release);
+  const Clock::time_point deadline = deadline_of(timeout_ms);
+  int spins = 0;
+  for (int q = 0; q < nranks; ++q) {
+    HostSlot* sq = L->slot(q);
+    while (!sq->joined.load(std::memory_order_acquire)) {
+      if (Clock::now() > deadline) return -ETIMEDOUT;
+      backoff(spins);
+    }
+    if (sq->nranks != static_cast<uint64_t>(nranks) || sq->obox != L->obox) return -EPROTO;
+  }
+  sdgpu_comm* m = new (std::nothrow) sdgpu_comm;
+  if (!m) return -ENOMEM;
+  m->nranks = nranks;
+  m->rank = rank;
+  m->transport = SDGPU_TRANSPORT_HOST;
+  m->device = c->device;
+  m->timeout_ms = timeout_ms;
+  m->host = std::move(L);
+  *out = m;
+  return 0;
+}
+
 int sdgpu_comm_set_timeout(sdgpu_comm* m, int timeout_ms) {
   if (!m || timeout_ms <= 0) return -EINVAL;
   m->timeout_ms = timeout_ms;
@@ -978,25 +1234,36 @@ int sdgpu_comm_set_timeout(sdgpu_comm* m, int timeout_ms) {
 
 int sdgpu_comm_wait(sdgpu_comm* m, void* stream) {
   if (!m) return -EINVAL;
+  int rc = 0;
   if (m->pending) {
     // the padded call's summary, and its counted re-run on an overflow
     sdgpu_ctx* c = m->pend.c;
     std::lock_guard<std::mutex> g(c->mu);
-    const int rc = resolve_pending(m);
-    if (rc != 0) return rc;
+    rc = resolve_pending(m);
   }
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : m->last_stream;
+  // an earlier call's -ENOSPC found by a later call is reported now, once
+  // (ADVICE r5): a hard error of this resolution first, then the deferred
+  // -ENOSPC, then this resolution's own
+  const int deferred = m->deferred_rc;
+  m->deferred_rc = 0;
+  if (rc != 0 && rc != -ENOSPC) return rc;
+  if (deferred) return deferred;
+  if (rc) return rc;
   if (m->aborted) return -ECONNABORTED;
-  if (m->deferred_rc) {
-    const int rc = m->deferred_rc;
-    m->deferred_rc = 0;
-    return rc;
-  }
-  if (!s) return 0;
+  // the given stream, and the stream of the last exchange when it differs
+  // (a re-run goes on the pending call's own stream)
+  hipStream_t ss[2] = {stream ? static_cast<hipStream_t>(stream) : m->last_stream, m->last_stream};
+  if (ss[1] == ss[0]) ss[1] = nullptr;
   SD_TRY(hipSetDevice(m->device));
-  if (m->transport != SDGPU_TRANSPORT_RCCL || !m->nccl)
-    return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
-  return stream_wait(m, s, deadline_of(m->timeout_ms));
+  for (hipStream_t s : ss) {
+    if (!s) continue;
+    if (m->transport != SDGPU_TRANSPORT_RCCL || !m->nccl) {
+      if (hipStreamSynchronize(s) != hipSuccess) return -EIO;
+    } else {
+      SD_TRY_RC(stream_wait(m, s, deadline_of(m->timeout_ms)));
+    }
+  }
+  return 0;
 }
 
 int sdgpu_comm_set_exchange(sdgpu_comm* m, int mode, uint64_t rows_hint) {
@@ -1005,6 +1272,7 @@ int sdgpu_comm_set_exchange(sdgpu_comm* m, int mode, uint64_t rows_hint) {
     return -EINVAL;
   m->exchange = mode;
   if (rows_hint) m->agreed_n = rows_hint;
+  m->layout_dirty = true;  // checked with the peers at the next call
   return 0;
 }
 
@@ -1013,6 +1281,7 @@ int sdgpu_comm_set_return(sdgpu_comm* m, int mode) {
              mode != SDGPU_RETURN_AUTO))
     return -EINVAL;
   m->return_mode = mode;
+  m->layout_dirty = true;
   return 0;
 }
 
@@ -1100,6 +1369,7 @@ int sdgpu_comm_destroy(sdgpu_comm* m) {
     }
     m->nccl = nullptr;
   }
+  if (m->host && m->rank == 0) (void)unlink(m->host->path.c_str());
   if (m->summ.p) (void)hipHostFree(m->summ.p);
   delete m;
   return 0;
@@ -1310,8 +1580,10 @@ int sdgpu_group_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, sdgpu_index* x,
                                uint32_t* d_rep, void* stream) {
   if (!c || !comm || chunk_rows == 0 || (n && (!d_key || !d_rank || !d_rep))) return -EINVAL;
   if (comm->device != c->device || (x && x->ctx->device != c->device)) return -EINVAL;
-  if (comm->transport != SDGPU_TRANSPORT_RCCL) return -EINVAL;  // peer: sdgpu_group_sharded_all_device
-  if (n >= (1ull << 32)) return -EINVAL;
+  if (!per_process(comm)) return -EINVAL;  // peer: sdgpu_group_sharded_all_device
+  // global ranks are < 2^31 and unique, so n < 2^31 (the padded header's
+  // count shares its word with the overflow bit)
+  if (n >= (1ull << 31)) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
   std::vector<RankJob> J(1);
@@ -1319,7 +1591,7 @@ int sdgpu_group_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, sdgpu_index* x,
   j.c = c;
   j.comm = comm;
   j.idx = x;
-  j.s = pick(c, stream);
+  j.s = given_stream(c, stream);
   j.key = d_key;
   j.has = d_has_key;
   j.rank = d_rank;
@@ -1343,7 +1615,7 @@ int sdgpu_group_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* com
         comm[r]->device != ctx[r]->device || comm[r]->transport != comm[0]->transport)
       return -EINVAL;
     if (n[r] && (!d_key[r] || !d_rank[r] || !d_rep[r])) return -EINVAL;
-    if (n[r] >= (1ull << 32)) return -EINVAL;
+    if (n[r] >= (1ull << 31)) return -EINVAL;
     if (idx && idx[r] && idx[r]->ctx->device != ctx[r]->device) return -EINVAL;
   }
   // contexts may repeat a device (peer transport on one GPU); lock each once
@@ -1361,7 +1633,7 @@ int sdgpu_group_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* com
     j.comm = comm[r];
     j.idx = idx ? idx[r] : nullptr;
     SD_TRY(hipSetDevice(ctx[r]->device));
-    j.s = pick(ctx[r], streams ? streams[r] : nullptr);
+    j.s = given_stream(ctx[r], streams ? streams[r] : nullptr);
     j.key = d_key[r];
     j.has = d_has_key ? d_has_key[r] : nullptr;
     j.rank = d_rank[r];
@@ -1380,7 +1652,7 @@ int sdgpu_group_link_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, const uint64
       (n && (!d_key || !d_rank)))
     return -EINVAL;
   if (comm->device != c->device) return -EINVAL;
-  if (comm->transport != SDGPU_TRANSPORT_RCCL) return -EINVAL;  // peer: the _all form
+  if (!per_process(comm)) return -EINVAL;  // peer: the _all form
   if (n >= (1ull << 31)) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   SD_TRY(hipSetDevice(c->device));
@@ -1388,7 +1660,7 @@ int sdgpu_group_link_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, const uint64
   RankJob& j = J[0];
   j.c = c;
   j.comm = comm;
-  j.s = pick(c, stream);
+  j.s = given_stream(c, stream);
   j.key = d_key;
   j.has = d_has_key;
   j.valid = d_valid;
@@ -1430,7 +1702,7 @@ int sdgpu_group_link_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const
     j.c = ctx[r];
     j.comm = comm[r];
     SD_TRY(hipSetDevice(ctx[r]->device));
-    j.s = pick(ctx[r], streams ? streams[r] : nullptr);
+    j.s = given_stream(ctx[r], streams ? streams[r] : nullptr);
     j.key = d_key[r];
     j.has = d_has_key ? d_has_key[r] : nullptr;
     j.valid = d_valid ? d_valid[r] : nullptr;

@@ -19,6 +19,7 @@ built from libsdgpu's single steps.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -271,7 +272,7 @@ def dedup_batch(key, has_key, first_rank: int, index: ObjectIndex | None = None,
 
 # ---- multi-GPU grouping inside libsdgpu (RCCL / peer transport) -----------------
 
-TRANSPORT_AUTO, TRANSPORT_RCCL, TRANSPORT_PEER = 0, 1, 2
+TRANSPORT_AUTO, TRANSPORT_RCCL, TRANSPORT_PEER, TRANSPORT_HOST = 0, 1, 2, 3
 
 
 RETURN_FULL, RETURN_COMPACT, RETURN_AUTO = 0, 1, 2  # SDGPU_RETURN_*
@@ -285,7 +286,8 @@ class CommStats(ctypes.Structure):
                 ("bytes_received", ctypes.c_uint64), ("bytes_remote", ctypes.c_uint64),
                 ("count_wait_ms", ctypes.c_double), ("host_ms", ctypes.c_double),
                 ("rows_returned", ctypes.c_uint64), ("padded_calls", ctypes.c_uint64),
-                ("overflow_reruns", ctypes.c_uint64), ("resolve_wait_ms", ctypes.c_double)]
+                ("overflow_reruns", ctypes.c_uint64), ("resolve_wait_ms", ctypes.c_double),
+                ("agreements", ctypes.c_uint64), ("nospc_call", ctypes.c_uint64)]
 
 
 class Comm:
@@ -319,6 +321,20 @@ class Comm:
             check(ctx.lib.sdgpu_comm_init_rank_timeout(ctx.h, nranks, rank, buf, int(timeout_ms),
                                                        ctypes.byref(h)),
                   "sdgpu_comm_init_rank_timeout")
+        return cls(ctx, h)
+
+    @classmethod
+    def init_host(cls, ctx, nranks: int, rank: int, path: str, msg_bytes: int = 64 << 20,
+                  timeout_ms: int = 60000) -> "Comm":
+        """One process per rank on one host, through a shared file mapping
+        (sdgpu_comm_init_host, ABI 6): the per-process exchange of the RCCL
+        transport, host-staged, for ranks that share a GPU.  path: a fresh
+        file name every rank passes; msg_bytes: one rank's messages of one
+        all-to-all round."""
+        h = ctypes.c_void_p()
+        check(ctx.lib.sdgpu_comm_init_host(ctx.h, nranks, rank, os.fsencode(path), int(msg_bytes),
+                                           int(timeout_ms), ctypes.byref(h)),
+              "sdgpu_comm_init_host")
         return cls(ctx, h)
 
     def set_timeout(self, timeout_ms: int):

@@ -54,7 +54,7 @@ class IdentifyResult:
     cas8: np.ndarray      # [n, 8] uint8 (zeros where has_key == 0)
     has_key: np.ndarray   # [n] uint8: 1 = cas_id present
     status: np.ndarray    # [n] int32: 0 or -errno (row dropped, mod.rs:113,127)
-    sizes: np.ndarray     # [n] uint64 (fs::metadata len, mod.rs:65)
+    sizes: np.ndarray | None  # [n] uint64 as passed; None: stat-ed by the library
 
     def cas_ids(self) -> list[str | None]:
         return [bytes(self.cas8[i]).hex() if self.has_key[i] else None
@@ -86,25 +86,18 @@ def identify(paths, sizes=None, ctx=None) -> IdentifyResult:
     paths, or a PathList)."""
     ctx = ctx or default_context()
     n = len(paths)
-    st = np.zeros(n, np.int32)
-    if sizes is None:
-        sizes = np.zeros(n, np.uint64)
-        for i, p in enumerate(paths):
-            try:
-                sizes[i] = os.stat(p).st_size
-            except OSError as e:
-                st[i] = -e.errno
-    sizes = np.ascontiguousarray(sizes, np.uint64)
+    # sizes None: the library stats every path in its read pool (the
+    # reference's fresh fs::metadata(path).len(), mod.rs:65,80-81; a failed
+    # stat is status -errno, the row dropped)
+    if sizes is not None:
+        sizes = np.ascontiguousarray(sizes, np.uint64)
     arr = paths.c_paths if isinstance(paths, PathList) else PathList(paths).c_paths
     out = np.zeros((n, 8), np.uint8)
     has = np.zeros(n, np.uint8)
     status = np.zeros(n, np.int32)
-    check(ctx.lib.sdgpu_identify_files(ctx.h, arr, sizes.ctypes.data, n, out.ctypes.data,
-                                       has.ctypes.data, status.ctypes.data),
+    check(ctx.lib.sdgpu_identify_files(ctx.h, arr, sizes.ctypes.data if sizes is not None else None,
+                                       n, out.ctypes.data, has.ctypes.data, status.ctypes.data),
           "sdgpu_identify_files")
-    failed_stat = st != 0
-    status[failed_stat] = st[failed_stat]
-    has[failed_stat] = 0
     return IdentifyResult(out, has, status, sizes)
 
 

@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     lib = _native.load()
-    assert lib.sdgpu_abi_version() == 5
+    assert lib.sdgpu_abi_version() == 6
     assert lib.sdgpu_strerror(0) == b"success"
     assert lib.sdgpu_strerror(-22) == b"Invalid argument"
 
@@ -33,6 +33,7 @@ def test_null_arguments_rejected_without_device():
     assert lib.sdgpu_index_create(None, 10, None) == -22
     assert lib.sdgpu_comm_unique_id(None) == -22
     assert lib.sdgpu_comm_init_all(None, 2, 0, None) == -22
+    assert lib.sdgpu_comm_init_host(None, 2, 0, b"/tmp/sd_none", 4096, 1000, None) == -22
     assert lib.sdgpu_dedup_sharded(None, 2, None, None, 0, 100, None) == -22
     assert lib.sdgpu_group_sharded_device(None, None, None, None, None, None, 0, 100, None,
                                           None) == -22
@@ -151,3 +152,12 @@ def test_rust_job_queries_mirror_the_python_job():
     init = job[job.index("pub fn init("):job.index("pub fn resume(")]
     assert "count_orphans(" in init and "first_orphan(" in init and ".orphans(" not in init
     assert "existing_objects_page(" in job and "fn existing_objects(" not in trait
+    # no stored size (the selectable has none, file_path_
+    # helper/mod.rs:32-40; the library stats the paths: identify(.., None)),
+    # and the step's cas_id updates in one write (mod.rs:144-165)
+    orphan = job[job.index("pub struct Orphan"):]
+    orphan = orphan[:orphan.index("}")]
+    assert "size" not in orphan.replace("no size", "")
+    assert "identify(self.gpu, &paths, None)" in job
+    assert "fn set_cas_ids(&mut self, rows: &[(i32, Option<String>)])" in trait
+    assert "fn set_cas_id(" not in trait and job.count("set_cas_ids(") == 2

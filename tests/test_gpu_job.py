@@ -215,3 +215,64 @@ def test_file_grown_between_stat_and_read(ctx, tmp_path):
     for p, (stat_size, _), g in zip(paths, cases, res.cas_ids()):
         assert g == O.cas_id_path(p, stat_size)
         assert cas.generate_cas_id(p, stat_size, ctx) == g
+
+
+def test_job_sizes_are_fresh_at_identification(ctx, tmp_path):
+    """the job passes no stored size; the library stats
+    every path when it identifies it (the reference's fresh fs::metadata,
+    file_identifier/mod.rs:65,80-81).  Files changed between the job's orphan
+    query and the step -- emptied (cas_id None), grown past the 100 KiB
+    sampling threshold, shrunk below it, deleted (ENOENT: the row stays an
+    orphan) -- get the oracle's Objects for their content at that moment."""
+    from spacedrive_amd.file_identifier import FileIdentifierJob
+    t0, loc = _make_library(str(tmp_path), n=400, seed=11)
+    fids = t0.orphans(1)
+    ta = _clone(t0)
+    job = FileIdentifierJob(ta, 1, loc, chunks_per_step=2, ctx=ctx).init()
+    changed = {}
+    for k, f in enumerate(fids[5:45]):
+        p = os.path.join(loc, t0.rel_path(f))
+        if not os.path.exists(p):
+            continue
+        mode = k % 4
+        if mode == 0:
+            open(p, "wb").close()
+        elif mode == 1:
+            with open(p, "wb") as fh:
+                fh.write(O.synth_file_bytes(900 + k, 0, 150_000 + k))
+        elif mode == 2:
+            with open(p, "wb") as fh:
+                fh.write(O.synth_file_bytes(950 + k, 0, 777 + k))
+        else:
+            os.remove(p)
+        changed[f] = mode
+    assert len(set(changed.values())) == 4
+    job.run()
+    job.close()
+    _check_against_oracle(t0, ta, loc, fids)
+    for f, mode in changed.items():
+        if mode == 0:
+            assert ta.cas_id[f - 1] is None and ta.object_id[f - 1] is not None
+        elif mode == 3:
+            assert ta.object_id[f - 1] is None
+
+
+def test_identify_stats_paths_itself(ctx, tmp_path):
+    """identify(paths) with no sizes: sdgpu_identify_files(size = NULL) stats
+    in its read pool -- cas ids equal the oracle's at the current sizes, a
+    missing path is -ENOENT and an empty file has no cas_id."""
+    import errno
+    from spacedrive_amd import file_identifier as fi
+    sizes = [0, 1, 4096, 102_400, 102_401, 250_000]
+    paths = []
+    for i, s in enumerate(sizes):
+        p = tmp_path / f"s{i}"
+        p.write_bytes(O.synth_file_bytes(1200 + i, 0, s))
+        paths.append(str(p))
+    paths.append(str(tmp_path / "missing"))
+    res = fi.identify(paths, ctx=ctx)
+    assert res.sizes is None
+    assert res.status[-1] == -errno.ENOENT and res.has_key[-1] == 0
+    ids = res.cas_ids()
+    for p, s, g in zip(paths, sizes, ids):
+        assert g == (O.cas_id_path(p, s) if s else None)

@@ -1,0 +1,196 @@
+"""GPU: shard.cpp's one-rank-per-process exchange with W > 1 processes
+(VERDICT r5 item 2 / missing 1).
+
+Each rank is its own process on the one GPU, joined through
+sdgpu_comm_init_host (SDGPU_TRANSPORT_HOST, ABI 6: the same messages in the
+same order as the RCCL transport, staged through a shared host mapping,
+because RCCL refuses two ranks on one device).  So every call goes through
+the path `bench.py --gpus N` takes under RCCL: run_call's single-rank branch,
+a padded call left pending and resolved by the next call or Comm.wait()
+(resolve_pending), agreed_n learned by each rank on its own, the overflow
+re-run issued by every rank in the same collective order, the deferred
+-ENOSPC, the layout agreement and the bounded failure when a rank leaves.
+Every result is checked against the oracle's grouping of all rows
+(file_identifier/mod.rs:136-333; O.group_reps / O.link_batch) by this parent
+process; the ranks (tests/_host_rank.py) never import the oracle.
+"""
+import errno
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from spacedrive_amd import dedup
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CASES = ("uniform", "one_key_40k", "all_one_key")
+TOTAL = 300_000
+
+
+def _rows(case, total, seed):
+    rng = np.random.default_rng(seed)
+    if case == "uniform":
+        k, h, _ = O.synth_dedup_rows(seed, total, int(total * 0.8), 0, total)
+        return k, h
+    pool = rng.integers(0, 2**64 - 1, total, dtype=np.uint64, endpoint=True)
+    k = pool[rng.integers(0, pool.size // 2, total)]
+    if case == "one_key_40k":
+        k[rng.choice(total, 40_000, replace=False)] = pool[7]
+    else:
+        k[:] = pool[7]
+    h = (rng.random(total) > 0.01).astype(np.uint8)
+    return k, h
+
+
+def _spans(total, world):  # uneven shares, contiguous, in rank order
+    return np.array([(total * r * (r + 1) // (world * (world + 1)),
+                      total * (r + 1) * (r + 2) // (world * (world + 1))) for r in range(world)],
+                    np.int64)
+
+
+def _run_ranks(work, world, scenarios, timeout_ms=60000):
+    env = dict(os.environ, SD_HOST_TIMEOUT_MS=str(timeout_ms))
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "_host_rank.py"),
+                               ROOT, str(world), str(r), work, ",".join(scenarios)],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+             for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            out, err = p.communicate(timeout=150)
+            assert p.returncode == 0, err[-3000:]
+            outs.append([json.loads(x) for x in out.splitlines() if x.startswith("{")])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return outs  # [rank][scenario] -> dict
+
+
+def _load(work, sc, world):
+    return [dict(np.load(os.path.join(work, f"{sc}_{r}.npz"))) for r in range(world)]
+
+
+def _check_union(parts, ref_link, tag):
+    w = np.concatenate([p[f"{tag}_who"] for p in parts])
+    o = np.concatenate([p[f"{tag}_obj"] for p in parts])
+    c, lr, lo = dedup.split_link_lists(w, o)
+    np.testing.assert_array_equal(c, ref_link[0], err_msg=tag)
+    np.testing.assert_array_equal(lr, ref_link[1], err_msg=tag)
+    np.testing.assert_array_equal(lo, ref_link[2], err_msg=tag)
+
+
+@pytest.fixture(scope="module", params=[2, 3])
+def world_run(request):
+    """All scenarios but the rank exit, one process per rank, W = 2 and 3."""
+    world = request.param
+    work = tempfile.mkdtemp(prefix=f"sd_mp{world}_")
+    data, refs = {}, {}
+    for i, case in enumerate(CASES):
+        k, h = _rows(case, TOTAL, 90 + 7 * world + i)
+        sp = _spans(TOTAL, world)
+        data[f"k_{case}"], data[f"h_{case}"], data[f"span_{case}"] = k, h, sp
+        ref = O.group_reps(k, h, 100)
+        refs[case] = (ref, O.link_batch(ref, None, np.ones(TOTAL, np.uint8), 0))
+        data[f"B_{case}"] = np.int64((sp[:, 1] - sp[:, 0]).max())
+    data["msg_bytes"] = np.int64(16 * world * (TOTAL + 4096))
+    np.savez(os.path.join(work, "data.npz"), **data)
+    scenarios = [f"mix_{c}" for c in CASES] + ["hint_overflow", "nospc", "agree_hint", "agree_mode"]
+    outs = _run_ranks(work, world, scenarios)
+    res = {sc: [outs[r][i] for r in range(world)] for i, sc in enumerate(scenarios)}
+    return world, work, res, refs, data
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_mixed_forms_pending_across_processes(world_run, case):
+    """rep (counted) -> write set (padded, pending) -> rep (padded; resolves
+    the write set) -> write set (padded; resolves the rep call) -> wait: every
+    result equals the oracle, every rank re-ran the same calls."""
+    world, work, res, refs, data = world_run
+    ref, ref_link = refs[case]
+    assert all(r["wait"] == 0 for r in res[f"mix_{case}"]), res[f"mix_{case}"]
+    parts = _load(work, f"mix_{case}", world)
+    for tag in ("r1", "r3"):
+        np.testing.assert_array_equal(np.concatenate([p[tag] for p in parts]).view(np.uint32),
+                                      ref, err_msg=tag)
+    _check_union(parts, ref_link, "l2")
+    _check_union(parts, ref_link, "l4")
+    sts = [r["stats"] for r in res[f"mix_{case}"]]
+    assert all(st["padded_calls"] == 3 for st in sts), sts
+    reruns = {st["overflow_reruns"] for st in sts}
+    assert len(reruns) == 1, sts  # every rank saw the same overflow bits
+    if case == "uniform":
+        assert reruns == {0}
+    else:
+        assert reruns.pop() >= 1
+    assert sum(st["rows_sent"] for st in sts) == sum(st["rows_received"] for st in sts)
+
+
+def test_forced_overflow_rerun_in_order(world_run):
+    """B set to a quarter of the rows on every rank: the first padded call
+    overflows everywhere and is re-run counted when the second call (the
+    other form) resolves it; all three results equal the oracle."""
+    world, work, res, refs, data = world_run
+    ref, ref_link = refs["uniform"]
+    parts = _load(work, "hint_overflow", world)
+    for tag in ("r1", "r3"):
+        np.testing.assert_array_equal(np.concatenate([p[tag] for p in parts]).view(np.uint32),
+                                      ref, err_msg=tag)
+    _check_union(parts, ref_link, "l2")
+    sts = [r["stats"] for r in res["hint_overflow"]]
+    assert all(st["overflow_reruns"] == 1 and st["padded_calls"] == 3 for st in sts), sts
+    assert all(st["agreements"] == 1 for st in sts), sts  # set_exchange -> one agreement round
+
+
+def test_deferred_enospc_reported_once(world_run):
+    """Rank 0's first write set exceeds its capacity: found when the second
+    call resolves the first, reported by the next wait (once, naming call 1);
+    the other ranks and the later calls are unaffected."""
+    world, work, res, refs, data = world_run
+    ref, ref_link = refs["uniform"]
+    rs = res["nospc"]
+    assert rs[0]["wait1"] == -errno.ENOSPC and rs[0]["wait2"] == 0, rs[0]
+    assert rs[0]["stats"]["nospc_call"] == 1
+    for r in rs[1:]:
+        assert r["wait1"] == 0 and r["wait2"] == 0 and r["stats"]["nospc_call"] == 0, r
+    parts = _load(work, "nospc", world)
+    _check_union(parts, ref_link, "l2")
+    _check_union(parts, ref_link, "l3")
+
+
+@pytest.mark.parametrize("sc", ["agree_hint", "agree_mode"])
+def test_layout_disagreement_is_eproto(world_run, sc):
+    """Ranks that set different rows_hint, or counted against padded, fail
+    with -EPROTO on every rank before any record moves, and the
+    aborted communicator refuses the next call."""
+    world, work, res, refs, data = world_run
+    for r in res[sc]:
+        assert r["rc1"] == -errno.EPROTO and r["rc2"] == -errno.ECONNABORTED, r
+
+
+def test_rank_exit_times_out_the_others():
+    """Rank 1 leaves after one call: rank 0's next call fails with
+    -ETIMEDOUT within the communicator's 3 s timeout (no hang), the one
+    after with -ECONNABORTED; the good call equals the oracle."""
+    world = 2
+    work = tempfile.mkdtemp(prefix="sd_mpx_")
+    k, h = _rows("uniform", 100_000, 5)
+    sp = _spans(100_000, world)
+    np.savez(os.path.join(work, "data.npz"), k_uniform=k, h_uniform=h, span_uniform=sp,
+             B_uniform=np.int64((sp[:, 1] - sp[:, 0]).max()),
+             msg_bytes=np.int64(16 * world * 110_000))
+    outs = _run_ranks(work, world, ["exit"], timeout_ms=3000)
+    r0 = outs[0][0]
+    assert r0["rc2"] == -errno.ETIMEDOUT, r0
+    assert 2.5 < r0["s2"] < 60, r0
+    assert r0["rc3"] == -errno.ECONNABORTED, r0
+    parts = _load(work, "exit", world)
+    np.testing.assert_array_equal(np.concatenate([p["r1"] for p in parts]).view(np.uint32),
+                                  O.group_reps(k, h, 100))

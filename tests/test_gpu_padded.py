@@ -184,6 +184,46 @@ def test_padded_one_rank_rccl_rep_form(ctx):
     comm.close()
 
 
+def test_overflow_rerun_then_next_call_on_another_stream(ctx):
+    """a padded call that overflowed is re-run (counted) on
+    ITS stream when the next call resolves it; a next call issued on another
+    stream must be ordered after that re-run (they share the exchange
+    buffers and the communicator).  Both results equal the oracle, for the
+    rep form and the write-set form."""
+    import torch
+    from spacedrive_amd import dedup
+    comm = dedup.Comm.init_rank(ctx, 1, 0, dedup.Comm.unique_id())
+    n = 600_000
+    k, h, rk = O.synth_dedup_rows(83, n, 480_000, 0, n)
+    dk = torch.from_numpy(k.view(np.int64)).cuda()
+    dh = torch.from_numpy(h).cuda()
+    dr = torch.from_numpy(rk.view(np.int32)).cuda()
+    dv = torch.ones(n, dtype=torch.uint8, device="cuda")
+    ref = O.group_reps(k, h, 100)
+    rc, rlr, rlo = O.link_batch(ref, None, None, 0)
+    other = torch.cuda.Stream()
+    for _ in range(2):
+        comm.set_exchange(dedup.EXCHANGE_PADDED, n // 3)  # B below the rows: overflow
+        s0 = comm.stats()
+        r1 = dedup.group_sharded(dk, dh, dr, comm, None, 100, wait=False)
+        other.wait_stream(torch.cuda.current_stream())  # the inputs are ready
+        with torch.cuda.stream(other):
+            who, obj, cnt = dedup.group_link_sharded(dk, dh, dv, dr, comm, 100, trim=False)
+            r3 = dedup.group_sharded(dk, dh, dr, comm, None, 100, wait=False)
+        comm.wait()
+        torch.cuda.synchronize()
+        d = {x: comm.stats()[x] - s0[x] for x in s0}
+        assert d["overflow_reruns"] == 1 and d["padded_calls"] == 3, d
+        np.testing.assert_array_equal(r1.cpu().numpy().view(np.uint32), ref)
+        np.testing.assert_array_equal(r3.cpu().numpy().view(np.uint32), ref)
+        c, l, e = (int(x) for x in cnt.cpu().tolist())
+        fc, flr, flo = dedup.split_link_lists(who[:e].cpu().numpy(), obj[:e].cpu().numpy())
+        np.testing.assert_array_equal(fc, rc)
+        np.testing.assert_array_equal(flr, rlr)
+        np.testing.assert_array_equal(flo, rlo)
+    comm.close()
+
+
 @pytest.mark.parametrize("shares", [(0, 5, 120_000), (60_000, 0, 0), (1, 0, 90_000, 7)])
 def test_padded_empty_and_tiny_ranks(ctxs, shares):
     """Ragged padded calls: ranks holding no rows or a handful send only
