@@ -153,12 +153,15 @@ class Runner:
         self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(self.local)
         self.dev = torch.device("cuda", self.local)
-        backend = os.environ.get("SD_BENCH_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        # nccl = RCCL over xGMI; host = the one-GPU rehearsal of libsdgpu's
+        # per-process exchange (SDGPU_TRANSPORT_HOST, ranks sharing the card,
+        # torch.distributed over gloo); gloo = the Python exchange (rehearsal)
+        backend = os.environ.get("SD_BENCH_BACKEND", "nccl")
         if self.world > 1:
             if backend == "nccl":
                 dist.init_process_group("nccl", device_id=self.dev)
             else:
-                dist.init_process_group(backend)
+                dist.init_process_group("gloo" if backend == "host" else backend)
         from spacedrive_amd import dedup
         from spacedrive_amd._native import default_context
         self.ctx = default_context(self.local)
@@ -175,6 +178,17 @@ class Runner:
         if force:
             self.backend = "nccl (one-rank rehearsal)"
             self.comm = dedup.Comm.init_rank(self.ctx, 1, 0, dedup.Comm.unique_id(),
+                                             timeout_ms=self.comm_timeout_ms)
+        if self.world > 1 and backend == "host":
+            # the same libsdgpu calls as under RCCL (sdgpu_group_link_sharded_
+            # device ...), their messages staged through a shared file: the
+            # N > 1 path of this bench rehearsed on a one-GPU box
+            import tempfile
+            obj = [tempfile.mktemp(prefix="sd_bench_comm_") if self.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            rows = max(args.files, args.dedup_rows, args.staged_files)
+            self.comm = dedup.Comm.init_host(self.ctx, self.world, self.rank, obj[0],
+                                             msg_bytes=16 * rows + (1 << 20),
                                              timeout_ms=self.comm_timeout_ms)
         if self.world > 1 and backend == "nccl":
             # the grouping's exchange runs INSIDE libsdgpu over RCCL (what the
@@ -236,6 +250,8 @@ class Runner:
             self.dist.destroy_process_group()
 
     def exchange_name(self) -> str:
+        if self.comm is not None and self.backend == "host":
+            return "libsdgpu host-staged all-to-all (SDGPU_TRANSPORT_HOST rehearsal, one GPU)"
         if self.comm is not None:
             return "libsdgpu RCCL all-to-all (sdgpu_group_sharded_device)"
         if self.world == 1:
