@@ -1,10 +1,10 @@
-# Round-5 checkpoint on one box: the whole GPU test suite,
+# Round checkpoint on one box: the whole GPU test suite,
 # smoke, then the driver's exact bench command (wall-clocked).
-#   TAG=r5x bash scripts/gpu_r5_full.sh
+#   TAG=r6x bash scripts/gpu_full.sh
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests \
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests \
   > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?
 tail -3 gpurun_out/${TAG}_pytest.log

@@ -87,9 +87,9 @@ def _check_union(parts, ref_link, tag):
     np.testing.assert_array_equal(lo, ref_link[2], err_msg=tag)
 
 
-@pytest.fixture(scope="module", params=[2, 3])
+@pytest.fixture(scope="module", params=[2, 3, 4])
 def world_run(request):
-    """All scenarios but the rank exit, one process per rank, W = 2 and 3."""
+    """All scenarios but the rank exit, one process per rank, W = 2, 3 and 4."""
     world = request.param
     work = tempfile.mkdtemp(prefix=f"sd_mp{world}_")
     data, refs = {}, {}
