@@ -351,7 +351,8 @@ int sdgpu_comm_wait(sdgpu_comm *comm, void *stream);
  * sets B when > 0).  The _all entry points (one process, all ranks) resolve
  * a padded call before they return.
  * Agreement (ABI 6): a communicator's first call and its first call after
- * sdgpu_comm_set_exchange / sdgpu_comm_set_return check that every rank
+ * sdgpu_comm_set_exchange / sdgpu_comm_set_return (which every rank must
+ * call alike, between the same two exchange calls) check that every rank
  * chose the same layout -- a counted call through the code in its count
  * messages (form, return mode, exchange mode), a padded call through one
  * 24-byte agreement message per peer {slots per message, B, code} of the
