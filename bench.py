@@ -572,7 +572,9 @@ class Runner:
                                        f"({nsteps} steps x {n} files/GPU x {W} GPU), windows in "
                                        "pinned host memory, staged H2D (3-slab ring) + K1 + "
                                        "grouping against the run's Object index "
-                                       + ("(sharded, RCCL) + Object link batch"
+                                       + (("(sharded, host-transport rehearsal) + Object link batch"
+                                           if self.backend == "host" else
+                                           "(sharded, RCCL) + Object link batch")
                                           if self.comm is not None else
                                           "+ Object write set in one pass (one GPU)" if W == 1
                                           else "(no index: rehearsal) + Object link batch"),
