@@ -175,6 +175,39 @@ def test_layout_disagreement_is_eproto(world_run, sc):
         assert r["rc1"] == -errno.EPROTO and r["rc2"] == -errno.ECONNABORTED, r
 
 
+def test_eight_processes_padded_and_overflow():
+    """The N = 8 shape of the driver's scaling run, as 8 processes on the one
+    GPU (the box allows 16 GPU processes): a counted call, padded calls of
+    both forms left pending and resolved across the processes, then a forced
+    overflow re-run in the same order on all 8 ranks -- every result equal
+    to the oracle."""
+    world = 8
+    work = tempfile.mkdtemp(prefix="sd_mp8_")
+    total = 240_000
+    k, h = _rows("uniform", total, 8)
+    sp = _spans(total, world)
+    np.savez(os.path.join(work, "data.npz"), k_uniform=k, h_uniform=h, span_uniform=sp,
+             B_uniform=np.int64((sp[:, 1] - sp[:, 0]).max()),
+             msg_bytes=np.int64(16 * world * (total + 4096)))
+    outs = _run_ranks(work, world, ["mix_uniform", "hint_overflow"])
+    ref = O.group_reps(k, h, 100)
+    ref_link = O.link_batch(ref, None, np.ones(total, np.uint8), 0)
+    assert all(o[0]["wait"] == 0 for o in outs), [o[0] for o in outs]
+    parts = _load(work, "mix_uniform", world)
+    for tag in ("r1", "r3"):
+        np.testing.assert_array_equal(np.concatenate([p[tag] for p in parts]).view(np.uint32),
+                                      ref, err_msg=tag)
+    _check_union(parts, ref_link, "l2")
+    _check_union(parts, ref_link, "l4")
+    parts = _load(work, "hint_overflow", world)
+    for tag in ("r1", "r3"):
+        np.testing.assert_array_equal(np.concatenate([p[tag] for p in parts]).view(np.uint32),
+                                      ref, err_msg=tag)
+    _check_union(parts, ref_link, "l2")
+    sts = [o[1]["stats"] for o in outs]
+    assert all(st["overflow_reruns"] == 1 and st["padded_calls"] == 3 for st in sts), sts
+
+
 def test_rank_exit_times_out_the_others():
     """Rank 1 leaves after one call: rank 0's next call fails with
     -ETIMEDOUT within the communicator's 3 s timeout (no hang), the one
