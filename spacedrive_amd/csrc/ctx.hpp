@@ -4,6 +4,7 @@
 #pragma once
 
 #include <errno.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <mutex>
@@ -235,6 +236,12 @@ inline int ensure_dev(sdgpu_ctx* c, DevBuf& b, size_t bytes) {
   const size_t want = align_up(std::max<size_t>(bytes, 1), size_t(1) << 20);
   SD_TRY(hipMalloc(&b.p, want));
   b.cap = want;
+  // SDGPU_POISON_WS=1 (tests only): a new workspace is filled with 0xA5
+  // bytes, so a kernel that reads a word no earlier kernel of the call wrote
+  // sees garbage rather than a fresh allocation's zeros or the previous
+  // call's values (round 6: the class of the SDGPU_SEG_GROUPS fault)
+  static const bool poison = std::getenv("SDGPU_POISON_WS") && std::getenv("SDGPU_POISON_WS")[0] == '1';
+  if (poison) SD_TRY(hipMemset(b.p, 0xA5, want));
   return 0;
 }
 
