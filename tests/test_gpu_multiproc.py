@@ -175,6 +175,34 @@ def test_layout_disagreement_is_eproto(world_run, sc):
         assert r["rc1"] == -errno.EPROTO and r["rc2"] == -errno.ECONNABORTED, r
 
 
+@pytest.mark.parametrize("shares", [(0, 5, 120_000), (60_000, 0, 0, 1)])
+def test_empty_and_tiny_ranks_across_processes(shares):
+    """Ragged worlds over the per-process path: a rank with no rows or a
+    handful still sends headers and padding and receives its owned rows;
+    the mixed counted / padded sequence equals the oracle (as
+    test_gpu_padded.py's _all form does in one process)."""
+    world, total = len(shares), sum(shares)
+    work = tempfile.mkdtemp(prefix="sd_mpr_")
+    k, h = _rows("uniform", total, 31 + world)
+    b = np.concatenate([[0], np.cumsum(shares)]).astype(np.int64)
+    sp = np.stack([b[:-1], b[1:]], axis=1)
+    np.savez(os.path.join(work, "data.npz"), k_uniform=k, h_uniform=h, span_uniform=sp,
+             B_uniform=np.int64(max(shares)), msg_bytes=np.int64(16 * world * (total + 4096)))
+    outs = _run_ranks(work, world, ["mix_uniform"])
+    assert all(o[0]["wait"] == 0 for o in outs), [o[0] for o in outs]
+    ref = O.group_reps(k, h, 100)
+    ref_link = O.link_batch(ref, None, np.ones(total, np.uint8), 0)
+    parts = _load(work, "mix_uniform", world)
+    for tag in ("r1", "r3"):
+        np.testing.assert_array_equal(np.concatenate([p[tag] for p in parts]).view(np.uint32),
+                                      ref, err_msg=tag)
+    _check_union(parts, ref_link, "l2")
+    _check_union(parts, ref_link, "l4")
+    sts = [o[0]["stats"] for o in outs]
+    assert all(st["padded_calls"] == 3 for st in sts), sts
+    assert len({st["overflow_reruns"] for st in sts}) == 1, sts
+
+
 def test_eight_processes_padded_and_overflow():
     """The N = 8 shape of the driver's scaling run, as 8 processes on the one
     GPU (the box allows 16 GPU processes): a counted call, padded calls of
