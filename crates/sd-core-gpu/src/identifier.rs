@@ -13,7 +13,7 @@
 //! rep[i] & SDGPU_REP_EXISTING: connect to the existing Object `rep & 0x7fff_ffff`;
 //! otherwise connect to the Object created for the row of rank rep[i].
 
-use std::{io, os::raw::c_char, path::PathBuf, ptr};
+use std::{io, marker::PhantomData, os::raw::c_char, path::PathBuf, ptr};
 
 use sdgpu_sys as sys;
 
@@ -36,25 +36,27 @@ pub struct IdentifiedRow {
     pub link: Link,
 }
 
-/// The library-wide Object index of one job (mod.rs:168-185).
-pub struct ObjectIndex(*mut sys::sdgpu_index);
-unsafe impl Send for ObjectIndex {}
+/// The library-wide Object index of one job (mod.rs:168-185).  It borrows
+/// its `Gpu`: sdgpu_close frees what the index points into, so the index
+/// must be dropped first (include/sdgpu.h, sdgpu_close).
+pub struct ObjectIndex<'g>(*mut sys::sdgpu_index, PhantomData<&'g Gpu>);
+unsafe impl Send for ObjectIndex<'_> {}
 
-impl ObjectIndex {
-    pub fn new(gpu: &Gpu, capacity: u64) -> io::Result<Self> {
+impl<'g> ObjectIndex<'g> {
+    pub fn new(gpu: &'g Gpu, capacity: u64) -> io::Result<Self> {
         let mut idx = ptr::null_mut();
         check(unsafe { sys::sdgpu_index_create(*gpu.ctx(), capacity, &mut idx) })?;
-        Ok(ObjectIndex(idx))
+        Ok(ObjectIndex(idx, PhantomData))
     }
 }
 
-impl Drop for ObjectIndex {
+impl Drop for ObjectIndex<'_> {
     fn drop(&mut self) {
         unsafe { sys::sdgpu_index_destroy(self.0) };
     }
 }
 
-impl ObjectIndex {
+impl ObjectIndex<'_> {
     /// Objects that exist before the job (mod.rs:168-185): key -> object id.
     pub fn add_objects(&self, gpu: &Gpu, keys: &[u64], ids: &[u32]) -> io::Result<()> {
         if keys.is_empty() {
@@ -111,7 +113,7 @@ pub fn identify(gpu: &Gpu, paths: &[PathBuf], sizes: Option<&[u64]>) -> io::Resu
 
 /// The grouping of one batch of identified rows against the index (rows in
 /// id order, ranks first_rank + i); rows whose read failed take no part.
-pub fn group(gpu: &Gpu, idx: &ObjectIndex, rows: &Identified, first_rank: u32) -> io::Result<Vec<IdentifiedRow>> {
+pub fn group(gpu: &Gpu, idx: &ObjectIndex<'_>, rows: &Identified, first_rank: u32) -> io::Result<Vec<IdentifiedRow>> {
     let n = rows.cas8.len();
     let mut rep = vec![0u32; n];
     let grouped: Vec<u8> =
@@ -145,7 +147,7 @@ pub fn group(gpu: &Gpu, idx: &ObjectIndex, rows: &Identified, first_rank: u32) -
 
 /// One job step over `paths` (rows in id order; `sizes` from fs::metadata,
 /// mod.rs:65) whose first row has rank `first_rank`.
-pub fn identify_step(gpu: &Gpu, idx: &ObjectIndex, paths: &[PathBuf], sizes: Option<&[u64]>,
+pub fn identify_step(gpu: &Gpu, idx: &ObjectIndex<'_>, paths: &[PathBuf], sizes: Option<&[u64]>,
                      first_rank: u32) -> io::Result<Vec<IdentifiedRow>> {
     let rows = identify(gpu, paths, sizes)?;
     group(gpu, idx, &rows, first_rank)

@@ -91,7 +91,7 @@ pub struct JobState {
 pub struct FileIdentifierJob<'a, T: OrphanTable> {
     gpu: &'a Gpu,
     table: T,
-    index: ObjectIndex,
+    index: ObjectIndex<'a>,
     pub state: JobState,
     /// rank -> Object id of the Objects created by this run (linked rows of a
     /// later step name their Object by the creator row's rank)

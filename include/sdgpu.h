@@ -60,6 +60,8 @@ const char *sdgpu_strerror(int rc);
 /* ---- context / memory ------------------------------------------------------ */
 int sdgpu_device_count(int *count);
 int sdgpu_open(int device, sdgpu_ctx **out);
+/* Frees the context.  Destroy its indexes (sdgpu_index_destroy) and
+ * communicators (sdgpu_comm_destroy) first: they point into it. */
 int sdgpu_close(sdgpu_ctx *ctx);
 /* Waits for all work issued through ctx (its stream and the last stream
  * passed to a _device call). */

@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 import re
+import weakref
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsdgpu.so")
@@ -163,9 +164,19 @@ class Context:
         check(self.lib.sdgpu_open(device, ctypes.byref(h)), f"sdgpu_open({device})")
         self.h = h
         self.device = device
+        # indexes and communicators made on this context: sdgpu_close frees
+        # what they point into, so close() destroys them first (a handle
+        # outliving its context would otherwise be destroyed after it)
+        self._deps = weakref.WeakSet()
+
+    def adopt(self, obj):
+        """Registers an object with a close() that must run before sdgpu_close."""
+        self._deps.add(obj)
 
     def close(self):
         if self.h:
+            for d in list(self._deps):
+                d.close()
             self.lib.sdgpu_close(self.h)
             self.h = None
 

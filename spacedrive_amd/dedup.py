@@ -212,6 +212,7 @@ class ObjectIndex:
         check(self.ctx.lib.sdgpu_index_create(self.ctx.h, capacity, ctypes.byref(h)),
               "sdgpu_index_create")
         self.h = h
+        self.ctx.adopt(self)
 
     def close(self):
         if self.h:
@@ -296,6 +297,7 @@ class Comm:
     def __init__(self, ctx, handle):
         self.ctx, self.h = ctx, handle
         self._hold = None  # an unresolved padded call's tensors (_held)
+        ctx.adopt(self)
 
     @staticmethod
     def unique_id() -> bytes:

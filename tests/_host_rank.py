@@ -103,6 +103,31 @@ def main():
                 calls[-1]["stats"] = comm.stats()
             res["calls"] = calls
             comm.close()
+        elif sc.startswith("index_"):
+            # batches through per-rank shares of the Object index, with
+            # pre-existing Objects; the second batch overflows (a key 40 k
+            # times): its creators must reach the index only through the
+            # counted re-run, which every process issues in the same order
+            ret = dedup.RETURN_FULL if sc == "index_full" else dedup.RETURN_COMPACT
+            k, h = data["k_index"], data["h_index"]
+            batch, total = int(data["batch"]), int(data["k_index"].size)
+            comm = comm_for(sc)
+            comm.set_return(ret)
+            comm.set_exchange(dedup.EXCHANGE_AUTO, batch // world + 1)
+            idx = dedup.ObjectIndex(ctx, 1000)
+            dev = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()  # noqa: E731
+            idx.add_objects(dev(data["ek"].view(np.int64)), dev(data["eh"].view(np.int32)), world, rank)
+            pos, reps = [], []
+            for b0 in range(0, total, batch):
+                a, b = b0 + batch * rank // world, b0 + batch * (rank + 1) // world
+                rep = dedup.group_sharded(dev(k[a:b].view(np.int64)), dev(h[a:b]),
+                                          torch.arange(a, b, dtype=torch.int64).to(torch.int32).cuda(),
+                                          comm, idx, 100)
+                pos.append(np.arange(a, b))
+                reps.append(rep.cpu().numpy())
+            save["pos"], save["rep"] = np.concatenate(pos), np.concatenate(reps)
+            res["stats"] = comm.stats()
+            comm.close()
         elif sc == "hint_overflow":
             # B set below the rows: the first padded call overflows on every
             # rank and is re-run counted when the next call resolves it

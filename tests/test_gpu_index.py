@@ -146,3 +146,20 @@ def test_two_level_batch_through_index(ctx):
                     torch.from_numpy(eh.view(np.int32)).cuda())
     rep = _run_batches(ctx, key, has, [0, 500_000, n], 100, idx)
     np.testing.assert_array_equal(rep, O.group_reps_existing(key, has, 100, ek, eh))
+
+
+def test_context_close_destroys_its_index_and_comm_first():
+    """A Python index or communicator that outlives Context.close() (e.g. a
+    local still alive when the context is closed) used to be destroyed after
+    sdgpu_close, reading the freed context: Context.close() now destroys its
+    indexes and communicators first (include/sdgpu.h, sdgpu_close)."""
+    import gc
+    from spacedrive_amd import dedup
+    from spacedrive_amd._native import Context
+    c = Context(0)
+    idx = dedup.ObjectIndex(c, 1000)
+    comm = dedup.Comm.init_rank(c, 1, 0, dedup.Comm.unique_id())
+    c.close()
+    assert idx.h is None and comm.h is None
+    del idx, comm
+    gc.collect()

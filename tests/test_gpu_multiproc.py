@@ -56,17 +56,21 @@ def _spans(total, world):  # uneven shares, contiguous, in rank order
 
 
 def _run_ranks(work, world, scenarios, timeout_ms=60000):
-    env = dict(os.environ, SD_HOST_TIMEOUT_MS=str(timeout_ms))
+    # PYTHONFAULTHANDLER: a rank that dies on a signal names its Python frame
+    env = dict(os.environ, SD_HOST_TIMEOUT_MS=str(timeout_ms), PYTHONFAULTHANDLER="1")
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "_host_rank.py"),
                                ROOT, str(world), str(r), work, ",".join(scenarios)],
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
              for r in range(world)]
     outs = []
     try:
-        for p in procs:
+        errs = []
+        for r, p in enumerate(procs):
             out, err = p.communicate(timeout=150)
-            assert p.returncode == 0, err[-3000:]
+            if p.returncode != 0:
+                errs.append(f"rank {r} rc {p.returncode}: {err[-2500:]}")
             outs.append([json.loads(x) for x in out.splitlines() if x.startswith("{")])
+        assert not errs, "\n".join(errs)
     finally:
         for p in procs:
             if p.poll() is None:
@@ -173,6 +177,40 @@ def test_layout_disagreement_is_eproto(world_run, sc):
     world, work, res, refs, data = world_run
     for r in res[sc]:
         assert r["rc1"] == -errno.EPROTO and r["rc2"] == -errno.ECONNABORTED, r
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_object_index_batches_with_overflow_across_processes(world):
+    """Per-rank shares of the Object index over three batches, pre-existing
+    Objects (one with handle 0x7FFFFFFF), the second batch
+    overflowing (a key 40 k times) and re-run counted by every process; full
+    and compact return legs.  The reps equal the oracle's grouping with the
+    library's existing Objects (file_identifier/mod.rs:168-241)."""
+    work = tempfile.mkdtemp(prefix="sd_mpi_")
+    total, batch = 450_000, 150_000
+    k, h, _ = O.synth_dedup_rows(61 + world, total, 280_000, 0, total)
+    rng = np.random.default_rng(world)
+    k[batch + rng.choice(batch, 40_000, replace=False)] = k[5]
+    ek = rng.choice(k, 1500)
+    ek[0] = k[5]
+    eh = np.arange(ek.size, dtype=np.uint32) + 3
+    eh[0] = 0x7FFFFFFF
+    ref = O.group_reps_existing(k, h, 100, ek, eh)
+    np.savez(os.path.join(work, "data.npz"), k_index=k, h_index=h, ek=ek, eh=eh,
+             batch=np.int64(batch), msg_bytes=np.int64(16 * world * (batch + 4096)))
+    outs = _run_ranks(work, world, ["index_full", "index_compact"])
+    for i, sc in enumerate(("index_full", "index_compact")):
+        out = np.zeros(total, np.uint32)
+        for p in _load(work, sc, world):
+            out[p["pos"]] = p["rep"].view(np.uint32)
+        bad = np.flatnonzero(out != ref)
+        assert bad.size == 0, (sc, bad.size, bad[:5], out[bad[:5]], ref[bad[:5]])
+        sts = [o[i]["stats"] for o in outs]
+        assert len({st["overflow_reruns"] for st in sts}) == 1, sts
+        if sc == "index_full":
+            assert all(st["padded_calls"] == 3 and st["overflow_reruns"] == 1 for st in sts), sts
+        else:  # compact return leg: counted exchange only
+            assert all(st["padded_calls"] == 0 for st in sts), sts
 
 
 @pytest.mark.parametrize("shares", [(0, 5, 120_000), (60_000, 0, 0, 1)])
