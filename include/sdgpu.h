@@ -123,7 +123,8 @@ int sdgpu_generate_cas_id(sdgpu_ctx *ctx, const char *path, uint64_t size, char 
  * and has_key 0 (row dropped, mod.rs:113,127).  has_key may be NULL.
  * size may be NULL (ABI 6): every path is stat-ed by the read pool first --
  * the reference's fresh fs::metadata(path).len() at identification time, not
- * a size stored with the row; a failed stat is status -errno. */
+ * a size stored with the row; a failed stat is status -errno, a directory
+ * -EISDIR (the reference asserts the path is not one, mod.rs:69-72). */
 int sdgpu_identify_files(sdgpu_ctx *ctx, const char *const *paths, const uint64_t *size,
                          uint32_t n, uint8_t (*out8)[8], uint8_t *has_key, int32_t *status);
 

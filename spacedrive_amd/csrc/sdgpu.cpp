@@ -574,7 +574,9 @@ int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t*
   // size NULL (ABI 6): the fresh fs::metadata(path).len() of the reference
   // (file_identifier/mod.rs:65,80-81), stat-ed here by the read pool; a path
   // whose stat fails gets status -errno and no key (the row is dropped,
-  // mod.rs:113,127)
+  // mod.rs:113,127).  A directory gets -EISDIR (the reference asserts it is
+  // not one, mod.rs:69-72), also when its st_size is 0 -- it is not an
+  // empty file
   std::vector<uint64_t> fresh;
   std::vector<int32_t> stat_rc;
   if (!size_in && n) {
@@ -583,6 +585,7 @@ int sdgpu_identify_files(sdgpu_ctx* c, const char* const* paths, const uint64_t*
     parallel_for(n, [&](uint32_t i) {
       struct stat st;
       if (stat(paths[i], &st) != 0) stat_rc[i] = -errno;
+      else if (S_ISDIR(st.st_mode)) stat_rc[i] = -EISDIR;
       else fresh[i] = static_cast<uint64_t>(st.st_size);
     });
   }

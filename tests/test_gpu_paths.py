@@ -124,3 +124,19 @@ def test_checksum_files_batched_validator(ctx, tmp_path):
     assert job[paths[5]] == O.file_checksum_path(paths[5])
     with pytest.raises(OSError):
         validation.validator_job(paths, ctx)
+
+
+def test_identify_fresh_sizes_directory_is_an_error(ctx, files, tmp_path):
+    """With sizes stat-ed by the library (size NULL), a directory is -EISDIR
+    with no key -- also an empty one, whatever st_size the filesystem gives
+    it -- never an empty file's cas_id None with status 0 (the reference
+    asserts the path is not a directory, file_identifier/mod.rs:69-72)."""
+    from spacedrive_amd import file_identifier as fi
+    empty_dir = tmp_path / "empty_dir"
+    empty_dir.mkdir()
+    paths = [files[3], str(tmp_path), str(empty_dir), files[0]]
+    res = fi.identify(paths, ctx=ctx)
+    assert list(res.status) == [0, -21, -21, 0], res.status
+    assert list(res.has_key) == [1, 0, 0, 0]
+    assert bytes(res.cas8[0]).hex() == O.cas_id_path(files[3], SIZES[3])
+    assert not res.cas8[1:].any()
