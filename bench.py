@@ -184,7 +184,10 @@ class Runner:
             # device ...), their messages staged through a shared file: the
             # N > 1 path of this bench rehearsed on a one-GPU box
             import tempfile
-            obj = [tempfile.mktemp(prefix="sd_bench_comm_") if self.rank == 0 else None]
+            # a fresh private directory (not mktemp's race-prone name); the
+            # file inside is created by the first rank to join
+            obj = [os.path.join(tempfile.mkdtemp(prefix="sd_bench_comm_"), "comm")
+                   if self.rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             rows = max(args.files, args.dedup_rows, args.staged_files)
             self.comm = dedup.Comm.init_host(self.ctx, self.world, self.rank, obj[0],
