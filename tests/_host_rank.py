@@ -128,6 +128,53 @@ def main():
             save["pos"], save["rep"] = np.concatenate(pos), np.concatenate(reps)
             res["stats"] = comm.stats()
             comm.close()
+        elif sc.startswith("fuzz_"):
+            # a random sequence of exchange calls, the same on every rank (a
+            # shared seed): rep / write-set forms, resolved at once or left
+            # pending, layouts and return legs changed between calls (padded
+            # with a hint of a quarter / one / two times the rows, auto,
+            # counted; full / compact / auto return), on the three key cases
+            rng = np.random.default_rng(int(sc[5:]))
+            cases = [str(c) for c in data["cases"]]
+            comm = comm_for(sc)
+            held, ops = [], []
+            for i in range(int(data["fuzz_ops"])):
+                u = rng.random()
+                if u < 0.15:
+                    mode = int(rng.choice([dedup.EXCHANGE_PADDED, dedup.EXCHANGE_AUTO,
+                                           dedup.EXCHANGE_COUNTED]))
+                    B = int(data[f"B_{cases[int(rng.integers(len(cases)))]}"])
+                    hint = int(rng.choice([max(1, B // 4), B, 2 * B]))
+                    comm.set_exchange(mode, hint)
+                    ops.append(["exchange", mode, hint])
+                    continue
+                if u < 0.25:
+                    ret = int(rng.choice([dedup.RETURN_FULL, dedup.RETURN_COMPACT, dedup.RETURN_AUTO]))
+                    comm.set_return(ret)
+                    ops.append(["return", ret])
+                    continue
+                case = cases[int(rng.integers(len(cases)))]
+                form = "rep" if rng.random() < 0.5 else "list"
+                wait = bool(rng.random() < 0.4)
+                key, has, val, rk, n = rows(case)
+                if form == "rep":
+                    out = dedup.group_sharded(key, has, rk, comm, None, 100, wait=wait)
+                else:
+                    cap = int(data[f"k_{case}"].size) + n
+                    out = dedup.group_link_sharded(key, has, val, rk, comm, 100, cap=cap, trim=False)
+                    if wait:
+                        comm.wait()
+                held.append((i, form, out))
+                ops.append([form, case, int(wait), i])
+            res["wait"] = rc_of(comm.wait)
+            for i, form, out in held:  # every call is resolved now
+                if form == "rep":
+                    save[f"op{i}_rep"] = out.cpu().numpy()
+                else:
+                    save[f"op{i}_who"], save[f"op{i}_obj"] = lists(out)
+            res["ops"] = ops
+            res["stats"] = comm.stats()
+            comm.close()
         elif sc == "hint_overflow":
             # B set below the rows: the first padded call overflows on every
             # rank and is re-run counted when the next call resolves it

@@ -179,6 +179,55 @@ def test_layout_disagreement_is_eproto(world_run, sc):
         assert r["rc1"] == -errno.EPROTO and r["rc2"] == -errno.ECONNABORTED, r
 
 
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_random_call_sequences_across_processes(world):
+    """Seeded random sequences of exchange calls, the same on every rank:
+    rep and write-set forms, resolved at once or left pending for the next
+    call, exchange layouts (padded with a hint of 1/4, 1 or 2 times the rows,
+    auto, counted) and return legs changed between calls, over uniform keys,
+    one key 40 k times and all one key.  Every call's result equals the
+    oracle's grouping of all rows (file_identifier/mod.rs:136-333), and every
+    rank re-ran the same overflowed calls."""
+    work = tempfile.mkdtemp(prefix=f"sd_mpf{world}_")
+    data, refs = {}, {}
+    for i, case in enumerate(CASES):
+        k, h = _rows(case, TOTAL, 300 + 7 * world + i)
+        sp = _spans(TOTAL, world)
+        data[f"k_{case}"], data[f"h_{case}"], data[f"span_{case}"] = k, h, sp
+        data[f"B_{case}"] = np.int64((sp[:, 1] - sp[:, 0]).max())
+        ref = O.group_reps(k, h, 100)
+        refs[case] = (ref, O.link_batch(ref, None, np.ones(TOTAL, np.uint8), 0))
+    data["cases"] = np.array(CASES)
+    data["fuzz_ops"] = np.int64(20)
+    data["msg_bytes"] = np.int64(16 * world * (TOTAL + 4096))
+    np.savez(os.path.join(work, "data.npz"), **data)
+    seeds = [f"fuzz_{world * 100 + s}" for s in range(5)]
+    outs = _run_ranks(work, world, seeds)
+    calls = reruns = padded = 0
+    for j, sc in enumerate(seeds):
+        rs = [outs[r][j] for r in range(world)]
+        assert all(r["wait"] == 0 for r in rs), rs
+        assert all(r["ops"] == rs[0]["ops"] for r in rs)
+        assert len({r["stats"]["overflow_reruns"] for r in rs}) == 1, [r["stats"] for r in rs]
+        parts = _load(work, sc, world)
+        for op in rs[0]["ops"]:
+            if op[0] not in ("rep", "list"):
+                continue
+            form, case, _, i = op
+            ref, ref_link = refs[case]
+            if form == "rep":
+                np.testing.assert_array_equal(
+                    np.concatenate([p[f"op{i}_rep"] for p in parts]).view(np.uint32), ref,
+                    err_msg=f"{sc} op {i} {case}")
+            else:
+                _check_union(parts, ref_link, f"op{i}")
+            calls += 1
+        reruns += rs[0]["stats"]["overflow_reruns"]
+        padded += rs[0]["stats"]["padded_calls"]
+    # the sequences reached the paths they are for
+    assert calls >= 40 and padded >= 10 and reruns >= 2, (calls, padded, reruns)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_object_index_batches_with_overflow_across_processes(world):
     """Per-rank shares of the Object index over three batches, pre-existing
