@@ -140,3 +140,45 @@ def test_identify_fresh_sizes_directory_is_an_error(ctx, files, tmp_path):
     assert list(res.has_key) == [1, 0, 0, 0]
     assert bytes(res.cas8[0]).hex() == O.cas_id_path(files[3], SIZES[3])
     assert not res.cas8[1:].any()
+
+
+_IO_CHILD = r'''
+import json, sys
+sys.path.insert(0, sys.argv[1])
+from spacedrive_amd import file_identifier as fi
+from spacedrive_amd._native import Context
+paths = json.loads(sys.argv[2])
+ctx = Context(0)
+res = fi.identify(paths, ctx=ctx)
+print(json.dumps({"cas": [bytes(c).hex() for c in res.cas8], "status": [int(s) for s in res.status],
+                  "has": [int(h) for h in res.has_key]}))
+'''
+
+
+@pytest.mark.parametrize("io", ["pread", "uring", "bounce"])
+def test_identify_read_paths_agree(io, files, tmp_path):
+    """The three staging readers of sdgpu_identify_files -- pread into the
+    slab (SDGPU_IO=pread), io_uring chains (SDGPU_IO=uring; where the ring is
+    refused it finishes through pread), and the default per-thread buffer
+    streamed into the slab -- give the oracle's cas ids and statuses, in a
+    fresh process each (the variable is read when the context opens)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = files + [str(tmp_path / "missing"), str(tmp_path)]
+    env = dict(os.environ)
+    env.pop("SDGPU_IO", None)
+    if io != "bounce":
+        env["SDGPU_IO"] = io
+    p = subprocess.run([sys.executable, "-c", _IO_CHILD, root, json.dumps(paths)],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    for i, s in enumerate(SIZES):
+        assert res["status"][i] == 0, (io, i)
+        if s == 0:
+            assert res["has"][i] == 0
+        else:
+            assert res["has"][i] == 1 and res["cas"][i] == O.cas_id_path(files[i], s), (io, i)
+    assert res["status"][-2:] == [-2, -21] and res["has"][-2:] == [0, 0], res["status"][-2:]
