@@ -192,8 +192,8 @@ hipError_t dedup_list_launch(const GroupInput& in, uint32_t chunk_rows, uint32_t
                              uint32_t* nospc = nullptr, const KeylessSink* moved = nullptr);
 // extra_list_launch then appends, in row order, the valid keyless rows and
 // (with an index: grouped = the probe's mask, hitrep = its reps) the keyed
-// rows the probe decided -- the index path, the owner's keyless rows of the
-// sharded write set, and SDGPU_KEYLESS_PASS=1.
+// rows the probe decided -- the index path and the owner's keyless rows of
+// the sharded write set.
 size_t extra_workspace_bytes(uint64_t n);
 hipError_t extra_list_launch(const uint8_t* has, const uint8_t* valid, const uint8_t* grouped,
                              const uint32_t* hitrep, const uint32_t* rank, uint32_t first_rank,

@@ -182,3 +182,37 @@ def test_identify_read_paths_agree(io, files, tmp_path):
         else:
             assert res["has"][i] == 1 and res["cas"][i] == O.cas_id_path(files[i], s), (io, i)
     assert res["status"][-2:] == [-2, -21] and res["has"][-2:] == [0, 0], res["status"][-2:]
+
+
+@pytest.fixture(scope="module")
+def config1_dir(tmp_path_factory):
+    """2000 sparse config-1 files (1 KiB-10 MiB) and the oracle's cas ids."""
+    from spacedrive_amd import corpus
+    root = str(tmp_path_factory.mktemp("cfg1"))
+    paths, sizes = corpus.write_config1_dir(root, 2000, seed=7)
+    return paths, [O.cas_id_path(p, int(s)) for p, s in zip(paths, sizes)]
+
+
+@pytest.mark.parametrize("env", [{"SDGPU_SLAB_DIV": "64"}, {"SDGPU_SLAB_TAPER": "1"},
+                                 {"SDGPU_SLAB_DIV": "2", "SDGPU_SLAB_TAPER": "1"},
+                                 {"SDGPU_IO_THREADS": "3"}, {"SDGPU_IO": "uring"}],
+                         ids=["div64", "taper", "div2_taper", "threads3", "uring"])
+def test_identify_staging_schedules_agree(env, config1_dir):
+    """The staging schedule's settings (slab = call bytes / SDGPU_SLAB_DIV,
+    a tail taper, the read-pool size, the io_uring reader) change how 2000
+    config-1 files are cut into slabs and read, never their cas ids: each
+    variant in a fresh process equals the oracle on every file."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths, want = config1_dir
+    e = {k: v for k, v in os.environ.items() if not k.startswith("SDGPU_")}
+    e.update(env)
+    p = subprocess.run([sys.executable, "-c", _IO_CHILD, root, json.dumps(paths)],
+                       capture_output=True, text=True, timeout=180, env=e)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert all(s == 0 for s in res["status"]) and all(h == 1 for h in res["has"])
+    bad = [i for i, (g, w) in enumerate(zip(res["cas"], want)) if g != w]
+    assert not bad, (env, len(bad), bad[:5])
