@@ -1480,6 +1480,11 @@ def build_roofline(c, compress_peak, valu_peak, classes):
             "peak_g_mix_probe": valu_peak / 1e12 if valu_peak else None,
             "peak_by_class_measured": classes,
             "frac_of_measured": achieved / compress_peak if compress_peak else None,
+            # the guide's SIMD-32 full-rate issue (MI355X_MICROARCH.md: 32
+            # lanes per cycle), which only the VOP2 classes above approach;
+            # `peak` is the rate of the VOP3 classes the compression needs
+            "peak_guide_full_rate": 2 * VALU_PEAK_SPEC / 1e12,
+            "frac_of_guide_full_rate": achieved / (2 * VALU_PEAK_SPEC),
             "algorithmic_per_launch": {"compressions": ri["leaf_compressions"],
                                        "int32_ops": ops, "window_bytes": ri["bytes"]},
             "compressions_per_s": ri["leaf_compressions"] / t_leaf if t_leaf else None,
