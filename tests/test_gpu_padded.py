@@ -261,3 +261,75 @@ def test_padded_empty_and_tiny_ranks(ctxs, shares):
     assert len({st["overflow_reruns"] for st in sts}) == 1
     for cm in comms:
         cm.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_sequences_one_rank_rccl(ctx, seed):
+    """Seeded random call sequences through a one-rank RCCL communicator (the
+    RCCL transport's grouped send / receive and completion polling under the
+    per-process state machine): rep and write-set calls on uniform keys, one
+    key 40 k times and all one key, resolved at once or left pending, with
+    `set_exchange` (padded with a hint of 1/4, 1 or 2 times the rows, auto,
+    counted) and `set_return` (full, compact, auto) between calls; every
+    call equals the oracle (file_identifier/mod.rs:136-333)."""
+    import torch
+    from spacedrive_amd import dedup
+    rng = np.random.default_rng(700 + seed)
+    n = 200_000
+    cases = {}
+    for j, name in enumerate(("uniform", "one_key", "all_one")):
+        r2 = np.random.default_rng(800 + 10 * seed + j)
+        pool = r2.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+        k = pool[r2.integers(0, n // 2, n)]
+        if name == "one_key":
+            k[r2.choice(n, 40_000, replace=False)] = pool[3]
+        elif name == "all_one":
+            k[:] = pool[3]
+        h = (r2.random(n) > 0.01).astype(np.uint8)
+        ref = O.group_reps(k, h, 100)
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+        cases[name] = (dev(k.view(np.int64)), dev(h), dev(np.ones(n, np.uint8)),
+                       torch.arange(n, dtype=torch.int32).cuda(), ref,
+                       O.link_batch(ref, None, np.ones(n, np.uint8), 0))
+    comm = dedup.Comm.init_rank(ctx, 1, 0, dedup.Comm.unique_id())
+    held = []
+    try:
+        for i in range(24):
+            u = rng.random()
+            if u < 0.15:
+                comm.set_exchange(int(rng.choice([dedup.EXCHANGE_PADDED, dedup.EXCHANGE_AUTO,
+                                                  dedup.EXCHANGE_COUNTED])),
+                                  int(rng.choice([n // 4, n, 2 * n])))
+                continue
+            if u < 0.25:
+                comm.set_return(int(rng.choice([dedup.RETURN_FULL, dedup.RETURN_COMPACT,
+                                                dedup.RETURN_AUTO])))
+                continue
+            name = str(rng.choice(list(cases)))
+            key, has, val, rk, ref, link = cases[name]
+            wait = bool(rng.random() < 0.4)
+            if rng.random() < 0.5:
+                held.append((i, name, "rep", dedup.group_sharded(key, has, rk, comm, None, 100,
+                                                                 wait=wait)))
+            else:
+                out = dedup.group_link_sharded(key, has, val, rk, comm, 100, cap=2 * n, trim=False)
+                if wait:
+                    comm.wait()
+                held.append((i, name, "list", out))
+        comm.wait()
+        st = comm.stats()
+        for i, name, form, out in held:
+            ref, link = cases[name][4], cases[name][5]
+            if form == "rep":
+                np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref,
+                                              err_msg=f"op {i} {name}")
+            else:
+                who, obj, cnt = out
+                e = int(cnt.cpu()[2])
+                c, lr, lo = dedup.split_link_lists(who[:e].cpu().numpy(), obj[:e].cpu().numpy())
+                np.testing.assert_array_equal(c, link[0], err_msg=f"op {i} {name} creates")
+                np.testing.assert_array_equal(lr, link[1], err_msg=f"op {i} {name} linked rows")
+                np.testing.assert_array_equal(lo, link[2], err_msg=f"op {i} {name} linked objects")
+        assert len(held) >= 10 and st["calls"] >= len(held), st
+    finally:
+        comm.close()
