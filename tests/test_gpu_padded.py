@@ -333,3 +333,70 @@ def test_random_sequences_one_rank_rccl(ctx, seed):
         assert len(held) >= 10 and st["calls"] >= len(held), st
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("world", [2, 3, 5, 8])
+def test_random_sequences_peer_ranks(ctxs, world):
+    """Seeded random call sequences with every rank in this process (peer
+    transport, the _all entry points, each call resolved inside it): rep and
+    write-set calls on uneven shares of uniform keys / one key 40 k times /
+    all one key, `set_exchange` and `set_return` changed on every
+    communicator between calls; every call equals the oracle."""
+    import torch
+    from spacedrive_amd import dedup
+    rng = np.random.default_rng(900 + world)
+    n = 240_000
+    bounds = [n * r * (r + 1) // (world * (world + 1)) for r in range(world + 1)]
+    cases = {}
+    for j, name in enumerate(("uniform", "one_key", "all_one")):
+        r2 = np.random.default_rng(1000 + 10 * world + j)
+        pool = r2.integers(0, 2**64 - 1, n, dtype=np.uint64, endpoint=True)
+        k = pool[r2.integers(0, n // 2, n)]
+        if name == "one_key":
+            k[r2.choice(n, 40_000, replace=False)] = pool[3]
+        elif name == "all_one":
+            k[:] = pool[3]
+        h = (r2.random(n) > 0.01).astype(np.uint8)
+        ref = O.group_reps(k, h, 100)
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+        parts = [(dev(k[a:b].view(np.int64)), dev(h[a:b]), dev(np.ones(b - a, np.uint8)),
+                  torch.arange(a, b, dtype=torch.int64).to(torch.int32).cuda())
+                 for a, b in zip(bounds[:-1], bounds[1:])]
+        cases[name] = (parts, ref, O.link_batch(ref, None, np.ones(n, np.uint8), 0))
+    comms = dedup.Comm.init_all(ctxs[:world])
+    try:
+        calls = 0
+        for i in range(20):
+            u = rng.random()
+            if u < 0.15:
+                mode = int(rng.choice([dedup.EXCHANGE_PADDED, dedup.EXCHANGE_AUTO,
+                                       dedup.EXCHANGE_COUNTED]))
+                hint = int(rng.choice([n // (4 * world), n // world, 2 * n // world]))
+                for c in comms:
+                    c.set_exchange(mode, hint)
+                continue
+            if u < 0.25:
+                ret = int(rng.choice([dedup.RETURN_FULL, dedup.RETURN_COMPACT, dedup.RETURN_AUTO]))
+                for c in comms:
+                    c.set_return(ret)
+                continue
+            name = str(rng.choice(list(cases)))
+            parts, ref, link = cases[name]
+            keys, hass, vals, rks = (list(x) for x in zip(*parts))
+            if rng.random() < 0.5:
+                reps = dedup.group_sharded_all(keys, hass, rks, comms, None, 100)
+                got = np.concatenate([r.cpu().numpy() for r in reps]).view(np.uint32)
+                np.testing.assert_array_equal(got, ref, err_msg=f"op {i} {name}")
+            else:
+                outs = dedup.group_link_sharded_all(keys, hass, vals, rks, comms, 100)
+                w = np.concatenate([o[0].cpu().numpy() for o in outs])
+                ob = np.concatenate([o[1].cpu().numpy() for o in outs])
+                c, lr, lo = dedup.split_link_lists(w, ob)
+                np.testing.assert_array_equal(c, link[0], err_msg=f"op {i} {name} creates")
+                np.testing.assert_array_equal(lr, link[1], err_msg=f"op {i} {name} linked rows")
+                np.testing.assert_array_equal(lo, link[2], err_msg=f"op {i} {name} linked objects")
+            calls += 1
+        assert calls >= 10
+    finally:
+        for c in comms:
+            c.close()
