@@ -1039,7 +1039,11 @@ int resolve_pending(sdgpu_comm* m) {
 // returned; -ENOSPC of the write set comes after the last collective and
 // leaves the peers fine.  J[k].s: the stream the entry point was given (the
 // context's default when NULL); picked here, after the pending call.
-int run_call(std::vector<RankJob>& J, int W, uint32_t chunk_rows, bool list) {
+// all_form: an _all entry point, which resolves its padded call before it
+// returns -- also when it holds a single per-process communicator (one
+// context: a one-rank RCCL communicator), whose call would otherwise be
+// left pending like a per-process entry point's.
+int run_call(std::vector<RankJob>& J, int W, uint32_t chunk_rows, bool list, bool all_form) {
   for (auto& j : J)
     if (j.comm->aborted || (j.comm->transport == SDGPU_TRANSPORT_RCCL && !j.comm->nccl))
       return -ECONNABORTED;
@@ -1072,7 +1076,7 @@ int run_call(std::vector<RankJob>& J, int W, uint32_t chunk_rows, bool list) {
   int rc = list ? run_lists_impl(J, W, chunk_rows, c1) : run_sharded_impl(J, W, chunk_rows, c1);
   if (rc == 0 && !c1) J[0].comm->layout_dirty = false;  // the count messages agreed
   if (rc == 0 && c1) {
-    if (single) {
+    if (single && !all_form) {
       sdgpu_comm* m = J[0].comm;
       m->pending = true;
       m->pending_list = list;
@@ -1593,7 +1597,7 @@ int sdgpu_group_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, sdgpu_index* x,
   j.rank = d_rank;
   j.n = n;
   j.rep = d_rep;
-  return run_call(J, comm->nranks, chunk_rows, false);
+  return run_call(J, comm->nranks, chunk_rows, false, false);
 }
 
 int sdgpu_group_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* comm,
@@ -1636,7 +1640,7 @@ int sdgpu_group_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* com
     j.n = n[r];
     j.rep = d_rep[r];
   }
-  return run_call(J, ngpu, chunk_rows, false);
+  return run_call(J, ngpu, chunk_rows, false, true);
 }
 
 int sdgpu_group_link_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, const uint64_t* d_key,
@@ -1666,7 +1670,7 @@ int sdgpu_group_link_sharded_device(sdgpu_ctx* c, sdgpu_comm* comm, const uint64
   j.obj = d_obj;
   j.counts = d_counts;
   j.cap = cap;
-  return run_call(J, comm->nranks, chunk_rows, true);
+  return run_call(J, comm->nranks, chunk_rows, true, false);
 }
 
 int sdgpu_group_link_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const* comm, int ngpu,
@@ -1709,7 +1713,7 @@ int sdgpu_group_link_sharded_all_device(sdgpu_ctx* const* ctx, sdgpu_comm* const
     j.counts = d_counts[r];
     j.cap = cap[r];
   }
-  return run_call(J, ngpu, chunk_rows, true);
+  return run_call(J, ngpu, chunk_rows, true, true);
 }
 
 int sdgpu_dedup_sharded(sdgpu_ctx* const* ctx, int ngpu, const uint64_t* key,

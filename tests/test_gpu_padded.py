@@ -335,7 +335,7 @@ def test_random_sequences_one_rank_rccl(ctx, seed):
         comm.close()
 
 
-@pytest.mark.parametrize("world", [2, 3, 5, 8])
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
 def test_random_sequences_peer_ranks(ctxs, world):
     """Seeded random call sequences with every rank in this process (peer
     transport, the _all entry points, each call resolved inside it): rep and
@@ -398,5 +398,63 @@ def test_random_sequences_peer_ranks(ctxs, world):
             calls += 1
         assert calls >= 10
     finally:
+        for c in comms:
+            c.close()
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_random_batches_through_sharded_indexes(ctxs, world):
+    """A run cut into random consecutive batches, each grouped over `world`
+    peer ranks against per-rank shares of the Object index (with pre-existing
+    Objects, one of handle 0x7FFFFFFF), the exchange layout and return leg
+    re-drawn before each batch (padded with a hint far below the rows, so
+    some batches overflow and are re-run counted; auto; counted; full /
+    compact return): the reps of the whole run equal the oracle's grouping of
+    all its rows with the library's Objects (file_identifier/mod.rs:168-241).
+    world 1 is the regression case of round 6: one context makes a one-rank
+    per-process communicator, and the _all entry point used to leave its
+    overflowed padded call pending (unresolved reps returned) instead of
+    resolving it before returning as sdgpu.h states."""
+    import torch
+    from spacedrive_amd import dedup
+    rng = np.random.default_rng(1200 + world)
+    total = 600_000
+    k, h, _ = O.synth_dedup_rows(1300 + world, total, 400_000, 0, total)
+    hot = rng.choice(total, 30_000, replace=False)
+    k[hot[hot > 100_000]] = k[17]  # one key many times, mostly in later batches
+    ek = rng.choice(k, 2000)
+    ek[0] = k[17]
+    eh = np.arange(ek.size, dtype=np.uint32) + 5
+    eh[0] = 0x7FFFFFFF
+    ref = O.group_reps_existing(k, h, 100, ek, eh)
+    cuts = np.unique(np.concatenate([[0, total], rng.integers(1, total, 5)]))
+    comms = dedup.Comm.init_all(ctxs[:world])
+    idxs = [dedup.ObjectIndex(c, 1000) for c in ctxs[:world]]
+    try:
+        for r, ix in enumerate(idxs):
+            ix.add_objects(torch.from_numpy(ek.view(np.int64)).cuda(),
+                           torch.from_numpy(eh.view(np.int32)).cuda(), world, r)
+        out = np.zeros(total, np.uint32)
+        for b0, b1 in zip(cuts[:-1], cuts[1:]):
+            m = b1 - b0
+            mode = int(rng.choice([dedup.EXCHANGE_PADDED, dedup.EXCHANGE_AUTO, dedup.EXCHANGE_COUNTED]))
+            hint = int(rng.choice([max(1, m // (8 * world)), m // world + 1]))
+            ret = int(rng.choice([dedup.RETURN_FULL, dedup.RETURN_COMPACT, dedup.RETURN_AUTO]))
+            for c in comms:
+                c.set_exchange(mode, hint)
+                c.set_return(ret)
+            spans = [(b0 + m * r // world, b0 + m * (r + 1) // world) for r in range(world)]
+            dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+            reps = dedup.group_sharded_all(
+                [dev(k[a:b].view(np.int64)) for a, b in spans], [dev(h[a:b]) for a, b in spans],
+                [torch.arange(a, b, dtype=torch.int64).to(torch.int32).cuda() for a, b in spans],
+                comms, idxs, 100)
+            for (a, b), rp in zip(spans, reps):
+                out[a:b] = rp.cpu().numpy().view(np.uint32)
+            bad = np.flatnonzero(out[b0:b1] != ref[b0:b1])
+            assert bad.size == 0, (world, b0, b1, mode, hint, ret, bad.size, bad[:5] + b0)
+    finally:
+        for ix in idxs:
+            ix.close()
         for c in comms:
             c.close()
