@@ -201,7 +201,8 @@ def test_random_call_sequences_across_processes(world):
     data["fuzz_ops"] = np.int64(20)
     data["msg_bytes"] = np.int64(16 * world * (TOTAL + 4096))
     np.savez(os.path.join(work, "data.npz"), **data)
-    seeds = [f"fuzz_{world * 100 + s}" for s in range(5)]
+    soak = int(os.environ.get("SD_SOAK", "0"))  # SD_SOAK=k: 5 k more seeds
+    seeds = [f"fuzz_{world * 100 + s}" for s in range(5 + 5 * soak)]
     outs = _run_ranks(work, world, seeds)
     calls = reruns = padded = 0
     for j, sc in enumerate(seeds):

@@ -8,12 +8,18 @@ all rows (file_identifier/mod.rs:136-333 canonical rule):
 uniform keys (no overflow), one key repeated 40 k times and an all-one-key
 batch (overflow, re-run) at 1 / 2 / 3 / 8 ranks (peer transport: contexts
 sharing the one GPU) and through a one-rank RCCL communicator."""
+import os
+
 import numpy as np
 import pytest
 
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
+
+# SD_SOAK=k: k more rounds of seeds for the random call-sequence tests (a
+# longer bug hunt than the default run)
+SOAK = int(os.environ.get("SD_SOAK", "0"))
 
 
 @pytest.fixture(scope="module")
@@ -263,7 +269,7 @@ def test_padded_empty_and_tiny_ranks(ctxs, shares):
         cm.close()
 
 
-@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("seed", range(4 + 4 * SOAK))
 def test_random_sequences_one_rank_rccl(ctx, seed):
     """Seeded random call sequences through a one-rank RCCL communicator (the
     RCCL transport's grouped send / receive and completion polling under the
@@ -335,8 +341,9 @@ def test_random_sequences_one_rank_rccl(ctx, seed):
         comm.close()
 
 
+@pytest.mark.parametrize("rep", range(1 + SOAK))
 @pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
-def test_random_sequences_peer_ranks(ctxs, world):
+def test_random_sequences_peer_ranks(ctxs, world, rep):
     """Seeded random call sequences with every rank in this process (peer
     transport, the _all entry points, each call resolved inside it): rep and
     write-set calls on uneven shares of uniform keys / one key 40 k times /
@@ -344,7 +351,7 @@ def test_random_sequences_peer_ranks(ctxs, world):
     communicator between calls; every call equals the oracle."""
     import torch
     from spacedrive_amd import dedup
-    rng = np.random.default_rng(900 + world)
+    rng = np.random.default_rng(900 + world + 10_000 * rep)
     n = 240_000
     bounds = [n * r * (r + 1) // (world * (world + 1)) for r in range(world + 1)]
     cases = {}
@@ -402,8 +409,9 @@ def test_random_sequences_peer_ranks(ctxs, world):
             c.close()
 
 
+@pytest.mark.parametrize("rep", range(1 + SOAK))
 @pytest.mark.parametrize("world", [1, 3, 8])
-def test_random_batches_through_sharded_indexes(ctxs, world):
+def test_random_batches_through_sharded_indexes(ctxs, world, rep):
     """A run cut into random consecutive batches, each grouped over `world`
     peer ranks against per-rank shares of the Object index (with pre-existing
     Objects, one of handle 0x7FFFFFFF), the exchange layout and return leg
@@ -417,7 +425,7 @@ def test_random_batches_through_sharded_indexes(ctxs, world):
     resolving it before returning as sdgpu.h states."""
     import torch
     from spacedrive_amd import dedup
-    rng = np.random.default_rng(1200 + world)
+    rng = np.random.default_rng(1200 + world + 10_000 * rep)
     total = 600_000
     k, h, _ = O.synth_dedup_rows(1300 + world, total, 400_000, 0, total)
     hot = rng.choice(total, 30_000, replace=False)
