@@ -29,6 +29,7 @@ def main():
     ctx = Context(0)
     data = np.load(os.path.join(work, "data.npz"))
     timeout = int(os.environ.get("SD_HOST_TIMEOUT_MS", "60000"))
+    trace = os.environ.get("SD_HOST_TRACE") == "1"  # per-call progress on stderr
 
     def rows(case):
         k, h = data[f"k_{case}"], data[f"h_{case}"]
@@ -166,7 +167,13 @@ def main():
                         comm.wait()
                 held.append((i, form, out))
                 ops.append([form, case, int(wait), i])
+                if trace:
+                    print(json.dumps({"rank": rank, "sc": sc, "op": ops[-1], "stats": comm.stats()}),
+                          file=sys.stderr, flush=True)
             res["wait"] = rc_of(comm.wait)
+            if trace:
+                print(json.dumps({"rank": rank, "sc": sc, "final_wait": res["wait"],
+                                  "stats": comm.stats()}), file=sys.stderr, flush=True)
             for i, form, out in held:  # every call is resolved now
                 if form == "rep":
                     save[f"op{i}_rep"] = out.cpu().numpy()

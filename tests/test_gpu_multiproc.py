@@ -55,18 +55,27 @@ def _spans(total, world):  # uneven shares, contiguous, in rank order
                     np.int64)
 
 
-def _run_ranks(work, world, scenarios, timeout_ms=60000):
-    # PYTHONFAULTHANDLER: a rank that dies on a signal names its Python frame
+def _run_ranks(work, world, scenarios, timeout_ms=60000, proc_timeout=150):
+    # PYTHONFAULTHANDLER: a rank that dies on a signal names its Python frame.
+    # Each rank writes to files, not pipes: a pipe read only after an earlier
+    # rank exits fills up (64 KiB) and blocks the later rank mid-exchange --
+    # the ranks then wait on each other until the communicator times out
     env = dict(os.environ, SD_HOST_TIMEOUT_MS=str(timeout_ms), PYTHONFAULTHANDLER="1")
+    files = [(open(os.path.join(work, f"rank{r}.out"), "w+"), open(os.path.join(work, f"rank{r}.err"), "w+"))
+             for r in range(world)]
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "_host_rank.py"),
                                ROOT, str(world), str(r), work, ",".join(scenarios)],
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+                              stdout=files[r][0], stderr=files[r][1], text=True, env=env)
              for r in range(world)]
     outs = []
     try:
         errs = []
         for r, p in enumerate(procs):
-            out, err = p.communicate(timeout=150)
+            p.wait(timeout=proc_timeout)
+            fo, fe = files[r]
+            fo.seek(0)
+            fe.seek(0)
+            out, err = fo.read(), fe.read()
             if p.returncode != 0:
                 errs.append(f"rank {r} rc {p.returncode}: {err[-2500:]}")
             outs.append([json.loads(x) for x in out.splitlines() if x.startswith("{")])
@@ -75,6 +84,9 @@ def _run_ranks(work, world, scenarios, timeout_ms=60000):
         for p in procs:
             if p.poll() is None:
                 p.kill()
+        for fo, fe in files:
+            fo.close()
+            fe.close()
     return outs  # [rank][scenario] -> dict
 
 
@@ -203,7 +215,7 @@ def test_random_call_sequences_across_processes(world):
     np.savez(os.path.join(work, "data.npz"), **data)
     soak = int(os.environ.get("SD_SOAK", "0"))  # SD_SOAK=k: 5 k more seeds
     seeds = [f"fuzz_{world * 100 + s}" for s in range(5 + 5 * soak)]
-    outs = _run_ranks(work, world, seeds)
+    outs = _run_ranks(work, world, seeds, proc_timeout=150 + 30 * soak)
     calls = reruns = padded = 0
     for j, sc in enumerate(seeds):
         rs = [outs[r][j] for r in range(world)]
