@@ -1,12 +1,17 @@
 """Seeded randomized GPU parity sweeps (bounded: ~1 min in all): many small
 random configurations of each hot-path kernel against the oracle, bit-exact.
 Each case prints nothing unless it fails; the seed identifies it."""
+import os
+
 import numpy as np
 import pytest
 
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
+
+# SD_SOAK=k: (1 + k) times the seeds of every sweep (a longer bug hunt)
+SOAK = 1 + int(os.environ.get("SD_SOAK", "0"))
 
 
 def _lengths(rng, n):
@@ -20,7 +25,7 @@ def _lengths(rng, n):
     return out.astype(np.uint32)
 
 
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(40 * SOAK))
 def test_fuzz_k1_device_batches(ctx, seed):
     """K1 over random batches (1..6000 messages, random gaps between 16-B
     aligned messages, random content) through the device entry point."""
@@ -45,7 +50,7 @@ def test_fuzz_k1_device_batches(ctx, seed):
     np.testing.assert_array_equal(out.cpu().numpy(), O.cas_batch(arena, off, ln, 4))
 
 
-@pytest.mark.parametrize("seed", range(48))
+@pytest.mark.parametrize("seed", range(48 * SOAK))
 def test_fuzz_grouping_device(ctx, seed):
     """Grouping over random shapes: 1..3 M rows, few to all-distinct keys,
     small-integer or all-ones keys, random ranks (a permutation), chunk sizes
@@ -80,7 +85,7 @@ def test_fuzz_grouping_device(ctx, seed):
     np.testing.assert_array_equal(rep, ref[rank])
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(8 * SOAK))
 def test_fuzz_grouping_large(ctx, seed):
     """The 12-bit path (block-major counts, one-launch offsets) and the
     two-level path (fine counts from the coarse pass) over random large shapes:
@@ -116,7 +121,7 @@ def test_fuzz_grouping_large(ctx, seed):
     np.testing.assert_array_equal(rep, ref[rank])
 
 
-@pytest.mark.parametrize("seed", range(20))
+@pytest.mark.parametrize("seed", range(20 * SOAK))
 def test_fuzz_checksum_batches(ctx, seed):
     """Tree hashing of random device-resident file batches (1..40 files,
     0..24 MiB each, lengths near chunk / group / power-of-two edges)."""
@@ -153,7 +158,7 @@ def ctxs():
         c.close()
 
 
-@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("seed", range(16 * SOAK))
 def test_fuzz_sharded_and_indexed(ctxs, seed):
     """The multi-GPU grouping (peer transport between contexts on the one
     GPU) at a random world size, and the same rows grouped in random batches
