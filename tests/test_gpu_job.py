@@ -147,6 +147,39 @@ def test_job_uninterrupted_vs_resumed_vs_oracle(ctx, tmp_path):
     assert ta.object_id[fids[2] - 1] is None  # the missing file stays an orphan
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_job_resumed_at_random_points(ctx, tmp_path, seed):
+    """The job paused and resumed from its JSON state several times at random
+    step counts, with a random number of reference chunks per GPU step, in a
+    fresh job (and a fresh Object index) each time: the table ends equal to
+    the uninterrupted run's and to the oracle's Objects
+    (file_identifier_job.rs:32-309: the cursor and the counts carry over)."""
+    from spacedrive_amd.file_identifier import FileIdentifierJob
+    rng = np.random.default_rng(500 + seed)
+    t0, loc = _make_library(str(tmp_path), n=1800, seed=40 + seed)
+    fids = t0.orphans(1)
+    per = int(rng.choice([1, 2, 5]))  # >= 4 GPU steps over ~19 chunks
+    ta = _clone(t0)
+    ja = FileIdentifierJob(ta, 1, loc, chunks_per_step=per, ctx=ctx).init()
+    ja.run()
+    ja.close()
+    tb = _clone(t0)
+    job = FileIdentifierJob(tb, 1, loc, chunks_per_step=per, ctx=ctx).init()
+    legs = 0
+    while True:
+        job.run(max_steps=int(rng.integers(1, 3)))
+        state = json.loads(json.dumps(job.state()))
+        done = job.step_number >= job.task_count
+        job.close()
+        legs += 1
+        if done:
+            break
+        job = FileIdentifierJob.resume(tb, state, ctx=ctx)
+    assert legs >= 2
+    assert tb.object_id == ta.object_id and tb.cas_id == ta.cas_id
+    _check_against_oracle(t0, tb, loc, fids)
+
+
 def test_job_sub_path_and_early_finish(ctx, tmp_path):
     from spacedrive_amd.file_identifier import EarlyFinish, FileIdentifierJob
     t0, loc = _make_library(str(tmp_path), n=800)
