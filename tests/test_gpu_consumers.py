@@ -78,3 +78,28 @@ def test_thumbnail_shards_skewed_bytes(ctx, values):
     eo, ec = O.thumbnail_shards(cas8, valid)
     np.testing.assert_array_equal(counts.cpu().numpy(), ec)
     np.testing.assert_array_equal(order.cpu().numpy(), eo)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_orphan_objects_random(ctx, seed):
+    """Random shapes: Object ids from 0 up (unique, any order), file_paths
+    pointing at Objects, at ids no Object has (also past max_id), NULL (-1),
+    or all at one Object; sizes across tile edges. Equal to the oracle."""
+    import torch
+    from spacedrive_amd import consumers
+    rng = np.random.default_rng(4000 + seed)
+    n_obj = int(rng.choice([1, 2, 4095, 4097, 65_536, 250_001]))
+    n_fp = int(rng.choice([0, 1, 100, 5000, 300_000]))
+    objs = rng.permutation(int(n_obj * rng.choice([1, 1.5, 4])))[:n_obj].astype(np.int32)
+    maxid = int(objs.max())
+    kind = seed % 3
+    if kind == 0:
+        fp = rng.choice(objs, n_fp).astype(np.int32)
+    elif kind == 1:
+        fp = rng.integers(-1, 2 * maxid + 3, n_fp).astype(np.int32)
+    else:
+        fp = np.full(n_fp, objs[0], np.int32)
+    fp[rng.random(n_fp) < 0.05] = -1
+    got = consumers.orphan_objects(torch.from_numpy(objs).cuda(), torch.from_numpy(fp).cuda(),
+                                   maxid, ctx)
+    np.testing.assert_array_equal(got.cpu().numpy(), O.orphan_objects(objs, fp))
