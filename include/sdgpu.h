@@ -352,7 +352,8 @@ int sdgpu_comm_wait(sdgpu_comm *comm, void *stream);
  *     COUNTED.
  * Every rank of a communicator must set the same mode (and rows_hint, which
  * sets B when > 0).  The _all entry points (one process, all ranks) resolve
- * a padded call before they return.
+ * a padded call before they return -- also with ngpu = 1, whose communicator
+ * is a one-rank per-process one.
  * Agreement (ABI 6): a communicator's first call and its first call after
  * sdgpu_comm_set_exchange / sdgpu_comm_set_return (which every rank must
  * call alike, between the same two exchange calls) check that every rank
